@@ -1,0 +1,179 @@
+#!/usr/bin/env python3
+"""Decode throughput benchmark (BASELINE.json metric) for the MI355X engine.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model llama3-8b]
+
+Workload (BASELINE.json configs[2]/[3]): Llama-3-8B bf16 with
+synthetic weights (seed 0; no checkpoint exists offline), 32 concurrent
+sequences per micro-batch, prompts U[16,256] tokens from seed 2 (prefilled,
+untimed), then K greedy decode steps timed.  A "step" = one decode token for
+every sequence of every micro-batch.
+
+N = 1: one GPU runs the whole model, one micro-batch of 32 sequences.
+N > 1: launched by torch.distributed.run, one rank per GPU; rank r holds a
+contiguous, byte-balanced layer shard (pipeline stage r); N micro-batches of 32
+sequences are in flight; hidden states go stage->stage with RCCL send/recv
+over xGMI and the sampled token ids go back from the last stage to stage 0
+(llama-p2p_amd/pipeline.py).  Per-GPU work is fixed as N grows (weak scaling).
+
+Output: one JSON line (rank 0) with value = total decode tokens/s over all
+GPUs, the dominant kernel's roofline (HIP-event timed, same stream) and the CPU
+oracle timed on this host's cores (N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "decode tokens/sec (node) + % HBM roofline, Llama-3-8B at 1/2/4/8-stage"
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
+MB_SEQS = 32
+
+
+def make_prompts(vocab: int, n: int, seed: int = 2, lo: int = 16, hi: int = 256):
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(lo, hi + 1, n)
+    return [np.concatenate([[1], rng.integers(3, vocab, L - 1)]).astype(np.int32) for L in lens]
+
+
+def cpu_baseline(shape_name: str, n_prompt: int = 4, n_decode: int = 6):
+    """The CPU oracle (C/OpenMP restatement of llama.cpp's CPU forward, bf16
+    weights, f32 accumulation) doing what the reference does: batch-1 greedy
+    decode, timed on this host's cores.  Bounded sample: n_decode tokens."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES[shape_name]
+    t0 = time.time()
+    m = O.OracleModel(shape, seed=0)
+    ctx = m.context(64)
+    t_gen = time.time() - t0
+    prompt = make_prompts(shape.n_vocab, 1, seed=5, lo=n_prompt, hi=n_prompt)[0]
+    lg = ctx.eval(prompt, 0)
+    tok = int(lg[0].argmax())
+    t1 = time.time()
+    for i in range(n_decode):
+        lg = ctx.eval([tok], n_prompt + i)
+        tok = int(lg[0].argmax())
+    dt = time.time() - t1
+    cores = O.lib().orc_num_threads()
+    ctx.close()
+    m.close()
+    return {"value": round(n_decode / dt, 3), "unit": "tokens/s", "cores": cores, "kind": "port",
+            "sample": f"{shape_name} bf16, batch 1 (the reference's serial path), {n_prompt}-token prompt then "
+                      f"{n_decode} greedy decode tokens timed; weight synthesis {t_gen:.1f}s untimed"}
+
+
+def run_single(args):
+    import numpy as np
+
+    from llama_p2p_amd import synth
+    from llama_p2p_amd.engine import Engine
+
+    shape = synth.SHAPES[args.model]
+    M = args.seqs
+    eng = Engine(f"synthetic:{args.model}:seed=0", n_ctx=args.n_ctx, n_seq_max=max(M, 1))
+    prompts = make_prompts(shape.n_vocab, M)
+    # prefill (untimed): chunked rows through the engine; first token = greedy
+    first = []
+    for i, p in enumerate(prompts):
+        lg = eng.forward_logits(p, 0, slot=i)
+        first.append(int(lg[-1].argmax()))
+    b = eng.batch(slots=list(range(M)), pos=[len(p) for p in prompts], ids=first,
+                  max_steps=args.warmup + args.steps)
+    for _ in range(args.warmup):
+        b.step()
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        b.step()
+    eng.sync()
+    dt = time.perf_counter() - t0
+    toks = b.tokens()
+    assert toks.shape[1] == args.warmup + args.steps
+    # algorithmic bytes per decode step: weights + KV read/write + logits
+    ctx_sum = sum(len(p) + args.warmup + args.steps / 2 for p in prompts)
+    step_bytes = eng.info.weight_bytes + ctx_sum * shape.kv_bytes_per_pos() + M * shape.kv_bytes_per_pos() + \
+        M * shape.n_vocab * 4
+    res = {"tok_s": M * args.steps / dt, "ms_per_step": dt * 1e3 / args.steps,
+           "step_gbs": step_bytes / (dt / args.steps) / 1e9, "step_bytes": step_bytes}
+    # dominant kernel: ffn gate/up (fused, 2 x n_ff x n_embd bf16 per layer) -- HIP events on the engine stream
+    us, wbytes = eng.profile_kernel(2, M, iters=3)
+    kbytes = wbytes + M * shape.n_embd * 2 + M * shape.n_ff * 2  # weights + activations in/out
+    res["roofline"] = {"bound": "hbm", "achieved": round(kbytes / us / 1e3, 1), "peak": HBM_PEAK_GBS,
+                       "unit": "GB/s", "frac": round(kbytes / us / 1e3 / HBM_PEAK_GBS, 4), "traffic": None,
+                       "kernel": "mm_kernel<EPI_SWIGLU> (ffn_gate+ffn_up+SiLU*up)", "us_per_launch": round(us, 2),
+                       "bytes_per_launch": int(kbytes)}
+    # batch-1 decode (the north_star's 70% target), same engine
+    if args.batch1_steps > 0:
+        b1 = eng.batch(slots=[M if M < eng.info.n_seq_max else 0], pos=[len(prompts[0])], ids=[first[0]],
+                       max_steps=args.batch1_steps + 4)
+        for _ in range(4):
+            b1.step()
+        eng.sync()
+        t0 = time.perf_counter()
+        for _ in range(args.batch1_steps):
+            b1.step()
+        eng.sync()
+        d1 = (time.perf_counter() - t0) / args.batch1_steps
+        b1_bytes = eng.info.weight_bytes + (len(prompts[0]) + 4 + args.batch1_steps / 2) * shape.kv_bytes_per_pos()
+        res["batch1"] = {"tok_s": round(1.0 / d1, 2), "ms_per_token": round(d1 * 1e3, 3),
+                         "hbm_frac": round(b1_bytes / d1 / 1e9 / HBM_PEAK_GBS, 4),
+                         "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / b1_bytes, 1)}
+        b1.close()
+    b.close()
+    eng.close()
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--seqs", type=int, default=MB_SEQS, help="sequences per micro-batch")
+    ap.add_argument("--n-ctx", type=int, default=512)
+    ap.add_argument("--batch1-steps", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 or args.gpus > 1:
+        from llama_p2p_amd import pipeline
+
+        return pipeline.bench_main(args, METRIC, make_prompts)
+
+    res = run_single(args)
+    line = {
+        "metric": METRIC, "value": round(res["tok_s"], 2), "unit": "tokens/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(res["ms_per_step"], 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (seeded random bf16 weights of the exact shape; random prompt ids)",
+        "config": {"workload": f"{args.model} greedy decode, {args.seqs} concurrent sequences, prompts U[16,256] "
+                               f"(seed 2), n_ctx {args.n_ctx}", "model": args.model, "stages": 1,
+                   "micro_batches": 1, "seqs_per_micro_batch": args.seqs, "parallelism": "pp1"},
+        "step_hbm_gbs": round(res["step_gbs"], 1), "step_hbm_frac": round(res["step_gbs"] / HBM_PEAK_GBS, 4),
+        "roofline": res["roofline"],
+    }
+    if "batch1" in res:
+        line["batch1"] = res["batch1"]
+    if not args.no_cpu_baseline:
+        try:
+            line["cpu_baseline"] = cpu_baseline(args.model)
+        except Exception as ex:  # report, never hide
+            line["cpu_baseline"] = {"error": repr(ex)}
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,1022 @@
+// engine.cpp -- host side of the MI355X-native engine behind include/mx_engine.h.
+//
+// Replaces llama-cpp-python/llama.cpp as used by the reference node:
+//   Llama(model_path=...)                 /root/reference/llama_p2p_network.py:19  -> mx_engine_create
+//   self.model(prompt, max_tokens=100)    /root/reference/llama_p2p_network.py:125 -> mx_submit/mx_wait
+// The forward pass is llama.cpp's llm_build_llama expressed as
+// five fused gfx950 kernels per layer (kernels.hip).  Decode steps are captured
+// once per batch shape as hipGraphs and replayed; a scheduler thread replaces
+// the reference's serialising lock (p2p:121) with micro-batched decode of all
+// active requests.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/mx_engine.h"
+#include "gguf.h"
+#include "kernels.h"
+
+using namespace mx;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPC(expr)                                                                                  \
+  do {                                                                                              \
+    hipError_t _e = (expr);                                                                         \
+    if (_e != hipSuccess)                                                                           \
+      return fail(MX_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e) + " @" + __FILE__ + \
+                                  ":" + std::to_string(__LINE__));                                  \
+  } while (0)
+
+struct Shape {
+  const char* name;
+  int n_embd, n_layer, n_head, n_head_kv, n_ff, n_vocab;
+  float rope_base, eps;
+  int n_ctx_train;
+};
+// keep in sync with llama-p2p_amd/synth.py SHAPES
+const Shape kShapes[] = {
+    {"tinyllama-1.1b", 2048, 22, 32, 4, 5632, 32000, 10000.f, 1e-5f, 2048},
+    {"llama3-8b", 4096, 32, 32, 8, 14336, 128256, 500000.f, 1e-5f, 8192},
+    {"llama3-70b", 8192, 80, 64, 8, 28672, 128256, 500000.f, 1e-5f, 8192},
+    {"test-tiny", 256, 2, 4, 2, 512, 512, 10000.f, 1e-5f, 2048},
+    {"test-gqa8", 512, 3, 8, 1, 1024, 1024, 500000.f, 1e-5f, 2048},
+    {"test-d128", 1024, 2, 8, 2, 2816, 2048, 500000.f, 1e-5f, 2048},
+};
+
+// synth.py tensor ids
+constexpr uint64_t TID_TOK_EMBD = 1, TID_OUT_NORM = 2, TID_OUTPUT = 3;
+enum { L_ATTN_NORM, L_Q, L_K, L_V, L_O, L_FFN_NORM, L_GATE, L_UP, L_DOWN };
+uint64_t layer_tid(int l, int k) { return 16u + 16u * (uint64_t)l + (uint64_t)k; }
+float std_scale(double std) { return (float)(std / sqrt(4294967295.0 / 3.0)); }
+
+struct Layer {
+  uint16_t *qkv = nullptr, *o = nullptr, *gu = nullptr, *down = nullptr;
+  float *attn_norm = nullptr, *ffn_norm = nullptr;
+};
+
+struct Request {
+  uint64_t id = 0;
+  std::vector<int32_t> prompt;
+  mx_sampling samp{};
+  int max_tokens = 0;
+  std::vector<int32_t> out;
+  int finish = -1;
+  bool done = false;
+  int slot = -1;
+  int pos = 0;  // next position to write
+  int32_t next_tok = 0;
+  std::mt19937_64 rng;
+  std::string error;
+};
+
+struct GraphKey {
+  int M;
+  const void* xin;
+  void* xout;
+  hipStream_t stream;
+  bool operator<(const GraphKey& o) const {
+    if (M != o.M) return M < o.M;
+    if (xin != o.xin) return xin < o.xin;
+    if (xout != o.xout) return xout < o.xout;
+    return stream < o.stream;
+  }
+};
+}  // namespace
+
+struct mx_batch {
+  int M = 0, max_steps = 0;
+  int max_pos = 0;  // host mirror of the largest position, so steps never run past n_ctx
+  int *d_ids = nullptr, *d_pos = nullptr, *d_slot = nullptr, *d_hist = nullptr, *d_hist_count = nullptr;
+  std::map<GraphKey, hipGraphExec_t> graphs;
+};
+
+struct mx_engine {
+  // hyper-parameters
+  int n_embd = 0, n_layer = 0, n_head = 0, n_head_kv = 0, head_dim = 0, n_embd_kv = 0, n_ff = 0, n_vocab = 0;
+  int n_ctx_train = 0;
+  float eps = 1e-5f, rope_base = 10000.f;
+  int bos = 1, eos = 2;
+  int n_ctx = 512, n_seq_max = 64, lb = 0, le = 0, device = 0;
+  bool has_embed = true, has_head = true, use_graphs = true;
+  int n_chunks = 0;
+  uint64_t weight_bytes = 0;
+
+  // device state
+  hipStream_t stream = nullptr;
+  uint16_t *tok_embd = nullptr, *output = nullptr;
+  float* out_norm = nullptr;
+  std::vector<Layer> layers;  // local layers [lb, le)
+  _Float16 *kcache = nullptr, *vcache = nullptr;
+  size_t slot_stride = 0, layer_kv_stride = 0;
+  float* rope_cs = nullptr;
+  // workspaces (MAX_ROWS rows)
+  float *x = nullptr, *q = nullptr, *o_part = nullptr, *ml_part = nullptr, *logits = nullptr;
+  uint16_t *xn = nullptr, *act = nullptr, *attn_out = nullptr;
+  float* am_val = nullptr;
+  int *am_idx = nullptr, *d_tok = nullptr;
+  int *d_ids = nullptr, *d_pos = nullptr, *d_slot = nullptr, *d_rowmap = nullptr;
+  std::vector<void*> allocations;
+
+  // graphs for the scheduler's decode steps, by M
+  std::map<int, hipGraphExec_t> sched_graphs;
+
+  // scheduler
+  std::mutex gpu_mu;  // serialises all GPU work issued through the API
+  std::mutex mu;
+  std::condition_variable cv, cv_done;
+  std::deque<Request*> pending;
+  std::vector<Request*> active;
+  std::map<uint64_t, std::unique_ptr<Request>> requests;
+  std::vector<int> free_slots;
+  uint64_t next_id = 1;
+  bool stop = false;
+  std::thread worker;
+  bool worker_started = false;
+
+  ~mx_engine();
+  int alloc(void** p, size_t bytes) {
+    HIPC(hipMalloc(p, bytes));
+    allocations.push_back(*p);
+    return 0;
+  }
+  int init_common();
+  int load_synthetic(const Shape& s, uint64_t seed);
+  int load_gguf(const std::string& path);
+  int enqueue_forward(int M, const int* ids, const int* pos, const int* slot, const void* x_in, void* x_out,
+                      bool head, const int* rowmap, int n_out, bool argmax, int* ids_next, int* pos_next, int* hist,
+                      int hist_stride, int* hist_count, int max_hist, hipStream_t s);
+  int forward_rows_chunk(int n, const int32_t* slots, const int32_t* pos, const int32_t* ids, const void* x_in,
+                         void* x_out, float* logits_host, hipStream_t s);
+  void scheduler_loop();
+  int sched_step(std::vector<Request*>& rows);
+  int prefill(Request* r, std::vector<float>& last_logits);
+  int32_t sample_host(Request* r, const float* logits);
+  void finish(Request* r, int why);
+};
+
+mx_engine::~mx_engine() {
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    stop = true;
+  }
+  cv.notify_all();
+  if (worker.joinable()) worker.join();
+  for (auto& kv : sched_graphs) hipGraphExecDestroy(kv.second);
+  if (stream) hipStreamSynchronize(stream);
+  for (void* p : allocations) hipFree(p);
+  if (stream) hipStreamDestroy(stream);
+}
+
+int mx_engine::init_common() {
+  head_dim = n_embd / n_head;
+  n_embd_kv = head_dim * n_head_kv;
+  if (n_embd % n_head || n_head % n_head_kv) return fail(MX_ERR_MODEL, "head counts do not divide n_embd/n_head");
+  if (head_dim != 64 && head_dim != 128) return fail(MX_ERR_ARG, "head_dim must be 64 or 128");
+  const int G = n_head / n_head_kv;
+  if (G != 1 && G != 2 && G != 4 && G != 8) return fail(MX_ERR_ARG, "n_head/n_head_kv must be 1,2,4 or 8");
+  if (n_embd % 32 || n_ff % 32 || n_vocab % 16 || n_embd_kv % 16)
+    return fail(MX_ERR_ARG, "n_embd, n_ff must be multiples of 32 and n_vocab, n_embd_kv of 16");
+  if (le < 0 || le > n_layer) le = n_layer;
+  if (lb < 0 || lb >= le) return fail(MX_ERR_ARG, "bad layer range");
+  has_embed = lb == 0;
+  has_head = le == n_layer;
+  n_chunks = (n_ctx + ATTN_CHUNK - 1) / ATTN_CHUNK;
+  const int nl = le - lb;
+  layers.resize(nl);
+
+  // KV cache [layer][slot][kv head][pos][dim] f16
+  slot_stride = (size_t)n_head_kv * n_ctx * head_dim;
+  layer_kv_stride = slot_stride * n_seq_max;
+  if (int rc = alloc((void**)&kcache, layer_kv_stride * nl * sizeof(_Float16))) return rc;
+  if (int rc = alloc((void**)&vcache, layer_kv_stride * nl * sizeof(_Float16))) return rc;
+  HIPC(hipMemsetAsync(kcache, 0, layer_kv_stride * nl * sizeof(_Float16), stream));
+  HIPC(hipMemsetAsync(vcache, 0, layer_kv_stride * nl * sizeof(_Float16), stream));
+
+  // RoPE table, ggml_rope_cache_init recipe: theta *= powf(base, -2/d) in f32
+  std::vector<float> cs((size_t)n_ctx * head_dim);
+  const float theta_scale = powf(rope_base, -2.0f / (float)head_dim);
+  for (int p = 0; p < n_ctx; p++) {
+    float theta = (float)p;
+    for (int i = 0; i < head_dim / 2; i++) {
+      cs[((size_t)p * (head_dim / 2) + i) * 2] = cosf(theta);
+      cs[((size_t)p * (head_dim / 2) + i) * 2 + 1] = sinf(theta);
+      theta *= theta_scale;
+    }
+  }
+  if (int rc = alloc((void**)&rope_cs, cs.size() * 4)) return rc;
+  HIPC(hipMemcpy(rope_cs, cs.data(), cs.size() * 4, hipMemcpyHostToDevice));
+
+  const int R = MAX_ROWS;
+  if (int rc = alloc((void**)&x, (size_t)R * n_embd * 4)) return rc;
+  if (int rc = alloc((void**)&q, (size_t)R * n_embd * 4)) return rc;
+  if (int rc = alloc((void**)&xn, (size_t)R * n_embd * 2)) return rc;
+  if (int rc = alloc((void**)&attn_out, (size_t)R * n_embd * 2)) return rc;
+  if (int rc = alloc((void**)&act, (size_t)R * n_ff * 2)) return rc;
+  if (int rc = alloc((void**)&o_part, (size_t)R * n_head * n_chunks * head_dim * 4)) return rc;
+  if (int rc = alloc((void**)&ml_part, (size_t)R * n_head * n_chunks * 2 * 4)) return rc;
+  if (has_head) {
+    if (int rc = alloc((void**)&logits, (size_t)R * n_vocab * 4)) return rc;
+  }
+  if (int rc = alloc((void**)&am_val, (size_t)R * 64 * 4)) return rc;
+  if (int rc = alloc((void**)&am_idx, (size_t)R * 64 * 4)) return rc;
+  if (int rc = alloc((void**)&d_tok, (size_t)R * 4)) return rc;
+  if (int rc = alloc((void**)&d_ids, (size_t)R * 4)) return rc;
+  if (int rc = alloc((void**)&d_pos, (size_t)R * 4)) return rc;
+  if (int rc = alloc((void**)&d_slot, (size_t)R * 4)) return rc;
+  if (int rc = alloc((void**)&d_rowmap, (size_t)R * 4)) return rc;
+  // poison-free start: zero activations so padded MFMA columns never read uninitialised memory
+  HIPC(hipMemsetAsync(xn, 0, (size_t)R * n_embd * 2, stream));
+  HIPC(hipMemsetAsync(attn_out, 0, (size_t)R * n_embd * 2, stream));
+  HIPC(hipMemsetAsync(act, 0, (size_t)R * n_ff * 2, stream));
+  for (int i = 0; i < n_seq_max; i++) free_slots.push_back(n_seq_max - 1 - i);
+  return 0;
+}
+
+static int alloc_layer(mx_engine* e, Layer& L) {
+  const size_t h = e->n_embd, kv = e->n_embd_kv, ff = e->n_ff;
+  if (int rc = e->alloc((void**)&L.qkv, (h + 2 * kv) * h * 2)) return rc;
+  if (int rc = e->alloc((void**)&L.o, h * h * 2)) return rc;
+  if (int rc = e->alloc((void**)&L.gu, 2 * ff * h * 2)) return rc;
+  if (int rc = e->alloc((void**)&L.down, h * ff * 2)) return rc;
+  if (int rc = e->alloc((void**)&L.attn_norm, h * 4)) return rc;
+  if (int rc = e->alloc((void**)&L.ffn_norm, h * 4)) return rc;
+  e->weight_bytes += ((h + 2 * kv) * h + h * h + 3 * ff * h) * 2 + 2 * h * 4;
+  return 0;
+}
+
+int mx_engine::load_synthetic(const Shape& s, uint64_t seed) {
+  n_embd = s.n_embd; n_layer = s.n_layer; n_head = s.n_head; n_head_kv = s.n_head_kv; n_ff = s.n_ff;
+  n_vocab = s.n_vocab; rope_base = s.rope_base; eps = s.eps; n_ctx_train = s.n_ctx_train;
+  if (le < 0 || le > n_layer) le = n_layer;
+  if (int rc = init_common()) return rc;
+  const float ws = std_scale(0.02), ns = std_scale(0.1);
+  const int h = n_embd, kv = n_embd_kv, ff = n_ff, V = n_vocab;
+  if (has_embed) {
+    if (int rc = alloc((void**)&tok_embd, (size_t)V * h * 2)) return rc;
+    launch_synth_rowmajor(tok_embd, (size_t)V * h, seed, TID_TOK_EMBD, ws, stream);
+    weight_bytes += (size_t)h * 2;  // one embedding row per token
+  }
+  if (has_head) {
+    if (int rc = alloc((void**)&output, (size_t)V * h * 2)) return rc;
+    if (int rc = alloc((void**)&out_norm, (size_t)h * 4)) return rc;
+    launch_synth_packed(output, V, h, seed, TID_OUTPUT, ws, 1, 0, stream);
+    launch_synth_norm(out_norm, h, seed, TID_OUT_NORM, ns, stream);
+    weight_bytes += (size_t)V * h * 2 + h * 4;
+  }
+  for (int l = lb; l < le; l++) {
+    Layer& L = layers[l - lb];
+    if (int rc = alloc_layer(this, L)) return rc;
+    launch_synth_norm(L.attn_norm, h, seed, layer_tid(l, L_ATTN_NORM), ns, stream);
+    launch_synth_norm(L.ffn_norm, h, seed, layer_tid(l, L_FFN_NORM), ns, stream);
+    launch_synth_packed(L.qkv, h, h, seed, layer_tid(l, L_Q), ws, 1, 0, stream);
+    launch_synth_packed(L.qkv, kv, h, seed, layer_tid(l, L_K), ws, 1, h / 16, stream);
+    launch_synth_packed(L.qkv, kv, h, seed, layer_tid(l, L_V), ws, 1, (h + kv) / 16, stream);
+    launch_synth_packed(L.o, h, h, seed, layer_tid(l, L_O), ws, 1, 0, stream);
+    launch_synth_packed(L.gu, ff, h, seed, layer_tid(l, L_GATE), ws, 2, 0, stream);
+    launch_synth_packed(L.gu, ff, h, seed, layer_tid(l, L_UP), ws, 2, 1, stream);
+    launch_synth_packed(L.down, h, ff, seed, layer_tid(l, L_DOWN), ws, 1, 0, stream);
+  }
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(stream));
+  return 0;
+}
+
+int mx_engine::load_gguf(const std::string& path) {
+  GGUFFile f;
+  std::string err = f.open(path);
+  if (!err.empty()) return fail(MX_ERR_MODEL, err);
+  const GGUFValue* arch = f.get("general.architecture");
+  if (!arch || arch->str != "llama") return fail(MX_ERR_MODEL, "general.architecture must be 'llama'");
+  n_embd = (int)f.get_num("llama.embedding_length", 0);
+  n_layer = (int)f.get_num("llama.block_count", 0);
+  n_head = (int)f.get_num("llama.attention.head_count", 0);
+  n_head_kv = (int)f.get_num("llama.attention.head_count_kv", n_head);
+  n_ff = (int)f.get_num("llama.feed_forward_length", 0);
+  eps = (float)f.get_num("llama.attention.layer_norm_rms_epsilon", 1e-5);
+  rope_base = (float)f.get_num("llama.rope.freq_base", 10000.0);
+  n_ctx_train = (int)f.get_num("llama.context_length", 2048);
+  bos = (int)f.get_num("tokenizer.ggml.bos_token_id", 1);
+  eos = (int)f.get_num("tokenizer.ggml.eos_token_id", 2);
+  const GGUFTensor* te = f.tensor("token_embd.weight");
+  if (!te || te->ne.size() != 2) return fail(MX_ERR_MODEL, "missing token_embd.weight");
+  n_vocab = (int)te->ne[1];
+  if (!n_embd || !n_layer || !n_head || !n_ff) return fail(MX_ERR_MODEL, "missing llama.* hyper-parameters");
+  if ((int)f.get_num("llama.rope.dimension_count", n_embd / n_head) != n_embd / n_head)
+    return fail(MX_ERR_MODEL, "partial RoPE (rope.dimension_count != head_dim) is not supported");
+  if (le < 0 || le > n_layer) le = n_layer;
+  if (int rc = init_common()) return rc;
+  const int h = n_embd, kv = n_embd_kv, ff = n_ff, V = n_vocab;
+
+  // staging buffer for the largest matrix
+  size_t stage_bytes = std::max({(size_t)V * h * 2, (size_t)ff * h * 2, (size_t)(h + 2 * kv) * h * 2});
+  uint16_t* stage = nullptr;
+  HIPC(hipMalloc((void**)&stage, stage_bytes));
+  auto get_mat = [&](const std::string& name, int rows, int cols, const GGUFTensor** out) -> int {
+    const GGUFTensor* t = f.tensor(name);
+    if (!t) return fail(MX_ERR_MODEL, "missing tensor " + name);
+    if (t->ne.size() != 2 || (int)t->ne[0] != cols || (int)t->ne[1] != rows)
+      return fail(MX_ERR_MODEL, "tensor " + name + " has unexpected shape");
+    if (t->type != 30)
+      return fail(MX_ERR_MODEL, "tensor " + name + ": only BF16 (ggml type 30) matrices are supported, got type " +
+                                    std::to_string(t->type));
+    *out = t;
+    return 0;
+  };
+  auto upload_packed = [&](const std::string& name, int rows, int cols, uint16_t* dst, int stride,
+                           int offset) -> int {
+    const GGUFTensor* t = nullptr;
+    if (int rc = get_mat(name, rows, cols, &t)) return rc;
+    HIPC(hipMemcpy(stage, f.data(*t), t->nbytes, hipMemcpyHostToDevice));
+    launch_pack(dst, stage, rows, cols, stride, offset, stream);
+    HIPC(hipStreamSynchronize(stream));
+    return 0;
+  };
+  auto upload_norm = [&](const std::string& name, float* dst) -> int {
+    const GGUFTensor* t = f.tensor(name);
+    if (!t || t->type != 0 || t->ne[0] != (uint64_t)h) return fail(MX_ERR_MODEL, "bad/missing f32 norm " + name);
+    HIPC(hipMemcpy(dst, f.data(*t), (size_t)h * 4, hipMemcpyHostToDevice));
+    return 0;
+  };
+  int rc = 0;
+  if (has_embed) {
+    const GGUFTensor* t = nullptr;
+    if ((rc = get_mat("token_embd.weight", V, h, &t))) goto out;
+    if ((rc = alloc((void**)&tok_embd, (size_t)V * h * 2))) goto out;
+    if (hipMemcpy(tok_embd, f.data(*t), t->nbytes, hipMemcpyHostToDevice) != hipSuccess) {
+      rc = fail(MX_ERR_HIP, "upload token_embd");
+      goto out;
+    }
+    weight_bytes += (size_t)h * 2;
+  }
+  if (has_head) {
+    if ((rc = alloc((void**)&output, (size_t)V * h * 2))) goto out;
+    if ((rc = alloc((void**)&out_norm, (size_t)h * 4))) goto out;
+    const char* oname = f.tensor("output.weight") ? "output.weight" : "token_embd.weight";  // tied embeddings
+    if ((rc = upload_packed(oname, V, h, output, 1, 0))) goto out;
+    if ((rc = upload_norm("output_norm.weight", out_norm))) goto out;
+    weight_bytes += (size_t)V * h * 2 + h * 4;
+  }
+  for (int l = lb; l < le; l++) {
+    Layer& L = layers[l - lb];
+    const std::string p = "blk." + std::to_string(l) + ".";
+    if ((rc = alloc_layer(this, L))) goto out;
+    if ((rc = upload_norm(p + "attn_norm.weight", L.attn_norm))) goto out;
+    if ((rc = upload_norm(p + "ffn_norm.weight", L.ffn_norm))) goto out;
+    if ((rc = upload_packed(p + "attn_q.weight", h, h, L.qkv, 1, 0))) goto out;
+    if ((rc = upload_packed(p + "attn_k.weight", kv, h, L.qkv, 1, h / 16))) goto out;
+    if ((rc = upload_packed(p + "attn_v.weight", kv, h, L.qkv, 1, (h + kv) / 16))) goto out;
+    if ((rc = upload_packed(p + "attn_output.weight", h, h, L.o, 1, 0))) goto out;
+    if ((rc = upload_packed(p + "ffn_gate.weight", ff, h, L.gu, 2, 0))) goto out;
+    if ((rc = upload_packed(p + "ffn_up.weight", ff, h, L.gu, 2, 1))) goto out;
+    if ((rc = upload_packed(p + "ffn_down.weight", h, ff, L.down, 1, 0))) goto out;
+  }
+out:
+  hipFree(stage);
+  return rc;
+}
+
+// One forward of M <= MAX_ROWS rows through this stage's layers.
+int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int* slot, const void* x_in, void* x_out,
+                               bool head, const int* rowmap, int n_out, bool argmax, int* ids_next, int* pos_next,
+                               int* hist, int hist_stride, int* hist_count, int max_hist, hipStream_t s) {
+  const int h = n_embd, kv = n_embd_kv, ff = n_ff;
+  if (x_in) {
+    HIPC(hipMemcpyAsync(x, x_in, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
+  } else {
+    if (!has_embed) return fail(MX_ERR_STATE, "this stage has no token embedding: x_in required");
+    launch_embed(x, tok_embd, ids, M, h, s);
+  }
+  for (int li = 0; li < (int)layers.size(); li++) {
+    const Layer& L = layers[li];
+    _Float16* kc = kcache + layer_kv_stride * li;
+    _Float16* vc = vcache + layer_kv_stride * li;
+    launch_rmsnorm(xn, h, x, L.attn_norm, nullptr, M, h, eps, s);
+    MMArgs a{};
+    a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.X = xn; a.ldx = h; a.M = M;
+    a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
+    a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.n_head_kv = n_head_kv; a.slot_stride = slot_stride;
+    if (launch_mm(EPI_QKV, a, s)) return fail(MX_ERR_ARG, "qkv launch shape");
+    AttnArgs at{};
+    at.q = q; at.kc = kc; at.vc = vc; at.pos = pos; at.slot = slot; at.o_part = o_part; at.ml_part = ml_part;
+    at.out = attn_out; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
+    at.n_ctx = n_ctx; at.n_chunks = n_chunks; at.slot_stride = slot_stride; at.scale = 1.0f / sqrtf((float)head_dim);
+    launch_attention(at, s);
+    MMArgs b{};
+    b.W = L.o; b.N = h; b.K = h; b.X = attn_out; b.ldx = h; b.M = M; b.out = x; b.ldo = h;
+    if (launch_mm(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "attn_output launch shape");
+    launch_rmsnorm(xn, h, x, L.ffn_norm, nullptr, M, h, eps, s);
+    MMArgs c{};
+    c.W = L.gu; c.N = 2 * ff; c.K = h; c.X = xn; c.ldx = h; c.M = M; c.act = act; c.lda = ff;
+    if (launch_mm(EPI_SWIGLU, c, s)) return fail(MX_ERR_ARG, "ffn gate/up launch shape");
+    MMArgs d{};
+    d.W = L.down; d.N = h; d.K = ff; d.X = act; d.ldx = ff; d.M = M; d.out = x; d.ldo = h;
+    if (launch_mm(EPI_RESID, d, s)) return fail(MX_ERR_ARG, "ffn_down launch shape");
+  }
+  if (x_out) {
+    HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
+  }
+  if (head) {
+    if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
+    launch_rmsnorm(xn, h, x, out_norm, rowmap, n_out, h, eps, s);
+    MMArgs g{};
+    g.W = output; g.N = n_vocab; g.K = h; g.X = xn; g.ldx = h; g.M = n_out; g.out = logits; g.ldo = n_vocab;
+    if (launch_mm(EPI_F32, g, s)) return fail(MX_ERR_ARG, "lm_head launch shape");
+    if (argmax)
+      launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, ids_next, pos_next, hist, hist_stride,
+                    hist_count, max_hist, s);
+  }
+  HIPC(hipGetLastError());
+  return 0;
+}
+
+__global__ void advance_pos_kernel(int* pos, int M) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < M) pos[i] += 1;
+}
+
+// rows forward, n <= MAX_ROWS, logits for all rows copied to host if requested
+int mx_engine::forward_rows_chunk(int n, const int32_t* slots, const int32_t* pos, const int32_t* ids,
+                                  const void* x_in, void* x_out, float* logits_host, hipStream_t s) {
+  for (int i = 0; i < n; i++) {
+    if (slots[i] < 0 || slots[i] >= n_seq_max) return fail(MX_ERR_ARG, "slot out of range");
+    if (pos[i] < 0 || pos[i] >= n_ctx) return fail(MX_ERR_CTX, "position outside n_ctx");
+    if (ids && has_embed && !x_in && (ids[i] < 0 || ids[i] >= n_vocab)) return fail(MX_ERR_ARG, "token id out of range");
+  }
+  if (ids) HIPC(hipMemcpyAsync(d_ids, ids, n * 4, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_pos, pos, n * 4, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_slot, slots, n * 4, hipMemcpyHostToDevice, s));
+  const bool head = has_head && !x_out;
+  if (int rc = enqueue_forward(n, d_ids, d_pos, d_slot, x_in, x_out, head, nullptr, n, false, nullptr, nullptr,
+                               nullptr, 0, nullptr, 0, s))
+    return rc;
+  if (head && logits_host) HIPC(hipMemcpyAsync(logits_host, logits, (size_t)n * n_vocab * 4, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+// ---------------------------------------------------------------- scheduler
+void mx_engine::finish(Request* r, int why) {
+  r->finish = why;
+  r->done = true;
+  if (r->slot >= 0) free_slots.push_back(r->slot);
+  r->slot = -1;
+}
+
+// llama.cpp default sampling chain (restricted to the parameters exposed in mx_sampling):
+// repetition penalty -> top_k -> top_p -> min_p -> temperature -> draw
+int32_t mx_engine::sample_host(Request* r, const float* lg) {
+  const mx_sampling& sp = r->samp;
+  std::vector<std::pair<float, int>> c;
+  c.reserve(n_vocab);
+  for (int i = 0; i < n_vocab; i++) c.push_back({lg[i], i});
+  if (sp.repeat_penalty != 1.0f && sp.repeat_last_n != 0) {
+    std::vector<int> hist(r->prompt);
+    hist.insert(hist.end(), r->out.begin(), r->out.end());
+    int n = sp.repeat_last_n < 0 ? (int)hist.size() : std::min<int>(sp.repeat_last_n, (int)hist.size());
+    std::vector<char> seen(n_vocab, 0);
+    for (int i = (int)hist.size() - n; i < (int)hist.size(); i++) seen[hist[i]] = 1;
+    for (auto& p : c)
+      if (seen[p.second]) p.first = p.first <= 0 ? p.first * sp.repeat_penalty : p.first / sp.repeat_penalty;
+  }
+  if (sp.temperature <= 0.f) {
+    auto best = std::max_element(c.begin(), c.end(), [](auto& a, auto& b) {
+      return a.first < b.first || (a.first == b.first && a.second > b.second);
+    });
+    return best->second;
+  }
+  std::sort(c.begin(), c.end(), [](auto& a, auto& b) { return a.first > b.first || (a.first == b.first && a.second < b.second); });
+  int k = sp.top_k > 0 ? std::min<int>(sp.top_k, n_vocab) : n_vocab;
+  c.resize(k);
+  std::vector<double> p(k);
+  double mx = c[0].first, sum = 0;
+  for (int i = 0; i < k; i++) sum += (p[i] = exp(c[i].first - mx));
+  for (auto& v : p) v /= sum;
+  if (sp.top_p < 1.0f) {
+    double cum = 0;
+    int keep = k;
+    for (int i = 0; i < k; i++) {
+      cum += p[i];
+      if (cum >= sp.top_p) { keep = i + 1; break; }
+    }
+    c.resize(keep);
+    p.resize(keep);
+  }
+  if (sp.min_p > 0.f) {
+    int keep = 1;
+    for (int i = 1; i < (int)c.size(); i++)
+      if (p[i] >= sp.min_p * p[0]) keep = i + 1;
+    c.resize(keep);
+  }
+  std::vector<double> w(c.size());
+  double m0 = c[0].first / sp.temperature, s2 = 0;
+  for (size_t i = 0; i < c.size(); i++) s2 += (w[i] = exp(c[i].first / sp.temperature - m0));
+  std::uniform_real_distribution<double> U(0.0, s2);
+  double u = U(r->rng), acc = 0;
+  for (size_t i = 0; i < c.size(); i++) {
+    acc += w[i];
+    if (u < acc) return c[i].second;
+  }
+  return c.back().second;
+}
+
+int mx_engine::prefill(Request* r, std::vector<float>& last) {
+  const int n = (int)r->prompt.size();
+  std::vector<int32_t> slots(MAX_ROWS, r->slot), pos(MAX_ROWS);
+  std::vector<float> lg((size_t)MAX_ROWS * n_vocab);
+  for (int i = 0; i < n; i += MAX_ROWS) {
+    int m = std::min(MAX_ROWS, n - i);
+    for (int j = 0; j < m; j++) pos[j] = i + j;
+    bool lastc = i + m == n;
+    if (int rc = forward_rows_chunk(m, slots.data(), pos.data(), r->prompt.data() + i, nullptr, nullptr,
+                                    lastc ? lg.data() : nullptr, stream))
+      return rc;
+    if (lastc) last.assign(lg.begin() + (size_t)(m - 1) * n_vocab, lg.begin() + (size_t)m * n_vocab);
+  }
+  r->pos = n;
+  return 0;
+}
+
+int mx_engine::sched_step(std::vector<Request*>& rows) {
+  const int M = (int)rows.size();
+  std::vector<int32_t> ids(M), pos(M), slots(M);
+  bool all_greedy = true;
+  for (int i = 0; i < M; i++) {
+    ids[i] = rows[i]->next_tok;
+    pos[i] = rows[i]->pos;
+    slots[i] = rows[i]->slot;
+    if (rows[i]->samp.temperature > 0.f || rows[i]->samp.repeat_penalty != 1.0f) all_greedy = false;
+  }
+  hipStream_t s = stream;
+  HIPC(hipMemcpyAsync(d_ids, ids.data(), M * 4, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_pos, pos.data(), M * 4, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_slot, slots.data(), M * 4, hipMemcpyHostToDevice, s));
+  auto it = sched_graphs.find(M);
+  if (use_graphs && it == sched_graphs.end()) {
+    hipGraph_t g;
+    HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    int rc = enqueue_forward(M, d_ids, d_pos, d_slot, nullptr, nullptr, true, nullptr, M, true, nullptr, nullptr,
+                             nullptr, 0, nullptr, 0, s);
+    hipError_t ce = hipStreamEndCapture(s, &g);
+    if (rc) return rc;
+    if (ce != hipSuccess) return fail(MX_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(ce));
+    hipGraphExec_t ex;
+    HIPC(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    hipGraphDestroy(g);
+    it = sched_graphs.emplace(M, ex).first;
+  }
+  if (use_graphs) {
+    HIPC(hipGraphLaunch(it->second, s));
+  } else if (int rc = enqueue_forward(M, d_ids, d_pos, d_slot, nullptr, nullptr, true, nullptr, M, true, nullptr,
+                                      nullptr, nullptr, 0, nullptr, 0, s)) {
+    return rc;
+  }
+  std::vector<int32_t> tok(M);
+  std::vector<float> lg;
+  HIPC(hipMemcpyAsync(tok.data(), d_tok, M * 4, hipMemcpyDeviceToHost, s));
+  if (!all_greedy) {
+    lg.resize((size_t)M * n_vocab);
+    HIPC(hipMemcpyAsync(lg.data(), logits, (size_t)M * n_vocab * 4, hipMemcpyDeviceToHost, s));
+  }
+  HIPC(hipStreamSynchronize(s));
+  std::lock_guard<std::mutex> lk(mu);
+  for (int i = 0; i < M; i++) {
+    Request* r = rows[i];
+    r->pos++;
+    int32_t t = tok[i];
+    if (!all_greedy && (r->samp.temperature > 0.f || r->samp.repeat_penalty != 1.0f))
+      t = sample_host(r, lg.data() + (size_t)i * n_vocab);
+    r->out.push_back(t);
+    r->next_tok = t;
+    if (t == eos && !r->samp.ignore_eos) finish(r, MX_FINISH_STOP);
+    else if ((int)r->out.size() >= r->max_tokens || r->pos >= n_ctx) finish(r, MX_FINISH_LENGTH);
+  }
+  return 0;
+}
+
+void mx_engine::scheduler_loop() {
+  hipSetDevice(device);
+  for (;;) {
+    std::vector<Request*> admit;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return stop || !pending.empty() || !active.empty(); });
+      if (stop) {
+        for (Request* r : pending) { r->error = "engine shutting down"; finish(r, MX_FINISH_ERROR); }
+        for (Request* r : active) { r->error = "engine shutting down"; finish(r, MX_FINISH_ERROR); }
+        pending.clear();
+        active.clear();
+        cv_done.notify_all();
+        return;
+      }
+      while (!pending.empty() && !free_slots.empty()) {
+        Request* r = pending.front();
+        pending.pop_front();
+        r->slot = free_slots.back();
+        free_slots.pop_back();
+        admit.push_back(r);
+      }
+    }
+    std::lock_guard<std::mutex> glk(gpu_mu);
+    for (Request* r : admit) {
+      std::vector<float> last;
+      int rc = prefill(r, last);
+      std::lock_guard<std::mutex> lk(mu);
+      if (rc) {
+        r->error = g_err;
+        finish(r, MX_FINISH_ERROR);
+        continue;
+      }
+      int32_t t = sample_host(r, last.data());
+      r->out.push_back(t);
+      r->next_tok = t;
+      if (t == eos && !r->samp.ignore_eos) finish(r, MX_FINISH_STOP);
+      else if ((int)r->out.size() >= r->max_tokens || r->pos >= n_ctx) finish(r, MX_FINISH_LENGTH);
+      else active.push_back(r);
+    }
+    std::vector<Request*> rows;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      active.erase(std::remove_if(active.begin(), active.end(), [](Request* r) { return r->done; }), active.end());
+      for (Request* r : active)
+        if ((int)rows.size() < MAX_ROWS) rows.push_back(r);
+      cv_done.notify_all();
+    }
+    if (rows.empty()) continue;
+    int rc = sched_step(rows);
+    std::lock_guard<std::mutex> lk(mu);
+    if (rc) {
+      for (Request* r : rows) {
+        r->error = g_err;
+        if (!r->done) finish(r, MX_FINISH_ERROR);
+      }
+    }
+    active.erase(std::remove_if(active.begin(), active.end(), [](Request* r) { return r->done; }), active.end());
+    cv_done.notify_all();
+  }
+}
+
+// ---------------------------------------------------------------- C ABI
+extern "C" {
+
+void mx_opts_default(mx_opts* o) {
+  o->n_ctx = 512;
+  o->n_seq_max = 64;
+  o->layer_begin = 0;
+  o->layer_end = -1;
+  o->device = -1;
+  o->use_graphs = 1;
+  o->seed = 0;
+}
+
+void mx_sampling_default(mx_sampling* s) {
+  s->temperature = 0.8f;
+  s->top_k = 40;
+  s->top_p = 0.95f;
+  s->min_p = 0.05f;
+  s->repeat_penalty = 1.0f;
+  s->repeat_last_n = 64;
+  s->seed = 0xFFFFFFFFull;
+  s->ignore_eos = 0;
+}
+
+const char* mx_last_error(void) { return g_err.c_str(); }
+
+int mx_engine_create(const char* model_path, const mx_opts* opts, mx_engine** out) {
+  if (!model_path || !out) return fail(MX_ERR_ARG, "null argument");
+  *out = nullptr;
+  mx_opts o;
+  mx_opts_default(&o);
+  if (opts) o = *opts;
+  if (o.n_ctx < 1 || o.n_seq_max < 1) return fail(MX_ERR_ARG, "n_ctx and n_seq_max must be >= 1");
+  std::unique_ptr<mx_engine> e(new mx_engine());
+  e->n_ctx = o.n_ctx;
+  e->n_seq_max = o.n_seq_max;
+  e->lb = o.layer_begin;
+  e->le = o.layer_end;
+  e->use_graphs = o.use_graphs != 0;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MX_ERR_HIP, "no HIP device visible");
+  if (o.device >= 0) HIPC(hipSetDevice(o.device));
+  HIPC(hipGetDevice(&e->device));
+  HIPC(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  std::string path(model_path);
+  int rc;
+  if (path.rfind("synthetic:", 0) == 0) {
+    std::string rest = path.substr(10), name = rest;
+    uint64_t seed = o.seed;
+    size_t c = rest.find(':');
+    if (c != std::string::npos) {
+      name = rest.substr(0, c);
+      std::string tail = rest.substr(c + 1);
+      if (tail.rfind("seed=", 0) == 0) seed = strtoull(tail.c_str() + 5, nullptr, 10);
+    }
+    const Shape* s = nullptr;
+    for (const Shape& k : kShapes)
+      if (name == k.name) s = &k;
+    if (!s) return fail(MX_ERR_MODEL, "unknown synthetic shape '" + name + "'");
+    rc = e->load_synthetic(*s, seed);
+  } else {
+    rc = e->load_gguf(path);
+  }
+  if (rc) return rc;
+  *out = e.release();
+  return 0;
+}
+
+void mx_engine_destroy(mx_engine* e) { delete e; }
+
+int mx_engine_info(const mx_engine* e, mx_model_info* o) {
+  if (!e || !o) return fail(MX_ERR_ARG, "null argument");
+  o->n_embd = e->n_embd; o->n_layer = e->n_layer; o->n_head = e->n_head; o->n_head_kv = e->n_head_kv;
+  o->head_dim = e->head_dim; o->n_ff = e->n_ff; o->n_vocab = e->n_vocab; o->n_ctx_train = e->n_ctx_train;
+  o->eps = e->eps; o->rope_base = e->rope_base; o->bos_id = e->bos; o->eos_id = e->eos;
+  o->n_ctx = e->n_ctx; o->n_seq_max = e->n_seq_max; o->layer_begin = e->lb; o->layer_end = e->le;
+  o->has_embed = e->has_embed; o->has_head = e->has_head; o->weight_bytes = e->weight_bytes;
+  return 0;
+}
+
+int mx_forward_rows(mx_engine* e, int n, const int32_t* slots, const int32_t* pos, const int32_t* ids,
+                    float* logits_out) {
+  if (!e || n < 0 || (n && (!slots || !pos || !ids))) return fail(MX_ERR_ARG, "bad arguments");
+  if (!e->has_embed || !e->has_head) return fail(MX_ERR_STATE, "mx_forward_rows needs a full-model engine");
+  std::lock_guard<std::mutex> lk(e->gpu_mu);
+  hipSetDevice(e->device);
+  for (int i = 0; i < n; i += MAX_ROWS) {
+    int m = std::min(MAX_ROWS, n - i);
+    if (int rc = e->forward_rows_chunk(m, slots + i, pos + i, ids + i, nullptr, nullptr,
+                                       logits_out ? logits_out + (size_t)i * e->n_vocab : nullptr, e->stream))
+      return rc;
+  }
+  return 0;
+}
+
+int mx_forward_logits(mx_engine* e, int slot, const int32_t* ids, int n, int pos0, float* logits_out) {
+  if (!e || n < 0) return fail(MX_ERR_ARG, "bad arguments");
+  if (pos0 < 0 || pos0 + n > e->n_ctx) return fail(MX_ERR_CTX, "tokens exceed n_ctx");
+  std::vector<int32_t> slots(n, slot), pos(n);
+  for (int i = 0; i < n; i++) pos[i] = pos0 + i;
+  return mx_forward_rows(e, n, slots.data(), pos.data(), ids, logits_out);
+}
+
+int mx_stage_rows(mx_engine* e, int n, const int32_t* slots, const int32_t* pos, const int32_t* ids,
+                  const void* x_in, void* x_out, float* logits_out, void* stream) {
+  if (!e || n < 1 || n > MAX_ROWS) return fail(MX_ERR_ARG, "mx_stage_rows: 1 <= n <= 64 rows per call");
+  std::lock_guard<std::mutex> lk(e->gpu_mu);
+  hipSetDevice(e->device);
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  return e->forward_rows_chunk(n, slots, pos, ids, x_in, x_out, logits_out, s);
+}
+
+int mx_submit(mx_engine* e, const int32_t* ids, int n, const mx_sampling* s, int max_tokens, uint64_t* req) {
+  if (!e || !ids || n < 1 || !req) return fail(MX_ERR_ARG, "bad arguments");
+  if (!e->has_embed || !e->has_head) return fail(MX_ERR_STATE, "mx_submit needs a full-model engine");
+  if (n >= e->n_ctx) return fail(MX_ERR_CTX, "Requested tokens (" + std::to_string(n) + ") exceed context window of " +
+                                                 std::to_string(e->n_ctx));
+  for (int i = 0; i < n; i++)
+    if (ids[i] < 0 || ids[i] >= e->n_vocab) return fail(MX_ERR_ARG, "token id out of range");
+  auto r = std::make_unique<Request>();
+  r->prompt.assign(ids, ids + n);
+  mx_sampling_default(&r->samp);
+  if (s) r->samp = *s;
+  r->max_tokens = max_tokens <= 0 ? e->n_ctx - n : std::min(max_tokens, e->n_ctx - n);
+  r->rng.seed(r->samp.seed == 0xFFFFFFFFull ? std::random_device{}() : r->samp.seed);
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (e->stop) return fail(MX_ERR_STATE, "engine shutting down");
+    r->id = e->next_id++;
+    *req = r->id;
+    e->pending.push_back(r.get());
+    e->requests[r->id] = std::move(r);
+    if (!e->worker_started) {
+      e->worker_started = true;
+      e->worker = std::thread([e] { e->scheduler_loop(); });
+    }
+  }
+  e->cv.notify_all();
+  return 0;
+}
+
+int mx_wait(mx_engine* e, uint64_t req, int32_t* out_ids, int cap, int* n_out, int* finish) {
+  if (!e) return fail(MX_ERR_ARG, "null engine");
+  std::unique_ptr<Request> r;
+  {
+    std::unique_lock<std::mutex> lk(e->mu);
+    auto it = e->requests.find(req);
+    if (it == e->requests.end()) return fail(MX_ERR_NOTFOUND, "unknown request id");
+    Request* rp = it->second.get();
+    e->cv_done.wait(lk, [&] { return rp->done; });
+    r = std::move(it->second);
+    e->requests.erase(it);
+  }
+  int n = std::min<int>(cap, (int)r->out.size());
+  if (out_ids && n > 0) memcpy(out_ids, r->out.data(), n * 4);
+  if (n_out) *n_out = (int)r->out.size();
+  if (finish) *finish = r->finish;
+  if (r->finish == MX_FINISH_ERROR) return fail(MX_ERR_STATE, "request failed: " + r->error);
+  return 0;
+}
+
+int mx_batch_create(mx_engine* e, int M, const int32_t* slots, const int32_t* pos, const int32_t* ids, int max_steps,
+                    mx_batch** out) {
+  if (!e || !out || M < 1 || M > MAX_ROWS || !slots || !pos || max_steps < 0) return fail(MX_ERR_ARG, "bad arguments");
+  int max_pos = 0;
+  for (int i = 0; i < M; i++) {
+    if (slots[i] < 0 || slots[i] >= e->n_seq_max) return fail(MX_ERR_ARG, "slot out of range");
+    if (pos[i] < 0 || pos[i] >= e->n_ctx) return fail(MX_ERR_CTX, "position outside n_ctx");
+    if (ids && (ids[i] < 0 || ids[i] >= e->n_vocab)) return fail(MX_ERR_ARG, "token id out of range");
+    max_pos = std::max(max_pos, (int)pos[i]);
+  }
+  std::lock_guard<std::mutex> lk(e->gpu_mu);
+  hipSetDevice(e->device);
+  std::unique_ptr<mx_batch> b(new mx_batch());
+  b->M = M;
+  b->max_steps = max_steps;
+  b->max_pos = max_pos;
+  HIPC(hipMalloc((void**)&b->d_ids, M * 4));
+  HIPC(hipMalloc((void**)&b->d_pos, M * 4));
+  HIPC(hipMalloc((void**)&b->d_slot, M * 4));
+  HIPC(hipMalloc((void**)&b->d_hist, (size_t)M * std::max(1, max_steps) * 4));
+  HIPC(hipMalloc((void**)&b->d_hist_count, M * 4));
+  HIPC(hipMemcpy(b->d_pos, pos, M * 4, hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(b->d_slot, slots, M * 4, hipMemcpyHostToDevice));
+  if (ids) HIPC(hipMemcpy(b->d_ids, ids, M * 4, hipMemcpyHostToDevice));
+  else HIPC(hipMemset(b->d_ids, 0, M * 4));
+  HIPC(hipMemset(b->d_hist_count, 0, M * 4));
+  *out = b.release();
+  return 0;
+}
+
+int32_t* mx_batch_ids_device(mx_batch* b) { return b ? b->d_ids : nullptr; }
+
+int mx_batch_step(mx_engine* e, mx_batch* b, const void* x_in, void* x_out, void* stream) {
+  if (!e || !b) return fail(MX_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(e->gpu_mu);
+  hipSetDevice(e->device);
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  const bool head = x_out == nullptr;
+  if (b->max_pos >= e->n_ctx) return fail(MX_ERR_CTX, "decode batch reached n_ctx");
+  b->max_pos++;
+  if (head && !e->has_head) return fail(MX_ERR_STATE, "x_out is required on a non-final pipeline stage");
+  if (!x_in && !e->has_embed) return fail(MX_ERR_STATE, "x_in is required on a non-first pipeline stage");
+  auto body = [&]() -> int {
+    if (int rc = e->enqueue_forward(b->M, b->d_ids, b->d_pos, b->d_slot, x_in, x_out, head, nullptr, b->M, head,
+                                    b->d_ids, b->d_pos, b->d_hist, b->max_steps, b->d_hist_count, b->max_steps, s))
+      return rc;
+    if (!head) advance_pos_kernel<<<(b->M + 63) / 64, 64, 0, s>>>(b->d_pos, b->M);
+    return 0;
+  };
+  if (!e->use_graphs) return body();
+  GraphKey key{b->M, x_in, x_out, s};
+  auto it = b->graphs.find(key);
+  if (it == b->graphs.end()) {
+    hipGraph_t g;
+    HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    int rc = body();
+    hipError_t ce = hipStreamEndCapture(s, &g);
+    if (rc) return rc;
+    if (ce != hipSuccess) return fail(MX_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(ce));
+    hipGraphExec_t ex;
+    HIPC(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    hipGraphDestroy(g);
+    it = b->graphs.emplace(key, ex).first;
+  }
+  HIPC(hipGraphLaunch(it->second, s));
+  return 0;
+}
+
+int mx_batch_tokens(mx_engine* e, mx_batch* b, int32_t* out, int cap, int* n_steps) {
+  if (!e || !b) return fail(MX_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(e->gpu_mu);
+  hipSetDevice(e->device);
+  HIPC(hipDeviceSynchronize());
+  std::vector<int32_t> cnt(b->M);
+  HIPC(hipMemcpy(cnt.data(), b->d_hist_count, b->M * 4, hipMemcpyDeviceToHost));
+  if (n_steps) *n_steps = cnt[0];
+  if (out && cap > 0 && b->max_steps > 0) {
+    std::vector<int32_t> h((size_t)b->M * b->max_steps);
+    HIPC(hipMemcpy(h.data(), b->d_hist, h.size() * 4, hipMemcpyDeviceToHost));
+    for (int i = 0; i < b->M; i++)
+      for (int j = 0; j < cap && j < b->max_steps; j++) out[(size_t)i * cap + j] = h[(size_t)i * b->max_steps + j];
+  }
+  return 0;
+}
+
+void mx_batch_destroy(mx_engine* e, mx_batch* b) {
+  if (!b) return;
+  if (e) {
+    std::lock_guard<std::mutex> lk(e->gpu_mu);
+    hipSetDevice(e->device);
+    hipDeviceSynchronize();
+  }
+  for (auto& kv : b->graphs) hipGraphExecDestroy(kv.second);
+  hipFree(b->d_ids);
+  hipFree(b->d_pos);
+  hipFree(b->d_slot);
+  hipFree(b->d_hist);
+  hipFree(b->d_hist_count);
+  delete b;
+}
+
+int mx_sync(mx_engine* e) {
+  if (!e) return fail(MX_ERR_ARG, "null engine");
+  hipSetDevice(e->device);
+  HIPC(hipDeviceSynchronize());
+  return 0;
+}
+
+int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, double* bytes) {
+  if (!e || M < 1 || M > MAX_ROWS || iters < 1) return fail(MX_ERR_ARG, "bad arguments");
+  std::lock_guard<std::mutex> lk(e->gpu_mu);
+  hipSetDevice(e->device);
+  hipStream_t s = e->stream;
+  const int h = e->n_embd, kv = e->n_embd_kv, ff = e->n_ff;
+  std::vector<int32_t> zero(M, 0), slots(M);
+  for (int i = 0; i < M; i++) slots[i] = i % e->n_seq_max;
+  HIPC(hipMemcpyAsync(e->d_pos, zero.data(), M * 4, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(e->d_slot, slots.data(), M * 4, hipMemcpyHostToDevice, s));
+  hipEvent_t t0, t1;
+  HIPC(hipEventCreate(&t0));
+  HIPC(hipEventCreate(&t1));
+  const int nl = (int)e->layers.size();
+  size_t per = 0;
+  int launches = 0;
+  auto one = [&](int li) -> int {
+    const Layer& L = e->layers[li];
+    MMArgs a{};
+    a.M = M;
+    switch (kind) {
+      case 0:
+        a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.X = e->xn; a.ldx = h; a.out = e->q; a.ldo = h; a.n_q = h;
+        a.n_kv = kv; a.head_dim = e->head_dim; a.pos = e->d_pos; a.slot = e->d_slot; a.rope_cs = e->rope_cs;
+        a.kc = e->kcache + e->layer_kv_stride * li; a.vc = e->vcache + e->layer_kv_stride * li; a.n_ctx = e->n_ctx;
+        a.n_head_kv = e->n_head_kv; a.slot_stride = e->slot_stride;
+        per = (size_t)(h + 2 * kv) * h * 2;
+        return launch_mm(EPI_QKV, a, s);
+      case 1:
+        a.W = L.o; a.N = h; a.K = h; a.X = e->attn_out; a.ldx = h; a.out = e->x; a.ldo = h;
+        per = (size_t)h * h * 2;
+        return launch_mm(EPI_RESID, a, s);
+      case 2:
+        a.W = L.gu; a.N = 2 * ff; a.K = h; a.X = e->xn; a.ldx = h; a.act = e->act; a.lda = ff;
+        per = (size_t)2 * ff * h * 2;
+        return launch_mm(EPI_SWIGLU, a, s);
+      case 3:
+        a.W = L.down; a.N = h; a.K = ff; a.X = e->act; a.ldx = ff; a.out = e->x; a.ldo = h;
+        per = (size_t)h * ff * 2;
+        return launch_mm(EPI_RESID, a, s);
+      case 4:
+        if (!e->has_head) return -1;
+        a.W = e->output; a.N = e->n_vocab; a.K = h; a.X = e->xn; a.ldx = h; a.out = e->logits; a.ldo = e->n_vocab;
+        per = (size_t)e->n_vocab * h * 2;
+        return launch_mm(EPI_F32, a, s);
+    }
+    return -1;
+  };
+  // warm-up pass, then timed passes; each pass walks every local layer so no
+  // launch re-reads weights that the previous one left in the caches
+  for (int li = 0; li < nl; li++)
+    if (one(li)) return fail(MX_ERR_ARG, "bad kernel kind");
+  HIPC(hipEventRecord(t0, s));
+  for (int it = 0; it < iters; it++) {
+    if (kind == 4) {
+      if (one(0)) return fail(MX_ERR_ARG, "bad kernel kind");
+      launches++;
+    } else {
+      for (int li = 0; li < nl; li++) {
+        one(li);
+        launches++;
+      }
+    }
+  }
+  HIPC(hipEventRecord(t1, s));
+  HIPC(hipEventSynchronize(t1));
+  float ms = 0;
+  HIPC(hipEventElapsedTime(&ms, t0, t1));
+  hipEventDestroy(t0);
+  hipEventDestroy(t1);
+  if (us) *us = ms * 1000.0 / launches;
+  if (bytes) *bytes = (double)per;
+  return 0;
+}
+
+}  // extern "C"

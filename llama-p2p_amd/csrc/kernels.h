@@ -1,0 +1,86 @@
+// kernels.h -- launch interface of the gfx950 kernels (kernels.hip).
+//
+// Every kernel here replaces one ggml CPU op of llama.cpp's llm_build_llama
+// (the forward pass behind /root/reference/llama_p2p_network.py:125; see
+// SURVEY.md §3.3 and §8a rows a5-a14).  Host code calls only these wrappers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace mx {
+
+// Weight matrices live in HBM as bf16 "MFMA tiles": tile (nt, kt) holds rows
+// [16nt, 16nt+16) x cols [32kt, 32kt+32) of W[N][K] (GGUF order) in exactly the
+// lane order of the A operand of v_mfma_f32_16x16x32_bf16, 1 KiB per tile,
+// tiles ordered nt-major so a wave streaming along K reads contiguous 1 KiB
+// pieces: element (lane, j) of tile = W[16nt + (lane&15)][32kt + 8(lane>>4) + j].
+constexpr int TILE_N = 16;
+constexpr int TILE_K = 32;
+constexpr int TILE_ELEMS = TILE_N * TILE_K;
+constexpr int MAX_ROWS = 64;       // tokens per forward (4 column tiles of 16)
+constexpr int ATTN_CHUNK = 64;     // positions per attention work-group
+
+enum Epilogue : int {
+  EPI_F32 = 0,     // out[col][row] = acc                         (lm_head logits)
+  EPI_RESID = 1,   // x[col][row] += acc                          (attn_output, ffn_down)
+  EPI_QKV = 2,     // rope(q,k); q -> f32 buffer, k/v -> f16 KV cache (attn_q/k/v)
+  EPI_SWIGLU = 3,  // act = bf16(silu(gate) * up)                  (ffn_gate/ffn_up)
+};
+
+struct MMArgs {
+  const uint16_t* W;   // packed tiles
+  int N, K;            // logical W[N][K]; for SWIGLU N = 2*n_ff (interleaved tiles)
+  const uint16_t* X;   // activations bf16 [>=16*NB rows][ldx]
+  int ldx;
+  int M;               // valid columns (tokens)
+  // epilogue operands
+  float* out;          // EPI_F32: [M][ldo]; EPI_RESID: residual x [M][ldo]; EPI_QKV: q [M][ldo]
+  int ldo;
+  uint16_t* act;       // EPI_SWIGLU: bf16 [M][lda]
+  int lda;
+  // EPI_QKV
+  int n_q, n_kv, head_dim;     // rows [0,n_q) q, [n_q,n_q+n_kv) k, rest v
+  const int* pos;              // [M]
+  const int* slot;             // [M]
+  const float* rope_cs;        // [n_ctx][head_dim/2][2]
+  _Float16* kc;                // K cache of this layer: [slots][n_head_kv][n_ctx][head_dim]
+  _Float16* vc;                // V cache of this layer
+  int n_ctx, n_head_kv;
+  size_t slot_stride;          // elements per slot in kc/vc = n_head_kv*n_ctx*head_dim
+};
+
+struct AttnArgs {
+  const float* q;        // [M][n_head*head_dim] f32 (post-RoPE)
+  const _Float16* kc;    // [slots][n_head_kv][n_ctx][head_dim]
+  const _Float16* vc;
+  const int* pos;        // [M]  query position; attends to [0, pos]
+  const int* slot;       // [M]
+  float* o_part;         // [M][n_head][n_chunks][head_dim]
+  float* ml_part;        // [M][n_head][n_chunks][2]  (max, sum)
+  uint16_t* out;         // combine output bf16 [M][ldo]
+  int ldo;
+  int M, n_head, n_head_kv, head_dim, n_ctx, n_chunks;
+  size_t slot_stride;
+  float scale;
+};
+
+// packing / synthetic weights
+void launch_synth_packed(uint16_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale,
+                         int row_tile_stride, int row_tile_offset, hipStream_t s);
+void launch_synth_rowmajor(uint16_t* dst, size_t n, uint64_t seed, uint64_t tid, float scale, hipStream_t s);
+void launch_synth_norm(float* dst, size_t n, uint64_t seed, uint64_t tid, float scale, hipStream_t s);
+void launch_pack(uint16_t* dst, const uint16_t* src_rowmajor, int N, int K, int row_tile_stride,
+                 int row_tile_offset, hipStream_t s);
+
+// forward-pass ops
+void launch_embed(float* x, const uint16_t* tok_embd, const int* ids, int M, int n_embd, hipStream_t s);
+void launch_rmsnorm(uint16_t* y, int ldy, const float* x, const float* w, const int* row_map, int M, int n,
+                    float eps, hipStream_t s);
+int launch_mm(int epi, const MMArgs& a, hipStream_t s);
+void launch_attention(const AttnArgs& a, hipStream_t s);
+void launch_argmax(const float* logits, int ldl, int M, int V, float* ws_val, int* ws_idx, int* tok_out,
+                   int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count, int max_hist,
+                   hipStream_t s);
+
+}  // namespace mx

@@ -1,0 +1,242 @@
+"""ctypes binding of the engine's C ABI (include/mx_engine.h).
+
+The shared library is built in-tree (``llama-p2p_amd/libmxllama.so``, see
+build.py).  There is deliberately no fallback: if the library is missing or no
+GPU is visible, every entry point raises -- the product never computes on the
+CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmxllama.so")
+
+MX_OK = 0
+MX_ERR_ARG, MX_ERR_HIP, MX_ERR_MODEL, MX_ERR_CTX, MX_ERR_NOTFOUND, MX_ERR_STATE = -1, -2, -3, -4, -5, -6
+FINISH_LENGTH, FINISH_STOP, FINISH_ERROR = 0, 1, 2
+
+# every symbol include/mx_engine.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "mx_opts_default", "mx_sampling_default", "mx_last_error", "mx_engine_create", "mx_engine_destroy",
+    "mx_engine_info", "mx_forward_logits", "mx_forward_rows", "mx_submit", "mx_wait", "mx_batch_create",
+    "mx_batch_step", "mx_batch_ids_device", "mx_batch_tokens", "mx_batch_destroy", "mx_stage_rows",
+    "mx_profile_kernel", "mx_sync",
+]
+
+
+class MxError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mx error {code}: {msg}")
+        self.code = code
+
+
+class MxOpts(ctypes.Structure):
+    _fields_ = [("n_ctx", ctypes.c_int32), ("n_seq_max", ctypes.c_int32), ("layer_begin", ctypes.c_int32),
+                ("layer_end", ctypes.c_int32), ("device", ctypes.c_int32), ("use_graphs", ctypes.c_int32),
+                ("seed", ctypes.c_uint64)]
+
+
+class MxModelInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("n_embd", "n_layer", "n_head", "n_head_kv", "head_dim", "n_ff",
+                                              "n_vocab", "n_ctx_train")] + \
+               [("eps", ctypes.c_float), ("rope_base", ctypes.c_float)] + \
+               [(n, ctypes.c_int32) for n in ("bos_id", "eos_id", "n_ctx", "n_seq_max", "layer_begin",
+                                              "layer_end", "has_embed", "has_head")] + \
+               [("weight_bytes", ctypes.c_uint64)]
+
+
+class MxSampling(ctypes.Structure):
+    _fields_ = [("temperature", ctypes.c_float), ("top_k", ctypes.c_int32), ("top_p", ctypes.c_float),
+                ("min_p", ctypes.c_float), ("repeat_penalty", ctypes.c_float), ("repeat_last_n", ctypes.c_int32),
+                ("seed", ctypes.c_uint64), ("ignore_eos", ctypes.c_int32)]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def lib() -> ctypes.CDLL:
+    """Load libmxllama.so (raises if it was not built)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not found: build it with `python llama-p2p_amd/build.py` "
+                              "(the engine has no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64
+        P = ctypes.POINTER
+        L.mx_opts_default.argtypes = [P(MxOpts)]
+        L.mx_sampling_default.argtypes = [P(MxSampling)]
+        L.mx_last_error.restype = ctypes.c_char_p
+        L.mx_engine_create.argtypes = [ctypes.c_char_p, P(MxOpts), P(vp)]
+        L.mx_engine_destroy.argtypes = [vp]
+        L.mx_engine_info.argtypes = [vp, P(MxModelInfo)]
+        L.mx_forward_logits.argtypes = [vp, i32, vp, i32, i32, vp]
+        L.mx_forward_rows.argtypes = [vp, i32, vp, vp, vp, vp]
+        L.mx_submit.argtypes = [vp, vp, i32, P(MxSampling), i32, P(u64)]
+        L.mx_wait.argtypes = [vp, u64, vp, i32, P(i32), P(i32)]
+        L.mx_batch_create.argtypes = [vp, i32, vp, vp, vp, i32, P(vp)]
+        L.mx_batch_step.argtypes = [vp, vp, vp, vp, vp]
+        L.mx_batch_ids_device.argtypes = [vp]
+        L.mx_batch_ids_device.restype = vp
+        L.mx_batch_tokens.argtypes = [vp, vp, vp, i32, P(i32)]
+        L.mx_batch_destroy.argtypes = [vp, vp]
+        L.mx_stage_rows.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp]
+        L.mx_profile_kernel.argtypes = [vp, i32, i32, i32, P(ctypes.c_double), P(ctypes.c_double)]
+        L.mx_sync.argtypes = [vp]
+        for name in EXPORTS:
+            if name not in ("mx_opts_default", "mx_sampling_default", "mx_last_error", "mx_engine_destroy",
+                            "mx_batch_destroy", "mx_batch_ids_device"):
+                getattr(L, name).restype = i32
+        _lib = L
+        return L
+
+
+def _check(rc: int):
+    if rc != MX_OK:
+        raise MxError(rc, lib().mx_last_error().decode(errors="replace"))
+
+
+def _i32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+class Engine:
+    """One engine instance = one GPU, one model (or one pipeline stage of it)."""
+
+    def __init__(self, model_path: str, n_ctx: int = 512, n_seq_max: int = 64, layer_begin: int = 0,
+                 layer_end: int = -1, device: int = -1, use_graphs: bool = True, seed: int = 0):
+        L = lib()
+        opts = MxOpts()
+        L.mx_opts_default(ctypes.byref(opts))
+        opts.n_ctx, opts.n_seq_max = n_ctx, n_seq_max
+        opts.layer_begin, opts.layer_end, opts.device = layer_begin, layer_end, device
+        opts.use_graphs, opts.seed = int(use_graphs), seed
+        h = ctypes.c_void_p()
+        _check(L.mx_engine_create(model_path.encode(), ctypes.byref(opts), ctypes.byref(h)))
+        self._h = h
+        info = MxModelInfo()
+        _check(L.mx_engine_info(self._h, ctypes.byref(info)))
+        self.info = info
+        self.n_vocab = info.n_vocab
+        self.n_embd = info.n_embd
+        self.n_ctx = info.n_ctx
+
+    # -- parity hooks --------------------------------------------------------
+    def forward_logits(self, ids: Sequence[int], pos0: int = 0, slot: int = 0) -> np.ndarray:
+        ids = _i32(ids)
+        out = np.empty((len(ids), self.n_vocab), dtype=np.float32)
+        _check(lib().mx_forward_logits(self._h, slot, ids.ctypes.data, len(ids), pos0, out.ctypes.data))
+        return out
+
+    def forward_rows(self, slots, pos, ids) -> np.ndarray:
+        slots, pos, ids = _i32(slots), _i32(pos), _i32(ids)
+        out = np.empty((len(ids), self.n_vocab), dtype=np.float32)
+        _check(lib().mx_forward_rows(self._h, len(ids), slots.ctypes.data, pos.ctypes.data, ids.ctypes.data,
+                                     out.ctypes.data))
+        return out
+
+    def stage_rows(self, slots, pos, ids, x_in: int = 0, x_out: int = 0, want_logits: bool = False,
+                   stream: int = 0) -> Optional[np.ndarray]:
+        slots, pos = _i32(slots), _i32(pos)
+        ids_p = _i32(ids).ctypes.data if ids is not None else None
+        ids_keep = _i32(ids) if ids is not None else None
+        if ids_keep is not None:
+            ids_p = ids_keep.ctypes.data
+        out = np.empty((len(slots), self.n_vocab), dtype=np.float32) if want_logits else None
+        _check(lib().mx_stage_rows(self._h, len(slots), slots.ctypes.data, pos.ctypes.data, ids_p,
+                                   x_in or None, x_out or None, out.ctypes.data if out is not None else None,
+                                   stream or None))
+        return out
+
+    # -- request API ---------------------------------------------------------
+    def submit(self, ids: Sequence[int], max_tokens: int, temperature: float = 0.0, top_k: int = 40,
+               top_p: float = 0.95, min_p: float = 0.05, repeat_penalty: float = 1.0, repeat_last_n: int = 64,
+               seed: Optional[int] = None, ignore_eos: bool = False) -> int:
+        ids = _i32(ids)
+        s = MxSampling()
+        lib().mx_sampling_default(ctypes.byref(s))
+        s.temperature, s.top_k, s.top_p, s.min_p = temperature, top_k, top_p, min_p
+        s.repeat_penalty, s.repeat_last_n, s.ignore_eos = repeat_penalty, repeat_last_n, int(ignore_eos)
+        if seed is not None and seed >= 0:
+            s.seed = seed
+        req = ctypes.c_uint64()
+        _check(lib().mx_submit(self._h, ids.ctypes.data, len(ids), ctypes.byref(s), max_tokens, ctypes.byref(req)))
+        return req.value
+
+    def wait(self, req: int, cap: int = 8192):
+        out = np.empty(cap, dtype=np.int32)
+        n, fin = ctypes.c_int32(), ctypes.c_int32()
+        _check(lib().mx_wait(self._h, req, out.ctypes.data, cap, ctypes.byref(n), ctypes.byref(fin)))
+        return out[: min(n.value, cap)].tolist(), fin.value
+
+    def generate(self, ids, max_tokens: int, **kw):
+        return self.wait(self.submit(ids, max_tokens, **kw))
+
+    # -- device-resident batches (bench, pipeline) ---------------------------
+    def batch(self, slots, pos, ids=None, max_steps: int = 0) -> "Batch":
+        return Batch(self, slots, pos, ids, max_steps)
+
+    def profile_kernel(self, kind: int, M: int, iters: int = 3):
+        us, nb = ctypes.c_double(), ctypes.c_double()
+        _check(lib().mx_profile_kernel(self._h, kind, M, iters, ctypes.byref(us), ctypes.byref(nb)))
+        return us.value, nb.value
+
+    def sync(self):
+        _check(lib().mx_sync(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().mx_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Batch:
+    def __init__(self, eng: Engine, slots, pos, ids, max_steps: int):
+        self.eng = eng
+        slots, pos = _i32(slots), _i32(pos)
+        self.M = len(slots)
+        ids_a = _i32(ids) if ids is not None else None
+        h = ctypes.c_void_p()
+        _check(lib().mx_batch_create(eng._h, self.M, slots.ctypes.data, pos.ctypes.data,
+                                     ids_a.ctypes.data if ids_a is not None else None, max_steps, ctypes.byref(h)))
+        self._h = h
+        self.max_steps = max_steps
+
+    @property
+    def ids_device_ptr(self) -> int:
+        return lib().mx_batch_ids_device(self._h)
+
+    def step(self, x_in: int = 0, x_out: int = 0, stream: int = 0):
+        _check(lib().mx_batch_step(self.eng._h, self._h, x_in or None, x_out or None, stream or None))
+
+    def tokens(self) -> np.ndarray:
+        out = np.zeros((self.M, max(1, self.max_steps)), dtype=np.int32)
+        n = ctypes.c_int32()
+        _check(lib().mx_batch_tokens(self.eng._h, self._h, out.ctypes.data, out.shape[1], ctypes.byref(n)))
+        return out[:, : min(n.value, self.max_steps)]
+
+    def close(self):
+        if getattr(self, "_h", None) and self.eng._h:
+            lib().mx_batch_destroy(self.eng._h, self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,499 @@
+/*
+ * llama_oracle.c -- CPU restatement of the reference's hot path.  TEST
+ * INFRASTRUCTURE ONLY: used by tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg as the checker / CPU baseline.  The product
+ * (llama-p2p_amd/) never links, loads or calls this file.
+ *
+ * What it restates.  The reference's hot path is one call,
+ *   result = self.model(prompt, max_tokens=100)   /root/reference/llama_p2p_network.py:125
+ * on   self.model = Llama(model_path=model_path)  /root/reference/llama_p2p_network.py:19
+ * i.e. llama-cpp-python (~0.3.1, Oct 2024; module llama_cpp) -> llama.cpp
+ * llm_build_llama -> ggml CPU ops.  That dependency is NOT vendored in
+ * /root/reference and is absent from this machine, so this is a
+ * restatement of its published algorithm:
+ *   - GET_ROWS token embedding (bf16 -> f32)                     SURVEY §8a a5
+ *   - RMS_NORM: sum of squares in double, scale = 1/sqrtf(mean+eps), then
+ *     MUL by the f32 norm weight                                 a6
+ *   - MUL_MAT with bf16 weights: activations rounded to bf16 (vec_dot_type of
+ *     GGML_TYPE_BF16), products accumulated in f32                a7, a11, a12, a13
+ *   - ROPE_EXT mode NORM: adjacent pairs (2i, 2i+1) rotated by theta_i, with
+ *     theta built by the f32 cumulative product theta *= powf(base, -2/d)  a8
+ *   - K and V stored as f16 (ggml_cpy f32->f16, round-nearest-even)          a9
+ *   - KQ = f16(q) . K (f32 accumulate); SOFT_MAX_EXT with scale 1/sqrt(d),
+ *     causal mask, max-subtracted expf, sum in double, probs *= (float)(1/sum);
+ *     KQV = f16(probs) . V (f32 accumulate); GQA head h -> kv head h/(nh/nkv)  a10
+ *   - SwiGLU: silu(g) = g/(1+expf(-g)) in f32, times up, rounded to bf16 for
+ *     ffn_down                                                   a12
+ *   - logits f32 for the requested rows; greedy = argmax, ties -> lowest id  a13, a14
+ * ORC_EXACT mode drops every bf16/f16 activation rounding (fp32 math over the
+ * same bf16 weights): that is what tests cross-check against
+ * transformers.LlamaForCausalLM (an independent implementation) to pin the
+ * layout conventions (tests/golden/make_golden.py).
+ *
+ * Weights: bf16 for every matrix, f32 for norms, GGUF data order W[out][in].
+ * Synthetic weights follow llama-p2p_amd/synth.py bit for bit (orc_synth_value).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORC_EXACT 1
+
+typedef struct {
+    int n_embd, n_layer, n_head, n_head_kv, n_ff, n_vocab;
+    float eps, rope_base;
+} orc_hparams;
+
+typedef struct {
+    uint16_t *wq, *wk, *wv, *wo, *wg, *wu, *wd; /* bf16 */
+    float *attn_norm, *ffn_norm;
+} orc_layer;
+
+typedef struct {
+    orc_hparams hp;
+    int flags;
+    int head_dim, n_embd_kv;
+    uint16_t *tok_embd, *output; /* bf16 [V][h] */
+    float *out_norm;
+    orc_layer *layers;
+} orc_model;
+
+typedef struct {
+    orc_model *m;
+    int n_ctx;
+    /* per layer: K [n_ctx][n_embd_kv], V [n_ctx][n_embd_kv]; f16 bits or f32 */
+    void **k, **v;
+    float *rope_cs; /* [n_ctx][head_dim/2][2] */
+} orc_ctx;
+
+/* ------------------------------------------------------------------ numerics */
+static inline float bf16_to_f32(uint16_t h) {
+    union { uint32_t u; float f; } v; v.u = (uint32_t)h << 16; return v.f;
+}
+static inline uint16_t f32_to_bf16(float f) {
+    union { uint32_t u; float f; } v; v.f = f;
+    if ((v.u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((v.u >> 16) | 64); /* NaN */
+    return (uint16_t)((v.u + (0x7fffu + ((v.u >> 16) & 1u))) >> 16);
+}
+static inline float round_bf16(float f) { return bf16_to_f32(f32_to_bf16(f)); }
+
+/* IEEE binary16, round-nearest-even (matches F16C _cvtss_sh(x, 0)). */
+static uint16_t f32_to_f16(float f) {
+    union { uint32_t u; float f; } v; v.f = f;
+    uint32_t x = v.u, sign = (x >> 16) & 0x8000u;
+    uint32_t ax = x & 0x7fffffffu;
+    if (ax >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (ax > 0x7f800000u ? 0x200u : 0));
+    if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u); /* overflow -> inf */
+    if (ax < 0x38800000u) { /* subnormal or zero in half */
+        if (ax < 0x33000000u) return (uint16_t)sign; /* < 2^-25 rounds to 0 */
+        uint32_t mant = (ax & 0x7fffffu) | 0x800000u;
+        int e = (int)(ax >> 23); /* 102..112 */
+        int shift = 126 - e; /* 14..24 */
+        uint32_t hm = mant >> shift;
+        uint32_t rem = mant & ((1u << shift) - 1), half = 1u << (shift - 1);
+        if (rem > half || (rem == half && (hm & 1u))) hm++;
+        return (uint16_t)(sign | hm);
+    }
+    uint32_t h = ((ax >> 13) - (112u << 10));
+    uint32_t rem = ax & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h++;
+    return (uint16_t)(sign | h);
+}
+static float f16_to_f32(uint16_t h) {
+    uint32_t sign = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 0x1f, m = h & 0x3ff;
+    union { uint32_t u; float f; } v;
+    if (e == 0) {
+        if (m == 0) { v.u = sign; return v.f; }
+        float r = ldexpf((float)m, -24); return sign ? -r : r;
+    }
+    if (e == 31) { v.u = sign | 0x7f800000u | (m << 13); return v.f; }
+    v.u = sign | ((e + 112u) << 23) | (m << 13);
+    return v.f;
+}
+static inline float round_f16(float f) { return f16_to_f32(f32_to_f16(f)); }
+
+float orc_round_f16(float f) { return round_f16(f); }
+float orc_round_bf16(float f) { return round_bf16(f); }
+
+/* --------------------------------------------------- synthetic weights (spec) */
+float orc_synth_value(uint64_t seed, uint64_t tid, uint64_t idx, float scale) {
+    uint64_t z = seed * 0x9E3779B97F4A7C15ull + tid * 0xD1B54A32D192ED03ull + idx;
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    uint32_t s = (uint32_t)(z & 0xffff) + (uint32_t)((z >> 16) & 0xffff) +
+                 (uint32_t)((z >> 32) & 0xffff) + (uint32_t)(z >> 48);
+    return (float)((int32_t)s - 131070) * scale;
+}
+static float std_scale(double std) { return (float)(std / sqrt(4294967295.0 / 3.0)); }
+
+static void synth_bf16(uint16_t *dst, uint64_t seed, uint64_t tid, size_t n) {
+    float sc = std_scale(0.02);
+#pragma omp parallel for schedule(static)
+    for (size_t i = 0; i < n; i++) dst[i] = f32_to_bf16(orc_synth_value(seed, tid, i, sc));
+}
+static void synth_norm(float *dst, uint64_t seed, uint64_t tid, size_t n) {
+    float sc = std_scale(0.1);
+    for (size_t i = 0; i < n; i++) dst[i] = 1.0f + orc_synth_value(seed, tid, i, sc);
+}
+
+/* ------------------------------------------------------------------ model */
+orc_model *orc_create(const orc_hparams *hp, int flags) {
+    orc_model *m = (orc_model *)calloc(1, sizeof(orc_model));
+    m->hp = *hp;
+    m->flags = flags;
+    m->head_dim = hp->n_embd / hp->n_head;
+    m->n_embd_kv = m->head_dim * hp->n_head_kv;
+    size_t h = hp->n_embd, kv = m->n_embd_kv, ff = hp->n_ff, V = hp->n_vocab;
+    m->tok_embd = (uint16_t *)malloc(V * h * 2);
+    m->output = (uint16_t *)malloc(V * h * 2);
+    m->out_norm = (float *)malloc(h * 4);
+    m->layers = (orc_layer *)calloc(hp->n_layer, sizeof(orc_layer));
+    for (int l = 0; l < hp->n_layer; l++) {
+        orc_layer *L = &m->layers[l];
+        L->wq = (uint16_t *)malloc(h * h * 2);
+        L->wk = (uint16_t *)malloc(kv * h * 2);
+        L->wv = (uint16_t *)malloc(kv * h * 2);
+        L->wo = (uint16_t *)malloc(h * h * 2);
+        L->wg = (uint16_t *)malloc(ff * h * 2);
+        L->wu = (uint16_t *)malloc(ff * h * 2);
+        L->wd = (uint16_t *)malloc(h * ff * 2);
+        L->attn_norm = (float *)malloc(h * 4);
+        L->ffn_norm = (float *)malloc(h * 4);
+    }
+    return m;
+}
+
+void orc_free(orc_model *m) {
+    if (!m) return;
+    for (int l = 0; l < m->hp.n_layer; l++) {
+        orc_layer *L = &m->layers[l];
+        free(L->wq); free(L->wk); free(L->wv); free(L->wo); free(L->wg); free(L->wu); free(L->wd);
+        free(L->attn_norm); free(L->ffn_norm);
+    }
+    free(m->layers); free(m->tok_embd); free(m->output); free(m->out_norm); free(m);
+}
+
+/* tensor kinds, matching llama-p2p_amd/synth.py */
+enum { K_TOK_EMBD = 1, K_OUT_NORM = 2, K_OUTPUT = 3 };
+enum { L_ATTN_NORM, L_Q, L_K, L_V, L_O, L_FFN_NORM, L_GATE, L_UP, L_DOWN };
+static uint64_t layer_tid(int l, int k) { return 16u + 16u * (uint64_t)l + (uint64_t)k; }
+
+void orc_fill_synthetic(orc_model *m, uint64_t seed) {
+    size_t h = m->hp.n_embd, kv = m->n_embd_kv, ff = m->hp.n_ff, V = m->hp.n_vocab;
+    synth_bf16(m->tok_embd, seed, K_TOK_EMBD, V * h);
+    synth_bf16(m->output, seed, K_OUTPUT, V * h);
+    synth_norm(m->out_norm, seed, K_OUT_NORM, h);
+    for (int l = 0; l < m->hp.n_layer; l++) {
+        orc_layer *L = &m->layers[l];
+        synth_norm(L->attn_norm, seed, layer_tid(l, L_ATTN_NORM), h);
+        synth_bf16(L->wq, seed, layer_tid(l, L_Q), h * h);
+        synth_bf16(L->wk, seed, layer_tid(l, L_K), kv * h);
+        synth_bf16(L->wv, seed, layer_tid(l, L_V), kv * h);
+        synth_bf16(L->wo, seed, layer_tid(l, L_O), h * h);
+        synth_norm(L->ffn_norm, seed, layer_tid(l, L_FFN_NORM), h);
+        synth_bf16(L->wg, seed, layer_tid(l, L_GATE), ff * h);
+        synth_bf16(L->wu, seed, layer_tid(l, L_UP), ff * h);
+        synth_bf16(L->wd, seed, layer_tid(l, L_DOWN), h * ff);
+    }
+}
+
+/* Set one tensor from caller memory (bf16 bits for matrices, f32 for norms).
+ * layer = -1 for global tensors; kind uses the synth.py numbering. */
+int orc_set_tensor(orc_model *m, int layer, int kind, const void *src) {
+    size_t h = m->hp.n_embd, kv = m->n_embd_kv, ff = m->hp.n_ff, V = m->hp.n_vocab;
+    if (layer < 0) {
+        switch (kind) {
+        case K_TOK_EMBD: memcpy(m->tok_embd, src, V * h * 2); return 0;
+        case K_OUTPUT: memcpy(m->output, src, V * h * 2); return 0;
+        case K_OUT_NORM: memcpy(m->out_norm, src, h * 4); return 0;
+        }
+        return -1;
+    }
+    if (layer >= m->hp.n_layer) return -1;
+    orc_layer *L = &m->layers[layer];
+    switch (kind) {
+    case L_ATTN_NORM: memcpy(L->attn_norm, src, h * 4); return 0;
+    case L_Q: memcpy(L->wq, src, h * h * 2); return 0;
+    case L_K: memcpy(L->wk, src, kv * h * 2); return 0;
+    case L_V: memcpy(L->wv, src, kv * h * 2); return 0;
+    case L_O: memcpy(L->wo, src, h * h * 2); return 0;
+    case L_FFN_NORM: memcpy(L->ffn_norm, src, h * 4); return 0;
+    case L_GATE: memcpy(L->wg, src, ff * h * 2); return 0;
+    case L_UP: memcpy(L->wu, src, ff * h * 2); return 0;
+    case L_DOWN: memcpy(L->wd, src, h * ff * 2); return 0;
+    }
+    return -1;
+}
+
+/* ------------------------------------------------------------------ context */
+orc_ctx *orc_ctx_create(orc_model *m, int n_ctx) {
+    orc_ctx *c = (orc_ctx *)calloc(1, sizeof(orc_ctx));
+    c->m = m;
+    c->n_ctx = n_ctx;
+    int L = m->hp.n_layer;
+    size_t esz = (m->flags & ORC_EXACT) ? 4 : 2;
+    c->k = (void **)calloc(L, sizeof(void *));
+    c->v = (void **)calloc(L, sizeof(void *));
+    for (int l = 0; l < L; l++) {
+        c->k[l] = calloc((size_t)n_ctx * m->n_embd_kv, esz);
+        c->v[l] = calloc((size_t)n_ctx * m->n_embd_kv, esz);
+    }
+    /* rope cache, ggml_rope_cache_init (ext_factor 0, freq_scale 1, mscale 1) */
+    int half = m->head_dim / 2;
+    c->rope_cs = (float *)malloc((size_t)n_ctx * half * 2 * sizeof(float));
+    float theta_scale = powf(m->hp.rope_base, -2.0f / (float)m->head_dim);
+    for (int p = 0; p < n_ctx; p++) {
+        float theta = (float)p;
+        for (int i = 0; i < half; i++) {
+            c->rope_cs[((size_t)p * half + i) * 2 + 0] = cosf(theta);
+            c->rope_cs[((size_t)p * half + i) * 2 + 1] = sinf(theta);
+            theta *= theta_scale;
+        }
+    }
+    return c;
+}
+
+void orc_ctx_free(orc_ctx *c) {
+    if (!c) return;
+    for (int l = 0; l < c->m->hp.n_layer; l++) { free(c->k[l]); free(c->v[l]); }
+    free(c->k); free(c->v); free(c->rope_cs); free(c);
+}
+
+/* --------------------------------------------------------------- kernels */
+static void rmsnorm(float *y, const float *x, const float *w, int n, float eps) {
+    double sum = 0.0;
+    for (int i = 0; i < n; i++) sum += (double)(x[i] * x[i]);
+    float mean = (float)(sum / n);
+    float scale = 1.0f / sqrtf(mean + eps);
+    for (int i = 0; i < n; i++) y[i] = (x[i] * scale) * w[i];
+}
+
+static float dot_bf16(const uint16_t *w, const uint16_t *x, int n) {
+    float acc[16] = {0};
+    int i = 0;
+    for (; i + 16 <= n; i += 16)
+        for (int j = 0; j < 16; j++) acc[j] += bf16_to_f32(w[i + j]) * bf16_to_f32(x[i + j]);
+    float s = 0.f;
+    for (int j = 0; j < 16; j++) s += acc[j];
+    for (; i < n; i++) s += bf16_to_f32(w[i]) * bf16_to_f32(x[i]);
+    return s;
+}
+static float dot_bf16_f32(const uint16_t *w, const float *x, int n) {
+    float acc[16] = {0};
+    int i = 0;
+    for (; i + 16 <= n; i += 16)
+        for (int j = 0; j < 16; j++) acc[j] += bf16_to_f32(w[i + j]) * x[i + j];
+    float s = 0.f;
+    for (int j = 0; j < 16; j++) s += acc[j];
+    for (; i < n; i++) s += bf16_to_f32(w[i]) * x[i];
+    return s;
+}
+
+/* y[t][o] = W[o] . x[t] for T rows; ggml converts x to bf16 first (unless exact). */
+static void matmul(float *y, const uint16_t *W, const float *x, int T, int n_in, int n_out, int exact,
+                   uint16_t *scratch /* T*n_in */) {
+    if (!exact) {
+        for (size_t i = 0; i < (size_t)T * n_in; i++) scratch[i] = f32_to_bf16(x[i]);
+#pragma omp parallel for schedule(static)
+        for (int o = 0; o < n_out; o++)
+            for (int t = 0; t < T; t++)
+                y[(size_t)t * n_out + o] = dot_bf16(W + (size_t)o * n_in, scratch + (size_t)t * n_in, n_in);
+    } else {
+#pragma omp parallel for schedule(static)
+        for (int o = 0; o < n_out; o++)
+            for (int t = 0; t < T; t++)
+                y[(size_t)t * n_out + o] = dot_bf16_f32(W + (size_t)o * n_in, x + (size_t)t * n_in, n_in);
+    }
+}
+
+static void rope_rows(float *v, int n_heads, int d, const float *cs /* [d/2][2] at pos */) {
+    for (int hh = 0; hh < n_heads; hh++) {
+        float *r = v + (size_t)hh * d;
+        for (int i = 0; i < d / 2; i++) {
+            float c = cs[2 * i], s = cs[2 * i + 1];
+            float x0 = r[2 * i], x1 = r[2 * i + 1];
+            r[2 * i] = x0 * c - x1 * s;
+            r[2 * i + 1] = x0 * s + x1 * c;
+        }
+    }
+}
+
+/*
+ * Evaluate n tokens at positions pos0..pos0+n-1 of this context (one llama_decode
+ * of a ubatch).  logits: if all_logits, [n][V]; else [V] for the last token.
+ * Returns 0 on success.
+ */
+int orc_eval(orc_ctx *c, const int32_t *ids, int n, int pos0, float *logits, int all_logits) {
+    orc_model *m = c->m;
+    const orc_hparams *hp = &m->hp;
+    int exact = m->flags & ORC_EXACT;
+    int h = hp->n_embd, kvd = m->n_embd_kv, ff = hp->n_ff, V = hp->n_vocab;
+    int nh = hp->n_head, nkv = hp->n_head_kv, d = m->head_dim, gq = nh / nkv;
+    if (n <= 0 || pos0 < 0 || pos0 + n > c->n_ctx) return -1;
+    for (int t = 0; t < n; t++)
+        if (ids[t] < 0 || ids[t] >= V) return -2;
+    int T = n;
+    int mx = ff > h ? ff : h;
+    float *x = (float *)malloc(sizeof(float) * T * h);
+    float *cur = (float *)malloc(sizeof(float) * T * mx);
+    float *q = (float *)malloc(sizeof(float) * T * h);
+    float *k = (float *)malloc(sizeof(float) * T * kvd);
+    float *v = (float *)malloc(sizeof(float) * T * kvd);
+    float *att = (float *)malloc(sizeof(float) * T * h);
+    float *g = (float *)malloc(sizeof(float) * T * ff);
+    float *u = (float *)malloc(sizeof(float) * T * ff);
+    float *tmp = (float *)malloc(sizeof(float) * T * h);
+    uint16_t *scratch = (uint16_t *)malloc(sizeof(uint16_t) * T * mx);
+    const float kq_scale = 1.0f / sqrtf((float)d);
+
+    for (int t = 0; t < T; t++)
+        for (int i = 0; i < h; i++) x[(size_t)t * h + i] = bf16_to_f32(m->tok_embd[(size_t)ids[t] * h + i]);
+
+    for (int l = 0; l < hp->n_layer; l++) {
+        orc_layer *L = &m->layers[l];
+        for (int t = 0; t < T; t++) rmsnorm(cur + (size_t)t * h, x + (size_t)t * h, L->attn_norm, h, hp->eps);
+        matmul(q, L->wq, cur, T, h, h, exact, scratch);
+        matmul(k, L->wk, cur, T, h, kvd, exact, scratch);
+        matmul(v, L->wv, cur, T, h, kvd, exact, scratch);
+        for (int t = 0; t < T; t++) {
+            const float *cs = c->rope_cs + (size_t)(pos0 + t) * (d / 2) * 2;
+            rope_rows(q + (size_t)t * h, nh, d, cs);
+            rope_rows(k + (size_t)t * kvd, nkv, d, cs);
+            size_t off = (size_t)(pos0 + t) * kvd;
+            if (exact) {
+                memcpy((float *)c->k[l] + off, k + (size_t)t * kvd, kvd * 4);
+                memcpy((float *)c->v[l] + off, v + (size_t)t * kvd, kvd * 4);
+            } else {
+                for (int i = 0; i < kvd; i++) {
+                    ((uint16_t *)c->k[l])[off + i] = f32_to_f16(k[(size_t)t * kvd + i]);
+                    ((uint16_t *)c->v[l])[off + i] = f32_to_f16(v[(size_t)t * kvd + i]);
+                }
+            }
+        }
+        /* attention */
+#pragma omp parallel for collapse(2) schedule(static)
+        for (int t = 0; t < T; t++) {
+            for (int hh = 0; hh < nh; hh++) {
+                int n_kv = pos0 + t + 1; /* causal */
+                int kh = hh / gq;
+                float qv[256];
+                double *dummy = NULL; (void)dummy;
+                for (int i = 0; i < d; i++) {
+                    float qq = q[(size_t)t * h + hh * d + i];
+                    qv[i] = exact ? qq : round_f16(qq);
+                }
+                float *s = (float *)malloc(sizeof(float) * n_kv);
+                float smax = -INFINITY;
+                for (int p = 0; p < n_kv; p++) {
+                    float acc = 0.f;
+                    size_t off = (size_t)p * kvd + (size_t)kh * d;
+                    if (exact) {
+                        const float *kr = (const float *)c->k[l] + off;
+                        for (int i = 0; i < d; i++) acc += qv[i] * kr[i];
+                    } else {
+                        const uint16_t *kr = (const uint16_t *)c->k[l] + off;
+                        for (int i = 0; i < d; i++) acc += qv[i] * f16_to_f32(kr[i]);
+                    }
+                    s[p] = acc * kq_scale;
+                    if (s[p] > smax) smax = s[p];
+                }
+                double sum = 0.0;
+                for (int p = 0; p < n_kv; p++) {
+                    float e = expf(s[p] - smax);
+                    sum += (double)e;
+                    s[p] = e;
+                }
+                float inv = (float)(1.0 / sum);
+                for (int p = 0; p < n_kv; p++) {
+                    s[p] *= inv;
+                    if (!exact) s[p] = round_f16(s[p]);
+                }
+                float o[256];
+                for (int i = 0; i < d; i++) o[i] = 0.f;
+                for (int p = 0; p < n_kv; p++) {
+                    size_t off = (size_t)p * kvd + (size_t)kh * d;
+                    if (exact) {
+                        const float *vr = (const float *)c->v[l] + off;
+                        for (int i = 0; i < d; i++) o[i] += s[p] * vr[i];
+                    } else {
+                        const uint16_t *vr = (const uint16_t *)c->v[l] + off;
+                        for (int i = 0; i < d; i++) o[i] += s[p] * f16_to_f32(vr[i]);
+                    }
+                }
+                for (int i = 0; i < d; i++) att[(size_t)t * h + hh * d + i] = o[i];
+                free(s);
+            }
+        }
+        matmul(tmp, L->wo, att, T, h, h, exact, scratch);
+        for (size_t i = 0; i < (size_t)T * h; i++) x[i] += tmp[i];
+        /* ffn */
+        for (int t = 0; t < T; t++) rmsnorm(cur + (size_t)t * h, x + (size_t)t * h, L->ffn_norm, h, hp->eps);
+        matmul(u, L->wu, cur, T, h, ff, exact, scratch);
+        matmul(g, L->wg, cur, T, h, ff, exact, scratch);
+        for (size_t i = 0; i < (size_t)T * ff; i++) {
+            float gg = g[i];
+            g[i] = (gg / (1.0f + expf(-gg))) * u[i];
+        }
+        matmul(tmp, L->wd, g, T, ff, h, exact, scratch);
+        for (size_t i = 0; i < (size_t)T * h; i++) x[i] += tmp[i];
+    }
+    int t0 = all_logits ? 0 : T - 1;
+    int nt = T - t0;
+    for (int t = 0; t < nt; t++) rmsnorm(cur + (size_t)t * h, x + (size_t)(t0 + t) * h, m->out_norm, h, hp->eps);
+    matmul(logits, m->output, cur, nt, h, V, exact, scratch);
+
+    free(x); free(cur); free(q); free(k); free(v); free(att); free(g); free(u); free(tmp); free(scratch);
+    return 0;
+}
+
+int orc_argmax(const float *logits, int n) {
+    int best = 0;
+    for (int i = 1; i < n; i++)
+        if (logits[i] > logits[best]) best = i; /* strict: ties keep the lowest id */
+    return best;
+}
+
+/* Greedy generation: prefill prompt in chunks of n_batch, then decode one token
+ * at a time (llama_cpp generate/eval loop at temperature 0).  out[n_gen]. */
+int orc_generate_greedy(orc_ctx *c, const int32_t *prompt, int n_prompt, int n_gen, int n_batch, int32_t *out) {
+    int V = c->m->hp.n_vocab;
+    float *logits = (float *)malloc(sizeof(float) * V);
+    int pos = 0, rc = 0;
+    for (int i = 0; i < n_prompt; i += n_batch) {
+        int nb = n_prompt - i < n_batch ? n_prompt - i : n_batch;
+        if ((rc = orc_eval(c, prompt + i, nb, pos, logits, 0))) goto done;
+        pos += nb;
+    }
+    for (int g = 0; g < n_gen; g++) {
+        int32_t tok = orc_argmax(logits, V);
+        out[g] = tok;
+        if (g + 1 == n_gen) break;
+        if ((rc = orc_eval(c, &tok, 1, pos, logits, 0))) goto done;
+        pos++;
+    }
+done:
+    free(logits);
+    return rc;
+}
+
+int orc_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+void orc_set_num_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}

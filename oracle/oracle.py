@@ -1,0 +1,140 @@
+"""ctypes wrapper of the CPU oracle (llama_oracle.c).
+
+TEST INFRASTRUCTURE ONLY -- imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by the product package.  See the header of
+llama_oracle.c for what it restates (llama.cpp llm_build_llama on CPU, the
+hot path behind /root/reference/llama_p2p_network.py:125).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liborc.so")
+
+ORC_EXACT = 1
+
+
+class _HP(ctypes.Structure):
+    _fields_ = [("n_embd", ctypes.c_int), ("n_layer", ctypes.c_int), ("n_head", ctypes.c_int),
+                ("n_head_kv", ctypes.c_int), ("n_ff", ctypes.c_int), ("n_vocab", ctypes.c_int),
+                ("eps", ctypes.c_float), ("rope_base", ctypes.c_float)]
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(HERE, "llama_oracle.c")
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", HERE, "liborc.so"])
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32, u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64
+        L.orc_create.restype = vp
+        L.orc_create.argtypes = [ctypes.POINTER(_HP), i32]
+        L.orc_free.argtypes = [vp]
+        L.orc_fill_synthetic.argtypes = [vp, u64]
+        L.orc_set_tensor.argtypes = [vp, i32, i32, vp]
+        L.orc_set_tensor.restype = i32
+        L.orc_ctx_create.restype = vp
+        L.orc_ctx_create.argtypes = [vp, i32]
+        L.orc_ctx_free.argtypes = [vp]
+        L.orc_eval.argtypes = [vp, vp, i32, i32, vp, i32]
+        L.orc_eval.restype = i32
+        L.orc_generate_greedy.argtypes = [vp, vp, i32, i32, i32, vp]
+        L.orc_generate_greedy.restype = i32
+        L.orc_num_threads.restype = i32
+        L.orc_set_num_threads.argtypes = [i32]
+        L.orc_synth_value.restype = ctypes.c_float
+        L.orc_synth_value.argtypes = [u64, u64, u64, ctypes.c_float]
+        L.orc_round_f16.restype = ctypes.c_float
+        L.orc_round_f16.argtypes = [ctypes.c_float]
+        L.orc_round_bf16.restype = ctypes.c_float
+        L.orc_round_bf16.argtypes = [ctypes.c_float]
+        _lib = L
+    return _lib
+
+
+class OracleModel:
+    """A LLaMA model on the CPU oracle.  ``shape`` is a synth.LlamaShape."""
+
+    def __init__(self, shape, seed: int | None = 0, exact: bool = False):
+        self.shape = shape
+        hp = _HP(shape.n_embd, shape.n_layer, shape.n_head, shape.n_head_kv, shape.n_ff, shape.n_vocab,
+                 shape.eps, shape.rope_base)
+        self._m = lib().orc_create(ctypes.byref(hp), ORC_EXACT if exact else 0)
+        if seed is not None:
+            lib().orc_fill_synthetic(self._m, seed)
+
+    def set_tensor(self, layer: int, kind: int, arr: np.ndarray):
+        arr = np.ascontiguousarray(arr)
+        rc = lib().orc_set_tensor(self._m, layer, kind, arr.ctypes.data)
+        if rc:
+            raise ValueError(f"orc_set_tensor({layer},{kind}) failed")
+
+    def context(self, n_ctx: int = 512) -> "OracleContext":
+        return OracleContext(self, n_ctx)
+
+    def close(self):
+        if self._m:
+            lib().orc_free(self._m)
+            self._m = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class OracleContext:
+    def __init__(self, model: OracleModel, n_ctx: int):
+        self.model = model
+        self.n_ctx = n_ctx
+        self._c = lib().orc_ctx_create(model._m, n_ctx)
+
+    def eval(self, ids, pos0: int, all_logits: bool = False) -> np.ndarray:
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        n = len(ids)
+        V = self.model.shape.n_vocab
+        out = np.zeros((n if all_logits else 1, V), dtype=np.float32)
+        rc = lib().orc_eval(self._c, ids.ctypes.data, n, pos0, out.ctypes.data, 1 if all_logits else 0)
+        if rc:
+            raise ValueError(f"orc_eval rc={rc}")
+        return out
+
+    def generate_greedy(self, prompt, n_gen: int, n_batch: int = 512) -> np.ndarray:
+        prompt = np.ascontiguousarray(prompt, dtype=np.int32)
+        out = np.zeros(n_gen, dtype=np.int32)
+        rc = lib().orc_generate_greedy(self._c, prompt.ctypes.data, len(prompt), n_gen, n_batch, out.ctypes.data)
+        if rc:
+            raise ValueError(f"orc_generate_greedy rc={rc}")
+        return out
+
+    def close(self):
+        if self._c:
+            lib().orc_ctx_free(self._c)
+            self._c = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def argmax_lowest(logits: np.ndarray) -> int:
+    """Greedy pick with ties -> lowest id (llama.cpp greedy sampler)."""
+    return int(np.argmax(logits))  # numpy argmax returns the first maximum
