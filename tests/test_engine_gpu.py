@@ -41,7 +41,12 @@ def test_prefill_logits_vs_oracle(mx, oracle_mod, name):
     ref = oracle_mod.OracleModel(shape, seed=0).context(256).eval(ids, 0, all_logits=True)
     assert_logits_close(got, ref, name)
     decided, agree = assert_tokens_match(got, ref, name)
-    assert decided > 0.8 * len(ids)
+    err = np.abs(got - ref)
+    print(f"{name}: max|d| {err.max():.3g} (max|ref| {np.abs(ref).max():.3g}), argmax agree {agree}/{len(ids)}, "
+          f"decided {decided}")
+    # engine and oracle follow the same ggml rounding points: the error is far inside the stated tolerance
+    assert err.max() < 0.25 * (2e-2 * np.abs(ref).max())
+    assert agree >= 0.9 * len(ids)
     eng.close()
 
 
