@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -118,7 +119,8 @@ struct mx_engine {
   int bos = 1, eos = 2;
   int n_ctx = 512, n_seq_max = 64, lb = 0, le = 0, device = 0;
   bool has_embed = true, has_head = true, use_graphs = true;
-  int n_chunks = 0;
+  bool fuse_norms = getenv("MX_NO_FUSED_NORM") == nullptr;
+  int ctx_stride = 0;  // KV positions allocated per slot (n_ctx rounded up to KV_POS_ALIGN)
   uint64_t weight_bytes = 0;
 
   // device state
@@ -130,7 +132,7 @@ struct mx_engine {
   size_t slot_stride = 0, layer_kv_stride = 0;
   float* rope_cs = nullptr;
   // workspaces (MAX_ROWS rows)
-  float *x = nullptr, *q = nullptr, *o_part = nullptr, *ml_part = nullptr, *logits = nullptr;
+  float *x = nullptr, *q = nullptr, *logits = nullptr;
   uint16_t *xn = nullptr, *act = nullptr, *attn_out = nullptr;
   float* am_val = nullptr;
   int *am_idx = nullptr, *d_tok = nullptr;
@@ -200,12 +202,12 @@ int mx_engine::init_common() {
   if (lb < 0 || lb >= le) return fail(MX_ERR_ARG, "bad layer range");
   has_embed = lb == 0;
   has_head = le == n_layer;
-  n_chunks = (n_ctx + ATTN_CHUNK - 1) / ATTN_CHUNK;
+  ctx_stride = (n_ctx + KV_POS_ALIGN - 1) / KV_POS_ALIGN * KV_POS_ALIGN;
   const int nl = le - lb;
   layers.resize(nl);
 
-  // KV cache [layer][slot][kv head][pos][dim] f16
-  slot_stride = (size_t)n_head_kv * n_ctx * head_dim;
+  // KV cache per layer and slot: K [kv head][pos][dim], V transposed [kv head][dim][pos], f16
+  slot_stride = (size_t)n_head_kv * ctx_stride * head_dim;
   layer_kv_stride = slot_stride * n_seq_max;
   if (int rc = alloc((void**)&kcache, layer_kv_stride * nl * sizeof(_Float16))) return rc;
   if (int rc = alloc((void**)&vcache, layer_kv_stride * nl * sizeof(_Float16))) return rc;
@@ -232,8 +234,6 @@ int mx_engine::init_common() {
   if (int rc = alloc((void**)&xn, (size_t)R * n_embd * 2)) return rc;
   if (int rc = alloc((void**)&attn_out, (size_t)R * n_embd * 2)) return rc;
   if (int rc = alloc((void**)&act, (size_t)R * n_ff * 2)) return rc;
-  if (int rc = alloc((void**)&o_part, (size_t)R * n_head * n_chunks * head_dim * 4)) return rc;
-  if (int rc = alloc((void**)&ml_part, (size_t)R * n_head * n_chunks * 2 * 4)) return rc;
   if (has_head) {
     if (int rc = alloc((void**)&logits, (size_t)R * n_vocab * 4)) return rc;
   }
@@ -279,7 +279,7 @@ int mx_engine::load_synthetic(const Shape& s, uint64_t seed) {
   if (has_head) {
     if (int rc = alloc((void**)&output, (size_t)V * h * 2)) return rc;
     if (int rc = alloc((void**)&out_norm, (size_t)h * 4)) return rc;
-    launch_synth_packed(output, V, h, seed, TID_OUTPUT, ws, 1, 0, stream);
+    launch_synth_packed(output, V, h, seed, TID_OUTPUT, ws, PACK_ROWS, 0, stream);
     launch_synth_norm(out_norm, h, seed, TID_OUT_NORM, ns, stream);
     weight_bytes += (size_t)V * h * 2 + h * 4;
   }
@@ -288,13 +288,13 @@ int mx_engine::load_synthetic(const Shape& s, uint64_t seed) {
     if (int rc = alloc_layer(this, L)) return rc;
     launch_synth_norm(L.attn_norm, h, seed, layer_tid(l, L_ATTN_NORM), ns, stream);
     launch_synth_norm(L.ffn_norm, h, seed, layer_tid(l, L_FFN_NORM), ns, stream);
-    launch_synth_packed(L.qkv, h, h, seed, layer_tid(l, L_Q), ws, 1, 0, stream);
-    launch_synth_packed(L.qkv, kv, h, seed, layer_tid(l, L_K), ws, 1, h / 16, stream);
-    launch_synth_packed(L.qkv, kv, h, seed, layer_tid(l, L_V), ws, 1, (h + kv) / 16, stream);
-    launch_synth_packed(L.o, h, h, seed, layer_tid(l, L_O), ws, 1, 0, stream);
-    launch_synth_packed(L.gu, ff, h, seed, layer_tid(l, L_GATE), ws, 2, 0, stream);
-    launch_synth_packed(L.gu, ff, h, seed, layer_tid(l, L_UP), ws, 2, 1, stream);
-    launch_synth_packed(L.down, h, ff, seed, layer_tid(l, L_DOWN), ws, 1, 0, stream);
+    launch_synth_packed(L.qkv, h, h, seed, layer_tid(l, L_Q), ws, PACK_ROWS, 0, stream);
+    launch_synth_packed(L.qkv, kv, h, seed, layer_tid(l, L_K), ws, PACK_ROWS, h, stream);
+    launch_synth_packed(L.qkv, kv, h, seed, layer_tid(l, L_V), ws, PACK_ROWS, h + kv, stream);
+    launch_synth_packed(L.o, h, h, seed, layer_tid(l, L_O), ws, PACK_ROWS, 0, stream);
+    launch_synth_packed(L.gu, ff, h, seed, layer_tid(l, L_GATE), ws, PACK_GATE, 0, stream);
+    launch_synth_packed(L.gu, ff, h, seed, layer_tid(l, L_UP), ws, PACK_UP, 0, stream);
+    launch_synth_packed(L.down, h, ff, seed, layer_tid(l, L_DOWN), ws, PACK_ROWS, 0, stream);
   }
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(stream));
@@ -342,12 +342,12 @@ int mx_engine::load_gguf(const std::string& path) {
     *out = t;
     return 0;
   };
-  auto upload_packed = [&](const std::string& name, int rows, int cols, uint16_t* dst, int stride,
+  auto upload_packed = [&](const std::string& name, int rows, int cols, uint16_t* dst, int mode,
                            int offset) -> int {
     const GGUFTensor* t = nullptr;
     if (int rc = get_mat(name, rows, cols, &t)) return rc;
     HIPC(hipMemcpy(stage, f.data(*t), t->nbytes, hipMemcpyHostToDevice));
-    launch_pack(dst, stage, rows, cols, stride, offset, stream);
+    launch_pack(dst, stage, rows, cols, mode, offset, stream);
     HIPC(hipStreamSynchronize(stream));
     return 0;
   };
@@ -372,7 +372,7 @@ int mx_engine::load_gguf(const std::string& path) {
     if ((rc = alloc((void**)&output, (size_t)V * h * 2))) goto out;
     if ((rc = alloc((void**)&out_norm, (size_t)h * 4))) goto out;
     const char* oname = f.tensor("output.weight") ? "output.weight" : "token_embd.weight";  // tied embeddings
-    if ((rc = upload_packed(oname, V, h, output, 1, 0))) goto out;
+    if ((rc = upload_packed(oname, V, h, output, PACK_ROWS, 0))) goto out;
     if ((rc = upload_norm("output_norm.weight", out_norm))) goto out;
     weight_bytes += (size_t)V * h * 2 + h * 4;
   }
@@ -382,13 +382,13 @@ int mx_engine::load_gguf(const std::string& path) {
     if ((rc = alloc_layer(this, L))) goto out;
     if ((rc = upload_norm(p + "attn_norm.weight", L.attn_norm))) goto out;
     if ((rc = upload_norm(p + "ffn_norm.weight", L.ffn_norm))) goto out;
-    if ((rc = upload_packed(p + "attn_q.weight", h, h, L.qkv, 1, 0))) goto out;
-    if ((rc = upload_packed(p + "attn_k.weight", kv, h, L.qkv, 1, h / 16))) goto out;
-    if ((rc = upload_packed(p + "attn_v.weight", kv, h, L.qkv, 1, (h + kv) / 16))) goto out;
-    if ((rc = upload_packed(p + "attn_output.weight", h, h, L.o, 1, 0))) goto out;
-    if ((rc = upload_packed(p + "ffn_gate.weight", ff, h, L.gu, 2, 0))) goto out;
-    if ((rc = upload_packed(p + "ffn_up.weight", ff, h, L.gu, 2, 1))) goto out;
-    if ((rc = upload_packed(p + "ffn_down.weight", h, ff, L.down, 1, 0))) goto out;
+    if ((rc = upload_packed(p + "attn_q.weight", h, h, L.qkv, PACK_ROWS, 0))) goto out;
+    if ((rc = upload_packed(p + "attn_k.weight", kv, h, L.qkv, PACK_ROWS, h))) goto out;
+    if ((rc = upload_packed(p + "attn_v.weight", kv, h, L.qkv, PACK_ROWS, h + kv))) goto out;
+    if ((rc = upload_packed(p + "attn_output.weight", h, h, L.o, PACK_ROWS, 0))) goto out;
+    if ((rc = upload_packed(p + "ffn_gate.weight", ff, h, L.gu, PACK_GATE, 0))) goto out;
+    if ((rc = upload_packed(p + "ffn_up.weight", ff, h, L.gu, PACK_UP, 0))) goto out;
+    if ((rc = upload_packed(p + "ffn_down.weight", h, ff, L.down, PACK_ROWS, 0))) goto out;
   }
 out:
   hipFree(stage);
@@ -406,27 +406,40 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     if (!has_embed) return fail(MX_ERR_STATE, "this stage has no token embedding: x_in required");
     launch_embed(x, tok_embd, ids, M, h, s);
   }
+  // RMS_NORM is fused into the consuming GEMV when the activation image fits LDS (M <= 8)
+  const bool fuse_norm = fuse_norms && mm_can_fuse_norm(M, h);
+  auto norm_operand = [&](MMArgs& m, const float* w) {
+    if (fuse_norm) {
+      m.X = nullptr; m.xf = x; m.norm_w = w; m.eps = eps;
+    } else {
+      launch_rmsnorm(xn, h, x, w, nullptr, M, h, eps, s);
+      m.X = xn; m.ldx = h;
+    }
+  };
   for (int li = 0; li < (int)layers.size(); li++) {
     const Layer& L = layers[li];
     _Float16* kc = kcache + layer_kv_stride * li;
     _Float16* vc = vcache + layer_kv_stride * li;
-    launch_rmsnorm(xn, h, x, L.attn_norm, nullptr, M, h, eps, s);
     MMArgs a{};
-    a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.X = xn; a.ldx = h; a.M = M;
+    a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M;
+    norm_operand(a, L.attn_norm);
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
-    a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.n_head_kv = n_head_kv; a.slot_stride = slot_stride;
+    a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
+    a.slot_stride = slot_stride;
     if (launch_mm(EPI_QKV, a, s)) return fail(MX_ERR_ARG, "qkv launch shape");
     AttnArgs at{};
-    at.q = q; at.kc = kc; at.vc = vc; at.pos = pos; at.slot = slot; at.o_part = o_part; at.ml_part = ml_part;
+    at.q = q; at.kc = kc; at.vc = vc; at.pos = pos; at.slot = slot;
     at.out = attn_out; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
-    at.n_ctx = n_ctx; at.n_chunks = n_chunks; at.slot_stride = slot_stride; at.scale = 1.0f / sqrtf((float)head_dim);
+    at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;
+    at.scale = 1.0f / sqrtf((float)head_dim);
     launch_attention(at, s);
     MMArgs b{};
     b.W = L.o; b.N = h; b.K = h; b.X = attn_out; b.ldx = h; b.M = M; b.out = x; b.ldo = h;
     if (launch_mm(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "attn_output launch shape");
-    launch_rmsnorm(xn, h, x, L.ffn_norm, nullptr, M, h, eps, s);
     MMArgs c{};
-    c.W = L.gu; c.N = 2 * ff; c.K = h; c.X = xn; c.ldx = h; c.M = M; c.act = act; c.lda = ff;
+    c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M;
+    norm_operand(c, L.ffn_norm);
+    c.act = act; c.lda = ff;
     if (launch_mm(EPI_SWIGLU, c, s)) return fail(MX_ERR_ARG, "ffn gate/up launch shape");
     MMArgs d{};
     d.W = L.down; d.N = h; d.K = ff; d.X = act; d.ldx = ff; d.M = M; d.out = x; d.ldo = h;
@@ -437,9 +450,14 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
   }
   if (head) {
     if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
-    launch_rmsnorm(xn, h, x, out_norm, rowmap, n_out, h, eps, s);
     MMArgs g{};
-    g.W = output; g.N = n_vocab; g.K = h; g.X = xn; g.ldx = h; g.M = n_out; g.out = logits; g.ldo = n_vocab;
+    g.W = output; g.N = n_vocab; g.K = h; g.M = n_out; g.out = logits; g.ldo = n_vocab;
+    if (!rowmap && n_out == M) {
+      norm_operand(g, out_norm);
+    } else {
+      launch_rmsnorm(xn, h, x, out_norm, rowmap, n_out, h, eps, s);
+      g.X = xn; g.ldx = h;
+    }
     if (launch_mm(EPI_F32, g, s)) return fail(MX_ERR_ARG, "lm_head launch shape");
     if (argmax)
       launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, ids_next, pos_next, hist, hist_stride,
@@ -713,7 +731,7 @@ int mx_engine_create(const char* model_path, const mx_opts* opts, mx_engine** ou
   e->n_seq_max = o.n_seq_max;
   e->lb = o.layer_begin;
   e->le = o.layer_end;
-  e->use_graphs = o.use_graphs != 0;
+  e->use_graphs = o.use_graphs != 0 && getenv("MX_NO_GRAPHS") == nullptr;  // rocprofv3 runs set MX_NO_GRAPHS
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MX_ERR_HIP, "no HIP device visible");
   if (o.device >= 0) HIPC(hipSetDevice(o.device));
@@ -969,6 +987,7 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
         a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.X = e->xn; a.ldx = h; a.out = e->q; a.ldo = h; a.n_q = h;
         a.n_kv = kv; a.head_dim = e->head_dim; a.pos = e->d_pos; a.slot = e->d_slot; a.rope_cs = e->rope_cs;
         a.kc = e->kcache + e->layer_kv_stride * li; a.vc = e->vcache + e->layer_kv_stride * li; a.n_ctx = e->n_ctx;
+        a.ctx_stride = e->ctx_stride;
         a.n_head_kv = e->n_head_kv; a.slot_stride = e->slot_stride;
         per = (size_t)(h + 2 * kv) * h * 2;
         return launch_mm(EPI_QKV, a, s);

@@ -19,13 +19,15 @@ constexpr int TILE_N = 16;
 constexpr int TILE_K = 32;
 constexpr int TILE_ELEMS = TILE_N * TILE_K;
 constexpr int MAX_ROWS = 64;       // tokens per forward (4 column tiles of 16)
-constexpr int ATTN_CHUNK = 64;     // positions per attention work-group
+constexpr int ATTN_CHUNK = 32;     // positions per attention wave-iteration
+constexpr int KV_POS_ALIGN = 64;   // KV rows per slot are allocated in multiples of this
+constexpr int XN_LDS_BYTES = 64 * 1024;  // budget for the fused-RMSNorm activation image in LDS
 
 enum Epilogue : int {
   EPI_F32 = 0,     // out[col][row] = acc                         (lm_head logits)
   EPI_RESID = 1,   // x[col][row] += acc                          (attn_output, ffn_down)
   EPI_QKV = 2,     // rope(q,k); q -> f32 buffer, k/v -> f16 KV cache (attn_q/k/v)
-  EPI_SWIGLU = 3,  // act = bf16(silu(gate) * up)                  (ffn_gate/ffn_up)
+  EPI_SWIGLU = 3,  // act = bf16(silu(gate) * up); tile = 8 gate + 8 up rows (ffn_gate/ffn_up)
 };
 
 struct MMArgs {
@@ -34,6 +36,10 @@ struct MMArgs {
   const uint16_t* X;   // activations bf16 [>=16*NB rows][ldx]
   int ldx;
   int M;               // valid columns (tokens)
+  // fused RMS_NORM (X == nullptr): the work-group normalises xf[M][K] with norm_w into LDS
+  const float* xf;
+  const float* norm_w;
+  float eps;
   // epilogue operands
   float* out;          // EPI_F32: [M][ldo]; EPI_RESID: residual x [M][ldo]; EPI_QKV: q [M][ldo]
   int ldo;
@@ -44,40 +50,41 @@ struct MMArgs {
   const int* pos;              // [M]
   const int* slot;             // [M]
   const float* rope_cs;        // [n_ctx][head_dim/2][2]
-  _Float16* kc;                // K cache of this layer: [slots][n_head_kv][n_ctx][head_dim]
-  _Float16* vc;                // V cache of this layer
-  int n_ctx, n_head_kv;
-  size_t slot_stride;          // elements per slot in kc/vc = n_head_kv*n_ctx*head_dim
+  _Float16* kc;                // K cache of this layer: [slots][n_head_kv][ctx_stride][head_dim]
+  _Float16* vc;                // V cache of this layer, transposed: [slots][n_head_kv][head_dim][ctx_stride]
+  int n_ctx, ctx_stride, n_head_kv;
+  size_t slot_stride;          // elements per slot in kc/vc = n_head_kv*ctx_stride*head_dim
 };
 
 struct AttnArgs {
   const float* q;        // [M][n_head*head_dim] f32 (post-RoPE)
-  const _Float16* kc;    // [slots][n_head_kv][n_ctx][head_dim]
-  const _Float16* vc;
+  const _Float16* kc;    // [slots][n_head_kv][ctx_stride][head_dim]
+  const _Float16* vc;    // [slots][n_head_kv][head_dim][ctx_stride]  (transposed)
   const int* pos;        // [M]  query position; attends to [0, pos]
   const int* slot;       // [M]
-  float* o_part;         // [M][n_head][n_chunks][head_dim]
-  float* ml_part;        // [M][n_head][n_chunks][2]  (max, sum)
-  uint16_t* out;         // combine output bf16 [M][ldo]
+  uint16_t* out;         // bf16 [M][ldo] (src1 of attn_output)
   int ldo;
-  int M, n_head, n_head_kv, head_dim, n_ctx, n_chunks;
+  int M, n_head, n_head_kv, head_dim, n_ctx, ctx_stride;
   size_t slot_stride;
   float scale;
 };
 
-// packing / synthetic weights
-void launch_synth_packed(uint16_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale,
-                         int row_tile_stride, int row_tile_offset, hipStream_t s);
+// packing / synthetic weights.  mode: PACK_ROWS (logical row r -> packed row r + offset),
+// PACK_GATE / PACK_UP (ffn_gate / ffn_up rows interleaved by 8-row halves of each tile)
+enum PackMode : int { PACK_ROWS = 0, PACK_GATE = 1, PACK_UP = 2 };
+void launch_synth_packed(uint16_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, int mode,
+                         int row_offset, hipStream_t s);
 void launch_synth_rowmajor(uint16_t* dst, size_t n, uint64_t seed, uint64_t tid, float scale, hipStream_t s);
 void launch_synth_norm(float* dst, size_t n, uint64_t seed, uint64_t tid, float scale, hipStream_t s);
-void launch_pack(uint16_t* dst, const uint16_t* src_rowmajor, int N, int K, int row_tile_stride,
-                 int row_tile_offset, hipStream_t s);
+void launch_pack(uint16_t* dst, const uint16_t* src_rowmajor, int N, int K, int mode, int row_offset,
+                 hipStream_t s);
 
 // forward-pass ops
 void launch_embed(float* x, const uint16_t* tok_embd, const int* ids, int M, int n_embd, hipStream_t s);
 void launch_rmsnorm(uint16_t* y, int ldy, const float* x, const float* w, const int* row_map, int M, int n,
                     float eps, hipStream_t s);
 int launch_mm(int epi, const MMArgs& a, hipStream_t s);
+bool mm_can_fuse_norm(int M, int K);  // X == nullptr path (RMS_NORM fused into the GEMV) is legal
 void launch_attention(const AttnArgs& a, hipStream_t s);
 void launch_argmax(const float* logits, int ldl, int M, int V, float* ws_val, int* ws_idx, int* tok_out,
                    int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count, int max_hist,

@@ -53,41 +53,37 @@ __device__ __forceinline__ float synth_value(uint64_t seed, uint64_t tid, uint64
   return (float)((int32_t)s - 131070) * scale;
 }
 
-// packed element p of a [N][K] matrix -> (row, col) of the logical matrix
-__device__ __forceinline__ void packed_coords(size_t p, int KT, int& row, int& col, size_t& tile) {
-  tile = p / TILE_ELEMS;
-  int within = (int)(p % TILE_ELEMS);
-  int lane = within >> 3, j = within & 7;
-  int nt = (int)(tile / KT), kt = (int)(tile % KT);
-  row = nt * TILE_N + (lane & 15);
-  col = kt * TILE_K + (lane >> 4) * 8 + j;
+// Destination row of logical row `row` in a packed matrix (see kernels.h):
+//   PACK_ROWS:     row + offset           (q|k|v stacked into one QKV matrix, or plain)
+//   PACK_GATE/UP:  16*(row/8) + (0|8) + row%8   -- ffn_gate and ffn_up rows interleaved by
+//                  halves of each 16-row tile, so one tile yields 8 SwiGLU outputs
+__device__ __forceinline__ int packed_row(int row, int mode, int offset) {
+  if (mode == PACK_GATE) return 16 * (row >> 3) + (row & 7);
+  if (mode == PACK_UP) return 16 * (row >> 3) + 8 + (row & 7);
+  return row + offset;
+}
+__device__ __forceinline__ size_t packed_index(int P, int col, int KT) {
+  const size_t tile = (size_t)(P >> 4) * KT + (col >> 5);
+  const int lane = (P & 15) + 16 * ((col & 31) >> 3);
+  return tile * TILE_ELEMS + lane * 8 + (col & 7);
 }
 
 __global__ void synth_packed_kernel(uint16_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale,
-                                    int stride, int offset) {
+                                    int mode, int offset) {
   const int KT = K / TILE_K;
   const size_t total = (size_t)N * K;
-  for (size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x; p < total; p += (size_t)gridDim.x * blockDim.x) {
-    int row, col;
-    size_t tile;
-    packed_coords(p, KT, row, col, tile);
-    size_t nt = tile / KT, kt = tile % KT;
-    size_t dtile = (nt * stride + offset) * KT + kt;
-    float v = synth_value(seed, tid, (uint64_t)row * K + col, scale);
-    dst[dtile * TILE_ELEMS + (p % TILE_ELEMS)] = (uint16_t)f2bf(v);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int row = (int)(i / K), col = (int)(i % K);
+    dst[packed_index(packed_row(row, mode, offset), col, KT)] = (uint16_t)f2bf(synth_value(seed, tid, i, scale));
   }
 }
 
-__global__ void pack_kernel(uint16_t* dst, const uint16_t* src, int N, int K, int stride, int offset) {
+__global__ void pack_kernel(uint16_t* dst, const uint16_t* src, int N, int K, int mode, int offset) {
   const int KT = K / TILE_K;
   const size_t total = (size_t)N * K;
-  for (size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x; p < total; p += (size_t)gridDim.x * blockDim.x) {
-    int row, col;
-    size_t tile;
-    packed_coords(p, KT, row, col, tile);
-    size_t nt = tile / KT, kt = tile % KT;
-    size_t dtile = (nt * stride + offset) * KT + kt;
-    dst[dtile * TILE_ELEMS + (p % TILE_ELEMS)] = src[(size_t)row * K + col];
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int row = (int)(i / K), col = (int)(i % K);
+    dst[packed_index(packed_row(row, mode, offset), col, KT)] = src[i];
   }
 }
 
@@ -106,12 +102,12 @@ static int fill_grid(size_t n) {
   return (int)(g > 8192 ? 8192 : (g == 0 ? 1 : g));
 }
 
-void launch_synth_packed(uint16_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, int stride,
+void launch_synth_packed(uint16_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, int mode,
                          int offset, hipStream_t s) {
-  synth_packed_kernel<<<fill_grid((size_t)N * K), 256, 0, s>>>(dst, N, K, seed, tid, scale, stride, offset);
+  synth_packed_kernel<<<fill_grid((size_t)N * K), 256, 0, s>>>(dst, N, K, seed, tid, scale, mode, offset);
 }
-void launch_pack(uint16_t* dst, const uint16_t* src, int N, int K, int stride, int offset, hipStream_t s) {
-  pack_kernel<<<fill_grid((size_t)N * K), 256, 0, s>>>(dst, src, N, K, stride, offset);
+void launch_pack(uint16_t* dst, const uint16_t* src, int N, int K, int mode, int offset, hipStream_t s) {
+  pack_kernel<<<fill_grid((size_t)N * K), 256, 0, s>>>(dst, src, N, K, mode, offset);
 }
 void launch_synth_rowmajor(uint16_t* dst, size_t n, uint64_t seed, uint64_t tid, float scale, hipStream_t s) {
   synth_rowmajor_kernel<<<fill_grid(n), 256, 0, s>>>(dst, n, seed, tid, scale);
@@ -191,10 +187,63 @@ void launch_rmsnorm(uint16_t* y, int ldy, const float* x, const float* w, const 
 //
 // Work-group = KS waves = RT row tiles (16 rows each) x all K; wave w owns the
 // K-tiles [KT*w/KS, KT*(w+1)/KS).  Per K-tile a wave issues RT weight loads
-// (1 KiB each, contiguous, non-temporal) and NB activation loads (L2 hits),
-// and RT*NB MFMAs.  A ring of U K-tiles per wave keeps U*(RT+NB) loads in flight.
+// (1 KiB each, contiguous, non-temporal) and NB activation fragments, and
+// RT*NB MFMAs.  A ring of U K-tiles per wave keeps U*RT weight loads in flight.
+//
+// XN (fused RMS_NORM, M <= 8 rows): the activation operand is not read from a
+// bf16 buffer; the work-group normalises x (f32, residual stream) itself into
+// an LDS image  bf16((x*scale)*w)  -- the exact value the unfused rmsnorm
+// kernel writes -- while its first U weight tiles are already in flight, and
+// reads the B fragments from LDS.  That removes one launch + one HBM round trip
+// per norm at batch sizes where a launch costs as much as the norm.
 // ---------------------------------------------------------------------------
-template <int KS, int RT, int NB, int EPI, int U>
+template <int KS>
+__device__ __forceinline__ void xn_prologue(const MMArgs& a, uint16_t* xs, int pitch, double* red) {
+  // red: [KS][8] doubles
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double acc[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) acc[c] = 0.0;
+  for (int k = tid * 4; k < a.K; k += 64 * KS * 4) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      if (c < a.M) {
+        f32x4 v = *reinterpret_cast<const f32x4*>(a.xf + (size_t)c * a.K + k);
+        acc[c] += (double)(v[0] * v[0]);
+        acc[c] += (double)(v[1] * v[1]);
+        acc[c] += (double)(v[2] * v[2]);
+        acc[c] += (double)(v[3] * v[3]);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    if (c < a.M) {
+      double v = acc[c];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if (lane == 0) red[w * 8 + c] = v;
+    }
+  }
+  __syncthreads();
+  for (int c = 0; c < a.M; ++c) {
+    double sum = 0.0;
+#pragma unroll
+    for (int ww = 0; ww < KS; ++ww) sum += red[ww * 8 + c];
+    const float mean = (float)(sum / a.K);
+    const float scale = 1.0f / sqrtf(mean + a.eps);
+    for (int k = tid * 4; k < a.K; k += 64 * KS * 4) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(a.xf + (size_t)c * a.K + k);
+      f32x4 g = *reinterpret_cast<const f32x4*>(a.norm_w + k);
+      u32x2 o;
+      o[0] = f2bf((v[0] * scale) * g[0]) | (f2bf((v[1] * scale) * g[1]) << 16);
+      o[1] = f2bf((v[2] * scale) * g[2]) | (f2bf((v[3] * scale) * g[3]) << 16);
+      *reinterpret_cast<u32x2*>(xs + (size_t)c * pitch + k) = o;
+    }
+  }
+  __syncthreads();
+}
+
+template <int KS, int RT, int NB, int EPI, int U, bool XN>
 __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -202,16 +251,24 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
   const int tile0 = blockIdx.x * RT;
   const int kb = (KT * w) / KS, ke = (KT * (w + 1)) / KS;
 
+  __shared__ f32x4 red[KS][RT][NB][64];
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs_dyn[];
+  const int pitch = a.K + 8;  // bf16 elements per LDS activation row (+16 B: rows land on different banks)
+
   const u32x4* Wp[RT];
 #pragma unroll
   for (int r = 0; r < RT; ++r)
     Wp[r] = reinterpret_cast<const u32x4*>(a.W) + (size_t)(tile0 + r) * KT * 64 + lane;
+  // B fragment source (lane -> token column, k offset); padded columns re-read a valid row (outputs dropped)
   const u32x4* Xp[NB];
 #pragma unroll
   for (int n = 0; n < NB; ++n) {
     int col = n * 16 + (lane & 15);
-    col = col < a.M ? col : a.M - 1;  // padded columns re-read a valid row; their outputs are dropped
-    Xp[n] = reinterpret_cast<const u32x4*>(a.X + (size_t)col * a.ldx + (lane >> 4) * 8);
+    col = col < a.M ? col : a.M - 1;
+    if constexpr (XN)
+      Xp[n] = reinterpret_cast<const u32x4*>(xs_dyn + (size_t)col * pitch + (lane >> 4) * 8);
+    else
+      Xp[n] = reinterpret_cast<const u32x4*>(a.X + (size_t)col * a.ldx + (lane >> 4) * 8);
   }
 
   f32x4 acc[RT][NB];
@@ -220,43 +277,46 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
 #pragma unroll
     for (int n = 0; n < NB; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  u32x4 ra[U][RT], rb[U][NB];
+  auto mma = [&](const u32x4 (&wa)[RT], const u32x4 (&xb)[NB]) {
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int n = 0; n < NB; ++n)
+        acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wa[r]),
+                                                             __builtin_bit_cast(bf16x8, xb[n]), acc[r][n], 0, 0, 0);
+  };
+
+  u32x4 ra[U][RT];
   int kt = kb;
   const int nfull = (ke - kb) / U;
   if (nfull > 0) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int r = 0; r < RT; ++r) ra[u][r] = __builtin_nontemporal_load(Wp[r] + (size_t)(kt + u) * 64);
-#pragma unroll
-      for (int n = 0; n < NB; ++n) rb[u][n] = Xp[n][(kt + u) * 4];
-    }
+  }
+  if constexpr (XN) xn_prologue<KS>(a, xs_dyn, pitch, reinterpret_cast<double*>(&red[0][0][0][0]));
+
+  if (nfull > 0) {
     for (int ch = 1; ch < nfull; ++ch) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
+        u32x4 xb[NB];
 #pragma unroll
-        for (int r = 0; r < RT; ++r)
-#pragma unroll
-          for (int n = 0; n < NB; ++n)
-            acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ra[u][r]),
-                                                                 __builtin_bit_cast(bf16x8, rb[u][n]), acc[r][n],
-                                                                 0, 0, 0);
+        for (int n = 0; n < NB; ++n) xb[n] = Xp[n][(kt + u) * 4];
+        mma(ra[u], xb);
 #pragma unroll
         for (int r = 0; r < RT; ++r) ra[u][r] = __builtin_nontemporal_load(Wp[r] + (size_t)(kt + U + u) * 64);
-#pragma unroll
-        for (int n = 0; n < NB; ++n) rb[u][n] = Xp[n][(kt + U + u) * 4];
       }
       kt += U;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
+      u32x4 xb[NB];
 #pragma unroll
-      for (int r = 0; r < RT; ++r)
-#pragma unroll
-        for (int n = 0; n < NB; ++n)
-          acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ra[u][r]),
-                                                               __builtin_bit_cast(bf16x8, rb[u][n]), acc[r][n], 0,
-                                                               0, 0);
+      for (int n = 0; n < NB; ++n) xb[n] = Xp[n][(kt + u) * 4];
+      mma(ra[u], xb);
+    }
     kt += U;
   }
   for (; kt < ke; ++kt) {
@@ -265,16 +325,11 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
     for (int r = 0; r < RT; ++r) sa[r] = __builtin_nontemporal_load(Wp[r] + (size_t)kt * 64);
 #pragma unroll
     for (int n = 0; n < NB; ++n) sb[n] = Xp[n][kt * 4];
-#pragma unroll
-    for (int r = 0; r < RT; ++r)
-#pragma unroll
-      for (int n = 0; n < NB; ++n)
-        acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[r]),
-                                                             __builtin_bit_cast(bf16x8, sb[n]), acc[r][n], 0, 0, 0);
+    mma(sa, sb);
   }
 
   // ---- sum the KS partial tiles through LDS
-  __shared__ f32x4 red[KS][RT][NB][64];
+  if constexpr (XN) __syncthreads();  // red[] doubled as the prologue's scratch
 #pragma unroll
   for (int r = 0; r < RT; ++r)
 #pragma unroll
@@ -282,12 +337,13 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
   __syncthreads();
 
   // ---- epilogue.  unit = (r, n, lane): rows 16*(tile0+r) + 4*(lane>>4) + i, i<4; col n*16 + (lane&15)
-  constexpr int RU = (EPI == EPI_SWIGLU) ? 1 : RT;  // SWIGLU consumes the (gate, up) tile pair per unit
-  constexpr int UNITS = RU * NB * 64;
+  // SWIGLU tiles hold 8 gate rows (lanes 0-31 of the C layout) and the matching 8 up rows (lanes 32-63)
+  constexpr int LU = (EPI == EPI_SWIGLU) ? 32 : 64;
+  constexpr int UNITS = RT * NB * LU;
   for (int u = threadIdx.x; u < UNITS; u += 64 * KS) {
-    const int l = u & 63;
-    const int n = (u >> 6) % NB;
-    const int r = (u >> 6) / NB;
+    const int l = u % LU;
+    const int n = (u / LU) % NB;
+    const int r = (u / LU) / NB;
     const int col = n * 16 + (l & 15);
     if (col >= a.M) continue;
     f32x4 s = red[0][r][n][l];
@@ -302,10 +358,10 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
       f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + row);
       *px = *px + s;
     } else if constexpr (EPI == EPI_SWIGLU) {
-      f32x4 up = red[0][1][n][l];
+      f32x4 up = red[0][r][n][l + 32];
 #pragma unroll
-      for (int ww = 1; ww < KS; ++ww) up += red[ww][1][n][l];
-      const int row = blockIdx.x * 16 + (l >> 4) * 4;  // gate/up tile pair index == blockIdx.x
+      for (int ww = 1; ww < KS; ++ww) up += red[ww][r][n][l + 32];
+      const int row = (tile0 + r) * 8 + (l >> 4) * 4;  // ffn row of gate lane l / up lane l+32
       uint32_t h[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -322,6 +378,7 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
       const int d = a.head_dim;
       const int pos = a.pos[col];
       if (pos < 0 || pos >= a.n_ctx) continue;  // never write outside the slot's KV rows
+      _Float16* kvbase = nullptr;
       if (row < a.n_q + a.n_kv) {
         // ROPE_EXT mode NORM: rotate adjacent pairs (2i, 2i+1) of each head
         const bool is_q = row < a.n_q;
@@ -338,188 +395,237 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
           *reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + row) = o;
         } else {
           const int kvh = rl / d;
-          _Float16* dst = a.kc + (size_t)a.slot[col] * a.slot_stride + ((size_t)kvh * a.n_ctx + pos) * d + dd;
-          *reinterpret_cast<f16x4*>(dst) = f16x4{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
+          kvbase = a.kc + (size_t)a.slot[col] * a.slot_stride + ((size_t)kvh * a.ctx_stride + pos) * d + dd;
+          *reinterpret_cast<f16x4*>(kvbase) = f16x4{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
         }
       } else {
+        // V stored transposed ([d][pos]) so attention's P.V operand is a contiguous 16 B load
         const int rl = row - a.n_q - a.n_kv;
         const int kvh = rl / d, dd = rl % d;
-        _Float16* dst = a.vc + (size_t)a.slot[col] * a.slot_stride + ((size_t)kvh * a.n_ctx + pos) * d + dd;
-        *reinterpret_cast<f16x4*>(dst) = f16x4{(_Float16)s[0], (_Float16)s[1], (_Float16)s[2], (_Float16)s[3]};
+        _Float16* vt = a.vc + (size_t)a.slot[col] * a.slot_stride + ((size_t)kvh * d + dd) * a.ctx_stride + pos;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) vt[(size_t)i * a.ctx_stride] = (_Float16)s[i];
       }
     }
   }
 }
 
 template <int KS, int RT, int EPI, int U>
-static int launch_mm_nb(const MMArgs& a, hipStream_t s) {
+static int launch_mm_cfg(const MMArgs& a, hipStream_t s) {
   const int nb = (a.M + 15) / 16;
+  if ((a.N / TILE_N) % RT) return -1;
   const int grid = a.N / (16 * RT);
-  switch (nb) {
-    case 1: mm_kernel<KS, RT, 1, EPI, U><<<grid, 64 * KS, 0, s>>>(a); break;
-    case 2: mm_kernel<KS, RT, 2, EPI, U><<<grid, 64 * KS, 0, s>>>(a); break;
-    case 3:
-    case 4: mm_kernel<KS, RT, 4, EPI, U><<<grid, 64 * KS, 0, s>>>(a); break;
-    default: return -1;
+  if (a.X == nullptr) {  // fused RMS_NORM: activation image in LDS
+    const size_t lds = (size_t)a.M * (a.K + 8) * 2;
+    if (a.M > 8 || lds > (size_t)XN_LDS_BYTES || !a.xf || !a.norm_w) return -1;
+    mm_kernel<KS, RT, 1, EPI, U, true><<<grid, 64 * KS, lds, s>>>(a);
+    return 0;
+  }
+  if (nb == 1) {
+    mm_kernel<KS, RT, 1, EPI, U, false><<<grid, 64 * KS, 0, s>>>(a);
+  } else if (nb == 2) {
+    if constexpr (KS * RT <= 32) mm_kernel<KS, RT, 2, EPI, U, false><<<grid, 64 * KS, 0, s>>>(a);
+    else return -1;
+  } else {
+    if constexpr (KS * RT <= 16) mm_kernel<KS, RT, 4, EPI, U, false><<<grid, 64 * KS, 0, s>>>(a);
+    else return -1;
   }
   return 0;
 }
 
+// Work-group geometry per (epilogue, token-column tiles), from tools/gemv_sweep.hip on MI355X
+// (Llama-3-8B shapes; profiles/).  One column tile (<= 16 tokens): 16 waves split K, 4-deep
+// ring.  Two or four tiles: several row tiles per wave so each activation fragment loaded
+// from L2 feeds RT MFMAs (the activation stream otherwise exceeds the weight stream).
 int launch_mm(int epi, const MMArgs& a, hipStream_t s) {
   if (a.M < 1 || a.M > MAX_ROWS || a.K % TILE_K != 0 || a.N % TILE_N != 0) return -1;
-  switch (epi) {
-    case EPI_F32: return launch_mm_nb<4, 1, EPI_F32, 8>(a, s);
-    case EPI_RESID: return launch_mm_nb<8, 1, EPI_RESID, 8>(a, s);
-    case EPI_QKV: return launch_mm_nb<4, 1, EPI_QKV, 8>(a, s);
+  const int ntiles = a.N / TILE_N;
+  const int nb = (a.M + 15) / 16;
+  if (nb == 1 || a.X == nullptr) {
+    switch (epi) {
+      case EPI_F32: return launch_mm_cfg<16, 1, EPI_F32, 4>(a, s);
+      case EPI_RESID: return launch_mm_cfg<16, 1, EPI_RESID, 4>(a, s);
+      case EPI_QKV: return launch_mm_cfg<16, 1, EPI_QKV, 4>(a, s);
+      case EPI_SWIGLU: return launch_mm_cfg<16, 1, EPI_SWIGLU, 4>(a, s);
+    }
+    return -1;
+  }
+  if (nb == 2) {
+    switch (epi) {
+      case EPI_F32:
+        return ntiles % 4 == 0 ? launch_mm_cfg<8, 4, EPI_F32, 4>(a, s) : launch_mm_cfg<8, 1, EPI_F32, 8>(a, s);
+      case EPI_RESID: return launch_mm_cfg<4, 1, EPI_RESID, 8>(a, s);
+      case EPI_QKV:
+        return ntiles % 2 == 0 ? launch_mm_cfg<8, 2, EPI_QKV, 8>(a, s) : launch_mm_cfg<8, 1, EPI_QKV, 8>(a, s);
+      case EPI_SWIGLU:
+        return ntiles % 4 == 0 ? launch_mm_cfg<4, 4, EPI_SWIGLU, 4>(a, s) : launch_mm_cfg<4, 1, EPI_SWIGLU, 8>(a, s);
+    }
+    return -1;
+  }
+  switch (epi) {  // 3-4 column tiles (prefill chunks)
+    case EPI_F32:
+      return ntiles % 2 == 0 ? launch_mm_cfg<4, 2, EPI_F32, 4>(a, s) : launch_mm_cfg<4, 1, EPI_F32, 4>(a, s);
+    case EPI_RESID: return launch_mm_cfg<4, 1, EPI_RESID, 8>(a, s);
+    case EPI_QKV:
+      return ntiles % 2 == 0 ? launch_mm_cfg<4, 2, EPI_QKV, 4>(a, s) : launch_mm_cfg<4, 1, EPI_QKV, 4>(a, s);
     case EPI_SWIGLU:
-      if (a.N % 32 != 0) return -1;
-      return launch_mm_nb<4, 2, EPI_SWIGLU, 4>(a, s);
+      return ntiles % 2 == 0 ? launch_mm_cfg<4, 2, EPI_SWIGLU, 4>(a, s) : launch_mm_cfg<4, 1, EPI_SWIGLU, 4>(a, s);
   }
   return -1;
 }
 
+bool mm_can_fuse_norm(int M, int K) { return M <= 8 && (size_t)M * (K + 8) * 2 <= (size_t)XN_LDS_BYTES; }
+
 // ---------------------------------------------------------------------------
 // Attention for one query token per row (decode, and prefill rows alike):
 // KQ = f16(q).K -> SOFT_MAX_EXT(scale, causal) -> f16(P).V   
-// Split over ATTN_CHUNK-position chunks (flash-decoding); each work-group does
-// one (chunk, kv head, row) for all G query heads of the group (GQA), writing
-// an unnormalised partial (m, l, O); attn_combine merges the chunks.
+//
+// One work-group (8 waves) per (kv head, row); the G query heads of the GQA
+// group are the rows of v_mfma_f32_16x16x32_f16 tiles, so q, K, P and V enter
+// the matrix cores as f16 -- the same roundings ggml's f16 dot products apply.
+// Wave w walks 32-position chunks w, w+8, ... with an online softmax; the 8
+// partial (m, l, O) are merged through LDS and the normalised output is
+// written as bf16 (the rounding ggml applies before attn_output).  K is stored
+// [pos][d] (B operand of QK^T = contiguous 16 B per lane) and V transposed
+// [d][pos] (B operand of P.V = contiguous 16 B per lane).
 // ---------------------------------------------------------------------------
 template <int D, int G>
-__global__ __launch_bounds__(256) void attn_chunk_kernel(AttnArgs a) {
+__global__ __launch_bounds__(512) void attn_decode_kernel(AttnArgs a) {
   constexpr int CH = ATTN_CHUNK;
-  constexpr int DQ = D / 4;  // dims per lane-quarter in the score phase
-  const int chunk = blockIdx.x, kvh = blockIdx.y, c = blockIdx.z;
+  constexpr int QK = D / 32;  // k-steps of QK^T
+  constexpr int DT = D / 16;  // d tiles of P.V
+  constexpr int NW = 8;
+  const int kvh = blockIdx.x, c = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r16 = lane & 15, q4 = lane >> 4;
   const int pos = a.pos[c];
   const int ctx = min(pos + 1, a.n_ctx);
-  const int p0 = chunk * CH;
-  if (p0 >= ctx) return;
-  const int np = min(CH, ctx - p0);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int slot = a.slot[c];
 
-  __shared__ float qs[G][4 * (DQ + 1)];  // padded per quarter: conflict-free broadcast reads
-  __shared__ float S[G][CH];
-  constexpr int DP = D / 2;
-  constexpr int NG = 256 / DP;
-  __shared__ float red[NG * G * D];
+  __shared__ __attribute__((aligned(16))) _Float16 Ps[NW][16][CH + 8];
+  __shared__ float Om[NW][G][D];
+  __shared__ float Mm[NW][G], Ll[NW][G];
 
-  const int ldq = a.n_head * D;
-  for (int i = tid; i < G * D; i += 256) {
-    const int g = i / D, dd = i % D;
-    qs[g][(dd / DQ) * (DQ + 1) + dd % DQ] = round_f16(a.q[(size_t)c * ldq + (kvh * G + g) * D + dd]);
+  // A operand of QK^T: rows = heads of the group (rows >= G are zero)
+  f16x8 qa[QK];
+  const float* qrow = a.q + (size_t)c * a.n_head * D + (size_t)(kvh * G + (r16 < G ? r16 : 0)) * D;
+#pragma unroll
+  for (int kk = 0; kk < QK; ++kk) {
+    f32x4 v0 = *reinterpret_cast<const f32x4*>(qrow + kk * 32 + 8 * q4);
+    f32x4 v1 = *reinterpret_cast<const f32x4*>(qrow + kk * 32 + 8 * q4 + 4);
+    const bool live = r16 < G;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      qa[kk][j] = live ? (_Float16)v0[j] : (_Float16)0.f;
+      qa[kk][4 + j] = live ? (_Float16)v1[j] : (_Float16)0.f;
+    }
   }
-  __syncthreads();
 
-  const _Float16* Kb = a.kc + (size_t)slot * a.slot_stride + (size_t)kvh * a.n_ctx * D;
-  const _Float16* Vb = a.vc + (size_t)slot * a.slot_stride + (size_t)kvh * a.n_ctx * D;
+  const _Float16* Kb = a.kc + (size_t)slot * a.slot_stride + (size_t)kvh * a.ctx_stride * D;
+  const _Float16* Vb = a.vc + (size_t)slot * a.slot_stride + (size_t)kvh * D * a.ctx_stride;
 
-  {  // scores: wave w -> positions [16w, 16w+16); 4 lanes per position
-    const int pl = w * 16 + (lane >> 2);
-    const int part = lane & 3;
-    float accg[G];
+  float m_i[4], l_i[4];
 #pragma unroll
-    for (int g = 0; g < G; ++g) accg[g] = 0.f;
-    if (pl < np) {
-      const f16x8* kr = reinterpret_cast<const f16x8*>(Kb + (size_t)(p0 + pl) * D + part * DQ);
+  for (int i = 0; i < 4; ++i) {
+    m_i[i] = -INFINITY;
+    l_i[i] = 0.f;
+  }
+  f32x4 o[DT];
 #pragma unroll
-      for (int v = 0; v < DQ / 8; ++v) {
-        f16x8 kv = kr[v];
+  for (int t = 0; t < DT; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int ch = w; ch * CH < ctx; ch += NW) {
+    const int p0 = ch * CH;
+    // S[head][pos] for two 16-position tiles
+    f32x4 s[2];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float kf = (float)kv[j];
+    for (int t = 0; t < 2; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const _Float16* kr = Kb + (size_t)(p0 + 16 * t + r16) * D + 8 * q4;
 #pragma unroll
-          for (int g = 0; g < G; ++g) accg[g] += qs[g][part * (DQ + 1) + v * 8 + j] * kf;
-        }
+      for (int kk = 0; kk < QK; ++kk) {
+        f16x8 kb = *reinterpret_cast<const f16x8*>(kr + kk * 32);
+        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qa[kk], kb, s[t], 0, 0, 0);
       }
     }
+    // online softmax: C layout rows = heads 4*q4+i, cols = positions (lane r16)
+    float e[2][4];
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      accg[g] += __shfl_xor(accg[g], 1);
-      accg[g] += __shfl_xor(accg[g], 2);
-    }
-    if (part == 0) {
+    for (int i = 0; i < 4; ++i) {
+      float v0 = (p0 + r16 < ctx) ? s[0][i] * a.scale : -INFINITY;
+      float v1 = (p0 + 16 + r16 < ctx) ? s[1][i] * a.scale : -INFINITY;
+      float mx = fmaxf(v0, v1);
 #pragma unroll
-      for (int g = 0; g < G; ++g) S[g][pl] = (pl < np) ? accg[g] * a.scale : -INFINITY;
+      for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+      const float m_new = fmaxf(m_i[i], mx);
+      const float alpha = expf(m_i[i] - m_new);  // 0 on the first chunk (m_i = -inf)
+      e[0][i] = expf(v0 - m_new);
+      e[1][i] = expf(v1 - m_new);
+      float ls = e[0][i] + e[1][i];
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) ls += __shfl_xor(ls, off);
+      l_i[i] = l_i[i] * alpha + ls;
+      m_i[i] = m_new;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) o[t][i] *= alpha;
     }
+    // P (f16) -> LDS as [head][pos], re-read as the A operand of P.V
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Ps[w][4 * q4 + i][16 * t + r16] = (4 * q4 + i < G) ? (_Float16)e[t][i] : (_Float16)0.f;
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+    const f16x8 pa = *reinterpret_cast<const f16x8*>(&Ps[w][r16][8 * q4]);
+    const int pb = p0 + 8 * q4;  // first position of this lane's B fragment
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      f16x8 vb = *reinterpret_cast<const f16x8*>(Vb + (size_t)(t * 16 + r16) * a.ctx_stride + pb);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vb[j] = (pb + j < ctx) ? vb[j] : (_Float16)0.f;
+      o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa, vb, o[t], 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();  // Ps[w] is rewritten next chunk only after every lane read it
   }
-  __syncthreads();
 
-  // chunk-local softmax: one wave per head, one lane per position
-  for (int g = w; g < G; g += 4) {
-    const float sv = S[g][lane];
-    float m = sv;
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    const float e = (lane < np) ? expf(sv - m) : 0.f;
-    float l = e;
-    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o);
-    S[g][lane] = round_f16(e);  // ggml rounds probabilities to f16 for the f16 V product
-    if (lane == 0) {
-      float* ml = a.ml_part + (((size_t)c * a.n_head + kvh * G + g) * a.n_chunks + chunk) * 2;
-      ml[0] = m;
-      ml[1] = l;
-    }
-  }
-  __syncthreads();
-
-  {  // O = P.V ; thread -> (dim pair dp, position group pg)
-    const int dp = tid % DP, pg = tid / DP;
-    float o0[G], o1[G];
+  // merge the NW wave partials
 #pragma unroll
-    for (int g = 0; g < G; ++g) o0[g] = o1[g] = 0.f;
-    for (int pl = pg; pl < np; pl += NG) {
-      const f16x2 v = *reinterpret_cast<const f16x2*>(Vb + (size_t)(p0 + pl) * D + 2 * dp);
-      const float v0 = (float)v[0], v1 = (float)v[1];
+  for (int i = 0; i < 4; ++i) {
+    const int h = 4 * q4 + i;
+    if (h < G) {
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const float p = S[g][pl];
-        o0[g] += p * v0;
-        o1[g] += p * v1;
+      for (int t = 0; t < DT; ++t) Om[w][h][t * 16 + r16] = o[t][i];
+      if (r16 == 0) {
+        Mm[w][h] = m_i[i];
+        Ll[w][h] = l_i[i];
       }
     }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      red[(pg * G + g) * D + 2 * dp] = o0[g];
-      red[(pg * G + g) * D + 2 * dp + 1] = o1[g];
-    }
   }
   __syncthreads();
-  for (int i = tid; i < G * D; i += 256) {
-    const int g = i / D, dd = i % D;
-    float sacc = 0.f;
+  for (int idx = threadIdx.x; idx < G * D; idx += 64 * NW) {
+    const int h = idx / D, d = idx % D;
+    float M = -INFINITY;
 #pragma unroll
-    for (int pg = 0; pg < NG; ++pg) sacc += red[(pg * G + g) * D + dd];
-    a.o_part[(((size_t)c * a.n_head + kvh * G + g) * a.n_chunks + chunk) * D + dd] = sacc;
-  }
-}
-
-// merge chunk partials: O = sum_i e^(m_i-M) O_i / sum_i e^(m_i-M) l_i  -> bf16 (src1 of attn_output)
-__global__ void attn_combine_kernel(AttnArgs a) {
-  const int h = blockIdx.x, c = blockIdx.y;
-  const int D = a.head_dim;
-  const int nch = (min(a.pos[c] + 1, a.n_ctx) + ATTN_CHUNK - 1) / ATTN_CHUNK;
-  const float* ml = a.ml_part + ((size_t)c * a.n_head + h) * a.n_chunks * 2;
-  float M = -INFINITY;
-  for (int i = 0; i < nch; ++i) M = fmaxf(M, ml[2 * i]);
-  float L = 0.f;
-  for (int i = 0; i < nch; ++i) L += expf(ml[2 * i] - M) * ml[2 * i + 1];
-  const float inv = 1.0f / L;
-  const float* op = a.o_part + ((size_t)c * a.n_head + h) * a.n_chunks * D;
-  for (int dd = threadIdx.x; dd < D; dd += blockDim.x) {
-    float o = 0.f;
-    for (int i = 0; i < nch; ++i) o += expf(ml[2 * i] - M) * op[(size_t)i * D + dd];
-    a.out[(size_t)c * a.ldo + h * D + dd] = (uint16_t)f2bf(o * inv);
+    for (int ww = 0; ww < NW; ++ww) M = fmaxf(M, Mm[ww][h]);
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) {
+      const float f = (Mm[ww][h] == -INFINITY) ? 0.f : expf(Mm[ww][h] - M);
+      L += f * Ll[ww][h];
+      acc += f * Om[ww][h][d];
+    }
+    a.out[(size_t)c * a.ldo + (kvh * G + h) * D + d] = (uint16_t)f2bf(acc / L);
   }
 }
 
 template <int D>
 static void launch_attn_d(const AttnArgs& a, hipStream_t s) {
-  dim3 grid(a.n_chunks, a.n_head_kv, a.M);
+  dim3 grid(a.n_head_kv, a.M);
   switch (a.n_head / a.n_head_kv) {
-    case 1: attn_chunk_kernel<D, 1><<<grid, 256, 0, s>>>(a); break;
-    case 2: attn_chunk_kernel<D, 2><<<grid, 256, 0, s>>>(a); break;
-    case 4: attn_chunk_kernel<D, 4><<<grid, 256, 0, s>>>(a); break;
-    case 8: attn_chunk_kernel<D, 8><<<grid, 256, 0, s>>>(a); break;
+    case 1: attn_decode_kernel<D, 1><<<grid, 512, 0, s>>>(a); break;
+    case 2: attn_decode_kernel<D, 2><<<grid, 512, 0, s>>>(a); break;
+    case 4: attn_decode_kernel<D, 4><<<grid, 512, 0, s>>>(a); break;
+    case 8: attn_decode_kernel<D, 8><<<grid, 512, 0, s>>>(a); break;
   }
 }
 
@@ -528,7 +634,6 @@ void launch_attention(const AttnArgs& a, hipStream_t s) {
     launch_attn_d<64>(a, s);
   else
     launch_attn_d<128>(a, s);
-  attn_combine_kernel<<<dim3(a.n_head, a.M), 64, 0, s>>>(a);
 }
 
 // ---------------------------------------------------------------------------

@@ -1,0 +1,106 @@
+"""The CPU oracle against the golden vectors (CPU-only).
+
+Pinning: llama.cpp (the reference's arithmetic) is absent, so the oracle is
+checked against transformers' LlamaForCausalLM run over the same bf16 weights
+(tests/golden/hf_*.npz, made by tests/golden/make_golden.py):
+  * ORC_EXACT mode (fp32 math)      must match HF to 5e-5 of the logit scale;
+  * ggml mode (bf16/f16 roundings)  must match within the bf16 tolerance.
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_logits_close
+
+SHAPES = ["test-tiny", "test-gqa8", "test-d128"]
+
+
+def _golden(name):
+    import os
+
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", f"hf_{name}.npz"))
+
+
+@pytest.mark.parametrize("name", SHAPES)
+def test_oracle_exact_matches_transformers(oracle_mod, name):
+    from llama_p2p_amd import synth
+
+    g = _golden(name)
+    m = oracle_mod.OracleModel(synth.SHAPES[name], seed=int(g["seed"]), exact=True)
+    got = m.context(64).eval(g["ids"], 0, all_logits=True)
+    ref = g["logits"]
+    assert np.abs(got - ref).max() < 5e-5 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("name", SHAPES)
+def test_oracle_ggml_mode_within_bf16_tolerance(oracle_mod, name):
+    from llama_p2p_amd import synth
+
+    g = _golden(name)
+    m = oracle_mod.OracleModel(synth.SHAPES[name], seed=int(g["seed"]))
+    got = m.context(64).eval(g["ids"], 0, all_logits=True)
+    assert_logits_close(got, g["logits"], name)
+
+
+def test_oracle_incremental_equals_batched(oracle_mod):
+    """KV-cache path: token-by-token evaluation == one batched prefill (same ubatch semantics)."""
+    from llama_p2p_amd import synth
+
+    sh = synth.SHAPES["test-gqa8"]
+    g = _golden("test-gqa8")
+    m = oracle_mod.OracleModel(sh, seed=0)
+    full = m.context(64).eval(g["ids"][:12], 0, all_logits=True)
+    c = m.context(64)
+    inc = np.stack([c.eval(g["ids"][i:i + 1], i)[0] for i in range(12)])
+    assert np.abs(full - inc).max() < 1e-5
+
+
+def test_synthetic_weights_bit_identical_numpy_vs_c(oracle_mod):
+    from llama_p2p_amd import synth
+
+    L = oracle_mod.lib()
+    sc = float(synth._std_scale(0.02))
+    for tid in (1, 17, 12345):
+        idx = np.array([0, 1, 2, 1000, 2 ** 33 + 7, 2 ** 40 + 3], dtype=np.uint64)
+        ref = np.array([L.orc_synth_value(0, tid, int(i), sc) for i in idx], dtype=np.float32)
+        got = np.array([synth.synth_values(0, tid, int(i), 1, 0.02)[0] for i in idx], dtype=np.float32)
+        assert np.array_equal(ref.view(np.uint32), got.view(np.uint32))
+
+
+def test_synthetic_weight_statistics():
+    from llama_p2p_amd import synth
+
+    v = synth.synth_values(0, 3, 0, 1 << 20, 0.02)
+    assert abs(v.mean()) < 1e-4 and abs(v.std() - 0.02) < 2e-4
+    n = synth.synth_norm_f32(0, 2, 4096)
+    assert abs(n.mean() - 1.0) < 0.01
+
+
+def test_f16_rounding_matches_numpy(oracle_mod):
+    L = oracle_mod.lib()
+    rng = np.random.default_rng(0)
+    vals = np.concatenate([rng.normal(0, 1, 2000), rng.normal(0, 1e-5, 500), [65504.0, 65520.0, 1e-8, -0.0, 6.1e-5]])
+    for v in vals.astype(np.float32):
+        assert np.float32(L.orc_round_f16(float(v))) == np.float32(np.float16(v)), v
+
+
+def test_bf16_rounding_matches_spec(oracle_mod):
+    from llama_p2p_amd import synth
+
+    L = oracle_mod.lib()
+    rng = np.random.default_rng(1)
+    vals = rng.normal(0, 3, 1000).astype(np.float32)
+    ref = synth.bf16_bits_to_f32(synth.f32_to_bf16_bits(vals))
+    got = np.array([L.orc_round_bf16(float(v)) for v in vals], dtype=np.float32)
+    assert np.array_equal(ref, got)
+
+
+def test_greedy_tie_breaks_to_lowest_id(oracle_mod):
+    assert oracle_mod.argmax_lowest(np.array([0.0, 2.0, 1.0, 2.0], dtype=np.float32)) == 1
+
+
+def test_context_overflow_rejected(oracle_mod):
+    from llama_p2p_amd import synth
+
+    m = oracle_mod.OracleModel(synth.SHAPES["test-tiny"], seed=0)
+    with pytest.raises(ValueError):
+        m.context(8).eval(list(range(3, 12)), 0)
