@@ -83,12 +83,16 @@ def run_single(args):
     M = args.seqs
     eng = Engine(f"synthetic:{args.model}:seed=0", n_ctx=args.n_ctx, n_seq_max=max(M, 1))
     prompts = make_prompts(shape.n_vocab, M)
-    # prefill (untimed): chunked rows through the engine; first token = greedy
-    first = []
+    # prefill (untimed): all but the last prompt token of every sequence, 64 rows per
+    # forward; the first decode step then consumes the last prompt token
+    slots, pos, ids = [], [], []
     for i, p in enumerate(prompts):
-        lg = eng.forward_logits(p, 0, slot=i)
-        first.append(int(lg[-1].argmax()))
-    b = eng.batch(slots=list(range(M)), pos=[len(p) for p in prompts], ids=first,
+        slots += [i] * (len(p) - 1)
+        pos += list(range(len(p) - 1))
+        ids += [int(t) for t in p[:-1]]
+    for i in range(0, len(slots), 64):
+        eng.stage_rows(slots[i:i + 64], pos[i:i + 64], ids[i:i + 64])
+    b = eng.batch(slots=list(range(M)), pos=[len(p) - 1 for p in prompts], ids=[int(p[-1]) for p in prompts],
                   max_steps=args.warmup + args.steps)
     for _ in range(args.warmup):
         b.step()
@@ -115,7 +119,7 @@ def run_single(args):
                        "bytes_per_launch": int(kbytes)}
     # batch-1 decode (the north_star's 70% target), same engine
     if args.batch1_steps > 0:
-        b1 = eng.batch(slots=[M if M < eng.info.n_seq_max else 0], pos=[len(prompts[0])], ids=[first[0]],
+        b1 = eng.batch(slots=[0], pos=[len(prompts[0]) - 1 + args.warmup + args.steps], ids=[int(toks[0, -1])],
                        max_steps=args.batch1_steps + 4)
         for _ in range(4):
             b1.step()

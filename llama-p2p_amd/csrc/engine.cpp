@@ -108,6 +108,7 @@ struct mx_batch {
   int M = 0, max_steps = 0;
   int max_pos = 0;  // host mirror of the largest position, so steps never run past n_ctx
   int *d_ids = nullptr, *d_pos = nullptr, *d_slot = nullptr, *d_hist = nullptr, *d_hist_count = nullptr;
+  bool ids_external = false;
   std::map<GraphKey, hipGraphExec_t> graphs;
 };
 
@@ -886,6 +887,20 @@ int mx_batch_create(mx_engine* e, int M, const int32_t* slots, const int32_t* po
 
 int32_t* mx_batch_ids_device(mx_batch* b) { return b ? b->d_ids : nullptr; }
 
+int mx_batch_bind_ids(mx_engine* e, mx_batch* b, int32_t* ids_device) {
+  if (!e || !b || !ids_device) return fail(MX_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(e->gpu_mu);
+  hipSetDevice(e->device);
+  HIPC(hipDeviceSynchronize());
+  HIPC(hipMemcpy(ids_device, b->d_ids, b->M * 4, hipMemcpyDeviceToDevice));
+  if (!b->ids_external) hipFree(b->d_ids);
+  b->d_ids = ids_device;
+  b->ids_external = true;
+  for (auto& kv : b->graphs) hipGraphExecDestroy(kv.second);
+  b->graphs.clear();
+  return 0;
+}
+
 int mx_batch_step(mx_engine* e, mx_batch* b, const void* x_in, void* x_out, void* stream) {
   if (!e || !b) return fail(MX_ERR_ARG, "null argument");
   std::lock_guard<std::mutex> lk(e->gpu_mu);
@@ -947,7 +962,7 @@ void mx_batch_destroy(mx_engine* e, mx_batch* b) {
     hipDeviceSynchronize();
   }
   for (auto& kv : b->graphs) hipGraphExecDestroy(kv.second);
-  hipFree(b->d_ids);
+  if (!b->ids_external) hipFree(b->d_ids);
   hipFree(b->d_pos);
   hipFree(b->d_slot);
   hipFree(b->d_hist);

@@ -25,7 +25,7 @@ FINISH_LENGTH, FINISH_STOP, FINISH_ERROR = 0, 1, 2
 EXPORTS = [
     "mx_opts_default", "mx_sampling_default", "mx_last_error", "mx_engine_create", "mx_engine_destroy",
     "mx_engine_info", "mx_forward_logits", "mx_forward_rows", "mx_submit", "mx_wait", "mx_batch_create",
-    "mx_batch_step", "mx_batch_ids_device", "mx_batch_tokens", "mx_batch_destroy", "mx_stage_rows",
+    "mx_batch_step", "mx_batch_ids_device", "mx_batch_bind_ids", "mx_batch_tokens", "mx_batch_destroy", "mx_stage_rows",
     "mx_profile_kernel", "mx_sync",
 ]
 
@@ -88,6 +88,7 @@ def lib() -> ctypes.CDLL:
         L.mx_batch_ids_device.argtypes = [vp]
         L.mx_batch_ids_device.restype = vp
         L.mx_batch_tokens.argtypes = [vp, vp, vp, i32, P(i32)]
+        L.mx_batch_bind_ids.argtypes = [vp, vp, vp]
         L.mx_batch_destroy.argtypes = [vp, vp]
         L.mx_stage_rows.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp]
         L.mx_profile_kernel.argtypes = [vp, i32, i32, i32, P(ctypes.c_double), P(ctypes.c_double)]
@@ -205,6 +206,18 @@ class Engine:
             pass
 
 
+def torch_stream_handle() -> int:
+    """hipStream_t of torch's current stream.  The engine's C ABI reads a NULL stream as
+    "the engine's own stream", so the legacy default stream (handle 0) is refused: work
+    enqueued there would not be ordered with the engine's kernels."""
+    import torch
+
+    h = torch.cuda.current_stream().cuda_stream
+    if not h:
+        raise RuntimeError("run engine tensor calls inside `with torch.cuda.stream(s):` (a non-default stream)")
+    return h
+
+
 class Batch:
     def __init__(self, eng: Engine, slots, pos, ids, max_steps: int):
         self.eng = eng
@@ -223,6 +236,19 @@ class Batch:
 
     def step(self, x_in: int = 0, x_out: int = 0, stream: int = 0):
         _check(lib().mx_batch_step(self.eng._h, self._h, x_in or None, x_out or None, stream or None))
+
+    def bind_ids(self, ids_device_ptr: int):
+        _check(lib().mx_batch_bind_ids(self.eng._h, self._h, ids_device_ptr))
+
+    # tensor-level interface used by the pipeline driver (torch device tensors)
+    def step_tensors(self, x_in=None, x_out=None):
+        stream = torch_stream_handle()
+        self.step(x_in.data_ptr() if x_in is not None else 0, x_out.data_ptr() if x_out is not None else 0,
+                  stream)
+
+    def bind_ids_tensor(self, t):
+        self._ids_tensor = t  # keep alive
+        self.bind_ids(t.data_ptr())
 
     def tokens(self) -> np.ndarray:
         out = np.zeros((self.M, max(1, self.max_steps)), dtype=np.int32)

@@ -1,0 +1,283 @@
+"""Pipeline-parallel decode: the reference's peer mesh mapped onto one 8-GPU node.
+
+The reference scales by forwarding whole requests to peers that each hold the
+full model (/root/reference/llama_p2p_network.py:135-154).  On an MI355X node
+the peers are GPUs and the model is sharded instead (BASELINE.json north_star,
+SURVEY.md §8e): rank r holds a contiguous, byte-balanced range of layers
+(stage r), hidden states go stage -> stage with send/recv (RCCL over xGMI on
+GPUs, gloo in CPU tests), and the greedy token ids go from the last stage back
+to stage 0.  S micro-batches are in flight so every stage is busy: aggregate
+throughput ~ S x one stage's rate (weak scaling: per-GPU work is fixed).
+
+This module is transport- and executor-agnostic: ``Stage`` drives any engine
+object with the ``Engine``/``Batch`` tensor interface (engine.py), and tests
+drive it on CPU with gloo and a numpy stand-in executor.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from typing import List, Sequence, Tuple
+
+
+def partition_layers(n_layer: int, layer_cost: float, head_cost: float, n_stages: int,
+                     embed_cost: float = 0.0) -> List[Tuple[int, int]]:
+    """Contiguous layer ranges minimising the most expensive stage.
+
+    Stage 0 also carries the embedding, the last stage the output norm + lm_head
+    (1.05 GB for Llama-3-8B = 2.4 layers' worth of bytes), so stages are balanced
+    by streamed bytes, not by layer count.  Every stage gets at least one layer.
+    """
+    if n_stages < 1 or n_stages > n_layer:
+        raise ValueError(f"need 1 <= stages <= {n_layer}, got {n_stages}")
+
+    def cost(lb, le, s):
+        c = (le - lb) * layer_cost
+        if s == 0:
+            c += embed_cost
+        if s == n_stages - 1:
+            c += head_cost
+        return c
+
+    # DP over (stage, boundary): minimise the max stage cost, then the sum of squared
+    # costs (spread the slack instead of dumping it on one stage)
+    import functools
+
+    @functools.lru_cache(maxsize=None)
+    def best(s, lb):
+        """Best split of layers [lb, n_layer) over stages s..n_stages-1 -> (max, sumsq, bounds)."""
+        if s == n_stages - 1:
+            c = cost(lb, n_layer, s)
+            return (c, c * c, ((lb, n_layer),))
+        out = None
+        for le in range(lb + 1, n_layer - (n_stages - 1 - s) + 1):
+            c = cost(lb, le, s)
+            m, q, rest = best(s + 1, le)
+            cand = (max(c, m), c * c + q, ((lb, le),) + rest)
+            if out is None or (round(cand[0], 6), cand[1]) < (round(out[0], 6), out[1]):
+                out = cand
+        return out
+
+    return [tuple(b) for b in best(0, 0)[2]]
+
+
+class TorchComm:
+    """Point-to-point hand-offs over torch.distributed (nccl = RCCL on ROCm, or gloo)."""
+
+    def __init__(self, rank: int, world: int):
+        import torch.distributed as dist
+
+        self.dist, self.rank, self.world = dist, rank, world
+        self._pending = []
+
+    def send(self, t, dst: int):
+        w = self.dist.isend(t, dst)
+        self._pending.append(w)
+        return w
+
+    def recv(self, t, src: int):
+        self.dist.recv(t, src)
+
+    def drain(self):
+        for w in self._pending:
+            w.wait()
+        self._pending.clear()
+
+
+class Stage:
+    """One pipeline stage: S micro-batches of M sequences, greedy decode."""
+
+    def __init__(self, eng, comm, rank: int, world: int, n_embd: int, device, micro_batches: int):
+        import torch
+
+        self.eng, self.comm, self.rank, self.world = eng, comm, rank, world
+        self.first, self.last = rank == 0, rank == world - 1
+        self.S = micro_batches
+        self.n_embd = n_embd
+        self.device = device
+        self.torch = torch
+        self.batches = []
+        self.x_in, self.x_out, self.tok = [], [], []
+        self.pending_tokens = False  # stage 0 has not yet received the last step's tokens
+
+    # -- prefill (untimed): prompt rows through every stage, 64 rows per hand-off
+    def prefill(self, mb_rows: Sequence[Tuple[List[int], List[int], List[int]]], chunk: int = 64):
+        """mb_rows[mb] = (slots, positions, ids) of every prompt row of micro-batch mb."""
+        torch = self.torch
+        buf_in = torch.empty((chunk, self.n_embd), dtype=torch.float32, device=self.device)
+        buf_out = torch.empty((chunk, self.n_embd), dtype=torch.float32, device=self.device)
+        for slots, pos, ids in mb_rows:
+            for i in range(0, len(slots), chunk):
+                n = min(chunk, len(slots) - i)
+                xin = None
+                if not self.first:
+                    self.comm.recv(buf_in[:n], self.rank - 1)
+                    xin = buf_in[:n]
+                xout = None if self.last else buf_out[:n]
+                self.eng.stage_rows_tensors(slots[i:i + n], pos[i:i + n], ids[i:i + n] if self.first else None,
+                                            xin, xout)
+                if not self.last:
+                    self.comm.send(xout, self.rank + 1)
+                    self.comm.drain()  # buf_out is reused by the next chunk
+
+    def setup_decode(self, mb_state: Sequence[Tuple[List[int], List[int], List[int]]], max_steps: int):
+        """mb_state[mb] = (slots, positions of the next token, next token ids)."""
+        torch = self.torch
+        M = len(mb_state[0][0])
+        for slots, pos, ids in mb_state:
+            b = self.eng.batch(slots, pos, ids if self.first else None, max_steps=max_steps if self.last else 0)
+            t = torch.tensor(ids if self.first else [0] * M, dtype=torch.int32, device=self.device)
+            if self.first or self.last:
+                b.bind_ids_tensor(t)
+            self.batches.append(b)
+            self.tok.append(t)
+            self.x_in.append(torch.empty((M, self.n_embd), dtype=torch.float32, device=self.device))
+            self.x_out.append(torch.empty((M, self.n_embd), dtype=torch.float32, device=self.device))
+
+    def decode_steps(self, n_steps: int, step0: int = 0):
+        """n_steps greedy tokens for every micro-batch, micro-batches interleaved."""
+        for st in range(step0, step0 + n_steps):
+            for mb, b in enumerate(self.batches):
+                if self.world == 1:
+                    b.step_tensors()
+                    continue
+                if self.first:
+                    if self.pending_tokens:
+                        self.comm.recv(self.tok[mb], self.world - 1)  # tokens of the previous step
+                    b.step_tensors(None, self.x_out[mb])
+                    self.comm.send(self.x_out[mb], 1)
+                elif self.last:
+                    self.comm.recv(self.x_in[mb], self.rank - 1)
+                    b.step_tensors(self.x_in[mb], None)
+                    self.comm.send(self.tok[mb], 0)
+                else:
+                    self.comm.recv(self.x_in[mb], self.rank - 1)
+                    b.step_tensors(self.x_in[mb], self.x_out[mb])
+                    self.comm.send(self.x_out[mb], self.rank + 1)
+            self.pending_tokens = True
+            # isends of this step must finish before their buffers are refilled next step
+            if self.world > 1:
+                self.comm.drain()
+
+    def finish(self):
+        """Drain the ring: stage 0 receives the tokens of the final step.  Must run
+        before any device-wide synchronize, or the last stage's pending send of
+        those tokens would never complete."""
+        if self.world > 1 and self.first and self.pending_tokens:
+            for mb in range(len(self.batches)):
+                self.comm.recv(self.tok[mb], self.world - 1)
+        self.pending_tokens = False
+        if self.world > 1:
+            self.comm.drain()
+
+    def tokens(self):
+        return [b.tokens() for b in self.batches] if self.last else None
+
+
+def bench_main(args, metric: str, make_prompts):
+    """bench.py --gpus N under torch.distributed.run: one pipeline stage per rank."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from . import synth
+    from .engine import Engine
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    shape = synth.SHAPES[args.model]
+    layer_bytes = 2 * (2 * shape.n_embd ** 2 + 2 * shape.n_embd * shape.n_embd_kv + 3 * shape.n_embd * shape.n_ff)
+    head_bytes = 2 * shape.n_vocab * shape.n_embd
+    parts = partition_layers(shape.n_layer, layer_bytes, head_bytes, world, embed_cost=0)
+    lb, le = parts[rank]
+    S, M = world, args.seqs
+    eng = Engine(f"synthetic:{args.model}:seed=0", n_ctx=args.n_ctx, n_seq_max=S * M, layer_begin=lb,
+                 layer_end=le, device=local)
+    comm = TorchComm(rank, world)
+    work_stream = torch.cuda.Stream(device=local)  # engine kernels and RCCL hand-offs are ordered on it
+    torch.cuda.set_stream(work_stream)
+    stage = Stage(EngineAdapter(eng), comm, rank, world, shape.n_embd, torch.device("cuda", local), S)
+    prompts = make_prompts(shape.n_vocab, S * M)
+    mb_rows, mb_state = [], []
+    for mb in range(S):
+        slots, pos, ids, st = [], [], [], ([], [], [])
+        for i in range(M):
+            p = prompts[mb * M + i]
+            sl = mb * M + i
+            slots += [sl] * (len(p) - 1)
+            pos += list(range(len(p) - 1))
+            ids += [int(t) for t in p[:-1]]
+            st[0].append(sl)
+            st[1].append(len(p) - 1)
+            st[2].append(int(p[-1]))
+        mb_rows.append((slots, pos, ids))
+        mb_state.append(st)
+    stage.prefill(mb_rows)
+    stage.setup_decode(mb_state, max_steps=args.warmup + args.steps)
+    torch.cuda.synchronize()
+    dist.barrier()
+    stage.decode_steps(args.warmup, 0)
+    stage.finish()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    stage.decode_steps(args.steps, args.warmup)
+    stage.finish()
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=torch.device("cuda", local))
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dt = float(dt.item())
+    us, wbytes = eng.profile_kernel(2, M, iters=2)
+    kbytes = wbytes + M * shape.n_embd * 2 + M * shape.n_ff * 2
+    info = eng.info
+    wb = torch.tensor([float(info.weight_bytes)], dtype=torch.float64, device=torch.device("cuda", local))
+    dist.all_reduce(wb)
+    total_tokens = args.steps * S * M
+    if rank == 0:
+        ctx_sum = sum(len(p) + args.warmup + args.steps / 2 for p in prompts)
+        step_bytes = float(wb.item()) * S + (ctx_sum + S * M) * shape.kv_bytes_per_pos() + S * M * shape.n_vocab * 4
+        line = {
+            "metric": metric, "value": round(total_tokens / dt, 2), "unit": "tokens/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (seeded random bf16 weights of the exact shape; random prompt ids)",
+            "config": {"workload": f"{args.model} greedy decode, {world}-stage pipeline, {S} micro-batches x {M} "
+                                   f"sequences in flight, prompts U[16,256] (seed 2), n_ctx {args.n_ctx}",
+                       "model": args.model, "stages": world, "micro_batches": S, "seqs_per_micro_batch": M,
+                       "layer_ranges": parts, "parallelism": f"pp{world}"},
+            "step_hbm_gbs": round(step_bytes / dt * args.steps / 1e9, 1),
+            "step_hbm_frac": round(step_bytes / (dt / args.steps) / 1e9 / 8000.0 / world, 4),
+            "roofline": {"bound": "hbm", "achieved": round(kbytes / us / 1e3, 1), "peak": 8000.0, "unit": "GB/s",
+                         "frac": round(kbytes / us / 1e3 / 8000.0, 4), "traffic": None,
+                         "kernel": "mm_kernel<EPI_SWIGLU> (ffn_gate+ffn_up+SiLU*up), rank 0",
+                         "us_per_launch": round(us, 2), "bytes_per_launch": int(kbytes)},
+        }
+        print(json.dumps(line), flush=True)
+    for b in stage.batches:
+        b.close()
+    eng.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+class EngineAdapter:
+    """Tensor-level view of engine.Engine used by Stage (device tensors in, device tensors out)."""
+
+    def __init__(self, eng):
+        self.eng = eng
+
+    def stage_rows_tensors(self, slots, pos, ids, x_in, x_out):
+        from .engine import torch_stream_handle
+
+        stream = torch_stream_handle()
+        self.eng.stage_rows(slots, pos, ids, x_in.data_ptr() if x_in is not None else 0,
+                            x_out.data_ptr() if x_out is not None else 0, False, stream)
+
+    def batch(self, slots, pos, ids, max_steps):
+        return self.eng.batch(slots, pos, ids, max_steps=max_steps)

@@ -3,6 +3,7 @@
 # status=transient (the box failed while being prepared: nothing of the command ran,
 # nothing charged).  A command that ran and failed is never retried.
 #   tools/gpu.sh <timeout_s> '<command>'
+python3 llama-p2p_amd/build.py > /dev/null || { echo "[gpu.sh] build failed" >&2; exit 1; }
 T=${1:-600}
 shift
 for attempt in 1 2 3 4 5 6; do
