@@ -149,10 +149,11 @@ def main():
     ap.add_argument("--n-ctx", type=int, default=512)
     ap.add_argument("--batch1-steps", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-pipeline", action="store_true", help="run the torch.distributed pipeline path even at N=1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1 or args.gpus > 1:
+    if world > 1 or args.gpus > 1 or args.force_pipeline:
         from llama_p2p_amd import pipeline
 
         return pipeline.bench_main(args, METRIC, make_prompts)
