@@ -120,7 +120,12 @@ struct mx_engine {
   int bos = 1, eos = 2;
   int n_ctx = 512, n_seq_max = 64, lb = 0, le = 0, device = 0;
   bool has_embed = true, has_head = true, use_graphs = true;
-  bool fuse_norms = getenv("MX_NO_FUSED_NORM") == nullptr;
+  // RMSNorm fused into the GEMV prologue costs more than a launch once a kernel needs several
+  // rounds of work-groups per CU (tools/kernel_probe.py: gate/up +16 us); opt in with MX_FUSED_NORM=1
+  bool fuse_norms = getenv("MX_FUSED_NORM") != nullptr;
+  bool use_wide = getenv("MX_NO_WIDE") == nullptr;  // 17..64-row forward through mm_wide (LDS-shared activations)
+  float* slabs = nullptr;                           // split-K partials [8][MAX_ROWS][n_embd + 2 n_embd_kv]
+  size_t slab_stride = 0;
   int ctx_stride = 0;  // KV positions allocated per slot (n_ctx rounded up to KV_POS_ALIGN)
   uint64_t weight_bytes = 0;
 
@@ -168,6 +173,9 @@ struct mx_engine {
   int enqueue_forward(int M, const int* ids, const int* pos, const int* slot, const void* x_in, void* x_out,
                       bool head, const int* rowmap, int n_out, bool argmax, int* ids_next, int* pos_next, int* hist,
                       int hist_stride, int* hist_count, int max_hist, hipStream_t s);
+  int enqueue_forward_wide(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap,
+                           int n_out, bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride,
+                           int* hist_count, int max_hist, hipStream_t s);
   int forward_rows_chunk(int n, const int32_t* slots, const int32_t* pos, const int32_t* ids, const void* x_in,
                          void* x_out, float* logits_host, hipStream_t s);
   void scheduler_loop();
@@ -195,6 +203,7 @@ int mx_engine::init_common() {
   n_embd_kv = head_dim * n_head_kv;
   if (n_embd % n_head || n_head % n_head_kv) return fail(MX_ERR_MODEL, "head counts do not divide n_embd/n_head");
   if (head_dim != 64 && head_dim != 128) return fail(MX_ERR_ARG, "head_dim must be 64 or 128");
+  if (n_embd > 8192) return fail(MX_ERR_ARG, "n_embd > 8192 is not supported");
   const int G = n_head / n_head_kv;
   if (G != 1 && G != 2 && G != 4 && G != 8) return fail(MX_ERR_ARG, "n_head/n_head_kv must be 1,2,4 or 8");
   if (n_embd % 32 || n_ff % 32 || n_vocab % 16 || n_embd_kv % 16)
@@ -238,6 +247,8 @@ int mx_engine::init_common() {
   if (has_head) {
     if (int rc = alloc((void**)&logits, (size_t)R * n_vocab * 4)) return rc;
   }
+  slab_stride = (size_t)R * (n_embd + 2 * n_embd_kv);
+  if (int rc = alloc((void**)&slabs, slab_stride * 8 * 4)) return rc;
   if (int rc = alloc((void**)&am_val, (size_t)R * 64 * 4)) return rc;
   if (int rc = alloc((void**)&am_idx, (size_t)R * 64 * 4)) return rc;
   if (int rc = alloc((void**)&d_tok, (size_t)R * 4)) return rc;
@@ -407,6 +418,8 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     if (!has_embed) return fail(MX_ERR_STATE, "this stage has no token embedding: x_in required");
     launch_embed(x, tok_embd, ids, M, h, s);
   }
+  if (use_wide && M > 16) return enqueue_forward_wide(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next,
+                                                     pos_next, hist, hist_stride, hist_count, max_hist, s);
   // RMS_NORM is fused into the consuming GEMV when the activation image fits LDS (M <= 8)
   const bool fuse_norm = fuse_norms && mm_can_fuse_norm(M, h);
   auto norm_operand = [&](MMArgs& m, const float* w) {
@@ -463,6 +476,72 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     if (argmax)
       launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, ids_next, pos_next, hist, hist_stride,
                     hist_count, max_hist, s);
+  }
+  HIPC(hipGetLastError());
+  return 0;
+}
+
+// 17..64 rows: wide GEMVs (activations shared through LDS); attn_output and ffn_down run split-K
+// into slabs that the next resid_norm folds into the residual stream in a fixed order.
+int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap,
+                                    int n_out, bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride,
+                                    int* hist_count, int max_hist, hipStream_t s) {
+  const int h = n_embd, kv = n_embd_kv, ff = n_ff;
+  int nslab = 0;  // partial slabs not yet folded into x
+  for (int li = 0; li < (int)layers.size(); li++) {
+    const Layer& L = layers[li];
+    _Float16* kc = kcache + layer_kv_stride * li;
+    _Float16* vc = vcache + layer_kv_stride * li;
+    launch_resid_norm(xn, h, x, slabs, nslab, slab_stride, L.attn_norm, M, h, eps, s);
+    nslab = 0;
+    MMArgs a{};
+    a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M; a.X = xn; a.ldx = h;
+    a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
+    a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
+    a.slot_stride = slot_stride;
+    if (launch_mm_wide(EPI_QKV, a, slabs, slab_stride, s) < 0) return fail(MX_ERR_ARG, "wide qkv launch shape");
+    AttnArgs at{};
+    at.q = q; at.kc = kc; at.vc = vc; at.pos = pos; at.slot = slot;
+    at.out = attn_out; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
+    at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;
+    at.scale = 1.0f / sqrtf((float)head_dim);
+    launch_attention(at, s);
+    MMArgs b{};
+    b.W = L.o; b.N = h; b.K = h; b.X = attn_out; b.ldx = h; b.M = M;
+    if ((nslab = launch_mm_wide(EPI_RESID, b, slabs, slab_stride, s)) < 0)
+      return fail(MX_ERR_ARG, "wide attn_output launch shape");
+    launch_resid_norm(xn, h, x, slabs, nslab, slab_stride, L.ffn_norm, M, h, eps, s);
+    nslab = 0;
+    MMArgs c{};
+    c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.X = xn; c.ldx = h; c.act = act; c.lda = ff;
+    if (launch_mm_wide(EPI_SWIGLU, c, slabs, slab_stride, s) < 0) return fail(MX_ERR_ARG, "wide gate/up launch shape");
+    MMArgs d{};
+    d.W = L.down; d.N = h; d.K = ff; d.X = act; d.ldx = ff; d.M = M;
+    if ((nslab = launch_mm_wide(EPI_RESID, d, slabs, slab_stride, s)) < 0)
+      return fail(MX_ERR_ARG, "wide ffn_down launch shape");
+  }
+  if (x_out || (head && rowmap)) {
+    launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);
+    nslab = 0;
+  }
+  if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
+  if (head) {
+    if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
+    if (rowmap || n_out != M) {
+      launch_rmsnorm(xn, h, x, out_norm, rowmap, n_out, h, eps, s);
+    } else {
+      launch_resid_norm(xn, h, x, slabs, nslab, slab_stride, out_norm, M, h, eps, s);
+      nslab = 0;
+    }
+    MMArgs g{};
+    g.W = output; g.N = n_vocab; g.K = h; g.M = n_out; g.X = xn; g.ldx = h; g.out = logits; g.ldo = n_vocab;
+    const int rc = n_out > 16 ? launch_mm_wide(EPI_F32, g, slabs, slab_stride, s) : launch_mm(EPI_F32, g, s);
+    if (rc < 0) return fail(MX_ERR_ARG, "lm_head launch shape");
+    if (argmax)
+      launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, ids_next, pos_next, hist, hist_stride,
+                    hist_count, max_hist, s);
+  } else if (nslab) {
+    launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);
   }
   HIPC(hipGetLastError());
   return 0;
@@ -983,7 +1062,8 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
   hipSetDevice(e->device);
   hipStream_t s = e->stream;
   const int h = e->n_embd, kv = e->n_embd_kv, ff = e->n_ff;
-  std::vector<int32_t> zero(M, 0), slots(M);
+  const int prof_pos = std::min(e->n_ctx - 1, std::max(0, getenv("MX_PROF_POS") ? atoi(getenv("MX_PROF_POS")) : 0));
+  std::vector<int32_t> zero(M, prof_pos), slots(M);
   for (int i = 0; i < M; i++) slots[i] = i % e->n_seq_max;
   HIPC(hipMemcpyAsync(e->d_pos, zero.data(), M * 4, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(e->d_slot, slots.data(), M * 4, hipMemcpyHostToDevice, s));
@@ -1005,24 +1085,47 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
         a.ctx_stride = e->ctx_stride;
         a.n_head_kv = e->n_head_kv; a.slot_stride = e->slot_stride;
         per = (size_t)(h + 2 * kv) * h * 2;
-        return launch_mm(EPI_QKV, a, s);
+        return (M > 16 && e->use_wide) ? (launch_mm_wide(EPI_QKV, a, e->slabs, e->slab_stride, s) < 0) : launch_mm(EPI_QKV, a, s);
       case 1:
         a.W = L.o; a.N = h; a.K = h; a.X = e->attn_out; a.ldx = h; a.out = e->x; a.ldo = h;
         per = (size_t)h * h * 2;
-        return launch_mm(EPI_RESID, a, s);
+        return (M > 16 && e->use_wide) ? (launch_mm_wide(EPI_RESID, a, e->slabs, e->slab_stride, s) < 0) : launch_mm(EPI_RESID, a, s);
       case 2:
         a.W = L.gu; a.N = 2 * ff; a.K = h; a.X = e->xn; a.ldx = h; a.act = e->act; a.lda = ff;
         per = (size_t)2 * ff * h * 2;
-        return launch_mm(EPI_SWIGLU, a, s);
+        return (M > 16 && e->use_wide) ? (launch_mm_wide(EPI_SWIGLU, a, e->slabs, e->slab_stride, s) < 0) : launch_mm(EPI_SWIGLU, a, s);
       case 3:
         a.W = L.down; a.N = h; a.K = ff; a.X = e->act; a.ldx = ff; a.out = e->x; a.ldo = h;
         per = (size_t)h * ff * 2;
-        return launch_mm(EPI_RESID, a, s);
+        return (M > 16 && e->use_wide) ? (launch_mm_wide(EPI_RESID, a, e->slabs, e->slab_stride, s) < 0) : launch_mm(EPI_RESID, a, s);
       case 4:
         if (!e->has_head) return -1;
         a.W = e->output; a.N = e->n_vocab; a.K = h; a.X = e->xn; a.ldx = h; a.out = e->logits; a.ldo = e->n_vocab;
         per = (size_t)e->n_vocab * h * 2;
-        return launch_mm(EPI_F32, a, s);
+        return (M > 16 && e->use_wide) ? (launch_mm_wide(EPI_F32, a, e->slabs, e->slab_stride, s) < 0) : launch_mm(EPI_F32, a, s);
+      case 5:  // qkv with the attention RMSNorm fused (M <= 8)
+        a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.X = nullptr; a.xf = e->x; a.norm_w = L.attn_norm; a.eps = e->eps;
+        a.out = e->q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = e->head_dim; a.pos = e->d_pos;
+        a.slot = e->d_slot; a.rope_cs = e->rope_cs; a.kc = e->kcache + e->layer_kv_stride * li;
+        a.vc = e->vcache + e->layer_kv_stride * li; a.n_ctx = e->n_ctx; a.ctx_stride = e->ctx_stride;
+        a.n_head_kv = e->n_head_kv; a.slot_stride = e->slot_stride;
+        per = (size_t)(h + 2 * kv) * h * 2;
+        return launch_mm(EPI_QKV, a, s);
+      case 6:  // gate/up with the ffn RMSNorm fused (M <= 8)
+        a.W = L.gu; a.N = 2 * ff; a.K = h; a.X = nullptr; a.xf = e->x; a.norm_w = L.ffn_norm; a.eps = e->eps;
+        a.act = e->act; a.lda = ff;
+        per = (size_t)2 * ff * h * 2;
+        return launch_mm(EPI_SWIGLU, a, s);
+      case 7: {  // attention at the positions set below (ctx = pos + 1)
+        AttnArgs at{};
+        at.q = e->q; at.kc = e->kcache + e->layer_kv_stride * li; at.vc = e->vcache + e->layer_kv_stride * li;
+        at.pos = e->d_pos; at.slot = e->d_slot; at.out = e->attn_out; at.ldo = h; at.M = M; at.n_head = e->n_head;
+        at.n_head_kv = e->n_head_kv; at.head_dim = e->head_dim; at.n_ctx = e->n_ctx; at.ctx_stride = e->ctx_stride;
+        at.slot_stride = e->slot_stride; at.scale = 1.0f / sqrtf((float)e->head_dim);
+        per = (size_t)M * (prof_pos + 1) * kv * 2 * 2;
+        launch_attention(at, s);
+        return 0;
+      }
     }
     return -1;
   };

@@ -28,6 +28,7 @@ enum Epilogue : int {
   EPI_RESID = 1,   // x[col][row] += acc                          (attn_output, ffn_down)
   EPI_QKV = 2,     // rope(q,k); q -> f32 buffer, k/v -> f16 KV cache (attn_q/k/v)
   EPI_SWIGLU = 3,  // act = bf16(silu(gate) * up); tile = 8 gate + 8 up rows (ffn_gate/ffn_up)
+  EPI_SLAB = 4,    // split-K partial: out = slab[ksplit][col][row] (reduced by resid_norm / qkv_finish)
 };
 
 struct MMArgs {
@@ -54,6 +55,7 @@ struct MMArgs {
   _Float16* vc;                // V cache of this layer, transposed: [slots][n_head_kv][head_dim][ctx_stride]
   int n_ctx, ctx_stride, n_head_kv;
   size_t slot_stride;          // elements per slot in kc/vc = n_head_kv*ctx_stride*head_dim
+  size_t slab_stride;          // EPI_SLAB: floats between consecutive K-split partial slabs
 };
 
 struct AttnArgs {
@@ -84,7 +86,14 @@ void launch_embed(float* x, const uint16_t* tok_embd, const int* ids, int M, int
 void launch_rmsnorm(uint16_t* y, int ldy, const float* x, const float* w, const int* row_map, int M, int n,
                     float eps, hipStream_t s);
 int launch_mm(int epi, const MMArgs& a, hipStream_t s);
-bool mm_can_fuse_norm(int M, int K);  // X == nullptr path (RMS_NORM fused into the GEMV) is legal
+bool mm_can_fuse_norm(int M, int K);
+// 17..64 rows: activation chunks shared through LDS.  EPI_QKV / EPI_RESID run split-K into
+// `slabs` ([ksplit][MAX_ROWS][N] floats, slab_stride apart); returns the split used (the caller
+// folds RESID partials with launch_resid_norm; QKV partials are finished inside), or -1.
+int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s);
+// x[c] += sum of nslab partial slabs (fixed order); then, if y, y = bf16(rmsnorm(x) * w)
+void launch_resid_norm(uint16_t* y, int ldy, float* x, const float* slabs, int nslab, size_t slab_stride,
+                       const float* w, int M, int n, float eps, hipStream_t s);  // X == nullptr path (RMS_NORM fused into the GEMV) is legal
 void launch_attention(const AttnArgs& a, hipStream_t s);
 void launch_argmax(const float* logits, int ldl, int M, int V, float* ws_val, int* ws_idx, int* tok_out,
                    int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count, int max_hist,

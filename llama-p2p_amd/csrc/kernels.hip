@@ -21,6 +21,9 @@
 
 #include <math.h>
 
+#include <algorithm>
+#include <type_traits>
+
 namespace mx {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -147,32 +150,45 @@ void launch_embed(float* x, const uint16_t* tok_embd, const int* ids, int M, int
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void rmsnorm_kernel(uint16_t* y, int ldy, const float* x, const float* w,
                                                       const int* row_map, int n, float eps) {
+  // single pass: the row slice stays in registers (n <= 8192), one global round trip
+  constexpr int IT = 8;
   const int c = blockIdx.x;
   const int r = row_map ? row_map[c] : c;
   const float* xr = x + (size_t)r * n;
+  f32x4 v[IT], g[IT];
   double acc = 0.0;
-  for (int i = threadIdx.x * 4; i < n; i += blockDim.x * 4) {
-    f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
-    acc += (double)(v[0] * v[0]);
-    acc += (double)(v[1] * v[1]);
-    acc += (double)(v[2] * v[2]);
-    acc += (double)(v[3] * v[3]);
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int i = (it * 256 + threadIdx.x) * 4;
+    if (i < n) {
+      v[it] = *reinterpret_cast<const f32x4*>(xr + i);
+      g[it] = *reinterpret_cast<const f32x4*>(w + i);
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int i = (it * 256 + threadIdx.x) * 4;
+    if (i < n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc += (double)(v[it][j] * v[it][j]);
   }
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
   __shared__ double part[4];
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
   __syncthreads();
-  double sum = part[0] + part[1] + part[2] + part[3];
+  const double sum = part[0] + part[1] + part[2] + part[3];
   const float mean = (float)(sum / n);
   const float scale = 1.0f / sqrtf(mean + eps);
   uint16_t* yr = y + (size_t)c * ldy;
-  for (int i = threadIdx.x * 4; i < n; i += blockDim.x * 4) {
-    f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
-    f32x4 g = *reinterpret_cast<const f32x4*>(w + i);
-    u32x2 o;
-    o[0] = f2bf((v[0] * scale) * g[0]) | (f2bf((v[1] * scale) * g[1]) << 16);
-    o[1] = f2bf((v[2] * scale) * g[2]) | (f2bf((v[3] * scale) * g[3]) << 16);
-    *reinterpret_cast<u32x2*>(yr + i) = o;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int i = (it * 256 + threadIdx.x) * 4;
+    if (i < n) {
+      u32x2 o;
+      o[0] = f2bf((v[it][0] * scale) * g[it][0]) | (f2bf((v[it][1] * scale) * g[it][1]) << 16);
+      o[1] = f2bf((v[it][2] * scale) * g[it][2]) | (f2bf((v[it][3] * scale) * g[it][3]) << 16);
+      *reinterpret_cast<u32x2*>(yr + i) = o;
+    }
   }
 }
 
@@ -197,50 +213,119 @@ void launch_rmsnorm(uint16_t* y, int ldy, const float* x, const float* w, const 
 // reads the B fragments from LDS.  That removes one launch + one HBM round trip
 // per norm at batch sizes where a launch costs as much as the norm.
 // ---------------------------------------------------------------------------
+// Single pass: each thread holds its slice of two rows in registers (K <= 8192), so x is
+// read once: load -> sum of squares (double, as ggml) -> block reduce -> scale -> bf16 LDS image.
 template <int KS>
 __device__ __forceinline__ void xn_prologue(const MMArgs& a, uint16_t* xs, int pitch, double* red) {
-  // red: [KS][8] doubles
+  constexpr int NT = 64 * KS;
+  constexpr int IT = 8192 / (NT * 4);  // f32x4 pieces per thread per row (K <= 8192)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  double acc[8];
+  f32x4 g[IT];
 #pragma unroll
-  for (int c = 0; c < 8; ++c) acc[c] = 0.0;
-  for (int k = tid * 4; k < a.K; k += 64 * KS * 4) {
+  for (int it = 0; it < IT; ++it) {
+    const int k = (it * NT + tid) * 4;
+    if (k < a.K) g[it] = *reinterpret_cast<const f32x4*>(a.norm_w + k);
+  }
+  for (int c0 = 0; c0 < a.M; c0 += 2) {
+    f32x4 v[2][IT];
+    double acc[2] = {0.0, 0.0};
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      if (c < a.M) {
-        f32x4 v = *reinterpret_cast<const f32x4*>(a.xf + (size_t)c * a.K + k);
-        acc[c] += (double)(v[0] * v[0]);
-        acc[c] += (double)(v[1] * v[1]);
-        acc[c] += (double)(v[2] * v[2]);
-        acc[c] += (double)(v[3] * v[3]);
+    for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int k = (it * NT + tid) * 4;
+        if (c0 + rr < a.M && k < a.K) {
+          v[rr][it] = *reinterpret_cast<const f32x4*>(a.xf + (size_t)(c0 + rr) * a.K + k);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[rr] += (double)(v[rr][it][j] * v[rr][it][j]);
+        }
+      }
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      double t = acc[rr];
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+      if (lane == 0) red[w * 2 + rr] = t;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int c = c0 + rr;
+      if (c >= a.M) break;
+      double sum = 0.0;
+#pragma unroll
+      for (int ww = 0; ww < KS; ++ww) sum += red[ww * 2 + rr];
+      const float scale = 1.0f / sqrtf((float)(sum / a.K) + a.eps);
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int k = (it * NT + tid) * 4;
+        if (k < a.K) {
+          u32x2 o;
+          o[0] = f2bf((v[rr][it][0] * scale) * g[it][0]) | (f2bf((v[rr][it][1] * scale) * g[it][1]) << 16);
+          o[1] = f2bf((v[rr][it][2] * scale) * g[it][2]) | (f2bf((v[rr][it][3] * scale) * g[it][3]) << 16);
+          *reinterpret_cast<u32x2*>(xs + (size_t)c * pitch + k) = o;
+        }
       }
     }
+    __syncthreads();  // red[] reused by the next row pair; LDS image complete before the main loop
   }
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    if (c < a.M) {
-      double v = acc[c];
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-      if (lane == 0) red[w * 8 + c] = v;
+}
+
+// q/k/v rows [row, row+4) of token column `col`: RoPE (mode NORM, adjacent pairs) on q and k,
+// q -> f32 buffer, k -> f16 K cache [pos][d], v -> f16 V cache transposed [d][pos].
+__device__ __forceinline__ void qkv_store(const MMArgs& a, int row, int col, f32x4 s) {
+  const int d = a.head_dim;
+  const int pos = a.pos[col];
+  if (pos < 0 || pos >= a.n_ctx) return;  // never write outside the slot's KV rows
+  if (row < a.n_q + a.n_kv) {
+    const bool is_q = row < a.n_q;
+    const int rl = is_q ? row : row - a.n_q;
+    const int dd = rl % d;  // multiple of 4
+    const f32x4 csv = *reinterpret_cast<const f32x4*>(a.rope_cs + ((size_t)pos * (d / 2) + dd / 2) * 2);
+    f32x4 o;
+    o[0] = s[0] * csv[0] - s[1] * csv[1];
+    o[1] = s[0] * csv[1] + s[1] * csv[0];
+    o[2] = s[2] * csv[2] - s[3] * csv[3];
+    o[3] = s[2] * csv[3] + s[3] * csv[2];
+    if (is_q) {
+      *reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + row) = o;
+    } else {
+      _Float16* kp = a.kc + (size_t)a.slot[col] * a.slot_stride + ((size_t)(rl / d) * a.ctx_stride + pos) * d + dd;
+      *reinterpret_cast<f16x4*>(kp) = f16x4{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
     }
-  }
-  __syncthreads();
-  for (int c = 0; c < a.M; ++c) {
-    double sum = 0.0;
+  } else {
+    const int rl = row - a.n_q - a.n_kv;
+    _Float16* vt = a.vc + (size_t)a.slot[col] * a.slot_stride + ((size_t)(rl / d) * d + rl % d) * a.ctx_stride + pos;
 #pragma unroll
-    for (int ww = 0; ww < KS; ++ww) sum += red[ww * 8 + c];
-    const float mean = (float)(sum / a.K);
-    const float scale = 1.0f / sqrtf(mean + a.eps);
-    for (int k = tid * 4; k < a.K; k += 64 * KS * 4) {
-      f32x4 v = *reinterpret_cast<const f32x4*>(a.xf + (size_t)c * a.K + k);
-      f32x4 g = *reinterpret_cast<const f32x4*>(a.norm_w + k);
-      u32x2 o;
-      o[0] = f2bf((v[0] * scale) * g[0]) | (f2bf((v[1] * scale) * g[1]) << 16);
-      o[1] = f2bf((v[2] * scale) * g[2]) | (f2bf((v[3] * scale) * g[3]) << 16);
-      *reinterpret_cast<u32x2*>(xs + (size_t)c * pitch + k) = o;
-    }
+    for (int i = 0; i < 4; ++i) vt[(size_t)i * a.ctx_stride] = (_Float16)s[i];
   }
-  __syncthreads();
+}
+
+// One C-layout unit of a finished 16-row tile: rows 16*tile + 4*(l>>4) + i (i < 4) of token
+// column `col`.  SWIGLU tiles hold 8 gate rows (lanes 0-31) and the matching up rows (lanes l+32).
+template <int EPI>
+__device__ __forceinline__ void epi_store(const MMArgs& a, int tile, int l, int col, f32x4 s, f32x4 up) {
+  if constexpr (EPI == EPI_F32 || EPI == EPI_SLAB) {
+    const int row = tile * 16 + (l >> 4) * 4;
+    *reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + row) = s;
+  } else if constexpr (EPI == EPI_RESID) {
+    const int row = tile * 16 + (l >> 4) * 4;
+    f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + row);
+    *px = *px + s;
+  } else if constexpr (EPI == EPI_SWIGLU) {
+    const int row = tile * 8 + (l >> 4) * 4;  // ffn row of gate lane l / up lane l+32
+    uint32_t h[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float g = s[i];
+      h[i] = f2bf((g / (1.0f + expf(-g))) * up[i]);
+    }
+    u32x2 o;
+    o[0] = h[0] | (h[1] << 16);
+    o[1] = h[2] | (h[3] << 16);
+    *reinterpret_cast<u32x2*>(a.act + (size_t)col * a.lda + row) = o;
+  } else {  // EPI_QKV
+    qkv_store(a, tile * 16 + (l >> 4) * 4, col, s);
+  }
 }
 
 template <int KS, int RT, int NB, int EPI, int U, bool XN>
@@ -350,76 +435,32 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
 #pragma unroll
     for (int ww = 1; ww < KS; ++ww) s += red[ww][r][n][l];
 
-    if constexpr (EPI == EPI_F32) {
-      const int row = (tile0 + r) * 16 + (l >> 4) * 4;
-      *reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + row) = s;
-    } else if constexpr (EPI == EPI_RESID) {
-      const int row = (tile0 + r) * 16 + (l >> 4) * 4;
-      f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + row);
-      *px = *px + s;
-    } else if constexpr (EPI == EPI_SWIGLU) {
-      f32x4 up = red[0][r][n][l + 32];
+    f32x4 up = s;
+    if constexpr (EPI == EPI_SWIGLU) {
+      up = red[0][r][n][l + 32];
 #pragma unroll
       for (int ww = 1; ww < KS; ++ww) up += red[ww][r][n][l + 32];
-      const int row = (tile0 + r) * 8 + (l >> 4) * 4;  // ffn row of gate lane l / up lane l+32
-      uint32_t h[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float g = s[i];
-        float sg = g / (1.0f + expf(-g));
-        h[i] = f2bf(sg * up[i]);
-      }
-      u32x2 o;
-      o[0] = h[0] | (h[1] << 16);
-      o[1] = h[2] | (h[3] << 16);
-      *reinterpret_cast<u32x2*>(a.act + (size_t)col * a.lda + row) = o;
-    } else {  // EPI_QKV
-      const int row = (tile0 + r) * 16 + (l >> 4) * 4;
-      const int d = a.head_dim;
-      const int pos = a.pos[col];
-      if (pos < 0 || pos >= a.n_ctx) continue;  // never write outside the slot's KV rows
-      _Float16* kvbase = nullptr;
-      if (row < a.n_q + a.n_kv) {
-        // ROPE_EXT mode NORM: rotate adjacent pairs (2i, 2i+1) of each head
-        const bool is_q = row < a.n_q;
-        const int rl = is_q ? row : row - a.n_q;
-        const int dd = rl % d;  // multiple of 4
-        const float* cs = a.rope_cs + ((size_t)pos * (d / 2) + dd / 2) * 2;
-        f32x4 csv = *reinterpret_cast<const f32x4*>(cs);  // cos0, sin0, cos1, sin1
-        f32x4 o;
-        o[0] = s[0] * csv[0] - s[1] * csv[1];
-        o[1] = s[0] * csv[1] + s[1] * csv[0];
-        o[2] = s[2] * csv[2] - s[3] * csv[3];
-        o[3] = s[2] * csv[3] + s[3] * csv[2];
-        if (is_q) {
-          *reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + row) = o;
-        } else {
-          const int kvh = rl / d;
-          kvbase = a.kc + (size_t)a.slot[col] * a.slot_stride + ((size_t)kvh * a.ctx_stride + pos) * d + dd;
-          *reinterpret_cast<f16x4*>(kvbase) = f16x4{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
-        }
-      } else {
-        // V stored transposed ([d][pos]) so attention's P.V operand is a contiguous 16 B load
-        const int rl = row - a.n_q - a.n_kv;
-        const int kvh = rl / d, dd = rl % d;
-        _Float16* vt = a.vc + (size_t)a.slot[col] * a.slot_stride + ((size_t)kvh * d + dd) * a.ctx_stride + pos;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) vt[(size_t)i * a.ctx_stride] = (_Float16)s[i];
-      }
     }
+    epi_store<EPI>(a, tile0 + r, l, col, s, up);
   }
 }
 
+#ifndef XN_RING
+#define XN_RING 4
+#endif
 template <int KS, int RT, int EPI, int U>
 static int launch_mm_cfg(const MMArgs& a, hipStream_t s) {
   const int nb = (a.M + 15) / 16;
   if ((a.N / TILE_N) % RT) return -1;
   const int grid = a.N / (16 * RT);
-  if (a.X == nullptr) {  // fused RMS_NORM: activation image in LDS
+  if (a.X == nullptr) {  // fused RMS_NORM: activation image in LDS; 4x deeper ring covers the prologue
     const size_t lds = (size_t)a.M * (a.K + 8) * 2;
     if (a.M > 8 || lds > (size_t)XN_LDS_BYTES || !a.xf || !a.norm_w) return -1;
-    mm_kernel<KS, RT, 1, EPI, U, true><<<grid, 64 * KS, lds, s>>>(a);
-    return 0;
+    if constexpr (RT == 1) {
+      mm_kernel<KS, RT, 1, EPI, XN_RING, true><<<grid, 64 * KS, lds, s>>>(a);
+      return 0;
+    }
+    return -1;
   }
   if (nb == 1) {
     mm_kernel<KS, RT, 1, EPI, U, false><<<grid, 64 * KS, 0, s>>>(a);
@@ -474,7 +515,288 @@ int launch_mm(int epi, const MMArgs& a, hipStream_t s) {
   return -1;
 }
 
-bool mm_can_fuse_norm(int M, int K) { return M <= 8 && (size_t)M * (K + 8) * 2 <= (size_t)XN_LDS_BYTES; }
+// ---------------------------------------------------------------------------
+// Wide GEMV for 17..64 token rows (32-sequence decode, prefill chunks).
+//
+// At 32 tokens the activation fragment per K-tile (16 tokens x 64 B per column
+// tile) is as large as the weight tile, so re-reading it per wave from L2 costs
+// as much as the weights (tools/gemv_sweep.hip).  Here the W waves of a
+// work-group split ROWS and share one activation chunk [rows][128 k] staged in
+// LDS (double-buffered, one barrier per chunk; plain register loads stay in
+// flight across __syncthreads), so activation traffic drops to 16*NB/(16*W*RTW)
+// of the weight traffic.  Each wave streams RTW weight tiles through a ring two
+// chunks deep.  Small N is split over K across work-groups (grid.y); partial
+// sums go to slabs [ksplit][token][N] that resid_norm / qkv_finish add in a
+// fixed order, so results stay bit-reproducible.
+// ---------------------------------------------------------------------------
+template <int W, int RTW, int NB, int EPI>
+__global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
+  constexpr int KCT = 4;             // K-tiles per staged activation chunk
+  constexpr int KC = KCT * TILE_K;   // 128 k
+  constexpr int PITCH = KC + 8;      // bf16 per LDS row: +16 B keeps fragment reads conflict-free
+  constexpr int ROWS = 16 * NB;
+  constexpr int SEGS = KC / 8;       // 16-B pieces per row and chunk
+  constexpr int PIECES = ROWS * SEGS;
+  constexpr int NT = 64 * W;
+  static_assert(PIECES % NT == 0, "chunk pieces must tile the work-group");
+  constexpr int PPT = PIECES / NT;
+  constexpr int U = 2 * KCT;         // weight ring: this chunk + the next
+  __shared__ __attribute__((aligned(16))) uint16_t xs[2][ROWS][PITCH];
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int KT = a.K / TILE_K;
+  const int ks = blockIdx.y, nks = gridDim.y;
+  const int kb = KT * ks / nks, ke = KT * (ks + 1) / nks;
+  const int nch = (ke - kb) / KCT;
+  const int tile0 = (blockIdx.x * W + w) * RTW;
+
+  const u32x4* Wp[RTW];
+#pragma unroll
+  for (int r = 0; r < RTW; ++r) Wp[r] = reinterpret_cast<const u32x4*>(a.W) + (size_t)(tile0 + r) * KT * 64 + lane;
+
+  // activation chunk staging: piece p -> (row, 16-B segment); rows >= M re-read row M-1 (outputs dropped)
+  const u32x4* xsrc[PPT];
+  int xrow[PPT], xseg[PPT];
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int p = threadIdx.x + i * NT;
+    xrow[i] = p / SEGS;
+    xseg[i] = p % SEGS;
+    const int rr = xrow[i] < a.M ? xrow[i] : a.M - 1;
+    xsrc[i] = reinterpret_cast<const u32x4*>(a.X + (size_t)rr * a.ldx + (size_t)kb * TILE_K + xseg[i] * 8);
+  }
+  u32x4 xr[PPT];
+  auto load_x = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) xr[i] = xsrc[i][c * (KC / 8)];
+  };
+  auto store_x = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(&xs[buf][xrow[i]][xseg[i] * 8]) = xr[i];
+  };
+
+  f32x4 acc[RTW][NB];
+#pragma unroll
+  for (int r = 0; r < RTW; ++r)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra[U][RTW];
+  load_x(0);
+#pragma unroll
+  for (int u = 0; u < KCT; ++u)
+#pragma unroll
+    for (int r = 0; r < RTW; ++r) ra[u][r] = __builtin_nontemporal_load(Wp[r] + (size_t)(kb + u) * 64);
+  if (nch > 1) {
+#pragma unroll
+    for (int u = 0; u < KCT; ++u)
+#pragma unroll
+      for (int r = 0; r < RTW; ++r)
+        ra[KCT + u][r] = __builtin_nontemporal_load(Wp[r] + (size_t)(kb + KCT + u) * 64);
+  }
+  store_x(0);
+  __syncthreads();
+
+  // one chunk: H = ring half (compile time), REFILL = load the chunk two ahead into that half
+  auto chunk = [&](auto Hc, auto Rc, int c) {
+    constexpr int H = decltype(Hc)::value;
+    constexpr bool REFILL = decltype(Rc)::value;
+    const int buf = c & 1;
+    load_x(c + 1 < nch ? c + 1 : c);  // the last chunk re-reads itself: loads stay unconditional
+#pragma unroll
+    for (int kk = 0; kk < KCT; ++kk) {
+      u32x4 xb[NB];
+#pragma unroll
+      for (int n = 0; n < NB; ++n)
+        xb[n] = *reinterpret_cast<const u32x4*>(&xs[buf][n * 16 + (lane & 15)][kk * 32 + (lane >> 4) * 8]);
+#pragma unroll
+      for (int r = 0; r < RTW; ++r)
+#pragma unroll
+        for (int n = 0; n < NB; ++n)
+          acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ra[H * KCT + kk][r]),
+                                                               __builtin_bit_cast(bf16x8, xb[n]), acc[r][n], 0, 0, 0);
+      if constexpr (REFILL) {
+#pragma unroll
+        for (int r = 0; r < RTW; ++r)
+          ra[H * KCT + kk][r] = __builtin_nontemporal_load(Wp[r] + (size_t)(kb + (c + 2) * KCT + kk) * 64);
+      }
+    }
+    store_x(buf ^ 1);
+    __syncthreads();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using T = std::true_type;
+  using F = std::false_type;
+  int c = 0;
+  for (; c + 3 < nch; c += 2) {
+    chunk(I0{}, T{}, c);
+    chunk(I1{}, T{}, c + 1);
+  }
+  const int rem = nch - c;
+  if (rem == 3) {
+    chunk(I0{}, T{}, c);
+    chunk(I1{}, F{}, c + 1);
+    chunk(I0{}, F{}, c + 2);
+  } else if (rem == 2) {
+    chunk(I0{}, F{}, c);
+    chunk(I1{}, F{}, c + 1);
+  } else if (rem == 1) {
+    chunk(I0{}, F{}, c);
+  }
+
+  // epilogue straight from registers: this wave owns whole tiles (over this block's K range)
+#pragma unroll
+  for (int r = 0; r < RTW; ++r)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const f32x4 s = acc[r][n];
+      f32x4 up = s;
+      if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(s[i], 32);
+      }
+      const int col = n * 16 + (lane & 15);
+      if (col >= a.M || (EPI == EPI_SWIGLU && lane >= 32)) continue;
+      if constexpr (EPI == EPI_SLAB) {
+        const int row = (tile0 + r) * 16 + (lane >> 4) * 4;
+        *reinterpret_cast<f32x4*>(a.out + (size_t)ks * a.slab_stride + (size_t)col * a.ldo + row) = s;
+      } else {
+        epi_store<EPI>(a, tile0 + r, lane, col, s, up);
+      }
+    }
+}
+
+// q/k/v split-K partials -> sum in slab order -> RoPE + q / KV-cache stores
+__global__ __launch_bounds__(256) void qkv_finish_kernel(MMArgs a, const float* slabs, int nslab, size_t stride) {
+  const int N = a.n_q + 2 * a.n_kv;
+  const int quads = N / 4;
+  const int total = a.M * quads;
+  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < total; u += gridDim.x * blockDim.x) {
+    const int col = u / quads, row = (u % quads) * 4;
+    f32x4 s = *reinterpret_cast<const f32x4*>(slabs + (size_t)col * N + row);
+    for (int k = 1; k < nslab; ++k) s += *reinterpret_cast<const f32x4*>(slabs + k * stride + (size_t)col * N + row);
+    qkv_store(a, row, col, s);
+  }
+}
+
+// x[c] += sum_k slab[k][c] (fixed order), then optionally y = bf16(rmsnorm(x) * w)
+__global__ __launch_bounds__(256) void resid_norm_kernel(uint16_t* y, int ldy, float* x, const float* slabs, int nslab,
+                                                         size_t stride, const float* w, int n, float eps) {
+  constexpr int IT = 8;  // n <= 8192
+  const int c = blockIdx.x;
+  float* xr = x + (size_t)c * n;
+  f32x4 v[IT], g[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int i = (it * 256 + threadIdx.x) * 4;
+    if (i < n) {
+      v[it] = *reinterpret_cast<const f32x4*>(xr + i);
+      if (y) g[it] = *reinterpret_cast<const f32x4*>(w + i);
+    }
+  }
+  if (nslab > 0) {
+    for (int k = 0; k < nslab; ++k) {
+      const float* sp = slabs + k * stride + (size_t)c * n;
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int i = (it * 256 + threadIdx.x) * 4;
+        if (i < n) v[it] += *reinterpret_cast<const f32x4*>(sp + i);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int i = (it * 256 + threadIdx.x) * 4;
+      if (i < n) *reinterpret_cast<f32x4*>(xr + i) = v[it];
+    }
+  }
+  if (!y) return;
+  double acc = 0.0;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int i = (it * 256 + threadIdx.x) * 4;
+    if (i < n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc += (double)(v[it][j] * v[it][j]);
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  __shared__ double part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  const double sum = part[0] + part[1] + part[2] + part[3];
+  const float scale = 1.0f / sqrtf((float)(sum / n) + eps);
+  uint16_t* yr = y + (size_t)c * ldy;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int i = (it * 256 + threadIdx.x) * 4;
+    if (i < n) {
+      u32x2 o;
+      o[0] = f2bf((v[it][0] * scale) * g[it][0]) | (f2bf((v[it][1] * scale) * g[it][1]) << 16);
+      o[1] = f2bf((v[it][2] * scale) * g[it][2]) | (f2bf((v[it][3] * scale) * g[it][3]) << 16);
+      *reinterpret_cast<u32x2*>(yr + i) = o;
+    }
+  }
+}
+
+void launch_resid_norm(uint16_t* y, int ldy, float* x, const float* slabs, int nslab, size_t stride, const float* w,
+                       int M, int n, float eps, hipStream_t s) {
+  resid_norm_kernel<<<M, 256, 0, s>>>(y, ldy, x, slabs, nslab, stride, w, n, eps);
+}
+
+template <int W, int RTW, int EPI>
+static int launch_wide_cfg(const MMArgs& a, int ksplit, hipStream_t s) {
+  const int ntiles = a.N / TILE_N;
+  const int KT = a.K / TILE_K;
+  if (ntiles % (W * RTW) || KT % (ksplit * 4)) return -1;
+  dim3 grid(ntiles / (W * RTW), ksplit);
+  const int nb = (a.M + 15) / 16;
+  if (nb <= 2)
+    mm_wide_kernel<W, RTW, 2, EPI><<<grid, 64 * W, 0, s>>>(a);
+  else
+    mm_wide_kernel<W, RTW, 4, EPI><<<grid, 64 * W, 0, s>>>(a);
+  return 0;
+}
+
+// largest power-of-two split <= target that keeps every K range a whole number of chunks
+static int pick_ksplit(int KT, int target) {
+  int k = 1;
+  while (k * 2 <= target && KT % (k * 2 * 4) == 0) k *= 2;
+  return KT % (k * 4) == 0 ? k : 0;
+}
+
+int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s) {
+  if (a.M < 1 || a.M > MAX_ROWS || a.K % TILE_K != 0 || a.N % TILE_N != 0 || !a.X) return -1;
+  const int ntiles = a.N / TILE_N, KT = a.K / TILE_K;
+  switch (epi) {
+    case EPI_F32:
+      if (ntiles % 8 == 0 && KT % 4 == 0) return launch_wide_cfg<4, 2, EPI_F32>(a, 1, s) ? -1 : 1;
+      return launch_wide_cfg<4, 1, EPI_F32>(a, 1, s) ? -1 : 1;
+    case EPI_SWIGLU:
+      return launch_wide_cfg<4, 1, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
+    case EPI_QKV:
+    case EPI_RESID: {
+      // split K until the grid covers the 256 CUs; partials -> slabs
+      const int groups = ntiles / 4;
+      const int ksplit = pick_ksplit(KT, std::min(8, std::max(1, (384 + groups - 1) / std::max(1, groups))));
+      if (!ksplit) return -1;
+      MMArgs p = a;
+      p.out = slabs;
+      p.ldo = a.N;
+      p.slab_stride = slab_stride;
+      if (launch_wide_cfg<4, 1, EPI_SLAB>(p, ksplit, s)) return -1;
+      if (epi == EPI_QKV) {
+        const int total = a.M * a.N / 4;
+        qkv_finish_kernel<<<(total + 255) / 256, 256, 0, s>>>(a, slabs, ksplit, slab_stride);
+      }
+      return ksplit;
+    }
+  }
+  return -1;
+}
+
+bool mm_can_fuse_norm(int M, int K) {
+  return M <= 8 && K <= 8192 && K % 4 == 0 && (size_t)M * (K + 8) * 2 <= (size_t)XN_LDS_BYTES;
+}
 
 // ---------------------------------------------------------------------------
 // Attention for one query token per row (decode, and prefill rows alike):
@@ -536,17 +858,24 @@ __global__ __launch_bounds__(512) void attn_decode_kernel(AttnArgs a) {
 
   for (int ch = w; ch * CH < ctx; ch += NW) {
     const int p0 = ch * CH;
+    // issue this chunk's K and V fragment loads together: one memory round trip per chunk
+    f16x8 kf[2][QK], vf[DT];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int kk = 0; kk < QK; ++kk)
+        kf[t][kk] = *reinterpret_cast<const f16x8*>(Kb + (size_t)(p0 + 16 * t + r16) * D + 8 * q4 + kk * 32);
+    const int pb = p0 + 8 * q4;  // first position of this lane's P.V B fragment
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+      vf[t] = *reinterpret_cast<const f16x8*>(Vb + (size_t)(t * 16 + r16) * a.ctx_stride + pb);
     // S[head][pos] for two 16-position tiles
     f32x4 s[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const _Float16* kr = Kb + (size_t)(p0 + 16 * t + r16) * D + 8 * q4;
 #pragma unroll
-      for (int kk = 0; kk < QK; ++kk) {
-        f16x8 kb = *reinterpret_cast<const f16x8*>(kr + kk * 32);
-        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qa[kk], kb, s[t], 0, 0, 0);
-      }
+      for (int kk = 0; kk < QK; ++kk) s[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qa[kk], kf[t][kk], s[t], 0, 0, 0);
     }
     // online softmax: C layout rows = heads 4*q4+i, cols = positions (lane r16)
     float e[2][4];
@@ -577,10 +906,9 @@ __global__ __launch_bounds__(512) void attn_decode_kernel(AttnArgs a) {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
     __builtin_amdgcn_wave_barrier();
     const f16x8 pa = *reinterpret_cast<const f16x8*>(&Ps[w][r16][8 * q4]);
-    const int pb = p0 + 8 * q4;  // first position of this lane's B fragment
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
-      f16x8 vb = *reinterpret_cast<const f16x8*>(Vb + (size_t)(t * 16 + r16) * a.ctx_stride + pb);
+      f16x8 vb = vf[t];
 #pragma unroll
       for (int j = 0; j < 8; ++j) vb[j] = (pb + j < ctx) ? vb[j] : (_Float16)0.f;
       o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa, vb, o[t], 0, 0, 0);

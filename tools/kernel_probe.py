@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Per-kernel timing on the GPU (HIP events, rotating through every layer's weights).
+
+    python tools/kernel_probe.py [--model llama3-8b] [--rows 1,32] [--pos 255]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+KINDS = {0: "qkv", 1: "attn_output", 2: "gate_up", 3: "down", 4: "lm_head", 5: "qkv+norm", 6: "gate_up+norm",
+         7: "attention"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--rows", default="1,32")
+    ap.add_argument("--pos", type=int, default=255)
+    args = ap.parse_args()
+    os.environ["MX_PROF_POS"] = str(args.pos)
+    from llama_p2p_amd.engine import Engine
+
+    eng = Engine(f"synthetic:{args.model}:seed=0", n_ctx=512, n_seq_max=64)
+    for M in [int(x) for x in args.rows.split(",")]:
+        for k, name in KINDS.items():
+            if k in (5, 6) and M > 8:
+                continue
+            us, b = eng.profile_kernel(k, M, iters=3)
+            print(f"M={M:<3d} {name:14s} {us:9.2f} us  {b / us / 1e3:8.1f} GB/s", flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
