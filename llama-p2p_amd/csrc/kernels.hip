@@ -764,26 +764,37 @@ static int pick_ksplit(int KT, int target) {
   return KT % (k * 4) == 0 ? k : 0;
 }
 
+// Geometry from tools/gemv_sweep.hip (wide) on MI355X, Llama-3-8B shapes at 32 rows
+// (profiles/round1_gemv_sweep_wide.txt): two row tiles per wave, K split until ~256 work-groups.
 int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s) {
   if (a.M < 1 || a.M > MAX_ROWS || a.K % TILE_K != 0 || a.N % TILE_N != 0 || !a.X) return -1;
   const int ntiles = a.N / TILE_N, KT = a.K / TILE_K;
+  if (KT % 4) return -1;
   switch (epi) {
     case EPI_F32:
-      if (ntiles % 8 == 0 && KT % 4 == 0) return launch_wide_cfg<4, 2, EPI_F32>(a, 1, s) ? -1 : 1;
+      if (ntiles % 16 == 0) return launch_wide_cfg<8, 2, EPI_F32>(a, 1, s) ? -1 : 1;
+      if (ntiles % 8 == 0) return launch_wide_cfg<4, 2, EPI_F32>(a, 1, s) ? -1 : 1;
       return launch_wide_cfg<4, 1, EPI_F32>(a, 1, s) ? -1 : 1;
     case EPI_SWIGLU:
+      if (ntiles % 8 == 0) return launch_wide_cfg<4, 2, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
       return launch_wide_cfg<4, 1, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
     case EPI_QKV:
     case EPI_RESID: {
-      // split K until the grid covers the 256 CUs; partials -> slabs
-      const int groups = ntiles / 4;
-      const int ksplit = pick_ksplit(KT, std::min(8, std::max(1, (384 + groups - 1) / std::max(1, groups))));
+      // at most 4 partial slabs: every extra slab is re-read by the reduce+norm that follows
+      int cfg, groups;  // 0: W4 RTW2 (qkv), 1: W2 RTW1 (K <= 8192), 2: W4 RTW1
+      if (epi == EPI_QKV && ntiles % 8 == 0) cfg = 0, groups = ntiles / 8;
+      else if (a.K <= 8192 && ntiles % 2 == 0) cfg = 1, groups = ntiles / 2;
+      else cfg = 2, groups = ntiles / 4;
+      const int ksplit = pick_ksplit(KT, std::min(4, std::max(1, (256 + groups - 1) / std::max(1, groups))));
       if (!ksplit) return -1;
       MMArgs p = a;
       p.out = slabs;
       p.ldo = a.N;
       p.slab_stride = slab_stride;
-      if (launch_wide_cfg<4, 1, EPI_SLAB>(p, ksplit, s)) return -1;
+      const int rc = cfg == 0 ? launch_wide_cfg<4, 2, EPI_SLAB>(p, ksplit, s)
+                   : cfg == 1 ? launch_wide_cfg<2, 1, EPI_SLAB>(p, ksplit, s)
+                              : launch_wide_cfg<4, 1, EPI_SLAB>(p, ksplit, s);
+      if (rc) return -1;
       if (epi == EPI_QKV) {
         const int total = a.M * a.N / 4;
         qkv_finish_kernel<<<(total + 255) / 256, 256, 0, s>>>(a, slabs, ksplit, slab_stride);
