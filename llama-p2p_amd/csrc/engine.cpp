@@ -62,6 +62,7 @@ const Shape kShapes[] = {
     {"test-tiny", 256, 2, 4, 2, 512, 512, 10000.f, 1e-5f, 2048},
     {"test-gqa8", 512, 3, 8, 1, 1024, 1024, 500000.f, 1e-5f, 2048},
     {"test-d128", 1024, 2, 8, 2, 2816, 2048, 500000.f, 1e-5f, 2048},
+    {"test-h4096", 4096, 1, 32, 8, 2048, 1024, 500000.f, 1e-5f, 2048},
 };
 
 // synth.py tensor ids

@@ -148,53 +148,116 @@ void launch_embed(float* x, const uint16_t* tok_embd, const int* ids, int M, int
 // ggml: sum of x*x in double, scale = 1/sqrtf(mean + eps), y = (x*scale)*w;
 // the bf16 rounding is the conversion ggml applies to src1 of the next MUL_MAT.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void rmsnorm_kernel(uint16_t* y, int ldy, const float* x, const float* w,
-                                                      const int* row_map, int n, float eps) {
-  // single pass: the row slice stays in registers (n <= 8192), one global round trip
-  constexpr int IT = 8;
+// x[r] += sum of NS partial slabs (fixed order, written back when NS > 0); then, if y,
+// y[c] = bf16((x[r] * 1/sqrtf(mean(x^2) + eps)) * w) with the sum of squares in double (ggml
+// RMS_NORM + MUL).  One 1024-thread work-group per row and every load issued up front: a
+// single memory round trip, which is what a row of 4096-8192 floats costs at decode.
+template <int NS, int IT>
+__global__ __launch_bounds__(1024) void norm_kernel(uint16_t* y, int ldy, float* x, const float* slabs, size_t stride,
+                                                    const float* w, const int* row_map, int n, float eps) {
   const int c = blockIdx.x;
   const int r = row_map ? row_map[c] : c;
-  const float* xr = x + (size_t)r * n;
-  f32x4 v[IT], g[IT];
-  double acc = 0.0;
+  float* xr = x + (size_t)r * n;
+  const int tid = threadIdx.x;
+  f32x4 v[IT], g[IT], sl[IT][NS > 0 ? NS : 1];
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
-    const int i = (it * 256 + threadIdx.x) * 4;
-    if (i < n) {
-      v[it] = *reinterpret_cast<const f32x4*>(xr + i);
-      g[it] = *reinterpret_cast<const f32x4*>(w + i);
+    const int i = (it * 1024 + tid) * 4;
+    v[it] = *reinterpret_cast<const f32x4*>(xr + i);
+    if (y) g[it] = *reinterpret_cast<const f32x4*>(w + i);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) sl[it][k] = *reinterpret_cast<const f32x4*>(slabs + k * stride + (size_t)r * n + i);
+  }
+  if constexpr (NS > 0) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+#pragma unroll
+      for (int k = 0; k < NS; ++k) v[it] += sl[it][k];
+      *reinterpret_cast<f32x4*>(xr + (it * 1024 + tid) * 4) = v[it];
     }
   }
+  if (!y) return;
+  double acc = 0.0;
+#pragma unroll
+  for (int it = 0; it < IT; ++it)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc += (double)(v[it][j] * v[it][j]);
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  __shared__ double part[16];
+  if ((tid & 63) == 0) part[tid >> 6] = acc;
+  __syncthreads();
+  double sum = 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) sum += part[k];
+  const float scale = 1.0f / sqrtf((float)(sum / n) + eps);
+  uint16_t* yr = y + (size_t)c * ldy;
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
-    const int i = (it * 256 + threadIdx.x) * 4;
-    if (i < n)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc += (double)(v[it][j] * v[it][j]);
+    u32x2 o;
+    o[0] = f2bf((v[it][0] * scale) * g[it][0]) | (f2bf((v[it][1] * scale) * g[it][1]) << 16);
+    o[1] = f2bf((v[it][2] * scale) * g[it][2]) | (f2bf((v[it][3] * scale) * g[it][3]) << 16);
+    *reinterpret_cast<u32x2*>(yr + (it * 1024 + tid) * 4) = o;
   }
+}
+
+template <int NS>
+static void launch_norm_ns(uint16_t* y, int ldy, float* x, const float* slabs, size_t stride, const float* w,
+                           const int* row_map, int M, int n, float eps, hipStream_t s) {
+  if (n == 4096)
+    norm_kernel<NS, 1><<<M, 1024, 0, s>>>(y, ldy, x, slabs, stride, w, row_map, n, eps);
+  else
+    norm_kernel<NS, 2><<<M, 1024, 0, s>>>(y, ldy, x, slabs, stride, w, row_map, n, eps);
+}
+
+// n must be 4096 or 8192 for the 1024-thread layout; other widths use the generic path below
+__global__ __launch_bounds__(256) void norm_generic_kernel(uint16_t* y, int ldy, float* x, const float* slabs,
+                                                           int nslab, size_t stride, const float* w,
+                                                           const int* row_map, int n, float eps) {
+  const int c = blockIdx.x;
+  const int r = row_map ? row_map[c] : c;
+  float* xr = x + (size_t)r * n;
+  double acc = 0.0;
+  for (int i = threadIdx.x * 4; i < n; i += 1024) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
+    for (int k = 0; k < nslab; ++k) v += *reinterpret_cast<const f32x4*>(slabs + k * stride + (size_t)r * n + i);
+    if (nslab) *reinterpret_cast<f32x4*>(xr + i) = v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc += (double)(v[j] * v[j]);
+  }
+  if (!y) return;
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
   __shared__ double part[4];
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
   __syncthreads();
   const double sum = part[0] + part[1] + part[2] + part[3];
-  const float mean = (float)(sum / n);
-  const float scale = 1.0f / sqrtf(mean + eps);
+  const float scale = 1.0f / sqrtf((float)(sum / n) + eps);
   uint16_t* yr = y + (size_t)c * ldy;
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int i = (it * 256 + threadIdx.x) * 4;
-    if (i < n) {
-      u32x2 o;
-      o[0] = f2bf((v[it][0] * scale) * g[it][0]) | (f2bf((v[it][1] * scale) * g[it][1]) << 16);
-      o[1] = f2bf((v[it][2] * scale) * g[it][2]) | (f2bf((v[it][3] * scale) * g[it][3]) << 16);
-      *reinterpret_cast<u32x2*>(yr + i) = o;
+  for (int i = threadIdx.x * 4; i < n; i += 1024) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
+    const f32x4 g = *reinterpret_cast<const f32x4*>(w + i);
+    u32x2 o;
+    o[0] = f2bf((v[0] * scale) * g[0]) | (f2bf((v[1] * scale) * g[1]) << 16);
+    o[1] = f2bf((v[2] * scale) * g[2]) | (f2bf((v[3] * scale) * g[3]) << 16);
+    *reinterpret_cast<u32x2*>(yr + i) = o;
+  }
+}
+
+static void launch_norm_impl(uint16_t* y, int ldy, float* x, const float* slabs, int nslab, size_t stride,
+                             const float* w, const int* row_map, int M, int n, float eps, hipStream_t s) {
+  if ((n == 4096 || n == 8192) && (nslab == 0 || nslab == 1 || nslab == 2 || nslab == 4)) {
+    switch (nslab) {
+      case 0: launch_norm_ns<0>(y, ldy, x, slabs, stride, w, row_map, M, n, eps, s); return;
+      case 1: launch_norm_ns<1>(y, ldy, x, slabs, stride, w, row_map, M, n, eps, s); return;
+      case 2: launch_norm_ns<2>(y, ldy, x, slabs, stride, w, row_map, M, n, eps, s); return;
+      case 4: launch_norm_ns<4>(y, ldy, x, slabs, stride, w, row_map, M, n, eps, s); return;
     }
   }
+  norm_generic_kernel<<<M, 256, 0, s>>>(y, ldy, x, slabs, nslab, stride, w, row_map, n, eps);
 }
 
 void launch_rmsnorm(uint16_t* y, int ldy, const float* x, const float* w, const int* row_map, int M, int n,
                     float eps, hipStream_t s) {
-  rmsnorm_kernel<<<M, 256, 0, s>>>(y, ldy, x, w, row_map, n, eps);
+  launch_norm_impl(y, ldy, const_cast<float*>(x), nullptr, 0, 0, w, row_map, M, n, eps, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -680,67 +743,9 @@ __global__ __launch_bounds__(256) void qkv_finish_kernel(MMArgs a, const float* 
   }
 }
 
-// x[c] += sum_k slab[k][c] (fixed order), then optionally y = bf16(rmsnorm(x) * w)
-__global__ __launch_bounds__(256) void resid_norm_kernel(uint16_t* y, int ldy, float* x, const float* slabs, int nslab,
-                                                         size_t stride, const float* w, int n, float eps) {
-  constexpr int IT = 8;  // n <= 8192
-  const int c = blockIdx.x;
-  float* xr = x + (size_t)c * n;
-  f32x4 v[IT], g[IT];
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int i = (it * 256 + threadIdx.x) * 4;
-    if (i < n) {
-      v[it] = *reinterpret_cast<const f32x4*>(xr + i);
-      if (y) g[it] = *reinterpret_cast<const f32x4*>(w + i);
-    }
-  }
-  if (nslab > 0) {
-    for (int k = 0; k < nslab; ++k) {
-      const float* sp = slabs + k * stride + (size_t)c * n;
-#pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int i = (it * 256 + threadIdx.x) * 4;
-        if (i < n) v[it] += *reinterpret_cast<const f32x4*>(sp + i);
-      }
-    }
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int i = (it * 256 + threadIdx.x) * 4;
-      if (i < n) *reinterpret_cast<f32x4*>(xr + i) = v[it];
-    }
-  }
-  if (!y) return;
-  double acc = 0.0;
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int i = (it * 256 + threadIdx.x) * 4;
-    if (i < n)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc += (double)(v[it][j] * v[it][j]);
-  }
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-  __shared__ double part[4];
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  const double sum = part[0] + part[1] + part[2] + part[3];
-  const float scale = 1.0f / sqrtf((float)(sum / n) + eps);
-  uint16_t* yr = y + (size_t)c * ldy;
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int i = (it * 256 + threadIdx.x) * 4;
-    if (i < n) {
-      u32x2 o;
-      o[0] = f2bf((v[it][0] * scale) * g[it][0]) | (f2bf((v[it][1] * scale) * g[it][1]) << 16);
-      o[1] = f2bf((v[it][2] * scale) * g[it][2]) | (f2bf((v[it][3] * scale) * g[it][3]) << 16);
-      *reinterpret_cast<u32x2*>(yr + i) = o;
-    }
-  }
-}
-
 void launch_resid_norm(uint16_t* y, int ldy, float* x, const float* slabs, int nslab, size_t stride, const float* w,
                        int M, int n, float eps, hipStream_t s) {
-  resid_norm_kernel<<<M, 256, 0, s>>>(y, ldy, x, slabs, nslab, stride, w, n, eps);
+  launch_norm_impl(y, ldy, x, slabs, nslab, stride, w, nullptr, M, n, eps, s);
 }
 
 template <int W, int RTW, int EPI>

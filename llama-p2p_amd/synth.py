@@ -85,6 +85,8 @@ SHAPES = {
     "test-tiny": LlamaShape("test-tiny", 256, 2, 4, 2, 512, 512, 10000.0, 1e-5),
     "test-gqa8": LlamaShape("test-gqa8", 512, 3, 8, 1, 1024, 1024, 500000.0, 1e-5),
     "test-d128": LlamaShape("test-d128", 1024, 2, 8, 2, 2816, 2048, 500000.0, 1e-5),
+    # Llama-3-8B hidden geometry (n_embd 4096, 32 q / 8 kv heads of 128), one layer, small FFN/vocab
+    "test-h4096": LlamaShape("test-h4096", 4096, 1, 32, 8, 2048, 1024, 500000.0, 1e-5),
 }
 
 _M64 = (1 << 64) - 1

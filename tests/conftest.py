@@ -52,3 +52,24 @@ def assert_tokens_match(got_logits, ref_logits, what=""):
     mism = decided & (ga != ra)
     assert not mism.any(), f"{what}: argmax mismatch at decided positions {np.nonzero(mism)[0].tolist()}"
     return int(decided.sum()), int((ga == ra).sum())
+
+
+def check_greedy_chain(octx, prompt, tokens, what=""):
+    """Teacher-force the oracle along the engine's greedy tokens: every engine pick must be
+    the oracle's argmax, or within 2x the logit tolerance of the oracle's max (a near tie).
+    Returns the number of exact argmax matches."""
+    import numpy as np
+
+    lg = octx.eval(prompt, 0)[0]
+    pos = len(prompt)
+    exact = 0
+    for k, t in enumerate(tokens):
+        t = int(t)
+        tol = 2 * (1e-2 * abs(float(lg.max())) + 2e-2 * float(np.abs(lg).max()))
+        assert float(lg.max() - lg[t]) <= tol, (f"{what}: step {k} picked {t} (logit {lg[t]:.4f}) "
+                                                f"but oracle max is {lg.max():.4f} at {int(lg.argmax())}")
+        exact += int(t == int(lg.argmax()))
+        if k + 1 < len(tokens):
+            lg = octx.eval([t], pos)[0]
+            pos += 1
+    return exact

@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 
 from llama_p2p_amd import synth  # noqa: E402
 
-SHAPES = ["test-tiny", "test-gqa8", "test-d128"]
+SHAPES = ["test-tiny", "test-gqa8", "test-d128", "test-h4096"]
 SEQ_LEN = 40
 SEED = 0
 

@@ -11,7 +11,7 @@ import pytest
 
 from conftest import assert_logits_close
 
-SHAPES = ["test-tiny", "test-gqa8", "test-d128"]
+SHAPES = ["test-tiny", "test-gqa8", "test-d128", "test-h4096"]
 
 
 def _golden(name):
