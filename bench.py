@@ -44,6 +44,16 @@ def make_prompts(vocab: int, n: int, seed: int = 2, lo: int = 16, hi: int = 256)
     return [np.concatenate([[1], rng.integers(3, vocab, L - 1)]).astype(np.int32) for L in lens]
 
 
+def measured_traffic(label: str):
+    """HBM bytes per launch of the dominant kernel, from the PMC passes committed under
+    profiles/ (tools/prof_summary.py traffic); None when that configuration was not profiled."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        return json.load(open(path)).get(label)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(shape_name: str, n_prompt: int = 4, n_decode: int = 6):
     """The CPU oracle (C/OpenMP restatement of llama.cpp's CPU forward, bf16
     weights, f32 accumulation) doing what the reference does: batch-1 greedy
@@ -113,9 +123,13 @@ def run_single(args):
     # dominant kernel: ffn gate/up (fused, 2 x n_ff x n_embd bf16 per layer) -- HIP events on the engine stream
     us, wbytes = eng.profile_kernel(2, M, iters=3)
     kbytes = wbytes + M * shape.n_embd * 2 + M * shape.n_ff * 2  # weights + activations in/out
+    traffic = measured_traffic(f"{args.model}/gate_up/M{M}")
     res["roofline"] = {"bound": "hbm", "achieved": round(kbytes / us / 1e3, 1), "peak": HBM_PEAK_GBS,
-                       "unit": "GB/s", "frac": round(kbytes / us / 1e3 / HBM_PEAK_GBS, 4), "traffic": None,
-                       "kernel": "mm_kernel<EPI_SWIGLU> (ffn_gate+ffn_up+SiLU*up)", "us_per_launch": round(us, 2),
+                       "unit": "GB/s", "frac": round(kbytes / us / 1e3 / HBM_PEAK_GBS, 4),
+                       "traffic": round(traffic["traffic_bytes"]) if traffic else None,
+                       "traffic_source": (f"profiles/traffic.json: {traffic['kernel']} ({traffic['method']})"
+                                          if traffic else None),
+                       "kernel": ("mm_wide_kernel" if M > 16 else "mm_kernel") + "<EPI_SWIGLU> (ffn_gate+ffn_up+SiLU*up)", "us_per_launch": round(us, 2),
                        "bytes_per_launch": int(kbytes)}
     # batch-1 decode (the north_star's 70% target), same engine
     if args.batch1_steps > 0:
