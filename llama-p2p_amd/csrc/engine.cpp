@@ -121,9 +121,10 @@ struct mx_engine {
   int bos = 1, eos = 2;
   int n_ctx = 512, n_seq_max = 64, lb = 0, le = 0, device = 0;
   bool has_embed = true, has_head = true, use_graphs = true;
-  // RMSNorm fused into the GEMV prologue costs more than a launch once a kernel needs several
-  // rounds of work-groups per CU (tools/kernel_probe.py: gate/up +16 us); opt in with MX_FUSED_NORM=1
-  bool fuse_norms = getenv("MX_FUSED_NORM") != nullptr;
+  // <= 16 rows: RMS_NORM applied while loading the GEMV's B operand, from per-tile sums of squares
+  // written by the residual-stream producer (no norm launches); MX_NO_NORM_ON_LOAD=1 for A/B runs
+  bool norm_on_load = getenv("MX_NO_NORM_ON_LOAD") == nullptr;
+  float* ssq = nullptr;  // [MAX_ROWS][n_embd/16] per-tile sums of squares of x
   bool use_wide = getenv("MX_NO_WIDE") == nullptr;  // 17..64-row forward through mm_wide (LDS-shared activations)
   float* slabs = nullptr;                           // split-K partials [8][MAX_ROWS][n_embd + 2 n_embd_kv]
   size_t slab_stride = 0;
@@ -250,6 +251,7 @@ int mx_engine::init_common() {
   }
   slab_stride = (size_t)R * (n_embd + 2 * n_embd_kv);
   if (int rc = alloc((void**)&slabs, slab_stride * 8 * 4)) return rc;
+  if (int rc = alloc((void**)&ssq, (size_t)R * (n_embd / 16) * 4)) return rc;
   if (int rc = alloc((void**)&am_val, (size_t)R * 64 * 4)) return rc;
   if (int rc = alloc((void**)&am_idx, (size_t)R * 64 * 4)) return rc;
   if (int rc = alloc((void**)&d_tok, (size_t)R * 4)) return rc;
@@ -413,19 +415,25 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
                                bool head, const int* rowmap, int n_out, bool argmax, int* ids_next, int* pos_next,
                                int* hist, int hist_stride, int* hist_count, int max_hist, hipStream_t s) {
   const int h = n_embd, kv = n_embd_kv, ff = n_ff;
+  const bool wide = use_wide && M > 16;
+  // RMS_NORM applied on load by the consuming GEMV (M <= 16); the residual-stream writers
+  // (embedding, attn_output, ffn_down, or ssq_kernel for a stage's x_in) leave per-tile partials
+  const bool nol = !wide && norm_on_load && mm_can_norm_on_load(M, h);
   if (x_in) {
     HIPC(hipMemcpyAsync(x, x_in, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
+    if (nol) launch_ssq(x, M, h, ssq, s);
   } else {
     if (!has_embed) return fail(MX_ERR_STATE, "this stage has no token embedding: x_in required");
-    launch_embed(x, tok_embd, ids, M, h, s);
+    launch_embed(x, tok_embd, ids, M, h, nol ? ssq : nullptr, s);
   }
-  if (use_wide && M > 16) return enqueue_forward_wide(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next,
-                                                     pos_next, hist, hist_stride, hist_count, max_hist, s);
-  // RMS_NORM is fused into the consuming GEMV when the activation image fits LDS (M <= 8)
-  const bool fuse_norm = fuse_norms && mm_can_fuse_norm(M, h);
-  auto norm_operand = [&](MMArgs& m, const float* w) {
-    if (fuse_norm) {
-      m.X = nullptr; m.xf = x; m.norm_w = w; m.eps = eps;
+  if (wide) return enqueue_forward_wide(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next,
+                                        pos_next, hist, hist_stride, hist_count, max_hist, s);
+  // on-load only for attn_norm -> qkv: qkv's 384 work-groups run 1.5 rounds, so its per-work-group
+  // prologue costs less than a norm launch; gate/up (7 rounds) and lm_head (31) keep the norm kernel
+  // (tools/kernel_probe.py, profiles/round1_norm_on_load.txt)
+  auto norm_operand = [&](MMArgs& m, const float* w, bool on_load) {
+    if (nol && on_load) {
+      m.X = nullptr; m.xf = x; m.norm_w = w; m.eps = eps; m.ssq = ssq; m.np = h / 16;
     } else {
       launch_rmsnorm(xn, h, x, w, nullptr, M, h, eps, s);
       m.X = xn; m.ldx = h;
@@ -437,7 +445,7 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     _Float16* vc = vcache + layer_kv_stride * li;
     MMArgs a{};
     a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M;
-    norm_operand(a, L.attn_norm);
+    norm_operand(a, L.attn_norm, true);
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
     a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
     a.slot_stride = slot_stride;
@@ -453,11 +461,12 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     if (launch_mm(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "attn_output launch shape");
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M;
-    norm_operand(c, L.ffn_norm);
+    norm_operand(c, L.ffn_norm, false);
     c.act = act; c.lda = ff;
     if (launch_mm(EPI_SWIGLU, c, s)) return fail(MX_ERR_ARG, "ffn gate/up launch shape");
     MMArgs d{};
     d.W = L.down; d.N = h; d.K = ff; d.X = act; d.ldx = ff; d.M = M; d.out = x; d.ldo = h;
+    d.ssq = nol ? ssq : nullptr; d.np = h / 16;
     if (launch_mm(EPI_RESID, d, s)) return fail(MX_ERR_ARG, "ffn_down launch shape");
   }
   if (x_out) {
@@ -468,7 +477,7 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     MMArgs g{};
     g.W = output; g.N = n_vocab; g.K = h; g.M = n_out; g.out = logits; g.ldo = n_vocab;
     if (!rowmap && n_out == M) {
-      norm_operand(g, out_norm);
+      norm_operand(g, out_norm, false);
     } else {
       launch_rmsnorm(xn, h, x, out_norm, rowmap, n_out, h, eps, s);
       g.X = xn; g.ldx = h;
@@ -1104,16 +1113,18 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
         a.W = e->output; a.N = e->n_vocab; a.K = h; a.X = e->xn; a.ldx = h; a.out = e->logits; a.ldo = e->n_vocab;
         per = (size_t)e->n_vocab * h * 2;
         return (M > 16 && e->use_wide) ? (launch_mm_wide(EPI_F32, a, e->slabs, e->slab_stride, s) < 0) : launch_mm(EPI_F32, a, s);
-      case 5:  // qkv with the attention RMSNorm fused (M <= 8)
+      case 5:  // qkv with the attention RMSNorm applied on load (M <= 16)
         a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.X = nullptr; a.xf = e->x; a.norm_w = L.attn_norm; a.eps = e->eps;
+        a.ssq = e->ssq; a.np = h / 16;
         a.out = e->q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = e->head_dim; a.pos = e->d_pos;
         a.slot = e->d_slot; a.rope_cs = e->rope_cs; a.kc = e->kcache + e->layer_kv_stride * li;
         a.vc = e->vcache + e->layer_kv_stride * li; a.n_ctx = e->n_ctx; a.ctx_stride = e->ctx_stride;
         a.n_head_kv = e->n_head_kv; a.slot_stride = e->slot_stride;
         per = (size_t)(h + 2 * kv) * h * 2;
         return launch_mm(EPI_QKV, a, s);
-      case 6:  // gate/up with the ffn RMSNorm fused (M <= 8)
+      case 6:  // gate/up with the ffn RMSNorm applied on load (M <= 16)
         a.W = L.gu; a.N = 2 * ff; a.K = h; a.X = nullptr; a.xf = e->x; a.norm_w = L.ffn_norm; a.eps = e->eps;
+        a.ssq = e->ssq; a.np = h / 16;
         a.act = e->act; a.lda = ff;
         per = (size_t)2 * ff * h * 2;
         return launch_mm(EPI_SWIGLU, a, s);

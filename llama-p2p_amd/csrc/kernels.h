@@ -21,7 +21,6 @@ constexpr int TILE_ELEMS = TILE_N * TILE_K;
 constexpr int MAX_ROWS = 64;       // tokens per forward (4 column tiles of 16)
 constexpr int ATTN_CHUNK = 32;     // positions per attention wave-iteration
 constexpr int KV_POS_ALIGN = 64;   // KV rows per slot are allocated in multiples of this
-constexpr int XN_LDS_BYTES = 64 * 1024;  // budget for the fused-RMSNorm activation image in LDS
 
 enum Epilogue : int {
   EPI_F32 = 0,     // out[col][row] = acc                         (lm_head logits)
@@ -37,10 +36,14 @@ struct MMArgs {
   const uint16_t* X;   // activations bf16 [>=16*NB rows][ldx]
   int ldx;
   int M;               // valid columns (tokens)
-  // fused RMS_NORM (X == nullptr): the work-group normalises xf[M][K] with norm_w into LDS
+  // RMS_NORM on load (X == nullptr, M <= 16): B = bf16((xf * scale) * norm_w), scale from ssq
   const float* xf;
   const float* norm_w;
   float eps;
+  // per-16-row-tile sums of squares of the residual stream, [M][np]: read by RMS_NORM-on-load
+  // consumers (np = K/16), written by EPI_RESID producers when non-null (np = N/16)
+  float* ssq;
+  int np;
   // epilogue operands
   float* out;          // EPI_F32: [M][ldo]; EPI_RESID: residual x [M][ldo]; EPI_QKV: q [M][ldo]
   int ldo;
@@ -82,11 +85,13 @@ void launch_pack(uint16_t* dst, const uint16_t* src_rowmajor, int N, int K, int 
                  hipStream_t s);
 
 // forward-pass ops
-void launch_embed(float* x, const uint16_t* tok_embd, const int* ids, int M, int n_embd, hipStream_t s);
+// ssq (optional): per-16-element-tile sums of squares of each embedded row, [M][n_embd/16]
+void launch_embed(float* x, const uint16_t* tok_embd, const int* ids, int M, int n_embd, float* ssq, hipStream_t s);
+void launch_ssq(const float* x, int M, int n, float* ssq, hipStream_t s);
 void launch_rmsnorm(uint16_t* y, int ldy, const float* x, const float* w, const int* row_map, int M, int n,
                     float eps, hipStream_t s);
 int launch_mm(int epi, const MMArgs& a, hipStream_t s);
-bool mm_can_fuse_norm(int M, int K);
+bool mm_can_norm_on_load(int M, int K);
 // 17..64 rows: activation chunks shared through LDS.  EPI_QKV / EPI_RESID run split-K into
 // `slabs` ([ksplit][MAX_ROWS][N] floats, slab_stride apart); returns the split used (the caller
 // folds RESID partials with launch_resid_norm; QKV partials are finished inside), or -1.

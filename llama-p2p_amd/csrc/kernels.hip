@@ -20,6 +20,7 @@
 #include "kernels.h"
 
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <type_traits>
@@ -122,26 +123,54 @@ void launch_synth_norm(float* dst, size_t n, uint64_t seed, uint64_t tid, float 
 // ---------------------------------------------------------------------------
 // GET_ROWS: token embedding, bf16 -> f32  
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void embed_kernel(float* x, const uint16_t* tok_embd, const int* ids, int n) {
+// One work-group per token; thread t converts 16-element tiles t, t+256, ... and, when ssq is
+// given, writes each tile's sum of squares (the partials XS consumers reduce, see mm_kernel).
+__global__ __launch_bounds__(256) void embed_kernel(float* x, const uint16_t* tok_embd, const int* ids, int n,
+                                                    float* ssq) {
   const int c = blockIdx.x;
   const int id = ids[c];
   const u32x4* src = reinterpret_cast<const u32x4*>(tok_embd + (size_t)id * n);
   f32x4* dst = reinterpret_cast<f32x4*>(x + (size_t)c * n);
-  for (int i = threadIdx.x; i < n / 8; i += blockDim.x) {
-    u32x4 v = src[i];
-    f32x4 lo, hi;
-    lo[0] = __uint_as_float(v[0] << 16); lo[1] = __uint_as_float(v[0] & 0xffff0000u);
-    lo[2] = __uint_as_float(v[1] << 16); lo[3] = __uint_as_float(v[1] & 0xffff0000u);
-    hi[0] = __uint_as_float(v[2] << 16); hi[1] = __uint_as_float(v[2] & 0xffff0000u);
-    hi[2] = __uint_as_float(v[3] << 16); hi[3] = __uint_as_float(v[3] & 0xffff0000u);
-    dst[2 * i] = lo;
-    dst[2 * i + 1] = hi;
+  for (int t = threadIdx.x; t < n / 16; t += blockDim.x) {
+    double q = 0.0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const u32x4 v = src[2 * t + h];
+      f32x4 lo, hi;
+      lo[0] = __uint_as_float(v[0] << 16); lo[1] = __uint_as_float(v[0] & 0xffff0000u);
+      lo[2] = __uint_as_float(v[1] << 16); lo[3] = __uint_as_float(v[1] & 0xffff0000u);
+      hi[0] = __uint_as_float(v[2] << 16); hi[1] = __uint_as_float(v[2] & 0xffff0000u);
+      hi[2] = __uint_as_float(v[3] << 16); hi[3] = __uint_as_float(v[3] & 0xffff0000u);
+      dst[4 * t + 2 * h] = lo;
+      dst[4 * t + 2 * h + 1] = hi;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) q += (double)(lo[i] * lo[i]) + (double)(hi[i] * hi[i]);
+    }
+    if (ssq) ssq[(size_t)c * (n / 16) + t] = (float)q;
   }
 }
 
-void launch_embed(float* x, const uint16_t* tok_embd, const int* ids, int M, int n, hipStream_t s) {
-  embed_kernel<<<M, 256, 0, s>>>(x, tok_embd, ids, n);
+void launch_embed(float* x, const uint16_t* tok_embd, const int* ids, int M, int n, float* ssq, hipStream_t s) {
+  embed_kernel<<<M, 256, 0, s>>>(x, tok_embd, ids, n, ssq);
 }
+
+// per-16-row-tile sums of squares of an existing residual stream (a pipeline stage's x_in)
+__global__ __launch_bounds__(256) void ssq_kernel(const float* x, int n, float* ssq) {
+  const int c = blockIdx.x;
+  const f32x4* src = reinterpret_cast<const f32x4*>(x + (size_t)c * n);
+  for (int t = threadIdx.x; t < n / 16; t += blockDim.x) {
+    double q = 0.0;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const f32x4 v = src[4 * t + h];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) q += (double)(v[i] * v[i]);
+    }
+    ssq[(size_t)c * (n / 16) + t] = (float)q;
+  }
+}
+
+void launch_ssq(const float* x, int M, int n, float* ssq, hipStream_t s) { ssq_kernel<<<M, 256, 0, s>>>(x, n, ssq); }
 
 // ---------------------------------------------------------------------------
 // RMS_NORM + MUL(norm weight) -> bf16 activation  
@@ -262,74 +291,74 @@ void launch_rmsnorm(uint16_t* y, int ldy, const float* x, const float* w, const 
 
 // ---------------------------------------------------------------------------
 // MUL_MAT with bf16 weights for 1..64 tokens (decode GEMV / skinny GEMM) with
-// fused epilogues.  (SURVEY §8a a7, a8, a9, a11, a12, a13)
+// fused epilogues.  (SURVEY §8a a6, a7, a8, a9, a11, a12, a13)
 //
 // Work-group = KS waves = RT row tiles (16 rows each) x all K; wave w owns the
 // K-tiles [KT*w/KS, KT*(w+1)/KS).  Per K-tile a wave issues RT weight loads
 // (1 KiB each, contiguous, non-temporal) and NB activation fragments, and
 // RT*NB MFMAs.  A ring of U K-tiles per wave keeps U*RT weight loads in flight.
 //
-// XN (fused RMS_NORM, M <= 8 rows): the activation operand is not read from a
-// bf16 buffer; the work-group normalises x (f32, residual stream) itself into
-// an LDS image  bf16((x*scale)*w)  -- the exact value the unfused rmsnorm
-// kernel writes -- while its first U weight tiles are already in flight, and
-// reads the B fragments from LDS.  That removes one launch + one HBM round trip
-// per norm at batch sizes where a launch costs as much as the norm.
+// XS (RMS_NORM on load, <= 4 tokens): there is no normalised activation
+// buffer and no norm launch.  The kernel that last wrote the residual stream x
+// (embedding, or an EPI_RESID GEMV) also wrote ssq[col][t] = sum of x^2 over
+// the 16 rows of its tile t.  Every wave sums those partials in a fixed order
+// (double, as ggml), derives 1/sqrt(mean+eps), and writes bf16((x*scale)*w) --
+// the exact value ggml's RMS_NORM+MUL feeds MUL_MAT -- for its own K-slice into
+// a wave-private LDS image that its B fragments are read from.
 // ---------------------------------------------------------------------------
-// Single pass: each thread holds its slice of two rows in registers (K <= 8192), so x is
-// read once: load -> sum of squares (double, as ggml) -> block reduce -> scale -> bf16 LDS image.
-template <int KS>
-__device__ __forceinline__ void xn_prologue(const MMArgs& a, uint16_t* xs, int pitch, double* red) {
-  constexpr int NT = 64 * KS;
-  constexpr int IT = 8192 / (NT * 4);  // f32x4 pieces per thread per row (K <= 8192)
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  f32x4 g[IT];
+// XS operands of one wave, loaded BEFORE its weight ring (a load issued behind the ring waits
+// for the ring: that ordering cost more than the norm launch it replaces).  Per column c < M:
+// this lane's 4 partials of ssq (whole wave = all np <= 512 of them, 2 pieces) and 4 values of
+// x and of w per 256-k piece of the wave's K-slice (nk <= 512: 2 pieces).
+constexpr int XS_MAX_M = 4;
+struct XsRegs {
+  f32x4 q[XS_MAX_M][2], x[XS_MAX_M][2], g[2];
+};
+
+__device__ __forceinline__ void xs_load(XsRegs& r, const MMArgs& a, int kbase, int nk, int lane) {
+  const int i0 = lane * 4;
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int k = (it * NT + tid) * 4;
-    if (k < a.K) g[it] = *reinterpret_cast<const f32x4*>(a.norm_w + k);
+  for (int p = 0; p < 2; ++p) {
+    const int i = i0 + 256 * p;
+    if (i < nk) r.g[p] = *reinterpret_cast<const f32x4*>(a.norm_w + kbase + i);
+#pragma unroll
+    for (int c = 0; c < XS_MAX_M; ++c) {
+      if (c < a.M) {
+        if (i < a.np) r.q[c][p] = *reinterpret_cast<const f32x4*>(a.ssq + (size_t)c * a.np + i);
+        if (i < nk) r.x[c][p] = *reinterpret_cast<const f32x4*>(a.xf + (size_t)c * a.K + kbase + i);
+      }
+    }
   }
-  for (int c0 = 0; c0 < a.M; c0 += 2) {
-    f32x4 v[2][IT];
-    double acc[2] = {0.0, 0.0};
+}
+
+// scale per column from the partials (fixed-order lane sum, then a fixed xor tree: every lane
+// agrees), then xs[c][k - kbase] = bf16((x * scale) * w): this wave's LDS image (only it reads it)
+__device__ __forceinline__ void xs_build(const XsRegs& r, const MMArgs& a, uint16_t* xs, int pitch, int nk,
+                                         int lane) {
+  const int i0 = lane * 4;
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr)
+  for (int c = 0; c < XS_MAX_M; ++c) {
+    if (c >= a.M) break;
+    double acc = 0.0;
 #pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int k = (it * NT + tid) * 4;
-        if (c0 + rr < a.M && k < a.K) {
-          v[rr][it] = *reinterpret_cast<const f32x4*>(a.xf + (size_t)(c0 + rr) * a.K + k);
+    for (int p = 0; p < 2; ++p)
+      if (i0 + 256 * p < a.np)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[rr] += (double)(v[rr][it][j] * v[rr][it][j]);
-        }
-      }
+        for (int j = 0; j < 4; ++j) acc += (double)r.q[c][p][j];
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-      double t = acc[rr];
-      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
-      if (lane == 0) red[w * 2 + rr] = t;
-    }
-    __syncthreads();
+    for (int o = 1; o < 64; o <<= 1) acc += __shfl_xor(acc, o);
+    const float sc = 1.0f / sqrtf((float)(acc / a.K) + a.eps);
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-      const int c = c0 + rr;
-      if (c >= a.M) break;
-      double sum = 0.0;
-#pragma unroll
-      for (int ww = 0; ww < KS; ++ww) sum += red[ww * 2 + rr];
-      const float scale = 1.0f / sqrtf((float)(sum / a.K) + a.eps);
-#pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int k = (it * NT + tid) * 4;
-        if (k < a.K) {
-          u32x2 o;
-          o[0] = f2bf((v[rr][it][0] * scale) * g[it][0]) | (f2bf((v[rr][it][1] * scale) * g[it][1]) << 16);
-          o[1] = f2bf((v[rr][it][2] * scale) * g[it][2]) | (f2bf((v[rr][it][3] * scale) * g[it][3]) << 16);
-          *reinterpret_cast<u32x2*>(xs + (size_t)c * pitch + k) = o;
-        }
+    for (int p = 0; p < 2; ++p) {
+      const int i = i0 + 256 * p;
+      if (i < nk) {
+        const f32x4 xv = r.x[c][p], g = r.g[p];
+        u32x2 o;
+        o[0] = f2bf((xv[0] * sc) * g[0]) | (f2bf((xv[1] * sc) * g[1]) << 16);
+        o[1] = f2bf((xv[2] * sc) * g[2]) | (f2bf((xv[3] * sc) * g[3]) << 16);
+        *reinterpret_cast<u32x2*>(xs + c * pitch + i) = o;
       }
     }
-    __syncthreads();  // red[] reused by the next row pair; LDS image complete before the main loop
   }
 }
 
@@ -391,7 +420,7 @@ __device__ __forceinline__ void epi_store(const MMArgs& a, int tile, int l, int 
   }
 }
 
-template <int KS, int RT, int NB, int EPI, int U, bool XN>
+template <int KS, int RT, int NB, int EPI, int U, bool XS>
 __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -400,8 +429,7 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
   const int kb = (KT * w) / KS, ke = (KT * (w + 1)) / KS;
 
   __shared__ f32x4 red[KS][RT][NB][64];
-  extern __shared__ __attribute__((aligned(16))) uint16_t xs_dyn[];
-  const int pitch = a.K + 8;  // bf16 elements per LDS activation row (+16 B: rows land on different banks)
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs_dyn[];  // XS: per-wave [M][xs_pitch] images
 
   const u32x4* Wp[RT];
 #pragma unroll
@@ -409,12 +437,14 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
     Wp[r] = reinterpret_cast<const u32x4*>(a.W) + (size_t)(tile0 + r) * KT * 64 + lane;
   // B fragment source (lane -> token column, k offset); padded columns re-read a valid row (outputs dropped)
   const u32x4* Xp[NB];
+  const int xs_pitch = (KT + KS - 1) / KS * TILE_K + 8;  // bf16 per image row (+16 B: conflict-free columns)
+  uint16_t* xsw = xs_dyn + (size_t)w * a.M * xs_pitch;
 #pragma unroll
   for (int n = 0; n < NB; ++n) {
     int col = n * 16 + (lane & 15);
     col = col < a.M ? col : a.M - 1;
-    if constexpr (XN)
-      Xp[n] = reinterpret_cast<const u32x4*>(xs_dyn + (size_t)col * pitch + (lane >> 4) * 8);
+    if constexpr (XS)  // image k index = (kt - kb) * 32 + k within tile
+      Xp[n] = reinterpret_cast<const u32x4*>(xsw + col * xs_pitch + (lane >> 4) * 8 - kb * TILE_K);
     else
       Xp[n] = reinterpret_cast<const u32x4*>(a.X + (size_t)col * a.ldx + (lane >> 4) * 8);
   }
@@ -434,6 +464,8 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
                                                              __builtin_bit_cast(bf16x8, xb[n]), acc[r][n], 0, 0, 0);
   };
 
+  XsRegs xr;
+  if constexpr (XS) xs_load(xr, a, kb * TILE_K, (ke - kb) * TILE_K, lane);
   u32x4 ra[U][RT];
   int kt = kb;
   const int nfull = (ke - kb) / U;
@@ -443,15 +475,22 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
 #pragma unroll
       for (int r = 0; r < RT; ++r) ra[u][r] = __builtin_nontemporal_load(Wp[r] + (size_t)(kt + u) * 64);
   }
-  if constexpr (XN) xn_prologue<KS>(a, xs_dyn, pitch, reinterpret_cast<double*>(&red[0][0][0][0]));
+  if constexpr (XS) {
+    xs_build(xr, a, xsw, xs_pitch, (ke - kb) * TILE_K, lane);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
+    __builtin_amdgcn_wave_barrier();
+  }
+  auto load_b = [&](u32x4 (&xb)[NB], int k) {
+#pragma unroll
+    for (int n = 0; n < NB; ++n) xb[n] = Xp[n][k * 4];
+  };
 
   if (nfull > 0) {
     for (int ch = 1; ch < nfull; ++ch) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         u32x4 xb[NB];
-#pragma unroll
-        for (int n = 0; n < NB; ++n) xb[n] = Xp[n][(kt + u) * 4];
+        load_b(xb, kt + u);
         mma(ra[u], xb);
 #pragma unroll
         for (int r = 0; r < RT; ++r) ra[u][r] = __builtin_nontemporal_load(Wp[r] + (size_t)(kt + U + u) * 64);
@@ -461,8 +500,7 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       u32x4 xb[NB];
-#pragma unroll
-      for (int n = 0; n < NB; ++n) xb[n] = Xp[n][(kt + u) * 4];
+      load_b(xb, kt + u);
       mma(ra[u], xb);
     }
     kt += U;
@@ -471,13 +509,11 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
     u32x4 sa[RT], sb[NB];
 #pragma unroll
     for (int r = 0; r < RT; ++r) sa[r] = __builtin_nontemporal_load(Wp[r] + (size_t)kt * 64);
-#pragma unroll
-    for (int n = 0; n < NB; ++n) sb[n] = Xp[n][kt * 4];
+    load_b(sb, kt);
     mma(sa, sb);
   }
 
   // ---- sum the KS partial tiles through LDS
-  if constexpr (XN) __syncthreads();  // red[] doubled as the prologue's scratch
 #pragma unroll
   for (int r = 0; r < RT; ++r)
 #pragma unroll
@@ -493,11 +529,28 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
     const int n = (u / LU) % NB;
     const int r = (u / LU) / NB;
     const int col = n * 16 + (l & 15);
-    if (col >= a.M) continue;
     f32x4 s = red[0][r][n][l];
 #pragma unroll
     for (int ww = 1; ww < KS; ++ww) s += red[ww][r][n][l];
-
+    if constexpr (EPI == EPI_RESID) {
+      // residual add, and this tile's share of the next RMS_NORM's sum of squares: a wave holds one
+      // whole (r, n) unit block (LU = 64), so lanes l, l^16, l^32, l^48 hold the tile's 16 rows of col
+      double q = 0.0;
+      if (col < a.M) {
+        f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + (tile0 + r) * 16 + (l >> 4) * 4);
+        const f32x4 xv = *px + s;
+        *px = xv;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q += (double)(xv[i] * xv[i]);
+      }
+      if (a.ssq) {
+        q += __shfl_xor(q, 16);
+        q += __shfl_xor(q, 32);
+        if (l < 16 && col < a.M) a.ssq[(size_t)col * a.np + tile0 + r] = (float)q;
+      }
+      continue;
+    }
+    if (col >= a.M) continue;
     f32x4 up = s;
     if constexpr (EPI == EPI_SWIGLU) {
       up = red[0][r][n][l + 32];
@@ -508,22 +561,19 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
   }
 }
 
-#ifndef XN_RING
-#define XN_RING 4
-#endif
 template <int KS, int RT, int EPI, int U>
 static int launch_mm_cfg(const MMArgs& a, hipStream_t s) {
   const int nb = (a.M + 15) / 16;
   if ((a.N / TILE_N) % RT) return -1;
   const int grid = a.N / (16 * RT);
-  if (a.X == nullptr) {  // fused RMS_NORM: activation image in LDS; 4x deeper ring covers the prologue
-    const size_t lds = (size_t)a.M * (a.K + 8) * 2;
-    if (a.M > 8 || lds > (size_t)XN_LDS_BYTES || !a.xf || !a.norm_w) return -1;
-    if constexpr (RT == 1) {
-      mm_kernel<KS, RT, 1, EPI, XN_RING, true><<<grid, 64 * KS, lds, s>>>(a);
-      return 0;
-    }
-    return -1;
+  if (a.X == nullptr) {  // RMS_NORM on load (<= 4 tokens): per-wave LDS images of the K-slices
+    const int KT = a.K / TILE_K;
+    if (a.M > XS_MAX_M || !a.xf || !a.norm_w || !a.ssq || a.np * 16 != a.K || a.np > 512 || KT % KS ||
+        a.K / KS > 512 || (a.K / KS) % 4)
+      return -1;
+    const size_t lds = (size_t)KS * a.M * (a.K / KS + 8) * 2;
+    mm_kernel<KS, RT, 1, EPI, U, true><<<grid, 64 * KS, lds, s>>>(a);
+    return 0;
   }
   if (nb == 1) {
     mm_kernel<KS, RT, 1, EPI, U, false><<<grid, 64 * KS, 0, s>>>(a);
@@ -810,8 +860,9 @@ int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, h
   return -1;
 }
 
-bool mm_can_fuse_norm(int M, int K) {
-  return M <= 8 && K <= 8192 && K % 4 == 0 && (size_t)M * (K + 8) * 2 <= (size_t)XN_LDS_BYTES;
+bool mm_can_norm_on_load(int M, int K) {
+  constexpr int KS = 16;  // launch_mm's one-column-tile geometry
+  return M <= XS_MAX_M && K % (32 * KS) == 0 && K / KS <= 512 && K / 16 <= 512;
 }
 
 // ---------------------------------------------------------------------------

@@ -9,7 +9,7 @@ import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
-KINDS = {0: "qkv", 1: "attn_output", 2: "gate_up", 3: "down", 4: "lm_head", 5: "qkv+norm", 6: "gate_up+norm",
+KINDS = {0: "qkv", 1: "attn_output", 2: "gate_up", 3: "down", 4: "lm_head", 5: "qkv+norm_on_load", 6: "gate_up+norm_on_load",
          7: "attention"}
 
 
@@ -25,7 +25,7 @@ def main():
     eng = Engine(f"synthetic:{args.model}:seed=0", n_ctx=512, n_seq_max=64)
     for M in [int(x) for x in args.rows.split(",")]:
         for k, name in KINDS.items():
-            if k in (5, 6) and M > 8:
+            if k in (5, 6) and M > 4:
                 continue
             us, b = eng.profile_kernel(k, M, iters=3)
             print(f"M={M:<3d} {name:14s} {us:9.2f} us  {b / us / 1e3:8.1f} GB/s", flush=True)

@@ -29,21 +29,21 @@ def _db(path):
     return sqlite3.connect(path)
 
 
-def stats(path):
+def stats(path, by_grid=False):
     con = _db(path)
     agg = collections.defaultdict(list)
     if con is not None:
-        for name, s, e in con.execute("select name, start, end from kernels"):
-            agg[name].append(e - s)
+        for name, s, e, gx, gy in con.execute("select name, start, end, grid_x, grid_y from kernels"):
+            agg[f"{name} [{gx}x{gy}]" if by_grid else name].append(e - s)
     else:
         for f in glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
                 agg[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     tot = sum(sum(v) for v in agg.values())
     rows = sorted(agg.items(), key=lambda kv: -sum(kv[1]))
-    print(f"{'kernel':90s} {'calls':>6s} {'avg_us':>9s} {'min_us':>9s} {'max_us':>9s} {'total_ms':>9s} {'share':>6s}")
+    print(f"{'kernel':100s} {'calls':>6s} {'avg_us':>9s} {'min_us':>9s} {'max_us':>9s} {'total_ms':>9s} {'share':>6s}")
     for name, d in rows:
-        print(f"{name[:90]:90s} {len(d):6d} {sum(d)/len(d)/1e3:9.2f} {min(d)/1e3:9.2f} {max(d)/1e3:9.2f} "
+        print(f"{name[-100:]:100s} {len(d):6d} {sum(d)/len(d)/1e3:9.2f} {min(d)/1e3:9.2f} {max(d)/1e3:9.2f} "
               f"{sum(d)/1e6:9.3f} {100*sum(d)/tot:5.1f}%")
 
 
@@ -53,12 +53,12 @@ def pmc(paths):
         con = _db(path)
         for name, cn, v in con.execute("select kernel_name, counter_name, value from counters_collection"):
             agg[name][cn].append(v)
-    print(f"{'kernel':90s} {'counter':12s} {'n':>5s} {'mean_KiB':>12s} {'HBM_MB/launch':>14s}")
+    print(f"{'kernel':100s} {'counter':12s} {'n':>5s} {'mean_KiB':>12s} {'HBM_MB/launch':>14s}")
     for name in sorted(agg, key=lambda n: -max(sum(v) for v in agg[n].values())):
         for cn, v in sorted(agg[name].items()):
             m = sum(v) / len(v)
             byt = m * 1024 * (2 if cn == "FETCH_SIZE" else 1)
-            print(f"{name[:90]:90s} {cn:12s} {len(v):5d} {m:12.1f} {byt/1e6:14.3f}")
+            print(f"{name[-100:]:100s} {cn:12s} {len(v):5d} {m:12.1f} {byt/1e6:14.3f}")
 
 
 def traffic(fetch_dir, write_dir, kernel, out, label):
@@ -87,7 +87,7 @@ def traffic(fetch_dir, write_dir, kernel, out, label):
 
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
-        stats(sys.argv[2])
+        stats(sys.argv[2], by_grid=len(sys.argv) > 3 and sys.argv[3] == "grid")
     elif sys.argv[1] == "traffic":
         traffic(*sys.argv[2:7])
     else:
