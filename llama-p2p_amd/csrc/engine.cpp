@@ -125,6 +125,16 @@ struct mx_engine {
   // written by the residual-stream producer (no norm launches); MX_NO_NORM_ON_LOAD=1 for A/B runs
   bool norm_on_load = getenv("MX_NO_NORM_ON_LOAD") == nullptr;
   float* ssq = nullptr;  // [MAX_ROWS][n_embd/16] per-tile sums of squares of x
+  // persistent decode kernel (pdk.hip) for <= PDK_MAX_M-token full-model steps: opt-in (MX_PDK=1) --
+  // correct, but measured slower than the per-op kernels this round (profiles/)
+  bool use_pdk = false;
+  int pdk_grid = 0;
+  PdkLayer* d_pdk_layers = nullptr;
+  float* kvs = nullptr;
+  unsigned* pdk_sync = nullptr;
+  unsigned long long* pdk_trace = nullptr;  // mx_debug_pdk_trace only
+  int init_pdk();
+  int check_pdk();
   bool use_wide = getenv("MX_NO_WIDE") == nullptr;  // 17..64-row forward through mm_wide (LDS-shared activations)
   float* slabs = nullptr;                           // split-K partials [8][MAX_ROWS][n_embd + 2 n_embd_kv]
   size_t slab_stride = 0;
@@ -264,6 +274,43 @@ int mx_engine::init_common() {
   HIPC(hipMemsetAsync(attn_out, 0, (size_t)R * n_embd * 2, stream));
   HIPC(hipMemsetAsync(act, 0, (size_t)R * n_ff * 2, stream));
   for (int i = 0; i < n_seq_max; i++) free_slots.push_back(n_seq_max - 1 - i);
+  return 0;
+}
+
+int mx_engine::init_pdk() {
+  if (!getenv("MX_PDK") || getenv("MX_NO_PDK") || !has_embed || !has_head) return 0;
+  hipDeviceProp_t prop;
+  HIPC(hipGetDeviceProperties(&prop, device));
+  const int grid = prop.multiProcessorCount;
+  if (!pdk_supported(1, n_embd, n_ff, n_head, n_head_kv, head_dim, n_vocab, grid)) return 0;
+  const size_t lds = pdk_lds_bytes(PDK_MAX_M, n_embd, n_ff, n_head, n_head_kv, head_dim);
+  if (lds > 160 * 1024 || pdk_occupancy(head_dim, n_head / n_head_kv, lds) < 1) return 0;
+  std::vector<PdkLayer> hl(layers.size());
+  for (size_t i = 0; i < layers.size(); i++) {
+    hl[i].qkv = layers[i].qkv; hl[i].o = layers[i].o; hl[i].gu = layers[i].gu; hl[i].down = layers[i].down;
+    hl[i].attn_norm = layers[i].attn_norm; hl[i].ffn_norm = layers[i].ffn_norm;
+    hl[i].kc = kcache + layer_kv_stride * i; hl[i].vc = vcache + layer_kv_stride * i;
+  }
+  if (int rc = alloc((void**)&d_pdk_layers, hl.size() * sizeof(PdkLayer))) return rc;
+  HIPC(hipMemcpy(d_pdk_layers, hl.data(), hl.size() * sizeof(PdkLayer), hipMemcpyHostToDevice));
+  if (int rc = alloc((void**)&kvs, (size_t)PDK_MAX_M * 2 * n_embd_kv * 4)) return rc;
+  if (int rc = alloc((void**)&pdk_sync, PDK_SYNC_BYTES)) return rc;
+  HIPC(hipMemset(pdk_sync, 0, PDK_SYNC_BYTES));
+  pdk_grid = grid;
+  use_pdk = true;
+  return 0;
+}
+
+// a persistent-kernel barrier that timed out (grid not co-resident) leaves sync[1] != 0
+int mx_engine::check_pdk() {
+  if (!use_pdk) return 0;
+  unsigned flag = 0;
+  HIPC(hipMemcpy(&flag, pdk_sync + 32 * 33, 4, hipMemcpyDeviceToHost));  // pdk.hip sync_err()
+  if (flag) {
+    use_pdk = false;
+    return fail(MX_ERR_HIP, "persistent decode kernel: grid barrier " + std::to_string(flag - 1) +
+                                " timed out (work-groups not co-resident); set MX_NO_PDK=1");
+  }
   return 0;
 }
 
@@ -428,6 +475,23 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
   }
   if (wide) return enqueue_forward_wide(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next,
                                         pos_next, hist, hist_stride, hist_count, max_hist, s);
+  if (use_pdk && nol && M <= PDK_MAX_M && !x_in && !x_out && head && !rowmap && n_out == M) {
+    PdkArgs pa{};
+    pa.M = M; pa.n_layer = (int)layers.size(); pa.h = h; pa.kv = kv; pa.ff = ff; pa.n_head = n_head;
+    pa.n_head_kv = n_head_kv; pa.head_dim = head_dim; pa.n_vocab = n_vocab; pa.eps = eps;
+    pa.attn_scale = 1.0f / sqrtf((float)head_dim); pa.layers = d_pdk_layers; pa.output = output;
+    pa.out_norm = out_norm; pa.pos = pos; pa.slot = slot; pa.x = x; pa.ssq = ssq; pa.q = q; pa.kvs = kvs;
+    pa.attn_out = attn_out; pa.act = act; pa.logits = logits; pa.rope_cs = rope_cs; pa.n_ctx = n_ctx;
+    pa.ctx_stride = ctx_stride; pa.slot_stride = slot_stride; pa.sync = pdk_sync; pa.img_pitch = pdk_pitch(h, ff);
+    pa.head = true;
+    pa.trace = pdk_trace;
+    if (launch_pdk(pa, pdk_grid, s)) return fail(MX_ERR_HIP, "persistent decode kernel launch");
+    if (argmax)
+      launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, ids_next, pos_next, hist, hist_stride,
+                    hist_count, max_hist, s);
+    HIPC(hipGetLastError());
+    return 0;
+  }
   // on-load only for attn_norm -> qkv: qkv's 384 work-groups run 1.5 rounds, so its per-work-group
   // prologue costs less than a norm launch; gate/up (7 rounds) and lm_head (31) keep the norm kernel
   // (tools/kernel_probe.py, profiles/round1_norm_on_load.txt)
@@ -579,7 +643,7 @@ int mx_engine::forward_rows_chunk(int n, const int32_t* slots, const int32_t* po
     return rc;
   if (head && logits_host) HIPC(hipMemcpyAsync(logits_host, logits, (size_t)n * n_vocab * 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
-  return 0;
+  return check_pdk();
 }
 
 // ---------------------------------------------------------------- scheduler
@@ -706,6 +770,7 @@ int mx_engine::sched_step(std::vector<Request*>& rows) {
     HIPC(hipMemcpyAsync(lg.data(), logits, (size_t)M * n_vocab * 4, hipMemcpyDeviceToHost, s));
   }
   HIPC(hipStreamSynchronize(s));
+  if (int rc = check_pdk()) return rc;
   std::lock_guard<std::mutex> lk(mu);
   for (int i = 0; i < M; i++) {
     Request* r = rows[i];
@@ -847,6 +912,7 @@ int mx_engine_create(const char* model_path, const mx_opts* opts, mx_engine** ou
     rc = e->load_gguf(path);
   }
   if (rc) return rc;
+  if ((rc = e->init_pdk())) return rc;
   *out = e.release();
   return 0;
 }
@@ -860,6 +926,7 @@ int mx_engine_info(const mx_engine* e, mx_model_info* o) {
   o->eps = e->eps; o->rope_base = e->rope_base; o->bos_id = e->bos; o->eos_id = e->eos;
   o->n_ctx = e->n_ctx; o->n_seq_max = e->n_seq_max; o->layer_begin = e->lb; o->layer_end = e->le;
   o->has_embed = e->has_embed; o->has_head = e->has_head; o->weight_bytes = e->weight_bytes;
+  o->persistent_decode = e->use_pdk ? 1 : 0; o->persistent_grid = e->pdk_grid;
   return 0;
 }
 
@@ -1031,6 +1098,7 @@ int mx_batch_tokens(mx_engine* e, mx_batch* b, int32_t* out, int cap, int* n_ste
   std::lock_guard<std::mutex> lk(e->gpu_mu);
   hipSetDevice(e->device);
   HIPC(hipDeviceSynchronize());
+  if (int rc = e->check_pdk()) return rc;
   std::vector<int32_t> cnt(b->M);
   HIPC(hipMemcpy(cnt.data(), b->d_hist_count, b->M * 4, hipMemcpyDeviceToHost));
   if (n_steps) *n_steps = cnt[0];
@@ -1059,11 +1127,40 @@ void mx_batch_destroy(mx_engine* e, mx_batch* b) {
   delete b;
 }
 
+// Diagnostics: one persistent-kernel step of M rows (slots 0..M-1 at position pos) with per-phase
+// wall-clock stamps; out receives [grid][5*n_layer+1][3] uint64 (start, image built, work end) at 100 MHz.
+int mx_debug_pdk_trace(mx_engine* e, int M, int pos, uint64_t* out, int cap, int* grid, int* nphase) {
+  if (!e || !e->use_pdk || M < 1 || M > PDK_MAX_M) return fail(MX_ERR_STATE, "persistent decode kernel not active");
+  std::lock_guard<std::mutex> lk(e->gpu_mu);
+  hipSetDevice(e->device);
+  hipStream_t s = e->stream;
+  const int np = 5 * (int)e->layers.size() + 1;
+  const size_t n = (size_t)e->pdk_grid * np * 3;
+  std::vector<int32_t> ids(M, 1), ps(M, pos), sl(M);
+  for (int i = 0; i < M; i++) sl[i] = i % e->n_seq_max;
+  HIPC(hipMemcpyAsync(e->d_ids, ids.data(), M * 4, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(e->d_pos, ps.data(), M * 4, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(e->d_slot, sl.data(), M * 4, hipMemcpyHostToDevice, s));
+  unsigned long long* ts = nullptr;
+  HIPC(hipMalloc((void**)&ts, n * 8));
+  HIPC(hipMemsetAsync(ts, 0, n * 8, s));
+  e->pdk_trace = ts;
+  int rc = e->enqueue_forward(M, e->d_ids, e->d_pos, e->d_slot, nullptr, nullptr, true, nullptr, M, false, nullptr,
+                              nullptr, nullptr, 0, nullptr, 0, s);
+  e->pdk_trace = nullptr;
+  if (!rc) rc = hipStreamSynchronize(s) == hipSuccess ? e->check_pdk() : fail(MX_ERR_HIP, "sync");
+  if (!rc && out) hipMemcpy(out, ts, std::min(n, (size_t)cap) * 8, hipMemcpyDeviceToHost);
+  hipFree(ts);
+  if (grid) *grid = e->pdk_grid;
+  if (nphase) *nphase = np;
+  return rc;
+}
+
 int mx_sync(mx_engine* e) {
   if (!e) return fail(MX_ERR_ARG, "null engine");
   hipSetDevice(e->device);
   HIPC(hipDeviceSynchronize());
-  return 0;
+  return e->check_pdk();
 }
 
 int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, double* bytes) {

@@ -74,6 +74,48 @@ struct AttnArgs {
   float scale;
 };
 
+// Persistent decode kernel (pdk.hip): one launch runs every layer + lm_head for <= PDK_MAX_M tokens
+constexpr int PDK_WAVES = 8;    // waves per work-group (one work-group per CU: 2 waves per SIMD, 256 VGPRs each)
+constexpr int PDK_MAX_M = 4;
+constexpr int PDK_MAX_XT = 4;   // residual tiles kept in LDS per work-group
+constexpr int PDK_SYNC_BYTES = 34 * 128;  // barrier counter tree + flags + timeout word
+
+struct PdkLayer {
+  const uint16_t *qkv, *o, *gu, *down;  // packed tiles
+  const float *attn_norm, *ffn_norm;
+  _Float16 *kc, *vc;                     // this layer's K / V^T cache
+};
+
+struct PdkArgs {
+  int M, n_layer, h, kv, ff, n_head, n_head_kv, head_dim, n_vocab;
+  float eps, attn_scale;
+  const PdkLayer* layers;  // device array [n_layer]
+  const uint16_t* output;
+  const float* out_norm;
+  const int* pos;          // [M]
+  const int* slot;         // [M]
+  float* x;                // residual stream [M][h] (embedded before the launch)
+  float* ssq;              // [M][h/16] per-tile sums of squares of x
+  float* q;                // [M][h]
+  float* kvs;              // [M][2*kv] this step's post-RoPE K and V (attention reads them here)
+  uint16_t* attn_out;      // [M][h] bf16
+  uint16_t* act;           // [M][ff] bf16
+  float* logits;           // [M][n_vocab]
+  const float* rope_cs;
+  int n_ctx, ctx_stride;
+  size_t slot_stride;
+  unsigned* sync;          // PDK_SYNC_BYTES: barrier counters, flags, timeout word (zeroed by launch_pdk)
+  int img_pitch;           // pdk_pitch(h, ff)
+  bool head;               // run lm_head after the last layer
+  unsigned long long* trace;  // optional [grid][n_phase][3] wall-clock (100 MHz) stamps: start, B image built, work end
+};
+
+int pdk_pitch(int h, int ff);
+size_t pdk_lds_bytes(int M, int h, int ff, int n_head, int n_head_kv, int head_dim);
+bool pdk_supported(int M, int h, int ff, int n_head, int n_head_kv, int head_dim, int n_vocab, int grid);
+int pdk_occupancy(int head_dim, int group, size_t lds);  // resident work-groups per CU
+int launch_pdk(const PdkArgs& a, int grid, hipStream_t s);
+
 // packing / synthetic weights.  mode: PACK_ROWS (logical row r -> packed row r + offset),
 // PACK_GATE / PACK_UP (ffn_gate / ffn_up rows interleaved by 8-row halves of each tile)
 enum PackMode : int { PACK_ROWS = 0, PACK_GATE = 1, PACK_UP = 2 };

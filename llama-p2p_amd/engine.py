@@ -26,7 +26,7 @@ EXPORTS = [
     "mx_opts_default", "mx_sampling_default", "mx_last_error", "mx_engine_create", "mx_engine_destroy",
     "mx_engine_info", "mx_forward_logits", "mx_forward_rows", "mx_submit", "mx_wait", "mx_batch_create",
     "mx_batch_step", "mx_batch_ids_device", "mx_batch_bind_ids", "mx_batch_tokens", "mx_batch_destroy", "mx_stage_rows",
-    "mx_profile_kernel", "mx_sync",
+    "mx_profile_kernel", "mx_sync", "mx_debug_pdk_trace",
 ]
 
 
@@ -48,7 +48,8 @@ class MxModelInfo(ctypes.Structure):
                [("eps", ctypes.c_float), ("rope_base", ctypes.c_float)] + \
                [(n, ctypes.c_int32) for n in ("bos_id", "eos_id", "n_ctx", "n_seq_max", "layer_begin",
                                               "layer_end", "has_embed", "has_head")] + \
-               [("weight_bytes", ctypes.c_uint64)]
+               [("weight_bytes", ctypes.c_uint64), ("persistent_decode", ctypes.c_int32),
+                ("persistent_grid", ctypes.c_int32)]
 
 
 class MxSampling(ctypes.Structure):
@@ -93,6 +94,7 @@ def lib() -> ctypes.CDLL:
         L.mx_stage_rows.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp]
         L.mx_profile_kernel.argtypes = [vp, i32, i32, i32, P(ctypes.c_double), P(ctypes.c_double)]
         L.mx_sync.argtypes = [vp]
+        L.mx_debug_pdk_trace.argtypes = [vp, i32, i32, vp, i32, P(i32), P(i32)]
         for name in EXPORTS:
             if name not in ("mx_opts_default", "mx_sampling_default", "mx_last_error", "mx_engine_destroy",
                             "mx_batch_destroy", "mx_batch_ids_device"):
@@ -190,6 +192,15 @@ class Engine:
         us, nb = ctypes.c_double(), ctypes.c_double()
         _check(lib().mx_profile_kernel(self._h, kind, M, iters, ctypes.byref(us), ctypes.byref(nb)))
         return us.value, nb.value
+
+    def pdk_trace(self, M: int = 1, pos: int = 100):
+        """One persistent-decode-kernel step with per-phase wall-clock stamps (100 MHz ticks):
+        returns uint64 [grid, nphase, 3] = (start, image built, work end) per work-group and phase."""
+        cap = 512 * (5 * self.info.n_layer + 1) * 3
+        buf = np.zeros(cap, dtype=np.uint64)
+        g, n = ctypes.c_int32(), ctypes.c_int32()
+        _check(lib().mx_debug_pdk_trace(self._h, M, pos, buf.ctypes.data, cap, ctypes.byref(g), ctypes.byref(n)))
+        return buf[:g.value * n.value * 3].reshape(g.value, n.value, 3)
 
     def sync(self):
         _check(lib().mx_sync(self._h))

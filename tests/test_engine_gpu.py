@@ -186,3 +186,51 @@ def test_wide_decode_batch_vs_oracle(mx, oracle_mod):
     assert exact >= 0.9 * M * (G + 1)
     b.close()
     eng.close()
+
+
+def test_persistent_decode_vs_kernels_and_oracle(mx, oracle_mod):
+    """<= 4-token steps on the Llama-3-8B hidden geometry run as ONE persistent kernel (pdk.hip:
+    grid barriers, sc1 hand-offs, weight ring across phases).  Its logits must match the oracle
+    and the per-op kernel path (MX_NO_PDK=1) within the bf16 tolerance, for 1..4 rows of
+    different slots/positions, and its greedy graph loop must follow the oracle."""
+    from llama_p2p_amd import synth
+
+    name = "test-h4096"
+    shape = synth.SHAPES[name]
+    os.environ["MX_PDK"] = "1"  # opt-in this round
+    try:
+        eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=128, n_seq_max=4)
+    finally:
+        del os.environ["MX_PDK"]
+    assert eng.info.persistent_decode == 1, "persistent decode kernel not enabled on this device"
+    ref_eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=128, n_seq_max=4)
+    assert ref_eng.info.persistent_decode == 0
+    seqs = [_seq(shape, 40, seed=90 + i) for i in range(4)]
+    for e in (eng, ref_eng):
+        for i, s in enumerate(seqs):
+            e.forward_logits(s[:30 + i], 0, slot=i)  # prefill (> 4 rows: kernel path in both)
+    om = oracle_mod.OracleModel(shape, seed=0)
+    for M in (1, 2, 3, 4):
+        slots = list(range(M))
+        pos = [30 + i for i in range(M)]
+        ids = [int(seqs[i][30 + i]) for i in range(M)]
+        got = eng.forward_rows(slots, pos, ids)
+        alt = ref_eng.forward_rows(slots, pos, ids)
+        for i in range(M):
+            ref = om.context(128).eval(seqs[i][:31 + i], 0, all_logits=True)[-1]
+            assert_logits_close(got[i:i + 1], ref[None], f"pdk M={M} row {i}")
+            assert_logits_close(got[i:i + 1], alt[i:i + 1], f"pdk vs kernels M={M} row {i}")
+    # device greedy loop (graph replay of the persistent kernel), 2 sequences
+    G = 16
+    first = [int(np.argmax(eng.forward_rows([i], [31 + i], [int(seqs[i][31 + i])])[0])) for i in range(2)]
+    b = eng.batch(slots=[0, 1], pos=[32, 33], ids=first, max_steps=G)
+    for _ in range(G):
+        b.step()
+    toks = b.tokens()
+    exact = 0
+    for i in range(2):
+        exact += check_greedy_chain(om.context(128), seqs[i][:32 + i], [first[i]] + toks[i].tolist(), f"pdk seq {i}")
+    assert exact >= 0.9 * 2 * (G + 1)
+    b.close()
+    eng.close()
+    ref_eng.close()
