@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "decode tokens/sec (node) + % HBM roofline, Llama-3-8B at 1/2/4/8-stage"
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
+MFMA_PEAK_BF16 = 2.5e15  # dense bf16 MFMA, MI355X spec (MI355X_MICROARCH.md; no sparsity)
 MB_SEQS = 32
 
 
@@ -149,8 +150,39 @@ def run_single(args):
                          "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / b1_bytes, 1)}
         b1.close()
     b.close()
+    if args.prefill_prompts > 0:
+        res["prefill"] = prefill_bench(eng, shape, args.prefill_prompts, args.prefill_len)
     eng.close()
     return res
+
+
+def prefill_bench(eng, shape, n_prompts: int, plen: int):
+    """Batched prefill: n_prompts prompts of plen tokens (seed 3) pushed through the
+    engine in 64-row chunks with no lm_head (logits of prompt tokens are not needed), timed on the
+    host around the whole pass.  MFMA utilisation = achieved dense bf16 FLOP/s / 2.5 PFLOP/s."""
+    import numpy as np
+
+    rng = np.random.default_rng(3)
+    slots, pos, ids = [], [], []
+    for i in range(n_prompts):
+        slots += [i] * plen
+        pos += list(range(plen))
+        ids += [1] + [int(t) for t in rng.integers(3, shape.n_vocab, plen - 1)]
+    eng.forward_rows(slots[:64], pos[:64], ids[:64], want_logits=False)  # warm
+    eng.sync()
+    t0 = time.perf_counter()
+    eng.forward_rows(slots, pos, ids, want_logits=False)
+    eng.sync()
+    dt = time.perf_counter() - t0
+    n_tok = len(ids)
+    h, ff, L = shape.n_embd, shape.n_ff, shape.n_layer
+    kv = h // shape.n_head * shape.n_head_kv
+    linear = L * (h * (h + 2 * kv) + h * h + 3 * h * ff)
+    attn = 4 * L * h * n_prompts * plen * (plen + 1) // 2  # QK^T + PV, causal
+    flops = 2 * n_tok * linear + attn
+    return {"tok_s": round(n_tok / dt, 1), "ms": round(dt * 1e3, 2), "tokens": n_tok,
+            "tflops": round(flops / dt / 1e12, 1), "mfma_frac": round(flops / dt / MFMA_PEAK_BF16, 4),
+            "sample": f"{n_prompts} prompts x {plen} tokens, 64-row chunks, no lm_head"}
 
 
 def main():
@@ -163,6 +195,8 @@ def main():
     ap.add_argument("--n-ctx", type=int, default=512)
     ap.add_argument("--batch1-steps", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--prefill-prompts", type=int, default=32)
+    ap.add_argument("--prefill-len", type=int, default=128)
     ap.add_argument("--force-pipeline", action="store_true", help="run the torch.distributed pipeline path even at N=1")
     args = ap.parse_args()
 
@@ -186,6 +220,8 @@ def main():
     }
     if "batch1" in res:
         line["batch1"] = res["batch1"]
+    if "prefill" in res:
+        line["prefill"] = res["prefill"]
     if not args.no_cpu_baseline:
         try:
             line["cpu_baseline"] = cpu_baseline(args.model)

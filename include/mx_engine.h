@@ -94,10 +94,10 @@ int mx_engine_info(const mx_engine* e, mx_model_info* out);
 
 /* Parity hook: evaluate n tokens of sequence `slot` at positions pos0..pos0+n-1
  * (prefill or decode, chunked internally by 64 rows) and copy the f32 logits of
- * every row to logits_out[n][n_vocab] (may be NULL). */
+ * every row to logits_out[n][n_vocab]; NULL skips lm_head entirely (prefill). */
 int mx_forward_logits(mx_engine* e, int slot, const int32_t* ids, int n, int pos0, float* logits_out);
 
-/* General rows forward: row i is token ids[i] of sequence slots[i] at pos[i]. */
+/* General rows forward: row i is token ids[i] of sequence slots[i] at pos[i]; logits_out as above. */
 int mx_forward_rows(mx_engine* e, int n, const int32_t* slots, const int32_t* pos, const int32_t* ids,
                     float* logits_out);
 

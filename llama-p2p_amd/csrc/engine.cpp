@@ -107,6 +107,7 @@ struct GraphKey {
 
 struct mx_batch {
   int M = 0, max_steps = 0;
+  bool distinct = false;  // every row its own slot (decode); see mx_engine::rows_distinct
   int max_pos = 0;  // host mirror of the largest position, so steps never run past n_ctx
   int *d_ids = nullptr, *d_pos = nullptr, *d_slot = nullptr, *d_hist = nullptr, *d_hist_count = nullptr;
   bool ids_external = false;
@@ -125,6 +126,9 @@ struct mx_engine {
   // written by the residual-stream producer (no norm launches); MX_NO_NORM_ON_LOAD=1 for A/B runs
   bool norm_on_load = getenv("MX_NO_NORM_ON_LOAD") == nullptr;
   float* ssq = nullptr;  // [MAX_ROWS][n_embd/16] per-tile sums of squares of x
+  // rows of the next forward belong to distinct sequences (decode): no row attends to another row's
+  // new K/V, so the wide path lets the attention kernel finish q/k/v from the split-K slabs
+  bool rows_distinct = false;
   // persistent decode kernel (pdk.hip) for <= PDK_MAX_M-token full-model steps: opt-in (MX_PDK=1) --
   // correct, but measured slower than the per-op kernels this round (profiles/)
   bool use_pdk = false;
@@ -189,7 +193,7 @@ struct mx_engine {
                            int n_out, bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride,
                            int* hist_count, int max_hist, hipStream_t s);
   int forward_rows_chunk(int n, const int32_t* slots, const int32_t* pos, const int32_t* ids, const void* x_in,
-                         void* x_out, float* logits_host, hipStream_t s);
+                         void* x_out, float* logits_host, hipStream_t s, bool last_row_only = false);
   void scheduler_loop();
   int sched_step(std::vector<Request*>& rows);
   int prefill(Request* r, std::vector<float>& last_logits);
@@ -573,8 +577,13 @@ int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
     a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
     a.slot_stride = slot_stride;
-    if (launch_mm_wide(EPI_QKV, a, slabs, slab_stride, s) < 0) return fail(MX_ERR_ARG, "wide qkv launch shape");
+    const int qsplit = launch_mm_wide(EPI_QKV, a, slabs, slab_stride, s, !rows_distinct);
+    if (qsplit < 0) return fail(MX_ERR_ARG, "wide qkv launch shape");
     AttnArgs at{};
+    if (rows_distinct) {  // the attention kernel finishes q/k/v from the split-K slabs
+      at.slabs = slabs; at.nslab = qsplit; at.slab_stride = slab_stride; at.rope_cs = rope_cs; at.kc_w = kc;
+      at.vc_w = vc;
+    }
     at.q = q; at.kc = kc; at.vc = vc; at.pos = pos; at.slot = slot;
     at.out = attn_out; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
     at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;
@@ -627,8 +636,11 @@ __global__ void advance_pos_kernel(int* pos, int M) {
 }
 
 // rows forward, n <= MAX_ROWS, logits for all rows copied to host if requested
+// lm_head runs only when logits are wanted: for every row, or (last_row_only, prompt chunks) for the
+// last row alone -- a prefill never streams the 1 GB output matrix per 64-row chunk.
 int mx_engine::forward_rows_chunk(int n, const int32_t* slots, const int32_t* pos, const int32_t* ids,
-                                  const void* x_in, void* x_out, float* logits_host, hipStream_t s) {
+                                  const void* x_in, void* x_out, float* logits_host, hipStream_t s,
+                                  bool last_row_only) {
   for (int i = 0; i < n; i++) {
     if (slots[i] < 0 || slots[i] >= n_seq_max) return fail(MX_ERR_ARG, "slot out of range");
     if (pos[i] < 0 || pos[i] >= n_ctx) return fail(MX_ERR_CTX, "position outside n_ctx");
@@ -637,11 +649,20 @@ int mx_engine::forward_rows_chunk(int n, const int32_t* slots, const int32_t* po
   if (ids) HIPC(hipMemcpyAsync(d_ids, ids, n * 4, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(d_pos, pos, n * 4, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(d_slot, slots, n * 4, hipMemcpyHostToDevice, s));
-  const bool head = has_head && !x_out;
-  if (int rc = enqueue_forward(n, d_ids, d_pos, d_slot, x_in, x_out, head, nullptr, n, false, nullptr, nullptr,
-                               nullptr, 0, nullptr, 0, s))
-    return rc;
-  if (head && logits_host) HIPC(hipMemcpyAsync(logits_host, logits, (size_t)n * n_vocab * 4, hipMemcpyDeviceToHost, s));
+  const bool head = has_head && !x_out && logits_host;
+  const int n_out = last_row_only ? 1 : n;
+  std::vector<int32_t> sorted(slots, slots + n);
+  std::sort(sorted.begin(), sorted.end());
+  rows_distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+  if (head && last_row_only) {
+    const int last = n - 1;
+    HIPC(hipMemcpyAsync(d_rowmap, &last, 4, hipMemcpyHostToDevice, s));
+  }
+  const int frc = enqueue_forward(n, d_ids, d_pos, d_slot, x_in, x_out, head, head && last_row_only ? d_rowmap : nullptr,
+                                  n_out, false, nullptr, nullptr, nullptr, 0, nullptr, 0, s);
+  rows_distinct = false;
+  if (frc) return frc;
+  if (head) HIPC(hipMemcpyAsync(logits_host, logits, (size_t)n_out * n_vocab * 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   return check_pdk();
 }
@@ -714,15 +735,14 @@ int32_t mx_engine::sample_host(Request* r, const float* lg) {
 int mx_engine::prefill(Request* r, std::vector<float>& last) {
   const int n = (int)r->prompt.size();
   std::vector<int32_t> slots(MAX_ROWS, r->slot), pos(MAX_ROWS);
-  std::vector<float> lg((size_t)MAX_ROWS * n_vocab);
+  last.resize(n_vocab);
   for (int i = 0; i < n; i += MAX_ROWS) {
     int m = std::min(MAX_ROWS, n - i);
     for (int j = 0; j < m; j++) pos[j] = i + j;
-    bool lastc = i + m == n;
+    const bool lastc = i + m == n;  // logits of the prompt's last token only
     if (int rc = forward_rows_chunk(m, slots.data(), pos.data(), r->prompt.data() + i, nullptr, nullptr,
-                                    lastc ? lg.data() : nullptr, stream))
+                                    lastc ? last.data() : nullptr, stream, true))
       return rc;
-    if (lastc) last.assign(lg.begin() + (size_t)(m - 1) * n_vocab, lg.begin() + (size_t)m * n_vocab);
   }
   r->pos = n;
   return 0;
@@ -742,6 +762,8 @@ int mx_engine::sched_step(std::vector<Request*>& rows) {
   HIPC(hipMemcpyAsync(d_ids, ids.data(), M * 4, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(d_pos, pos.data(), M * 4, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(d_slot, slots.data(), M * 4, hipMemcpyHostToDevice, s));
+  rows_distinct = true;  // one row per active request, each its own slot
+  struct Reset { bool& f; ~Reset() { f = false; } } reset_distinct{rows_distinct};
   auto it = sched_graphs.find(M);
   if (use_graphs && it == sched_graphs.end()) {
     hipGraph_t g;
@@ -1026,6 +1048,11 @@ int mx_batch_create(mx_engine* e, int M, const int32_t* slots, const int32_t* po
   std::unique_ptr<mx_batch> b(new mx_batch());
   b->M = M;
   b->max_steps = max_steps;
+  {
+    std::vector<int32_t> sorted(slots, slots + M);
+    std::sort(sorted.begin(), sorted.end());
+    b->distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+  }
   b->max_pos = max_pos;
   HIPC(hipMalloc((void**)&b->d_ids, M * 4));
   HIPC(hipMalloc((void**)&b->d_pos, M * 4));
@@ -1068,6 +1095,8 @@ int mx_batch_step(mx_engine* e, mx_batch* b, const void* x_in, void* x_out, void
   if (head && !e->has_head) return fail(MX_ERR_STATE, "x_out is required on a non-final pipeline stage");
   if (!x_in && !e->has_embed) return fail(MX_ERR_STATE, "x_in is required on a non-first pipeline stage");
   auto body = [&]() -> int {
+    e->rows_distinct = b->distinct;
+    struct Reset { bool& f; ~Reset() { f = false; } } reset_distinct{e->rows_distinct};
     if (int rc = e->enqueue_forward(b->M, b->d_ids, b->d_pos, b->d_slot, x_in, x_out, head, nullptr, b->M, head,
                                     b->d_ids, b->d_pos, b->d_hist, b->max_steps, b->d_hist_count, b->max_steps, s))
       return rc;

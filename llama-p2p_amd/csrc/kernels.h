@@ -72,6 +72,13 @@ struct AttnArgs {
   int M, n_head, n_head_kv, head_dim, n_ctx, ctx_stride;
   size_t slot_stride;
   float scale;
+  // qkv still as split-K partial slabs (wide path): the kernel sums them in slab order, applies
+  // RoPE, stores this position's K/V into the caches and keeps q and the new K/V in LDS
+  const float* slabs;    // [nslab][M][n_q + 2*n_kv] or nullptr (q / caches already final)
+  int nslab;
+  size_t slab_stride;
+  const float* rope_cs;  // [n_ctx][head_dim/2][2]
+  _Float16 *kc_w, *vc_w; // writable views of kc / vc
 };
 
 // Persistent decode kernel (pdk.hip): one launch runs every layer + lm_head for <= PDK_MAX_M tokens
@@ -137,7 +144,8 @@ bool mm_can_norm_on_load(int M, int K);
 // 17..64 rows: activation chunks shared through LDS.  EPI_QKV / EPI_RESID run split-K into
 // `slabs` ([ksplit][MAX_ROWS][N] floats, slab_stride apart); returns the split used (the caller
 // folds RESID partials with launch_resid_norm; QKV partials are finished inside), or -1.
-int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s);
+int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s,
+                   bool qkv_finish = true);  // EPI_QKV: false leaves the slabs to the attention kernel
 // x[c] += sum of nslab partial slabs (fixed order); then, if y, y = bf16(rmsnorm(x) * w)
 void launch_resid_norm(uint16_t* y, int ldy, float* x, const float* slabs, int nslab, size_t slab_stride,
                        const float* w, int M, int n, float eps, hipStream_t s);  // X == nullptr path (RMS_NORM fused into the GEMV) is legal

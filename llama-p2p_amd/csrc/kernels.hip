@@ -821,7 +821,7 @@ static int pick_ksplit(int KT, int target) {
 
 // Geometry from tools/gemv_sweep.hip (wide) on MI355X, Llama-3-8B shapes at 32 rows
 // (profiles/round1_gemv_sweep_wide.txt): two row tiles per wave, K split until ~256 work-groups.
-int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s) {
+int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s, bool qkv_finish) {
   if (a.M < 1 || a.M > MAX_ROWS || a.K % TILE_K != 0 || a.N % TILE_N != 0 || !a.X) return -1;
   const int ntiles = a.N / TILE_N, KT = a.K / TILE_K;
   if (KT % 4) return -1;
@@ -850,7 +850,7 @@ int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, h
                    : cfg == 1 ? launch_wide_cfg<2, 1, EPI_SLAB>(p, ksplit, s)
                               : launch_wide_cfg<4, 1, EPI_SLAB>(p, ksplit, s);
       if (rc) return -1;
-      if (epi == EPI_QKV) {
+      if (epi == EPI_QKV && qkv_finish) {
         const int total = a.M * a.N / 4;
         qkv_finish_kernel<<<(total + 255) / 256, 256, 0, s>>>(a, slabs, ksplit, slab_stride);
       }
@@ -894,10 +894,49 @@ __global__ __launch_bounds__(512) void attn_decode_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) _Float16 Ps[NW][16][CH + 8];
   __shared__ float Om[NW][G][D];
   __shared__ float Mm[NW][G], Ll[NW][G];
+  __shared__ __attribute__((aligned(16))) float qs[G * D + 2 * D];  // finished q rows, then this position's K, V
+
+  // wide path: q/k/v of this (kv head, token) are still split-K partial slabs -- sum them in slab
+  // order (bit-identical to qkv_finish_kernel), RoPE q and k, write this position's K and V into
+  // the caches for later steps, and keep all of it in LDS for this step
+  const bool fin = a.slabs != nullptr;
+  if (fin) {
+    const int nq = a.n_head * D, nkv = a.n_head_kv * D, N = nq + 2 * nkv;
+    for (int u = threadIdx.x; u < (G * D + 2 * D) / 4; u += 64 * NW) {
+      const int i = u * 4;  // qs index
+      const int row = i < G * D ? kvh * G * D + i : i < G * D + D ? nq + kvh * D + (i - G * D)
+                                                                   : nq + nkv + kvh * D + (i - G * D - D);
+      f32x4 v = *reinterpret_cast<const f32x4*>(a.slabs + (size_t)c * N + row);
+      for (int k = 1; k < a.nslab; ++k) v += *reinterpret_cast<const f32x4*>(a.slabs + k * a.slab_stride + (size_t)c * N + row);
+      const int dd = i % D;
+      if (i < G * D + D && pos < a.n_ctx) {  // RoPE (mode NORM: adjacent pairs) on q and k
+        const f32x4 csv = *reinterpret_cast<const f32x4*>(a.rope_cs + ((size_t)pos * (D / 2) + dd / 2) * 2);
+        const f32x4 s = v;
+        v[0] = s[0] * csv[0] - s[1] * csv[1];
+        v[1] = s[0] * csv[1] + s[1] * csv[0];
+        v[2] = s[2] * csv[2] - s[3] * csv[3];
+        v[3] = s[2] * csv[3] + s[3] * csv[2];
+      }
+      *reinterpret_cast<f32x4*>(qs + i) = v;
+      if (i >= G * D && pos < a.n_ctx) {
+        const size_t sb = (size_t)slot * a.slot_stride;
+        if (i < G * D + D) {
+          _Float16* kp = a.kc_w + sb + ((size_t)kvh * a.ctx_stride + pos) * D + dd;
+          *reinterpret_cast<f16x4*>(kp) = f16x4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+        } else {
+          _Float16* vt = a.vc_w + sb + ((size_t)kvh * D + dd) * a.ctx_stride + pos;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) vt[(size_t)j * a.ctx_stride] = (_Float16)v[j];
+        }
+      }
+    }
+    __syncthreads();
+  }
 
   // A operand of QK^T: rows = heads of the group (rows >= G are zero)
   f16x8 qa[QK];
-  const float* qrow = a.q + (size_t)c * a.n_head * D + (size_t)(kvh * G + (r16 < G ? r16 : 0)) * D;
+  const float* qrow = fin ? qs + (r16 < G ? r16 : 0) * D
+                          : a.q + (size_t)c * a.n_head * D + (size_t)(kvh * G + (r16 < G ? r16 : 0)) * D;
 #pragma unroll
   for (int kk = 0; kk < QK; ++kk) {
     f32x4 v0 = *reinterpret_cast<const f32x4*>(qrow + kk * 32 + 8 * q4);
@@ -936,6 +975,18 @@ __global__ __launch_bounds__(512) void attn_decode_kernel(AttnArgs a) {
 #pragma unroll
     for (int t = 0; t < DT; ++t)
       vf[t] = *reinterpret_cast<const f16x8*>(Vb + (size_t)(t * 16 + r16) * a.ctx_stride + pb);
+    if (fin) {  // this position's K/V: the values just finished in LDS (the cache lines may be in flight)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        if (p0 + 16 * t + r16 == pos)
+#pragma unroll
+          for (int kk = 0; kk < QK; ++kk)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) kf[t][kk][j] = (_Float16)qs[G * D + 8 * q4 + kk * 32 + j];
+      if (pos >= pb && pos < pb + 8)
+#pragma unroll
+        for (int t = 0; t < DT; ++t) vf[t][pos - pb] = (_Float16)qs[G * D + D + t * 16 + r16];
+    }
     // S[head][pos] for two 16-position tiles
     f32x4 s[2];
 #pragma unroll

@@ -140,11 +140,12 @@ class Engine:
         _check(lib().mx_forward_logits(self._h, slot, ids.ctypes.data, len(ids), pos0, out.ctypes.data))
         return out
 
-    def forward_rows(self, slots, pos, ids) -> np.ndarray:
+    def forward_rows(self, slots, pos, ids, want_logits: bool = True) -> Optional[np.ndarray]:
+        """Rows forward (chunked by 64); want_logits=False skips lm_head (prefill)."""
         slots, pos, ids = _i32(slots), _i32(pos), _i32(ids)
-        out = np.empty((len(ids), self.n_vocab), dtype=np.float32)
+        out = np.empty((len(ids), self.n_vocab), dtype=np.float32) if want_logits else None
         _check(lib().mx_forward_rows(self._h, len(ids), slots.ctypes.data, pos.ctypes.data, ids.ctypes.data,
-                                     out.ctypes.data))
+                                     out.ctypes.data if out is not None else None))
         return out
 
     def stage_rows(self, slots, pos, ids, x_in: int = 0, x_out: int = 0, want_logits: bool = False,
