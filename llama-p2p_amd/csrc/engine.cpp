@@ -189,6 +189,12 @@ struct mx_engine {
   int enqueue_forward(int M, const int* ids, const int* pos, const int* slot, const void* x_in, void* x_out,
                       bool head, const int* rowmap, int n_out, bool argmax, int* ids_next, int* pos_next, int* hist,
                       int hist_stride, int* hist_count, int max_hist, hipStream_t s);
+  int enqueue_forward_gemm(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap,
+                           int n_out, hipStream_t s);
+  bool gemm_ok() const {
+    return gemm_supported(n_embd + 2 * n_embd_kv, n_embd) && gemm_supported(n_embd, n_embd) &&
+           gemm_supported(2 * n_ff, n_embd) && gemm_supported(n_embd, n_ff);
+  }
   int enqueue_forward_wide(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap,
                            int n_out, bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride,
                            int* hist_count, int max_hist, hipStream_t s);
@@ -254,16 +260,16 @@ int mx_engine::init_common() {
   if (int rc = alloc((void**)&rope_cs, cs.size() * 4)) return rc;
   HIPC(hipMemcpy(rope_cs, cs.data(), cs.size() * 4, hipMemcpyHostToDevice));
 
-  const int R = MAX_ROWS;
+  const int R = PREFILL_ROWS;  // activation rows: prefill chunks (GEMM path); logits only for MAX_ROWS
   if (int rc = alloc((void**)&x, (size_t)R * n_embd * 4)) return rc;
   if (int rc = alloc((void**)&q, (size_t)R * n_embd * 4)) return rc;
   if (int rc = alloc((void**)&xn, (size_t)R * n_embd * 2)) return rc;
   if (int rc = alloc((void**)&attn_out, (size_t)R * n_embd * 2)) return rc;
   if (int rc = alloc((void**)&act, (size_t)R * n_ff * 2)) return rc;
   if (has_head) {
-    if (int rc = alloc((void**)&logits, (size_t)R * n_vocab * 4)) return rc;
+    if (int rc = alloc((void**)&logits, (size_t)MAX_ROWS * n_vocab * 4)) return rc;
   }
-  slab_stride = (size_t)R * (n_embd + 2 * n_embd_kv);
+  slab_stride = (size_t)MAX_ROWS * (n_embd + 2 * n_embd_kv);
   if (int rc = alloc((void**)&slabs, slab_stride * 8 * 4)) return rc;
   if (int rc = alloc((void**)&ssq, (size_t)R * (n_embd / 16) * 4)) return rc;
   if (int rc = alloc((void**)&am_val, (size_t)R * 64 * 4)) return rc;
@@ -477,6 +483,11 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     if (!has_embed) return fail(MX_ERR_STATE, "this stage has no token embedding: x_in required");
     launch_embed(x, tok_embd, ids, M, h, nol ? ssq : nullptr, s);
   }
+  if (M > MAX_ROWS) {
+    if (!gemm_ok() || argmax || (head && n_out > MAX_ROWS))
+      return fail(MX_ERR_ARG, "forward of > 64 rows: GEMM shapes only, logits for <= 64 rows");
+    return enqueue_forward_gemm(M, pos, slot, x_out, head, rowmap, n_out, s);
+  }
   if (wide) return enqueue_forward_wide(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next,
                                         pos_next, hist, hist_stride, hist_count, max_hist, s);
   if (use_pdk && nol && M <= PDK_MAX_M && !x_in && !x_out && head && !rowmap && n_out == M) {
@@ -630,6 +641,52 @@ int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void
   return 0;
 }
 
+// Prefill chunk of MAX_ROWS < M <= PREFILL_ROWS rows: MFMA GEMMs read each weight once per 256
+// rows (not once per 64 as the wide decode kernels would); RMS_NORM as its own launch.
+int mx_engine::enqueue_forward_gemm(int M, const int* pos, const int* slot, void* x_out, bool head,
+                                    const int* rowmap, int n_out, hipStream_t s) {
+  const int h = n_embd, kv = n_embd_kv, ff = n_ff;
+  for (int li = 0; li < (int)layers.size(); li++) {
+    const Layer& L = layers[li];
+    _Float16* kc = kcache + layer_kv_stride * li;
+    _Float16* vc = vcache + layer_kv_stride * li;
+    launch_rmsnorm(xn, h, x, L.attn_norm, nullptr, M, h, eps, s);
+    MMArgs a{};
+    a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M; a.X = xn; a.ldx = h;
+    a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
+    a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
+    a.slot_stride = slot_stride;
+    if (launch_gemm(EPI_QKV, a, s)) return fail(MX_ERR_ARG, "prefill qkv GEMM shape");
+    AttnArgs at{};
+    at.q = q; at.kc = kc; at.vc = vc; at.pos = pos; at.slot = slot;
+    at.out = attn_out; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
+    at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;
+    at.scale = 1.0f / sqrtf((float)head_dim);
+    launch_attention(at, s);
+    MMArgs b{};
+    b.W = L.o; b.N = h; b.K = h; b.X = attn_out; b.ldx = h; b.M = M; b.out = x; b.ldo = h;
+    if (launch_gemm(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "prefill attn_output GEMM shape");
+    launch_rmsnorm(xn, h, x, L.ffn_norm, nullptr, M, h, eps, s);
+    MMArgs c{};
+    c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.X = xn; c.ldx = h; c.act = act; c.lda = ff;
+    if (launch_gemm(EPI_SWIGLU, c, s)) return fail(MX_ERR_ARG, "prefill gate/up GEMM shape");
+    MMArgs d{};
+    d.W = L.down; d.N = h; d.K = ff; d.X = act; d.ldx = ff; d.M = M; d.out = x; d.ldo = h;
+    if (launch_gemm(EPI_RESID, d, s)) return fail(MX_ERR_ARG, "prefill ffn_down GEMM shape");
+  }
+  if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
+  if (head) {
+    if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
+    if (!rowmap) return fail(MX_ERR_ARG, "prefill head needs a row map");
+    launch_rmsnorm(xn, h, x, out_norm, rowmap, n_out, h, eps, s);
+    MMArgs g{};
+    g.W = output; g.N = n_vocab; g.K = h; g.M = n_out; g.X = xn; g.ldx = h; g.out = logits; g.ldo = n_vocab;
+    if (launch_mm(EPI_F32, g, s)) return fail(MX_ERR_ARG, "lm_head launch shape");
+  }
+  HIPC(hipGetLastError());
+  return 0;
+}
+
 __global__ void advance_pos_kernel(int* pos, int M) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < M) pos[i] += 1;
@@ -734,10 +791,11 @@ int32_t mx_engine::sample_host(Request* r, const float* lg) {
 
 int mx_engine::prefill(Request* r, std::vector<float>& last) {
   const int n = (int)r->prompt.size();
-  std::vector<int32_t> slots(MAX_ROWS, r->slot), pos(MAX_ROWS);
+  const int chunk = gemm_ok() ? PREFILL_ROWS : MAX_ROWS;
+  std::vector<int32_t> slots(chunk, r->slot), pos(chunk);
   last.resize(n_vocab);
-  for (int i = 0; i < n; i += MAX_ROWS) {
-    int m = std::min(MAX_ROWS, n - i);
+  for (int i = 0; i < n; i += chunk) {
+    int m = std::min(chunk, n - i);
     for (int j = 0; j < m; j++) pos[j] = i + j;
     const bool lastc = i + m == n;  // logits of the prompt's last token only
     if (int rc = forward_rows_chunk(m, slots.data(), pos.data(), r->prompt.data() + i, nullptr, nullptr,
@@ -958,8 +1016,9 @@ int mx_forward_rows(mx_engine* e, int n, const int32_t* slots, const int32_t* po
   if (!e->has_embed || !e->has_head) return fail(MX_ERR_STATE, "mx_forward_rows needs a full-model engine");
   std::lock_guard<std::mutex> lk(e->gpu_mu);
   hipSetDevice(e->device);
-  for (int i = 0; i < n; i += MAX_ROWS) {
-    int m = std::min(MAX_ROWS, n - i);
+  const int chunk = (!logits_out && e->gemm_ok()) ? PREFILL_ROWS : MAX_ROWS;  // logits: <= 64 rows per chunk
+  for (int i = 0; i < n; i += chunk) {
+    int m = std::min(chunk, n - i);
     if (int rc = e->forward_rows_chunk(m, slots + i, pos + i, ids + i, nullptr, nullptr,
                                        logits_out ? logits_out + (size_t)i * e->n_vocab : nullptr, e->stream))
       return rc;

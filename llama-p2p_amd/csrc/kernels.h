@@ -18,7 +18,8 @@ namespace mx {
 constexpr int TILE_N = 16;
 constexpr int TILE_K = 32;
 constexpr int TILE_ELEMS = TILE_N * TILE_K;
-constexpr int MAX_ROWS = 64;       // tokens per forward (4 column tiles of 16)
+constexpr int MAX_ROWS = 64;       // tokens per decode / logits forward (4 column tiles of 16)
+constexpr int PREFILL_ROWS = 4096;  // tokens per prefill forward (GEMM path, no logits): ~0.3 GB of activations for 8B
 constexpr int ATTN_CHUNK = 32;     // positions per attention wave-iteration
 constexpr int KV_POS_ALIGN = 64;   // KV rows per slot are allocated in multiples of this
 
@@ -150,6 +151,9 @@ int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, h
 void launch_resid_norm(uint16_t* y, int ldy, float* x, const float* slabs, int nslab, size_t slab_stride,
                        const float* w, int M, int n, float eps, hipStream_t s);  // X == nullptr path (RMS_NORM fused into the GEMV) is legal
 void launch_attention(const AttnArgs& a, hipStream_t s);
+// prefill (> MAX_ROWS rows): MFMA GEMM over packed weights with the same epilogues (N % 256, K % 64)
+bool gemm_supported(int N, int K);
+int launch_gemm(int epi, const MMArgs& a, hipStream_t s);
 void launch_argmax(const float* logits, int ldl, int M, int V, float* ws_val, int* ws_idx, int* tok_out,
                    int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count, int max_hist,
                    hipStream_t s);

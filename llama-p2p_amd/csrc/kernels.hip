@@ -1154,3 +1154,132 @@ void launch_argmax(const float* logits, int ldl, int M, int V, float* ws_val, in
 }
 
 }  // namespace mx
+
+namespace mx {
+
+// ---------------------------------------------------------------------------
+// Prefill GEMM (> 64 rows): out = X[M][K] . W[N][K]^T with the decode epilogues, bf16 MFMA
+// 16x16x32, f32 accumulation.  (SURVEY §8a a7, a11, a12 at prefill; §8d prefill FLOPs)
+//
+// Block = 8 waves, tile 256 weight rows x 256 tokens; wave (wn, wm) = 64 rows (4 packed row
+// tiles) x 128 tokens (8 column tiles): 32 MFMAs per 32-deep k-step.  The packed weight tiles are
+// already A fragments, so each wave streams its own straight from global memory one 64-deep
+// chunk ahead (no LDS, no transpose); the block's 256 token rows go through LDS in 64-deep chunks
+// (double buffer, one barrier per chunk) and every wave reads its B fragments there.  Blocks are
+// ordered token-block fastest, so the blocks resident at once share each weight tile through
+// L2 / Infinity Cache instead of re-reading it from HBM.
+// ---------------------------------------------------------------------------
+constexpr int GB_N = 256, GB_M = 256, GKC = 64, GPITCH = GKC + 8;
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_kernel(MMArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t xs[2][GB_M][GPITCH];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wn = w & 3, wm = w >> 2;
+  const int nmb = (a.M + GB_M - 1) / GB_M;
+  const int mb = blockIdx.x % nmb, nb = blockIdx.x / nmb;
+  const int KT = a.K / TILE_K, NC = a.K / GKC;
+  const int tile0 = nb * (GB_N / 16) + wn * 4;
+  const int m0 = mb * GB_M;
+  const int r16 = lane & 15, q4 = lane >> 4;
+
+  // token-row staging: piece p = tid + 512 i: row p / 8, 16-B segment p % 8 of the 128-B chunk row
+  const u32x4* xsrc[4];
+  int xrow[4], xseg[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = threadIdx.x + 512 * i;
+    xrow[i] = p >> 3;
+    xseg[i] = p & 7;
+    const int row = min(m0 + xrow[i], a.M - 1);  // rows past M re-read the last row (outputs dropped)
+    xsrc[i] = reinterpret_cast<const u32x4*>(a.X + (size_t)row * a.ldx + xseg[i] * 8);
+  }
+  u32x4 xr[4];
+  auto load_x = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xr[i] = xsrc[i][c * (GKC / 8)];
+  };
+  auto store_x = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(&xs[buf][xrow[i]][xseg[i] * 8]) = xr[i];
+  };
+  const u32x4* Wp = reinterpret_cast<const u32x4*>(a.W) + (size_t)tile0 * KT * 64 + lane;
+  u32x4 wa[2][4], wb[2][4];  // A fragments: this chunk's two k-steps, next chunk's
+  auto load_w = [&](u32x4 (&dst)[2][4], int c) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dst[ks][r] = Wp[((size_t)r * KT + c * 2 + ks) * 64];
+  };
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_x(0);
+  load_w(wa, 0);
+  store_x(0);
+  __syncthreads();
+  for (int c = 0; c < NC; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < NC;
+    if (more) {
+      load_x(c + 1);
+      load_w(wb, c + 1);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const u32x4 b = *reinterpret_cast<const u32x4*>(&xs[buf][wm * 128 + j * 16 + r16][ks * 32 + q4 * 8]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wa[ks][r]),
+                                                              __builtin_bit_cast(bf16x8, b), acc[r][j], 0, 0, 0);
+      }
+    }
+    if (more) {
+      store_x(buf ^ 1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wa[ks][r] = wb[ks][r];
+    }
+    __syncthreads();
+  }
+
+  // epilogue: lane holds rows 16*tile + 4*(lane>>4) + i of token column (lane & 15) per 16x16 tile
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 s = acc[r][j];
+      f32x4 up = s;
+      if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(s[i], 32);
+      }
+      const int col = m0 + wm * 128 + j * 16 + r16;
+      if (col >= a.M || (EPI == EPI_SWIGLU && lane >= 32)) continue;
+      epi_store<EPI>(a, tile0 + r, lane, col, s, up);
+    }
+}
+
+bool gemm_supported(int N, int K) { return N % GB_N == 0 && K % GKC == 0; }
+
+int launch_gemm(int epi, const MMArgs& a, hipStream_t s) {
+  if (a.M < 1 || !a.X || !gemm_supported(a.N, a.K)) return -1;
+  const int grid = (a.N / GB_N) * ((a.M + GB_M - 1) / GB_M);
+  switch (epi) {
+    case EPI_F32: gemm_kernel<EPI_F32><<<grid, 512, 0, s>>>(a); return 0;
+    case EPI_RESID: gemm_kernel<EPI_RESID><<<grid, 512, 0, s>>>(a); return 0;
+    case EPI_QKV: gemm_kernel<EPI_QKV><<<grid, 512, 0, s>>>(a); return 0;
+    case EPI_SWIGLU: gemm_kernel<EPI_SWIGLU><<<grid, 512, 0, s>>>(a); return 0;
+  }
+  return -1;
+}
+
+}  // namespace mx

@@ -234,3 +234,21 @@ def test_persistent_decode_vs_kernels_and_oracle(mx, oracle_mod):
     b.close()
     eng.close()
     ref_eng.close()
+
+
+@pytest.mark.parametrize("name,n_prompt", [("test-tiny", 700), ("test-d128", 300), ("test-h4096", 300)])
+def test_gemm_prefill_vs_oracle(mx, oracle_mod, name, n_prompt):
+    """Prompts of > 64 tokens without logits run as 512-row chunks of MFMA GEMMs (prefill path);
+    the next decode step attends to the K/V they stored: its logits must match the oracle, and the
+    prompt's last-row logits from a 64-row-chunk run must match the oracle too."""
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES[name]
+    ids = _seq(shape, n_prompt + 1, seed=31)
+    eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=1024, n_seq_max=2)
+    assert eng.forward_rows([0] * n_prompt, list(range(n_prompt)), ids[:n_prompt], want_logits=False) is None
+    got = eng.forward_logits(ids[n_prompt:], n_prompt, slot=0)
+    ref = oracle_mod.OracleModel(shape, seed=0).context(1024).eval(ids, 0)  # last row
+    assert_logits_close(got, ref, f"{name} after GEMM prefill")
+    assert_tokens_match(got, ref, name)
+    eng.close()

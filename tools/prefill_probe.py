@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Batched prefill timing (32 prompts x 128 tokens by default) for kernel profiling:
+    rocprofv3 --kernel-trace -d gpurun_out/pp -- python3 tools/prefill_probe.py
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--prompts", type=int, default=32)
+    ap.add_argument("--len", type=int, default=128)
+    args = ap.parse_args()
+    from llama_p2p_amd import synth
+    from llama_p2p_amd.engine import Engine
+
+    shape = synth.SHAPES[args.model]
+    eng = Engine(f"synthetic:{args.model}:seed=0", n_ctx=512, n_seq_max=args.prompts)
+    rng = np.random.default_rng(3)
+    slots = np.repeat(np.arange(args.prompts), args.len)
+    pos = np.tile(np.arange(args.len), args.prompts)
+    ids = rng.integers(3, shape.n_vocab, len(pos)).astype(np.int32)
+    for _ in range(2):
+        eng.sync()
+        t0 = time.perf_counter()
+        eng.forward_rows(slots, pos, ids, want_logits=False)
+        eng.sync()
+        dt = time.perf_counter() - t0
+    print(f"{len(ids)} tokens in {dt * 1e3:.1f} ms: {len(ids) / dt:.0f} tok/s")
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
