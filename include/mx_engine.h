@@ -140,6 +140,9 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us_per_l
 
 int mx_sync(mx_engine* e);
 
+/* Number of visible HIP devices (serving: one engine replica per GPU). */
+int mx_device_count(int32_t* n);
+
 /* Diagnostics: one persistent-decode-kernel step of M rows with per-phase wall-clock stamps
  * (100 MHz): out[grid][nphase][3] = {start, B image built, work end}; returns grid and nphase. */
 int mx_debug_pdk_trace(mx_engine* e, int M, int pos, uint64_t* out, int cap, int* grid, int* nphase);

@@ -1244,6 +1244,14 @@ int mx_debug_pdk_trace(mx_engine* e, int M, int pos, uint64_t* out, int cap, int
   return rc;
 }
 
+int mx_device_count(int32_t* n) {
+  if (!n) return fail(MX_ERR_ARG, "null argument");
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *n = c;
+  return 0;
+}
+
 int mx_sync(mx_engine* e) {
   if (!e) return fail(MX_ERR_ARG, "null engine");
   hipSetDevice(e->device);

@@ -26,7 +26,7 @@ EXPORTS = [
     "mx_opts_default", "mx_sampling_default", "mx_last_error", "mx_engine_create", "mx_engine_destroy",
     "mx_engine_info", "mx_forward_logits", "mx_forward_rows", "mx_submit", "mx_wait", "mx_batch_create",
     "mx_batch_step", "mx_batch_ids_device", "mx_batch_bind_ids", "mx_batch_tokens", "mx_batch_destroy", "mx_stage_rows",
-    "mx_profile_kernel", "mx_sync", "mx_debug_pdk_trace",
+    "mx_profile_kernel", "mx_sync", "mx_debug_pdk_trace", "mx_device_count",
 ]
 
 
@@ -95,12 +95,19 @@ def lib() -> ctypes.CDLL:
         L.mx_profile_kernel.argtypes = [vp, i32, i32, i32, P(ctypes.c_double), P(ctypes.c_double)]
         L.mx_sync.argtypes = [vp]
         L.mx_debug_pdk_trace.argtypes = [vp, i32, i32, vp, i32, P(i32), P(i32)]
+        L.mx_device_count.argtypes = [P(i32)]
         for name in EXPORTS:
             if name not in ("mx_opts_default", "mx_sampling_default", "mx_last_error", "mx_engine_destroy",
                             "mx_batch_destroy", "mx_batch_ids_device"):
                 getattr(L, name).restype = i32
         _lib = L
         return L
+
+
+def device_count() -> int:
+    n = ctypes.c_int32()
+    _check(lib().mx_device_count(ctypes.byref(n)))
+    return n.value
 
 
 def _check(rc: int):

@@ -252,3 +252,32 @@ def test_gemm_prefill_vs_oracle(mx, oracle_mod, name, n_prompt):
     assert_logits_close(got, ref, f"{name} after GEMM prefill")
     assert_tokens_match(got, ref, name)
     eng.close()
+
+
+def test_poisson_serving_with_gossip_placement(mx, oracle_mod):
+    """Config 5 mechanism on one GPU: two engine replicas as the 'peers', a Poisson stream placed
+    by the scoreboard (placement.py, p2p:156-168 bookkeeping); every request completes with the
+    oracle's greedy tokens, both replicas serve, and their scores count the successes."""
+    from llama_p2p_amd import synth
+    from llama_p2p_amd.placement import PeerScoreboard, poisson_schedule, serve
+
+    name = "test-d128"
+    shape = synth.SHAPES[name]
+    engines = {f"r{k}": mx.Engine(f"synthetic:{name}:seed=0", n_ctx=128, n_seq_max=16) for k in range(2)}
+    sched = poisson_schedule(200.0, 24, seed=3, prompt_lo=8, prompt_hi=40, vocab=shape.n_vocab)
+    outs = {}
+
+    def run(tgt, prompt, gen):
+        toks, _ = engines[tgt].generate(prompt, gen, temperature=0.0, ignore_eos=True)
+        outs[prompt.tobytes()] = toks
+        return len(toks)
+
+    res = serve(PeerScoreboard(list(engines), seed=0), run, sched, gen_tokens=8)
+    assert res["requests"] == 24 and res["failed"] == 0 and res["tokens"] == 24 * 8
+    assert all(v > 0 for v in res["per_target"].values()) and len(res["per_target"]) == 2
+    assert sum(s["success"] for s in res["scores"].values()) == 24
+    om = oracle_mod.OracleModel(shape, seed=0)
+    for _, prompt in sched[:6]:
+        check_greedy_chain(om.context(128), prompt, outs[prompt.tobytes()], "served")
+    for e in engines.values():
+        e.close()
