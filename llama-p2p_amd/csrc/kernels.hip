@@ -651,8 +651,7 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
   constexpr int SEGS = KC / 8;       // 16-B pieces per row and chunk
   constexpr int PIECES = ROWS * SEGS;
   constexpr int NT = 64 * W;
-  static_assert(PIECES % NT == 0, "chunk pieces must tile the work-group");
-  constexpr int PPT = PIECES / NT;
+  constexpr int PPT = (PIECES + NT - 1) / NT;  // W need not divide the chunk (W = 3, 6, 7 fill 256 CUs)
   constexpr int U = 2 * KCT;         // weight ring: this chunk + the next
   __shared__ __attribute__((aligned(16))) uint16_t xs[2][ROWS][PITCH];
 
@@ -672,7 +671,7 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
   int xrow[PPT], xseg[PPT];
 #pragma unroll
   for (int i = 0; i < PPT; ++i) {
-    const int p = threadIdx.x + i * NT;
+    const int p = min(threadIdx.x + i * NT, PIECES - 1);  // ragged tail: re-stage the last piece
     xrow[i] = p / SEGS;
     xseg[i] = p % SEGS;
     const int rr = xrow[i] < a.M ? xrow[i] : a.M - 1;
@@ -825,22 +824,28 @@ int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, h
   if (a.M < 1 || a.M > MAX_ROWS || a.K % TILE_K != 0 || a.N % TILE_N != 0 || !a.X) return -1;
   const int ntiles = a.N / TILE_N, KT = a.K / TILE_K;
   if (KT % 4) return -1;
+  // work-groups per launch are sized to the 256 CUs (tools/gemv_sweep.hip "odd" sweep,
+  // profiles/round1_gemv_sweep_odd.txt): 7 or 3 waves per group where 8/4 would leave CUs idle
   switch (epi) {
     case EPI_F32:
+      if (ntiles % 6 == 0) return launch_wide_cfg<3, 2, EPI_F32>(a, 1, s) ? -1 : 1;
       if (ntiles % 16 == 0) return launch_wide_cfg<8, 2, EPI_F32>(a, 1, s) ? -1 : 1;
       if (ntiles % 8 == 0) return launch_wide_cfg<4, 2, EPI_F32>(a, 1, s) ? -1 : 1;
       return launch_wide_cfg<4, 1, EPI_F32>(a, 1, s) ? -1 : 1;
     case EPI_SWIGLU:
+      if (ntiles % 7 == 0 && ntiles / 7 >= 128) return launch_wide_cfg<7, 1, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
       if (ntiles % 8 == 0) return launch_wide_cfg<4, 2, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
       return launch_wide_cfg<4, 1, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
     case EPI_QKV:
     case EPI_RESID: {
       // at most 4 partial slabs: every extra slab is re-read by the reduce+norm that follows
-      int cfg, groups;  // 0: W4 RTW2 (qkv), 1: W2 RTW1 (K <= 8192), 2: W4 RTW1
-      if (epi == EPI_QKV && ntiles % 8 == 0) cfg = 0, groups = ntiles / 8;
+      int cfg, groups;  // 0: W4 RTW2 (qkv), 1: W2 RTW1 (K <= 8192), 2: W4 RTW1, 3: W3 RTW1 (qkv)
+      if (epi == EPI_QKV && ntiles % 3 == 0) cfg = 3, groups = ntiles / 3;
+      else if (epi == EPI_QKV && ntiles % 8 == 0) cfg = 0, groups = ntiles / 8;
       else if (a.K <= 8192 && ntiles % 2 == 0) cfg = 1, groups = ntiles / 2;
       else cfg = 2, groups = ntiles / 4;
-      const int ksplit = pick_ksplit(KT, std::min(4, std::max(1, (256 + groups - 1) / std::max(1, groups))));
+      const int target = (cfg == 3 || cfg == 1) ? 4 : std::min(4, std::max(1, (256 + groups - 1) / std::max(1, groups)));
+      const int ksplit = pick_ksplit(KT, target);
       if (!ksplit) return -1;
       MMArgs p = a;
       p.out = slabs;
@@ -848,6 +853,7 @@ int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, h
       p.slab_stride = slab_stride;
       const int rc = cfg == 0 ? launch_wide_cfg<4, 2, EPI_SLAB>(p, ksplit, s)
                    : cfg == 1 ? launch_wide_cfg<2, 1, EPI_SLAB>(p, ksplit, s)
+                   : cfg == 3 ? launch_wide_cfg<3, 1, EPI_SLAB>(p, ksplit, s)
                               : launch_wide_cfg<4, 1, EPI_SLAB>(p, ksplit, s);
       if (rc) return -1;
       if (epi == EPI_QKV && qkv_finish) {

@@ -140,7 +140,19 @@ static void sweep_wide(const Shape& sh, int M) {
   }
 }
 
+static void sweep_wide_odd(const Shape& sh, int M) {
+  for (int ks : {1, 2, 4, 8}) {
+    runw<3, 1>(sh, M, ks);
+    runw<6, 1>(sh, M, ks);
+    runw<7, 1>(sh, M, ks);
+    runw<3, 2>(sh, M, ks);
+    runw<4, 2>(sh, M, ks);
+    runw<2, 1>(sh, M, ks);
+  }
+}
+
 int main(int argc, char** argv) {
+  const bool odd = argc > 1 && argv[1][0] == 'o';
   const bool wide_only = argc > 1;
   g_wbytes = (size_t)6 << 30;  // 6 GiB of distinct weights to rotate through
   CK(hipMalloc(&g_w, g_wbytes));
@@ -150,9 +162,13 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&g_out, (size_t)8 * 64 * 128256 * 4));  // room for 8 split-K slabs of the largest N
   const Shape shapes[] = {{"qkv", 6144, 4096}, {"wo", 4096, 4096}, {"gu", 28672, 4096},
                           {"down", 4096, 14336}, {"lmhead", 128256, 4096}};
-  if (!wide_only) {
+  if (!wide_only && !odd) {
     for (const Shape& sh : shapes) sweep<1>(sh, 1);
     for (const Shape& sh : shapes) sweep<2>(sh, 32);
+  }
+  if (odd) {
+    for (const Shape& sh : shapes) sweep_wide_odd(sh, 32);
+    return 0;
   }
   for (const Shape& sh : shapes) sweep_wide(sh, 32);
   return 0;
