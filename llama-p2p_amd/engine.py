@@ -15,7 +15,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmxllama.so")
+LIB_PATH = os.environ.get("MX_LIB") or os.path.join(HERE, "libmxllama.so")  # MX_LIB: A/B builds only
 
 MX_OK = 0
 MX_ERR_ARG, MX_ERR_HIP, MX_ERR_MODEL, MX_ERR_CTX, MX_ERR_NOTFOUND, MX_ERR_STATE = -1, -2, -3, -4, -5, -6
