@@ -273,8 +273,9 @@ __global__ __launch_bounds__(256) void norm_generic_kernel(uint16_t* y, int ldy,
 
 static void launch_norm_impl(uint16_t* y, int ldy, float* x, const float* slabs, int nslab, size_t stride,
                              const float* w, const int* row_map, int M, int n, float eps, hipStream_t s) {
-  if ((n == 4096 || n == 8192) && (nslab == 0 || nslab == 1 || nslab == 2 || nslab == 4)) {
+  if ((n == 4096 || n == 8192) && (nslab == 0 || nslab == 1 || nslab == 2 || nslab == 4 || nslab == 8)) {
     switch (nslab) {
+      case 8: launch_norm_ns<8>(y, ldy, x, slabs, stride, w, row_map, M, n, eps, s); return;
       case 0: launch_norm_ns<0>(y, ldy, x, slabs, stride, w, row_map, M, n, eps, s); return;
       case 1: launch_norm_ns<1>(y, ldy, x, slabs, stride, w, row_map, M, n, eps, s); return;
       case 2: launch_norm_ns<2>(y, ldy, x, slabs, stride, w, row_map, M, n, eps, s); return;
@@ -838,20 +839,22 @@ int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, h
       return launch_wide_cfg<4, 1, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
     case EPI_QKV:
     case EPI_RESID: {
-      // at most 4 partial slabs: every extra slab is re-read by the reduce+norm that follows
-      int cfg, groups;  // 0: W4 RTW2 (qkv), 1: W2 RTW1 (K <= 8192), 2: W4 RTW1, 3: W3 RTW1 (qkv)
+      // partial slabs are re-read by the reduce+norm that follows: 4 at most, 8 for ffn_down
+      int cfg, groups;  // 0: W4 RTW2 (qkv), 1: W2 RTW1 (K <= 8192), 2: W4 RTW1, 3: W3 RTW1 (qkv), 4: W4 RTW2 split 8
       if (epi == EPI_QKV && ntiles % 3 == 0) cfg = 3, groups = ntiles / 3;
+      else if (epi == EPI_RESID && a.K > 8192 && ntiles % 8 == 0 && ntiles / 8 <= 64) cfg = 4, groups = ntiles / 8;
       else if (epi == EPI_QKV && ntiles % 8 == 0) cfg = 0, groups = ntiles / 8;
       else if (a.K <= 8192 && ntiles % 2 == 0) cfg = 1, groups = ntiles / 2;
       else cfg = 2, groups = ntiles / 4;
-      const int target = (cfg == 3 || cfg == 1) ? 4 : std::min(4, std::max(1, (256 + groups - 1) / std::max(1, groups)));
+      const int target = cfg == 4 ? 8 : (cfg == 3 || cfg == 1) ? 4
+                                      : std::min(4, std::max(1, (256 + groups - 1) / std::max(1, groups)));
       const int ksplit = pick_ksplit(KT, target);
       if (!ksplit) return -1;
       MMArgs p = a;
       p.out = slabs;
       p.ldo = a.N;
       p.slab_stride = slab_stride;
-      const int rc = cfg == 0 ? launch_wide_cfg<4, 2, EPI_SLAB>(p, ksplit, s)
+      const int rc = (cfg == 0 || cfg == 4) ? launch_wide_cfg<4, 2, EPI_SLAB>(p, ksplit, s)
                    : cfg == 1 ? launch_wide_cfg<2, 1, EPI_SLAB>(p, ksplit, s)
                    : cfg == 3 ? launch_wide_cfg<3, 1, EPI_SLAB>(p, ksplit, s)
                               : launch_wide_cfg<4, 1, EPI_SLAB>(p, ksplit, s);
@@ -884,12 +887,11 @@ bool mm_can_norm_on_load(int M, int K) {
 // [pos][d] (B operand of QK^T = contiguous 16 B per lane) and V transposed
 // [d][pos] (B operand of P.V = contiguous 16 B per lane).
 // ---------------------------------------------------------------------------
-template <int D, int G>
-__global__ __launch_bounds__(512) void attn_decode_kernel(AttnArgs a) {
+template <int D, int G, int NW>
+__global__ __launch_bounds__(64 * NW) void attn_decode_kernel(AttnArgs a) {
   constexpr int CH = ATTN_CHUNK;
   constexpr int QK = D / 32;  // k-steps of QK^T
   constexpr int DT = D / 16;  // d tiles of P.V
-  constexpr int NW = 8;
   const int kvh = blockIdx.x, c = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r16 = lane & 15, q4 = lane >> 4;
@@ -1070,14 +1072,17 @@ __global__ __launch_bounds__(512) void attn_decode_kernel(AttnArgs a) {
   }
 }
 
+#ifndef ATTN_WAVES
+#define ATTN_WAVES 8  // 16 waves measured slower (merge of 16 partials; tools/gpu/ab_lib.sh)
+#endif
 template <int D>
 static void launch_attn_d(const AttnArgs& a, hipStream_t s) {
   dim3 grid(a.n_head_kv, a.M);
   switch (a.n_head / a.n_head_kv) {
-    case 1: attn_decode_kernel<D, 1><<<grid, 512, 0, s>>>(a); break;
-    case 2: attn_decode_kernel<D, 2><<<grid, 512, 0, s>>>(a); break;
-    case 4: attn_decode_kernel<D, 4><<<grid, 512, 0, s>>>(a); break;
-    case 8: attn_decode_kernel<D, 8><<<grid, 512, 0, s>>>(a); break;
+    case 1: attn_decode_kernel<D, 1, ATTN_WAVES><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
+    case 2: attn_decode_kernel<D, 2, ATTN_WAVES><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
+    case 4: attn_decode_kernel<D, 4, ATTN_WAVES><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
+    case 8: attn_decode_kernel<D, 8, ATTN_WAVES><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
   }
 }
 
