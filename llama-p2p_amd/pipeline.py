@@ -254,8 +254,9 @@ def bench_main(args, metric: str, make_prompts):
             "step_hbm_gbs": round(step_bytes / dt * args.steps / 1e9, 1),
             "step_hbm_frac": round(step_bytes / (dt / args.steps) / 1e9 / 8000.0 / world, 4),
             "roofline": {"bound": "hbm", "achieved": round(kbytes / us / 1e3, 1), "peak": 8000.0, "unit": "GB/s",
-                         "frac": round(kbytes / us / 1e3 / 8000.0, 4), "traffic": None,
-                         "kernel": "mm_kernel<EPI_SWIGLU> (ffn_gate+ffn_up+SiLU*up), rank 0",
+                         "frac": round(kbytes / us / 1e3 / 8000.0, 4), "traffic": traffic_bytes(args.model, M),
+                         "kernel": ("mm_wide_kernel" if M > 16 else "mm_kernel") +
+                                   "<EPI_SWIGLU> (ffn_gate+ffn_up+SiLU*up), rank 0",
                          "us_per_launch": round(us, 2), "bytes_per_launch": int(kbytes)},
         }
         print(json.dumps(line), flush=True)
@@ -264,6 +265,16 @@ def bench_main(args, metric: str, make_prompts):
     eng.close()
     dist.barrier()
     dist.destroy_process_group()
+
+
+def traffic_bytes(model: str, M: int):
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes (bench.py)."""
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "traffic.json")
+    try:
+        rec = json.load(open(path)).get(f"{model}/gate_up/M{M}")
+    except (OSError, ValueError):
+        return None
+    return round(rec["traffic_bytes"]) if rec else None
 
 
 class EngineAdapter:
