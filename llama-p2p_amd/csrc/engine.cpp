@@ -129,6 +129,9 @@ struct mx_engine {
   // rows of the next forward belong to distinct sequences (decode): no row attends to another row's
   // new K/V, so the wide path lets the attention kernel finish q/k/v from the split-K slabs
   bool rows_distinct = false;
+  // rows of the next forward come in blocks of 16 consecutive positions of one sequence (prefill):
+  // attention runs as attn_prefill_kernel, 16 queries per K/V pass
+  bool rows_blocked = false;
   // persistent decode kernel (pdk.hip) for <= PDK_MAX_M-token full-model steps: opt-in (MX_PDK=1) --
   // correct, but measured slower than the per-op kernels this round (profiles/)
   bool use_pdk = false;
@@ -662,7 +665,8 @@ int mx_engine::enqueue_forward_gemm(int M, const int* pos, const int* slot, void
     at.out = attn_out; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
     at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;
     at.scale = 1.0f / sqrtf((float)head_dim);
-    launch_attention(at, s);
+    if (rows_blocked) launch_attention_prefill(at, s);
+    else launch_attention(at, s);
     MMArgs b{};
     b.W = L.o; b.N = h; b.K = h; b.X = attn_out; b.ldx = h; b.M = M; b.out = x; b.ldo = h;
     if (launch_gemm(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "prefill attn_output GEMM shape");
@@ -711,6 +715,9 @@ int mx_engine::forward_rows_chunk(int n, const int32_t* slots, const int32_t* po
   std::vector<int32_t> sorted(slots, slots + n);
   std::sort(sorted.begin(), sorted.end());
   rows_distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+  rows_blocked = true;
+  for (int i = 0; i < n && rows_blocked; i++)
+    if (i % 16 && (slots[i] != slots[i - i % 16] || pos[i] != pos[i - i % 16] + i % 16)) rows_blocked = false;
   if (head && last_row_only) {
     const int last = n - 1;
     HIPC(hipMemcpyAsync(d_rowmap, &last, 4, hipMemcpyHostToDevice, s));
@@ -718,6 +725,7 @@ int mx_engine::forward_rows_chunk(int n, const int32_t* slots, const int32_t* po
   const int frc = enqueue_forward(n, d_ids, d_pos, d_slot, x_in, x_out, head, head && last_row_only ? d_rowmap : nullptr,
                                   n_out, false, nullptr, nullptr, nullptr, 0, nullptr, 0, s);
   rows_distinct = false;
+  rows_blocked = false;
   if (frc) return frc;
   if (head) HIPC(hipMemcpyAsync(logits_host, logits, (size_t)n_out * n_vocab * 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));

@@ -151,6 +151,9 @@ int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, h
 void launch_resid_norm(uint16_t* y, int ldy, float* x, const float* slabs, int nslab, size_t slab_stride,
                        const float* w, int M, int n, float eps, hipStream_t s);  // X == nullptr path (RMS_NORM fused into the GEMV) is legal
 void launch_attention(const AttnArgs& a, hipStream_t s);
+// rows in blocks of 16 consecutive positions of one sequence each (prefill chunks): one
+// work-group per (kv head, block), the 16 queries share every K/V chunk
+void launch_attention_prefill(const AttnArgs& a, hipStream_t s);
 // prefill (> MAX_ROWS rows): MFMA GEMM over packed weights with the same epilogues (N % 256, K % 64)
 bool gemm_supported(int N, int K);
 int launch_gemm(int epi, const MMArgs& a, hipStream_t s);

@@ -1294,3 +1294,141 @@ int launch_gemm(int epi, const MMArgs& a, hipStream_t s) {
 }
 
 }  // namespace mx
+
+namespace mx {
+
+// ---------------------------------------------------------------------------
+// Prefill attention over blocks of 16 consecutive positions of one sequence (flash-style).
+// (SURVEY §8a a10 at prefill)  Work-group = (kv head, 16-row block), one wave per query head
+// of the GQA group: the 16 queries are the rows of the f16 MFMA tiles, so each K/V chunk feeds
+// 16 queries instead of one (the per-row decode kernel re-reads the whole prefix for every
+// query).  Same roundings as the decode kernel (f16 q, K, P, V; f32 online softmax over
+// 32-position chunks); keys are visited in order, no cross-wave merge.
+// ---------------------------------------------------------------------------
+template <int D, int G>
+__global__ __launch_bounds__(64 * G) void attn_prefill_kernel(AttnArgs a) {
+  constexpr int CH = ATTN_CHUNK;
+  constexpr int QK = D / 32, DT = D / 16;
+  const int kvh = blockIdx.x, blk = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r16 = lane & 15, q4 = lane >> 4;
+  const int r0 = blk * 16;
+  const int pos0 = a.pos[r0];
+  const int slot = a.slot[r0];
+  const int hq = kvh * G + w;
+  __shared__ __attribute__((aligned(16))) _Float16 Ps[G][16][CH + 8];
+
+  // A operand of QK^T: rows = the block's 16 queries (rows past M re-read the last row)
+  f16x8 qa[QK];
+  {
+    const int row = min(r0 + r16, a.M - 1);
+    const float* qrow = a.q + (size_t)row * a.n_head * D + (size_t)hq * D;
+#pragma unroll
+    for (int kk = 0; kk < QK; ++kk) {
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(qrow + kk * 32 + 8 * q4);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(qrow + kk * 32 + 8 * q4 + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        qa[kk][j] = (_Float16)v0[j];
+        qa[kk][4 + j] = (_Float16)v1[j];
+      }
+    }
+  }
+  const _Float16* Kb = a.kc + (size_t)slot * a.slot_stride + (size_t)kvh * a.ctx_stride * D;
+  const _Float16* Vb = a.vc + (size_t)slot * a.slot_stride + (size_t)kvh * D * a.ctx_stride;
+  float m_i[4], l_i[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    m_i[i] = -INFINITY;
+    l_i[i] = 0.f;
+  }
+  f32x4 o[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int last = min(pos0 + 15, a.n_ctx - 1);  // newest key any query of the block sees
+  for (int p0 = 0; p0 <= last; p0 += CH) {
+    f16x8 kf[2][QK], vf[DT];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int kk = 0; kk < QK; ++kk)
+        kf[t][kk] = *reinterpret_cast<const f16x8*>(Kb + (size_t)(p0 + 16 * t + r16) * D + 8 * q4 + kk * 32);
+    const int pb = p0 + 8 * q4;
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+      vf[t] = *reinterpret_cast<const f16x8*>(Vb + (size_t)(t * 16 + r16) * a.ctx_stride + pb);
+    f32x4 s[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < QK; ++kk) s[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qa[kk], kf[t][kk], s[t], 0, 0, 0);
+    }
+    // C layout: rows = queries 4*q4+i (position pos0 + row), cols = keys p0 + 16t + r16; causal mask
+    float e[2][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int qp = pos0 + 4 * q4 + i;
+      const float v0 = (p0 + r16 <= qp) ? s[0][i] * a.scale : -INFINITY;
+      const float v1 = (p0 + 16 + r16 <= qp) ? s[1][i] * a.scale : -INFINITY;
+      float mx = fmaxf(v0, v1);
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+      const float m_new = fmaxf(m_i[i], mx);
+      const float alpha = (m_new == -INFINITY) ? 1.f : expf(m_i[i] - m_new);
+      e[0][i] = (m_new == -INFINITY) ? 0.f : expf(v0 - m_new);
+      e[1][i] = (m_new == -INFINITY) ? 0.f : expf(v1 - m_new);
+      float ls = e[0][i] + e[1][i];
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) ls += __shfl_xor(ls, off);
+      l_i[i] = l_i[i] * alpha + ls;
+      m_i[i] = m_new;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) o[t][i] *= alpha;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Ps[w][4 * q4 + i][16 * t + r16] = (_Float16)e[t][i];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P landed
+    __builtin_amdgcn_wave_barrier();
+    const f16x8 pa = *reinterpret_cast<const f16x8*>(&Ps[w][r16][8 * q4]);
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      f16x8 vb = vf[t];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vb[j] = (pb + j <= last) ? vb[j] : (_Float16)0.f;  // never-written keys
+      o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa, vb, o[t], 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();  // Ps[w] rewritten next chunk only after every lane read it
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = r0 + 4 * q4 + i;
+    if (row >= a.M) continue;
+    const float inv = 1.0f / l_i[i];
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+      a.out[(size_t)row * a.ldo + (size_t)hq * D + t * 16 + r16] = (uint16_t)f2bf(o[t][i] * inv);
+  }
+}
+
+template <int D>
+static void launch_attn_prefill_d(const AttnArgs& a, hipStream_t s) {
+  dim3 grid(a.n_head_kv, (a.M + 15) / 16);
+  switch (a.n_head / a.n_head_kv) {
+    case 1: attn_prefill_kernel<D, 1><<<grid, 64, 0, s>>>(a); break;
+    case 2: attn_prefill_kernel<D, 2><<<grid, 128, 0, s>>>(a); break;
+    case 4: attn_prefill_kernel<D, 4><<<grid, 256, 0, s>>>(a); break;
+    case 8: attn_prefill_kernel<D, 8><<<grid, 512, 0, s>>>(a); break;
+  }
+}
+
+void launch_attention_prefill(const AttnArgs& a, hipStream_t s) {
+  if (a.head_dim == 64)
+    launch_attn_prefill_d<64>(a, s);
+  else
+    launch_attn_prefill_d<128>(a, s);
+}
+
+}  // namespace mx

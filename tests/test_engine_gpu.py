@@ -281,3 +281,28 @@ def test_poisson_serving_with_gossip_placement(mx, oracle_mod):
         check_greedy_chain(om.context(128), prompt, outs[prompt.tobytes()], "served")
     for e in engines.values():
         e.close()
+
+
+@pytest.mark.parametrize("lens", [(80, 96, 112, 64, 128), (70, 90, 33)])
+def test_gemm_prefill_multi_sequence(mx, oracle_mod, lens):
+    """Several prompts in one GEMM prefill chunk: with 16-aligned lengths the rows form blocks of
+    16 consecutive positions (flash-style prefill attention), otherwise blocks straddle sequences
+    and the per-row attention kernel runs; either way every sequence's next-token logits match."""
+    from llama_p2p_amd import synth
+
+    name = "test-d128"
+    shape = synth.SHAPES[name]
+    seqs = [_seq(shape, L + 1, seed=50 + i) for i, L in enumerate(lens)]
+    eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=256, n_seq_max=len(lens))
+    slots, pos, ids = [], [], []
+    for i, (L, sq) in enumerate(zip(lens, seqs)):
+        slots += [i] * L
+        pos += list(range(L))
+        ids += list(sq[:L])
+    assert eng.forward_rows(slots, pos, ids, want_logits=False) is None
+    got = eng.forward_rows(list(range(len(lens))), list(lens), [int(sq[L]) for L, sq in zip(lens, seqs)])
+    om = oracle_mod.OracleModel(shape, seed=0)
+    for i, (L, sq) in enumerate(zip(lens, seqs)):
+        ref = om.context(256).eval(sq[:L + 1], 0)
+        assert_logits_close(got[i:i + 1], ref, f"seq {i} (len {L})")
+    eng.close()
