@@ -140,6 +140,13 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us_per_l
 
 int mx_sync(mx_engine* e);
 
+/* Request-path counters (mx_submit/mx_wait).  reused_prompt_tokens: prompt positions whose K/V were
+ * kept from the slot's previous request (longest common prefix, as llama-cpp-python's generate). */
+typedef struct {
+  uint64_t prompt_tokens, reused_prompt_tokens, generated_tokens;
+} mx_stats;
+int mx_engine_stats(mx_engine* e, mx_stats* out);
+
 /* Number of visible HIP devices (serving: one engine replica per GPU). */
 int mx_device_count(int32_t* n);
 

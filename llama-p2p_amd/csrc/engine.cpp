@@ -85,7 +85,8 @@ struct Request {
   int finish = -1;
   bool done = false;
   int slot = -1;
-  int pos = 0;  // next position to write
+  int pos = 0;     // next position to write
+  int reuse = 0;   // leading prompt positions whose K/V the slot already holds (prefix reuse)
   int32_t next_tok = 0;
   std::mt19937_64 rng;
   std::string error;
@@ -175,6 +176,10 @@ struct mx_engine {
   std::vector<Request*> active;
   std::map<uint64_t, std::unique_ptr<Request>> requests;
   std::vector<int> free_slots;
+  // prefix-KV reuse (llama-cpp-python's Llama.generate keeps the longest common prefix of the previous
+  // evaluation): tokens whose K/V each slot holds at positions 0..n-1, valid while the slot is free
+  std::vector<std::vector<int32_t>> slot_tokens;
+  uint64_t stat_prompt_tokens = 0, stat_reused_tokens = 0, stat_generated_tokens = 0;
   uint64_t next_id = 1;
   bool stop = false;
   std::thread worker;
@@ -287,6 +292,7 @@ int mx_engine::init_common() {
   HIPC(hipMemsetAsync(attn_out, 0, (size_t)R * n_embd * 2, stream));
   HIPC(hipMemsetAsync(act, 0, (size_t)R * n_ff * 2, stream));
   for (int i = 0; i < n_seq_max; i++) free_slots.push_back(n_seq_max - 1 - i);
+  slot_tokens.assign(n_seq_max, {});
   return 0;
 }
 
@@ -712,6 +718,10 @@ int mx_engine::forward_rows_chunk(int n, const int32_t* slots, const int32_t* po
   HIPC(hipMemcpyAsync(d_slot, slots, n * 4, hipMemcpyHostToDevice, s));
   const bool head = has_head && !x_out && logits_host;
   const int n_out = last_row_only ? 1 : n;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    for (int i = 0; i < n; i++) slot_tokens[slots[i]].clear();  // direct row writes: contents unknown
+  }
   std::vector<int32_t> sorted(slots, slots + n);
   std::sort(sorted.begin(), sorted.end());
   rows_distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
@@ -736,7 +746,15 @@ int mx_engine::forward_rows_chunk(int n, const int32_t* slots, const int32_t* po
 void mx_engine::finish(Request* r, int why) {
   r->finish = why;
   r->done = true;
-  if (r->slot >= 0) free_slots.push_back(r->slot);
+  if (r->slot >= 0) {
+    // K/V written for: the prompt and every generated token but the last (never fed back)
+    std::vector<int32_t>& st = slot_tokens[r->slot];
+    st = r->prompt;
+    if (!r->out.empty()) st.insert(st.end(), r->out.begin(), r->out.end() - 1);
+    if ((int)st.size() > r->pos) st.resize(std::max(0, r->pos));
+    free_slots.push_back(r->slot);
+  }
+  stat_generated_tokens += r->out.size();
   r->slot = -1;
 }
 
@@ -802,7 +820,7 @@ int mx_engine::prefill(Request* r, std::vector<float>& last) {
   const int chunk = gemm_ok() ? PREFILL_ROWS : MAX_ROWS;
   std::vector<int32_t> slots(chunk, r->slot), pos(chunk);
   last.resize(n_vocab);
-  for (int i = 0; i < n; i += chunk) {
+  for (int i = r->reuse; i < n; i += chunk) {
     int m = std::min(chunk, n - i);
     for (int j = 0; j < m; j++) pos[j] = i + j;
     const bool lastc = i + m == n;  // logits of the prompt's last token only
@@ -892,8 +910,22 @@ void mx_engine::scheduler_loop() {
       while (!pending.empty() && !free_slots.empty()) {
         Request* r = pending.front();
         pending.pop_front();
-        r->slot = free_slots.back();
-        free_slots.pop_back();
+        // the free slot sharing the longest prefix with this prompt (ties: most recently freed)
+        size_t best = free_slots.size() - 1;
+        int best_lcp = -1;
+        for (size_t k = free_slots.size(); k-- > 0;) {
+          const std::vector<int32_t>& st = slot_tokens[free_slots[k]];
+          int l = 0;
+          const int lim = (int)std::min(st.size(), r->prompt.size());
+          while (l < lim && st[l] == r->prompt[l]) l++;
+          if (l > best_lcp) best_lcp = l, best = k;
+        }
+        r->slot = free_slots[best];
+        free_slots.erase(free_slots.begin() + best);
+        // at least the last prompt token is evaluated (its logits start generation)
+        r->reuse = std::min(best_lcp, (int)r->prompt.size() - 1);
+        stat_prompt_tokens += r->prompt.size();
+        stat_reused_tokens += r->reuse;
         admit.push_back(r);
       }
     }
@@ -1110,6 +1142,10 @@ int mx_batch_create(mx_engine* e, int M, const int32_t* slots, const int32_t* po
     if (ids && (ids[i] < 0 || ids[i] >= e->n_vocab)) return fail(MX_ERR_ARG, "token id out of range");
     max_pos = std::max(max_pos, (int)pos[i]);
   }
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    for (int i = 0; i < M; i++) e->slot_tokens[slots[i]].clear();  // decode steps will overwrite them
+  }
   std::lock_guard<std::mutex> lk(e->gpu_mu);
   hipSetDevice(e->device);
   std::unique_ptr<mx_batch> b(new mx_batch());
@@ -1250,6 +1286,15 @@ int mx_debug_pdk_trace(mx_engine* e, int M, int pos, uint64_t* out, int cap, int
   if (grid) *grid = e->pdk_grid;
   if (nphase) *nphase = np;
   return rc;
+}
+
+int mx_engine_stats(mx_engine* e, mx_stats* out) {
+  if (!e || !out) return fail(MX_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(e->mu);
+  out->prompt_tokens = e->stat_prompt_tokens;
+  out->reused_prompt_tokens = e->stat_reused_tokens;
+  out->generated_tokens = e->stat_generated_tokens;
+  return 0;
 }
 
 int mx_device_count(int32_t* n) {

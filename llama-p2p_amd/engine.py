@@ -26,7 +26,7 @@ EXPORTS = [
     "mx_opts_default", "mx_sampling_default", "mx_last_error", "mx_engine_create", "mx_engine_destroy",
     "mx_engine_info", "mx_forward_logits", "mx_forward_rows", "mx_submit", "mx_wait", "mx_batch_create",
     "mx_batch_step", "mx_batch_ids_device", "mx_batch_bind_ids", "mx_batch_tokens", "mx_batch_destroy", "mx_stage_rows",
-    "mx_profile_kernel", "mx_sync", "mx_debug_pdk_trace", "mx_device_count",
+    "mx_profile_kernel", "mx_sync", "mx_debug_pdk_trace", "mx_device_count", "mx_engine_stats",
 ]
 
 
@@ -96,12 +96,18 @@ def lib() -> ctypes.CDLL:
         L.mx_sync.argtypes = [vp]
         L.mx_debug_pdk_trace.argtypes = [vp, i32, i32, vp, i32, P(i32), P(i32)]
         L.mx_device_count.argtypes = [P(i32)]
+        L.mx_engine_stats.argtypes = [vp, P(MxStats)]
         for name in EXPORTS:
             if name not in ("mx_opts_default", "mx_sampling_default", "mx_last_error", "mx_engine_destroy",
                             "mx_batch_destroy", "mx_batch_ids_device"):
                 getattr(L, name).restype = i32
         _lib = L
         return L
+
+
+class MxStats(ctypes.Structure):
+    _fields_ = [("prompt_tokens", ctypes.c_uint64), ("reused_prompt_tokens", ctypes.c_uint64),
+                ("generated_tokens", ctypes.c_uint64)]
 
 
 def device_count() -> int:
@@ -209,6 +215,11 @@ class Engine:
         g, n = ctypes.c_int32(), ctypes.c_int32()
         _check(lib().mx_debug_pdk_trace(self._h, M, pos, buf.ctypes.data, cap, ctypes.byref(g), ctypes.byref(n)))
         return buf[:g.value * n.value * 3].reshape(g.value, n.value, 3)
+
+    def stats(self) -> dict:
+        st = MxStats()
+        _check(lib().mx_engine_stats(self._h, ctypes.byref(st)))
+        return {k: getattr(st, k) for k, _ in MxStats._fields_}
 
     def sync(self):
         _check(lib().mx_sync(self._h))

@@ -306,3 +306,28 @@ def test_gemm_prefill_multi_sequence(mx, oracle_mod, lens):
         ref = om.context(256).eval(sq[:L + 1], 0)
         assert_logits_close(got[i:i + 1], ref, f"seq {i} (len {L})")
     eng.close()
+
+
+def test_prefix_kv_reuse(mx, oracle_mod):
+    """A request whose prompt extends an earlier one (a chat turn) gets the earlier request's slot
+    and skips re-evaluating the shared prefix (llama-cpp-python generate's longest-common-prefix
+    reuse); its tokens still follow the oracle's greedy chain."""
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES["test-d128"]
+    eng = mx.Engine("synthetic:test-d128:seed=0", n_ctx=256, n_seq_max=4)
+    p1 = _seq(shape, 40, seed=61)
+    t1, _ = eng.generate(p1, 8, temperature=0.0, ignore_eos=True)
+    p2 = np.concatenate([p1, np.array(t1[:7], np.int32), _seq(shape, 12, seed=62)[1:]]).astype(np.int32)
+    t2, _ = eng.generate(p2, 8, temperature=0.0, ignore_eos=True)
+    st = eng.stats()
+    assert st["reused_prompt_tokens"] >= 40 + 7 - 1, st  # prompt 1 + its fed-back tokens
+    om = oracle_mod.OracleModel(shape, seed=0)
+    check_greedy_chain(om.context(256), p1, t1, "first")
+    check_greedy_chain(om.context(256), p2, t2, "reused prefix")
+    p3 = _seq(shape, 30, seed=63)  # unrelated prompt: only BOS in common
+    before = eng.stats()["reused_prompt_tokens"]
+    t3, _ = eng.generate(p3, 4, temperature=0.0, ignore_eos=True)
+    assert eng.stats()["reused_prompt_tokens"] - before <= 1
+    check_greedy_chain(om.context(256), p3, t3, "fresh")
+    eng.close()
