@@ -597,10 +597,27 @@ int launch_mm(int epi, const MMArgs& a, hipStream_t s) {
   const int ntiles = a.N / TILE_N;
   const int nb = (a.M + 15) / 16;
   if (nb == 1 || a.X == nullptr) {
+    // RMS_NORM-on-load geometries under evaluation (tools/kernel_probe.py with MX_XS_CFG=n)
+    static const int xs_cfg = getenv("MX_XS_CFG") ? atoi(getenv("MX_XS_CFG")) : 0;
+    if (a.X == nullptr && xs_cfg) {
+      if (epi == EPI_SWIGLU && ntiles % 7 == 0) {
+        if (xs_cfg == 1) return launch_mm_cfg<8, 7, EPI_SWIGLU, 4>(a, s);
+        if (xs_cfg == 2) return launch_mm_cfg<16, 7, EPI_SWIGLU, 2>(a, s);
+        if (xs_cfg == 3) return launch_mm_cfg<8, 7, EPI_SWIGLU, 2>(a, s);
+        if (xs_cfg == 4) return launch_mm_cfg<16, 1, EPI_SWIGLU, 8>(a, s);
+      }
+      if (epi == EPI_QKV && ntiles % 3 == 0) {
+        if (xs_cfg == 1) return launch_mm_cfg<8, 1, EPI_QKV, 4>(a, s);
+        if (xs_cfg == 2) return launch_mm_cfg<8, 3, EPI_QKV, 4>(a, s);
+        if (xs_cfg == 3) return launch_mm_cfg<16, 3, EPI_QKV, 2>(a, s);
+        if (xs_cfg == 4) return launch_mm_cfg<16, 1, EPI_QKV, 8>(a, s);
+      }
+    }
     switch (epi) {
       case EPI_F32: return launch_mm_cfg<16, 1, EPI_F32, 4>(a, s);
       case EPI_RESID: return launch_mm_cfg<16, 1, EPI_RESID, 4>(a, s);
-      case EPI_QKV: return launch_mm_cfg<16, 1, EPI_QKV, 4>(a, s);
+      case EPI_QKV:  // norm on load: 8-wave groups, 3 per CU, all 384 in one round (profiles/round1_xs_probe.txt)
+        return a.X == nullptr ? launch_mm_cfg<8, 1, EPI_QKV, 4>(a, s) : launch_mm_cfg<16, 1, EPI_QKV, 4>(a, s);
       case EPI_SWIGLU: return launch_mm_cfg<16, 1, EPI_SWIGLU, 4>(a, s);
     }
     return -1;
