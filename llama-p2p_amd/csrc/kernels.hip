@@ -617,7 +617,8 @@ int launch_mm(int epi, const MMArgs& a, hipStream_t s) {
       case EPI_F32: return launch_mm_cfg<16, 1, EPI_F32, 4>(a, s);
       case EPI_RESID: return launch_mm_cfg<16, 1, EPI_RESID, 4>(a, s);
       case EPI_QKV:  // norm on load: 8-wave groups, 3 per CU, all 384 in one round (profiles/round1_xs_probe.txt)
-        return a.X == nullptr ? launch_mm_cfg<8, 1, EPI_QKV, 4>(a, s) : launch_mm_cfg<16, 1, EPI_QKV, 4>(a, s);
+        return (a.X == nullptr && a.K / 8 <= 512) ? launch_mm_cfg<8, 1, EPI_QKV, 4>(a, s)
+                                                  : launch_mm_cfg<16, 1, EPI_QKV, 4>(a, s);
       case EPI_SWIGLU: return launch_mm_cfg<16, 1, EPI_SWIGLU, 4>(a, s);
     }
     return -1;
