@@ -63,6 +63,7 @@ const Shape kShapes[] = {
     {"test-gqa8", 512, 3, 8, 1, 1024, 1024, 500000.f, 1e-5f, 2048},
     {"test-d128", 1024, 2, 8, 2, 2816, 2048, 500000.f, 1e-5f, 2048},
     {"test-h4096", 4096, 1, 32, 8, 2048, 1024, 500000.f, 1e-5f, 2048},
+    {"test-h8192", 8192, 1, 64, 8, 2048, 1024, 500000.f, 1e-5f, 2048},
 };
 
 // synth.py tensor ids

@@ -87,6 +87,8 @@ SHAPES = {
     "test-d128": LlamaShape("test-d128", 1024, 2, 8, 2, 2816, 2048, 500000.0, 1e-5),
     # Llama-3-8B hidden geometry (n_embd 4096, 32 q / 8 kv heads of 128), one layer, small FFN/vocab
     "test-h4096": LlamaShape("test-h4096", 4096, 1, 32, 8, 2048, 1024, 500000.0, 1e-5),
+    # Llama-3-70B hidden geometry (h 8192, 64 q / 8 kv heads: GQA group 8), one layer
+    "test-h8192": LlamaShape("test-h8192", 8192, 1, 64, 8, 2048, 1024, 500000.0, 1e-5),
 }
 
 _M64 = (1 << 64) - 1

@@ -331,3 +331,30 @@ def test_prefix_kv_reuse(mx, oracle_mod):
     assert eng.stats()["reused_prompt_tokens"] - before <= 1
     check_greedy_chain(om.context(256), p3, t3, "fresh")
     eng.close()
+
+
+def test_70b_geometry_all_paths(mx, oracle_mod):
+    """Llama-3-70B hidden geometry (h 8192, GQA group 8, one layer): GEMM prefill, 64-row logits
+    chunks, batch-1 decode (RMS_NORM on load with 16-wave groups) and a 24-row wide decode step,
+    all against the oracle."""
+    from llama_p2p_amd import synth
+
+    name = "test-h8192"
+    shape = synth.SHAPES[name]
+    eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=512, n_seq_max=24)
+    om = oracle_mod.OracleModel(shape, seed=0)
+    ids = _seq(shape, 200, seed=71)
+    assert eng.forward_rows([0] * 180, list(range(180)), ids[:180], want_logits=False) is None  # GEMM
+    got = eng.forward_logits(ids[180:200], 180, slot=0)                                       # 20 rows
+    ref = om.context(512).eval(ids, 0, all_logits=True)[180:]
+    assert_logits_close(got, ref, "h8192 prefill+chunk")
+    eng.forward_rows([1] * 199, list(range(199)), ids[:199], want_logits=False)
+    got1 = eng.forward_logits(ids[199:200], 199, slot=1)                                      # batch 1
+    assert_logits_close(got1, ref[-1:], "h8192 batch-1 decode")
+    seqs = [_seq(shape, 9, seed=80 + i) for i in range(24)]
+    for i, sq in enumerate(seqs):
+        eng.forward_rows([i] * 8, list(range(8)), sq[:8], want_logits=False)
+    gotw = eng.forward_rows(list(range(24)), [8] * 24, [int(sq[8]) for sq in seqs])            # wide
+    for i, sq in enumerate(seqs):
+        assert_logits_close(gotw[i:i + 1], om.context(64).eval(sq, 0), f"h8192 wide row {i}")
+    eng.close()
