@@ -156,6 +156,67 @@ def run_single(args):
     return res
 
 
+def q8_bench(args):
+    """The same model quantised to Q8_0 (a llama.cpp Q8_0 GGUF): batch-1 and
+    M-sequence greedy decode, and the Q8 gate/up kernel against the HBM roofline.  Algorithmic
+    bytes = the Q8_0 weights (1.0625 B/weight in packed tiles) + K/V + logits."""
+    from llama_p2p_amd import synth
+    from llama_p2p_amd.engine import Engine
+
+    shape = synth.SHAPES[args.model]
+    M = args.seqs
+    eng = Engine(f"synthetic:{args.model}:seed=0:q8_0", n_ctx=args.n_ctx, n_seq_max=max(M, 1))
+    assert eng.info.weight_type == 8
+    prompts = make_prompts(shape.n_vocab, M)
+    slots, pos, ids = [], [], []
+    for i, p in enumerate(prompts):
+        slots += [i] * (len(p) - 1)
+        pos += list(range(len(p) - 1))
+        ids += [int(t) for t in p[:-1]]
+    eng.forward_rows(slots, pos, ids, want_logits=False)
+    out = {"model": f"{args.model} Q8_0 (quantisation of the same synthetic bf16 weights)",
+           "weight_bytes": int(eng.info.weight_bytes)}
+    steps = args.q8_steps
+    b = eng.batch(slots=list(range(M)), pos=[len(p) - 1 for p in prompts], ids=[int(p[-1]) for p in prompts],
+                  max_steps=4 + steps)
+    for _ in range(4):
+        b.step()
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        b.step()
+    eng.sync()
+    dt = (time.perf_counter() - t0) / steps
+    toks = b.tokens()
+    b.close()
+    ctx_sum = sum(len(p) + 4 + steps / 2 for p in prompts)
+    step_bytes = eng.info.weight_bytes + ctx_sum * shape.kv_bytes_per_pos() + M * shape.n_vocab * 4
+    out[f"decode_M{M}"] = {"tok_s": round(M / dt, 1), "ms_per_step": round(dt * 1e3, 3),
+                           "hbm_frac": round(step_bytes / dt / 1e9 / HBM_PEAK_GBS, 4)}
+    b1 = eng.batch(slots=[0], pos=[len(prompts[0]) + 3 + steps], ids=[int(toks[0, -1])], max_steps=steps + 4)
+    for _ in range(4):
+        b1.step()
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        b1.step()
+    eng.sync()
+    d1 = (time.perf_counter() - t0) / steps
+    b1.close()
+    b1_bytes = eng.info.weight_bytes + (len(prompts[0]) + 8 + steps * 1.5) * shape.kv_bytes_per_pos()
+    out["batch1"] = {"tok_s": round(1.0 / d1, 2), "ms_per_token": round(d1 * 1e3, 3),
+                     "hbm_frac": round(b1_bytes / d1 / 1e9 / HBM_PEAK_GBS, 4),
+                     "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / b1_bytes, 1)}
+    for m in (1, M):
+        us, wbytes = eng.profile_kernel(2, m, iters=3)
+        kb = wbytes + m * shape.n_embd + m * shape.n_embd // 8 + m * shape.n_ff * 4
+        out[f"gate_up_M{m}"] = {"kernel": "mq8_kernel<EPI_SWIGLU>", "us_per_launch": round(us, 2),
+                                "bytes_per_launch": int(kb), "achieved_gbs": round(kb / us / 1e3, 1),
+                                "frac": round(kb / us / 1e3 / HBM_PEAK_GBS, 4)}
+    eng.close()
+    return out
+
+
 def prefill_bench(eng, shape, n_prompts: int, plen: int):
     """Batched prefill: n_prompts prompts of plen tokens (seed 3) pushed through the
     engine's GEMM path (chunks of up to PREFILL_ROWS = 4096 rows) with no lm_head (logits of prompt tokens are not needed), timed on the
@@ -197,6 +258,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--prefill-prompts", type=int, default=32)
     ap.add_argument("--prefill-len", type=int, default=128)
+    ap.add_argument("--q8-steps", type=int, default=32, help="Q8_0 decode steps (0: skip the Q8_0 section)")
     ap.add_argument("--force-pipeline", action="store_true", help="run the torch.distributed pipeline path even at N=1")
     args = ap.parse_args()
 
@@ -222,6 +284,11 @@ def main():
         line["batch1"] = res["batch1"]
     if "prefill" in res:
         line["prefill"] = res["prefill"]
+    if args.q8_steps > 0:
+        try:
+            line["q8_0"] = q8_bench(args)
+        except Exception as ex:  # report, never hide
+            line["q8_0"] = {"error": repr(ex)}
     if not args.no_cpu_baseline:
         try:
             line["cpu_baseline"] = cpu_baseline(args.model)

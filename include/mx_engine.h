@@ -70,6 +70,7 @@ typedef struct {
   uint64_t weight_bytes; /* device bytes of the weights this stage streams per decode step */
   int32_t persistent_decode; /* 1: steps of <= 4 tokens run as one persistent kernel (opt-in: MX_PDK=1) */
   int32_t persistent_grid;   /* its work-groups (one per CU) */
+  int32_t weight_type;       /* ggml type of the layer matrices: 30 BF16, 8 Q8_0 */
 } mx_model_info;
 
 typedef struct {

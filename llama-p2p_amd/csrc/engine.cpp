@@ -154,6 +154,13 @@ struct mx_engine {
   hipStream_t stream = nullptr;
   uint16_t *tok_embd = nullptr, *output = nullptr;
   float* out_norm = nullptr;
+  // Q8_0 model: layer matrices as packed Q8 tiles; token_embd / output may each
+  // be Q8_0 (tok_embd8: GGUF blocks, row-major) or BF16
+  bool wq8 = false, embd_q8 = false, out_q8 = false;
+  uint8_t* tok_embd8 = nullptr;
+  int8_t* xq8 = nullptr;    // Q8_0 activation rows [PREFILL_ROWS][max(h, ff)]
+  float* xqd = nullptr;     // their block scales
+  float *attn_f = nullptr, *act_f = nullptr;  // f32 attention output / SwiGLU product (quantised next)
   std::vector<Layer> layers;  // local layers [lb, le)
   _Float16 *kcache = nullptr, *vcache = nullptr;
   size_t slot_stride = 0, layer_kv_stride = 0;
@@ -193,14 +200,18 @@ struct mx_engine {
     return 0;
   }
   int init_common();
-  int load_synthetic(const Shape& s, uint64_t seed);
+  int load_synthetic(const Shape& s, uint64_t seed, bool q8 = false);
   int load_gguf(const std::string& path);
   int enqueue_forward(int M, const int* ids, const int* pos, const int* slot, const void* x_in, void* x_out,
                       bool head, const int* rowmap, int n_out, bool argmax, int* ids_next, int* pos_next, int* hist,
                       int hist_stride, int* hist_count, int max_hist, hipStream_t s);
+  int enqueue_forward_q8(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap, int n_out,
+                         bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count,
+                         int max_hist, hipStream_t s);
   int enqueue_forward_gemm(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap,
                            int n_out, hipStream_t s);
-  bool gemm_ok() const {
+  bool gemm_ok() const {  // chunks of PREFILL_ROWS rows can run (the Q8_0 path takes any row count)
+    if (wq8) return true;
     return gemm_supported(n_embd + 2 * n_embd_kv, n_embd) && gemm_supported(n_embd, n_embd) &&
            gemm_supported(2 * n_ff, n_embd) && gemm_supported(n_embd, n_ff);
   }
@@ -239,6 +250,8 @@ int mx_engine::init_common() {
   if (G != 1 && G != 2 && G != 4 && G != 8) return fail(MX_ERR_ARG, "n_head/n_head_kv must be 1,2,4 or 8");
   if (n_embd % 32 || n_ff % 32 || n_vocab % 16 || n_embd_kv % 16)
     return fail(MX_ERR_ARG, "n_embd, n_ff must be multiples of 32 and n_vocab, n_embd_kv of 16");
+  if (wq8 && (n_embd % Q8_TILE_K || n_ff % Q8_TILE_K))
+    return fail(MX_ERR_ARG, "Q8_0 models need n_embd and n_ff multiples of 64");
   if (le < 0 || le > n_layer) le = n_layer;
   if (lb < 0 || lb >= le) return fail(MX_ERR_ARG, "bad layer range");
   has_embed = lb == 0;
@@ -288,6 +301,13 @@ int mx_engine::init_common() {
   if (int rc = alloc((void**)&d_pos, (size_t)R * 4)) return rc;
   if (int rc = alloc((void**)&d_slot, (size_t)R * 4)) return rc;
   if (int rc = alloc((void**)&d_rowmap, (size_t)R * 4)) return rc;
+  if (wq8) {
+    const size_t kmax = std::max(n_embd, n_ff);
+    if (int rc = alloc((void**)&xq8, (size_t)R * kmax)) return rc;
+    if (int rc = alloc((void**)&xqd, (size_t)R * (kmax / 32) * 4)) return rc;
+    if (int rc = alloc((void**)&attn_f, (size_t)R * n_embd * 4)) return rc;
+    if (int rc = alloc((void**)&act_f, (size_t)R * n_ff * 4)) return rc;
+  }
   // poison-free start: zero activations so padded MFMA columns never read uninitialised memory
   HIPC(hipMemsetAsync(xn, 0, (size_t)R * n_embd * 2, stream));
   HIPC(hipMemsetAsync(attn_out, 0, (size_t)R * n_embd * 2, stream));
@@ -298,7 +318,7 @@ int mx_engine::init_common() {
 }
 
 int mx_engine::init_pdk() {
-  if (!getenv("MX_PDK") || getenv("MX_NO_PDK") || !has_embed || !has_head) return 0;
+  if (!getenv("MX_PDK") || getenv("MX_NO_PDK") || !has_embed || !has_head || wq8) return 0;
   hipDeviceProp_t prop;
   HIPC(hipGetDeviceProperties(&prop, device));
   const int grid = prop.multiProcessorCount;
@@ -336,6 +356,18 @@ int mx_engine::check_pdk() {
 
 static int alloc_layer(mx_engine* e, Layer& L) {
   const size_t h = e->n_embd, kv = e->n_embd_kv, ff = e->n_ff;
+  if (e->wq8) {
+    const size_t bq = q8_matrix_bytes(h + 2 * kv, h), bo = q8_matrix_bytes(h, h), bg = q8_matrix_bytes(2 * ff, h),
+                 bd = q8_matrix_bytes(h, ff);
+    if (int rc = e->alloc((void**)&L.qkv, bq)) return rc;
+    if (int rc = e->alloc((void**)&L.o, bo)) return rc;
+    if (int rc = e->alloc((void**)&L.gu, bg)) return rc;
+    if (int rc = e->alloc((void**)&L.down, bd)) return rc;
+    if (int rc = e->alloc((void**)&L.attn_norm, h * 4)) return rc;
+    if (int rc = e->alloc((void**)&L.ffn_norm, h * 4)) return rc;
+    e->weight_bytes += bq + bo + bg + bd + 2 * h * 4;
+    return 0;
+  }
   if (int rc = e->alloc((void**)&L.qkv, (h + 2 * kv) * h * 2)) return rc;
   if (int rc = e->alloc((void**)&L.o, h * h * 2)) return rc;
   if (int rc = e->alloc((void**)&L.gu, 2 * ff * h * 2)) return rc;
@@ -346,13 +378,45 @@ static int alloc_layer(mx_engine* e, Layer& L) {
   return 0;
 }
 
-int mx_engine::load_synthetic(const Shape& s, uint64_t seed) {
+int mx_engine::load_synthetic(const Shape& s, uint64_t seed, bool q8) {
   n_embd = s.n_embd; n_layer = s.n_layer; n_head = s.n_head; n_head_kv = s.n_head_kv; n_ff = s.n_ff;
   n_vocab = s.n_vocab; rope_base = s.rope_base; eps = s.eps; n_ctx_train = s.n_ctx_train;
   if (le < 0 || le > n_layer) le = n_layer;
+  wq8 = embd_q8 = out_q8 = q8;
   if (int rc = init_common()) return rc;
   const float ws = std_scale(0.02), ns = std_scale(0.1);
   const int h = n_embd, kv = n_embd_kv, ff = n_ff, V = n_vocab;
+  if (q8) {  // the Q8_0 quantisation of the bf16 synthetic model (what llama-quantize makes of it)
+    if (has_embed) {
+      if (int rc = alloc((void**)&tok_embd8, (size_t)V * (h / 32) * 34)) return rc;
+      launch_synth_q8_rowmajor(tok_embd8, V, h, seed, TID_TOK_EMBD, ws, stream);
+      weight_bytes += (size_t)h / 32 * 34;
+    }
+    if (has_head) {
+      if (int rc = alloc((void**)&output, q8_matrix_bytes(V, h))) return rc;
+      if (int rc = alloc((void**)&out_norm, (size_t)h * 4)) return rc;
+      launch_synth_q8_packed((uint8_t*)output, V, h, seed, TID_OUTPUT, ws, PACK_ROWS, 0, stream);
+      launch_synth_norm(out_norm, h, seed, TID_OUT_NORM, ns, stream);
+      weight_bytes += q8_matrix_bytes(V, h) + h * 4;
+    }
+    for (int l = lb; l < le; l++) {
+      Layer& L = layers[l - lb];
+      if (int rc = alloc_layer(this, L)) return rc;
+      uint8_t *qkv = (uint8_t*)L.qkv, *o = (uint8_t*)L.o, *gu = (uint8_t*)L.gu, *dn = (uint8_t*)L.down;
+      launch_synth_norm(L.attn_norm, h, seed, layer_tid(l, L_ATTN_NORM), ns, stream);
+      launch_synth_norm(L.ffn_norm, h, seed, layer_tid(l, L_FFN_NORM), ns, stream);
+      launch_synth_q8_packed(qkv, h, h, seed, layer_tid(l, L_Q), ws, PACK_ROWS, 0, stream);
+      launch_synth_q8_packed(qkv, kv, h, seed, layer_tid(l, L_K), ws, PACK_ROWS, h, stream);
+      launch_synth_q8_packed(qkv, kv, h, seed, layer_tid(l, L_V), ws, PACK_ROWS, h + kv, stream);
+      launch_synth_q8_packed(o, h, h, seed, layer_tid(l, L_O), ws, PACK_ROWS, 0, stream);
+      launch_synth_q8_packed(gu, ff, h, seed, layer_tid(l, L_GATE), ws, PACK_GATE, 0, stream);
+      launch_synth_q8_packed(gu, ff, h, seed, layer_tid(l, L_UP), ws, PACK_UP, 0, stream);
+      launch_synth_q8_packed(dn, h, ff, seed, layer_tid(l, L_DOWN), ws, PACK_ROWS, 0, stream);
+    }
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(stream));
+    return 0;
+  }
   if (has_embed) {
     if (int rc = alloc((void**)&tok_embd, (size_t)V * h * 2)) return rc;
     launch_synth_rowmajor(tok_embd, (size_t)V * h, seed, TID_TOK_EMBD, ws, stream);
@@ -406,30 +470,42 @@ int mx_engine::load_gguf(const std::string& path) {
   if ((int)f.get_num("llama.rope.dimension_count", n_embd / n_head) != n_embd / n_head)
     return fail(MX_ERR_MODEL, "partial RoPE (rope.dimension_count != head_dim) is not supported");
   if (le < 0 || le > n_layer) le = n_layer;
+  {  // matrix type: every layer matrix and the output BF16 (30), or all Q8_0 (8); token_embd either
+    const GGUFTensor* t0 = f.tensor("blk." + std::to_string(lb < 0 ? 0 : lb) + ".attn_q.weight");
+    if (!t0) return fail(MX_ERR_MODEL, "missing attn_q.weight");
+    if (t0->type != 30 && t0->type != 8)
+      return fail(MX_ERR_MODEL, "layer matrices must be BF16 (ggml type 30) or Q8_0 (type 8), got type " +
+                                    std::to_string(t0->type));
+    wq8 = out_q8 = t0->type == 8;
+    embd_q8 = te->type == 8;
+  }
   if (int rc = init_common()) return rc;
   const int h = n_embd, kv = n_embd_kv, ff = n_ff, V = n_vocab;
+  const int mat_type = wq8 ? 8 : 30;
 
   // staging buffer for the largest matrix
   size_t stage_bytes = std::max({(size_t)V * h * 2, (size_t)ff * h * 2, (size_t)(h + 2 * kv) * h * 2});
   uint16_t* stage = nullptr;
   HIPC(hipMalloc((void**)&stage, stage_bytes));
-  auto get_mat = [&](const std::string& name, int rows, int cols, const GGUFTensor** out) -> int {
+  auto get_mat = [&](const std::string& name, int rows, int cols, const GGUFTensor** out, int type) -> int {
     const GGUFTensor* t = f.tensor(name);
     if (!t) return fail(MX_ERR_MODEL, "missing tensor " + name);
     if (t->ne.size() != 2 || (int)t->ne[0] != cols || (int)t->ne[1] != rows)
       return fail(MX_ERR_MODEL, "tensor " + name + " has unexpected shape");
-    if (t->type != 30)
-      return fail(MX_ERR_MODEL, "tensor " + name + ": only BF16 (ggml type 30) matrices are supported, got type " +
-                                    std::to_string(t->type));
+    if (t->type != type)
+      return fail(MX_ERR_MODEL, "tensor " + name + ": expected ggml type " + std::to_string(type) +
+                                    (type == 8 ? " (Q8_0, like the other matrices)" : " (BF16, like the other matrices)") +
+                                    ", got type " + std::to_string(t->type));
     *out = t;
     return 0;
   };
   auto upload_packed = [&](const std::string& name, int rows, int cols, uint16_t* dst, int mode,
                            int offset) -> int {
     const GGUFTensor* t = nullptr;
-    if (int rc = get_mat(name, rows, cols, &t)) return rc;
+    if (int rc = get_mat(name, rows, cols, &t, mat_type)) return rc;
     HIPC(hipMemcpy(stage, f.data(*t), t->nbytes, hipMemcpyHostToDevice));
-    launch_pack(dst, stage, rows, cols, mode, offset, stream);
+    if (wq8) launch_pack_q8((uint8_t*)dst, (const uint8_t*)stage, rows, cols, mode, offset, stream);
+    else launch_pack(dst, stage, rows, cols, mode, offset, stream);
     HIPC(hipStreamSynchronize(stream));
     return 0;
   };
@@ -442,21 +518,22 @@ int mx_engine::load_gguf(const std::string& path) {
   int rc = 0;
   if (has_embed) {
     const GGUFTensor* t = nullptr;
-    if ((rc = get_mat("token_embd.weight", V, h, &t))) goto out;
-    if ((rc = alloc((void**)&tok_embd, (size_t)V * h * 2))) goto out;
-    if (hipMemcpy(tok_embd, f.data(*t), t->nbytes, hipMemcpyHostToDevice) != hipSuccess) {
+    if ((rc = get_mat("token_embd.weight", V, h, &t, embd_q8 ? 8 : 30))) goto out;
+    void** dst = embd_q8 ? (void**)&tok_embd8 : (void**)&tok_embd;
+    if ((rc = alloc(dst, t->nbytes))) goto out;
+    if (hipMemcpy(*dst, f.data(*t), t->nbytes, hipMemcpyHostToDevice) != hipSuccess) {
       rc = fail(MX_ERR_HIP, "upload token_embd");
       goto out;
     }
-    weight_bytes += (size_t)h * 2;
+    weight_bytes += t->nbytes / V;
   }
   if (has_head) {
-    if ((rc = alloc((void**)&output, (size_t)V * h * 2))) goto out;
+    if ((rc = alloc((void**)&output, wq8 ? q8_matrix_bytes(V, h) : (size_t)V * h * 2))) goto out;
     if ((rc = alloc((void**)&out_norm, (size_t)h * 4))) goto out;
     const char* oname = f.tensor("output.weight") ? "output.weight" : "token_embd.weight";  // tied embeddings
     if ((rc = upload_packed(oname, V, h, output, PACK_ROWS, 0))) goto out;
     if ((rc = upload_norm("output_norm.weight", out_norm))) goto out;
-    weight_bytes += (size_t)V * h * 2 + h * 4;
+    weight_bytes += (wq8 ? q8_matrix_bytes(V, h) : (size_t)V * h * 2) + h * 4;
   }
   for (int l = lb; l < le; l++) {
     Layer& L = layers[l - lb];
@@ -485,14 +562,17 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
   const bool wide = use_wide && M > 16;
   // RMS_NORM applied on load by the consuming GEMV (M <= 16); the residual-stream writers
   // (embedding, attn_output, ffn_down, or ssq_kernel for a stage's x_in) leave per-tile partials
-  const bool nol = !wide && norm_on_load && mm_can_norm_on_load(M, h);
+  const bool nol = !wide && !wq8 && norm_on_load && mm_can_norm_on_load(M, h);
   if (x_in) {
     HIPC(hipMemcpyAsync(x, x_in, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
     if (nol) launch_ssq(x, M, h, ssq, s);
   } else {
     if (!has_embed) return fail(MX_ERR_STATE, "this stage has no token embedding: x_in required");
-    launch_embed(x, tok_embd, ids, M, h, nol ? ssq : nullptr, s);
+    if (embd_q8) launch_embed_q8(x, tok_embd8, ids, M, h, s);
+    else launch_embed(x, tok_embd, ids, M, h, nol ? ssq : nullptr, s);
   }
+  if (wq8) return enqueue_forward_q8(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next, pos_next, hist,
+                                     hist_stride, hist_count, max_hist, s);
   if (M > MAX_ROWS) {
     if (!gemm_ok() || argmax || (head && n_out > MAX_ROWS))
       return fail(MX_ERR_ARG, "forward of > 64 rows: GEMM shapes only, logits for <= 64 rows");
@@ -646,6 +726,60 @@ int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void
                     hist_count, max_hist, s);
   } else if (nslab) {
     launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);
+  }
+  HIPC(hipGetLastError());
+  return 0;
+}
+
+// Q8_0 model, any M <= PREFILL_ROWS: every MUL_MAT takes Q8_0 activation rows made by the norm
+// (RMS_NORM + MUL + quantise) or by launch_quantize_q8 from the f32 attention output / SwiGLU
+// product -- ggml's conversion of src1 to the weight's vec_dot_type.
+int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap,
+                                  int n_out, bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride,
+                                  int* hist_count, int max_hist, hipStream_t s) {
+  const int h = n_embd, kv = n_embd_kv, ff = n_ff;
+  if (head && n_out > MAX_ROWS) return fail(MX_ERR_ARG, "logits for at most 64 rows per forward");
+  for (int li = 0; li < (int)layers.size(); li++) {
+    const Layer& L = layers[li];
+    _Float16* kc = kcache + layer_kv_stride * li;
+    _Float16* vc = vcache + layer_kv_stride * li;
+    launch_rmsnorm_q8(xq8, xqd, x, L.attn_norm, nullptr, M, h, eps, s);
+    MMArgs a{};
+    a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M; a.xq = xq8; a.xd = xqd;
+    a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
+    a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
+    a.slot_stride = slot_stride;
+    if (launch_mq8(EPI_QKV, a, s)) return fail(MX_ERR_ARG, "q8 qkv launch shape");
+    AttnArgs at{};
+    at.q = q; at.kc = kc; at.vc = vc; at.pos = pos; at.slot = slot;
+    at.outf = attn_f; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
+    at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;
+    at.scale = 1.0f / sqrtf((float)head_dim);
+    if (M > MAX_ROWS && rows_blocked) launch_attention_prefill(at, s);
+    else launch_attention(at, s);
+    launch_quantize_q8(xq8, xqd, attn_f, h, M, h, s);
+    MMArgs b{};
+    b.W = L.o; b.N = h; b.K = h; b.M = M; b.xq = xq8; b.xd = xqd; b.out = x; b.ldo = h;
+    if (launch_mq8(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "q8 attn_output launch shape");
+    launch_rmsnorm_q8(xq8, xqd, x, L.ffn_norm, nullptr, M, h, eps, s);
+    MMArgs c{};
+    c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.xq = xq8; c.xd = xqd; c.actf = act_f; c.lda = ff;
+    if (launch_mq8(EPI_SWIGLU, c, s)) return fail(MX_ERR_ARG, "q8 gate/up launch shape");
+    launch_quantize_q8(xq8, xqd, act_f, ff, M, ff, s);
+    MMArgs d{};
+    d.W = L.down; d.N = h; d.K = ff; d.M = M; d.xq = xq8; d.xd = xqd; d.out = x; d.ldo = h;
+    if (launch_mq8(EPI_RESID, d, s)) return fail(MX_ERR_ARG, "q8 ffn_down launch shape");
+  }
+  if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
+  if (head) {
+    if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
+    launch_rmsnorm_q8(xq8, xqd, x, out_norm, rowmap, n_out, h, eps, s);
+    MMArgs g{};
+    g.W = output; g.N = n_vocab; g.K = h; g.M = n_out; g.xq = xq8; g.xd = xqd; g.out = logits; g.ldo = n_vocab;
+    if (launch_mq8(EPI_F32, g, s)) return fail(MX_ERR_ARG, "q8 lm_head launch shape");
+    if (argmax)
+      launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, ids_next, pos_next, hist, hist_stride,
+                    hist_count, max_hist, s);
   }
   HIPC(hipGetLastError());
   return 0;
@@ -1018,17 +1152,25 @@ int mx_engine_create(const char* model_path, const mx_opts* opts, mx_engine** ou
   if (path.rfind("synthetic:", 0) == 0) {
     std::string rest = path.substr(10), name = rest;
     uint64_t seed = o.seed;
+    bool q8 = false;
     size_t c = rest.find(':');
     if (c != std::string::npos) {
       name = rest.substr(0, c);
       std::string tail = rest.substr(c + 1);
-      if (tail.rfind("seed=", 0) == 0) seed = strtoull(tail.c_str() + 5, nullptr, 10);
+      while (!tail.empty()) {  // ":seed=N" and/or ":q8_0"
+        const size_t e2 = tail.find(':');
+        const std::string part = tail.substr(0, e2);
+        if (part.rfind("seed=", 0) == 0) seed = strtoull(part.c_str() + 5, nullptr, 10);
+        else if (part == "q8_0") q8 = true;
+        else if (part != "bf16") return fail(MX_ERR_MODEL, "unknown synthetic option '" + part + "'");
+        tail = e2 == std::string::npos ? "" : tail.substr(e2 + 1);
+      }
     }
     const Shape* s = nullptr;
     for (const Shape& k : kShapes)
       if (name == k.name) s = &k;
     if (!s) return fail(MX_ERR_MODEL, "unknown synthetic shape '" + name + "'");
-    rc = e->load_synthetic(*s, seed);
+    rc = e->load_synthetic(*s, seed, q8);
   } else {
     rc = e->load_gguf(path);
   }
@@ -1048,6 +1190,7 @@ int mx_engine_info(const mx_engine* e, mx_model_info* o) {
   o->n_ctx = e->n_ctx; o->n_seq_max = e->n_seq_max; o->layer_begin = e->lb; o->layer_end = e->le;
   o->has_embed = e->has_embed; o->has_head = e->has_head; o->weight_bytes = e->weight_bytes;
   o->persistent_decode = e->use_pdk ? 1 : 0; o->persistent_grid = e->pdk_grid;
+  o->weight_type = e->wq8 ? 8 : 30;
   return 0;
 }
 
@@ -1334,6 +1477,32 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
     const Layer& L = e->layers[li];
     MMArgs a{};
     a.M = M;
+    if (e->wq8 && kind <= 4) {  // Q8_0 weights: the activations are Q8_0 rows in xq8/xqd
+      a.xq = e->xq8; a.xd = e->xqd;
+      switch (kind) {
+        case 0:
+          a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.out = e->q; a.ldo = h; a.n_q = h; a.n_kv = kv;
+          a.head_dim = e->head_dim; a.pos = e->d_pos; a.slot = e->d_slot; a.rope_cs = e->rope_cs;
+          a.kc = e->kcache + e->layer_kv_stride * li; a.vc = e->vcache + e->layer_kv_stride * li;
+          a.n_ctx = e->n_ctx; a.ctx_stride = e->ctx_stride; a.n_head_kv = e->n_head_kv; a.slot_stride = e->slot_stride;
+          per = q8_matrix_bytes(h + 2 * kv, h);
+          return launch_mq8(EPI_QKV, a, s);
+        case 1: case 3:
+          a.W = kind == 1 ? L.o : L.down; a.N = h; a.K = kind == 1 ? h : ff; a.out = e->x; a.ldo = h;
+          per = q8_matrix_bytes(h, a.K);
+          return launch_mq8(EPI_RESID, a, s);
+        case 2:
+          a.W = L.gu; a.N = 2 * ff; a.K = h; a.actf = e->act_f; a.lda = ff;
+          per = q8_matrix_bytes(2 * ff, h);
+          return launch_mq8(EPI_SWIGLU, a, s);
+        case 4:
+          if (!e->has_head) return -1;
+          a.W = e->output; a.N = e->n_vocab; a.K = h; a.out = e->logits; a.ldo = e->n_vocab;
+          per = q8_matrix_bytes(e->n_vocab, h);
+          return launch_mq8(EPI_F32, a, s);
+      }
+    }
+    if (e->wq8 && (kind == 5 || kind == 6)) return -1;
     switch (kind) {
       case 0:
         a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.X = e->xn; a.ldx = h; a.out = e->q; a.ldo = h; a.n_q = h;

@@ -50,6 +50,11 @@ struct MMArgs {
   int ldo;
   uint16_t* act;       // EPI_SWIGLU: bf16 [M][lda]
   int lda;
+  float* actf;         // EPI_SWIGLU: f32 [M][lda] instead of act (Q8_0 models quantise it next)
+  // Q8_0 weights (mq8_kernel): activations as Q8_0 rows, xq int8 [M][K] (k permuted within
+  // 64-k groups, see q8_perm) and xd f32 [M][K/32] (the f16-rounded block scales)
+  const int8_t* xq;
+  const float* xd;
   // EPI_QKV
   int n_q, n_kv, head_dim;     // rows [0,n_q) q, [n_q,n_q+n_kv) k, rest v
   const int* pos;              // [M]
@@ -70,6 +75,7 @@ struct AttnArgs {
   const int* slot;       // [M]
   uint16_t* out;         // bf16 [M][ldo] (src1 of attn_output)
   int ldo;
+  float* outf;           // f32 [M][ldo] instead of out (Q8_0 models quantise it next)
   int M, n_head, n_head_kv, head_dim, n_ctx, ctx_stride;
   size_t slot_stride;
   float scale;
@@ -157,6 +163,25 @@ void launch_attention_prefill(const AttnArgs& a, hipStream_t s);
 // prefill (> MAX_ROWS rows): MFMA GEMM over packed weights with the same epilogues (N % 256, K % 64)
 bool gemm_supported(int N, int K);
 int launch_gemm(int epi, const MMArgs& a, hipStream_t s);
+// ---- Q8_0 weights.  Packed tile = 16 rows x 64 k, Q8_TILE_BYTES:
+// [0,1024): int8 A operands of two v_mfma_i32_16x16x32_i8, lane l = row l&15 holds 8 bytes of
+// block 0 (k 8(l>>4)..+8) then 8 bytes of block 1 (k 32+8(l>>4)..+8); [1024,1088): f16 block
+// scales, row group g = rows 4g..4g+3: [block 0 x 4 rows][block 1 x 4 rows].  Tiles nt-major.
+constexpr int Q8_TILE_K = 64;
+constexpr int Q8_TILE_BYTES = 1088;
+inline size_t q8_matrix_bytes(int N, int K) { return (size_t)N / 16 * (K / Q8_TILE_K) * Q8_TILE_BYTES; }
+void launch_pack_q8(uint8_t* dst, const uint8_t* src_blocks, int N, int K, int mode, int row_offset, hipStream_t s);
+void launch_synth_q8_packed(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, int mode,
+                            int row_offset, hipStream_t s);
+void launch_synth_q8_rowmajor(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, hipStream_t s);
+void launch_embed_q8(float* x, const uint8_t* tok_embd_blocks, const int* ids, int M, int n_embd, hipStream_t s);
+// RMS_NORM + MUL, quantised to Q8_0 activation rows (xq [M][n], xd [M][n/32])
+void launch_rmsnorm_q8(int8_t* xq, float* xd, const float* x, const float* w, const int* row_map, int M, int n,
+                       float eps, hipStream_t s);
+void launch_quantize_q8(int8_t* xq, float* xd, const float* src, int ld, int M, int n, hipStream_t s);
+// Q8_0 x Q8_0 products for any M (column groups of <= 64 tokens on grid.y), same epilogues
+int launch_mq8(int epi, const MMArgs& a, hipStream_t s);
+
 void launch_argmax(const float* logits, int ldl, int M, int V, float* ws_val, int* ws_idx, int* tok_out,
                    int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count, int max_hist,
                    hipStream_t s);

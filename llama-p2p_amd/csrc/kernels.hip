@@ -406,16 +406,17 @@ __device__ __forceinline__ void epi_store(const MMArgs& a, int tile, int l, int 
     *px = *px + s;
   } else if constexpr (EPI == EPI_SWIGLU) {
     const int row = tile * 8 + (l >> 4) * 4;  // ffn row of gate lane l / up lane l+32
-    uint32_t h[4];
+    f32x4 f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float g = s[i];
-      h[i] = f2bf((g / (1.0f + expf(-g))) * up[i]);
+    for (int i = 0; i < 4; ++i) f[i] = (s[i] / (1.0f + expf(-s[i]))) * up[i];
+    if (a.actf) {
+      *reinterpret_cast<f32x4*>(a.actf + (size_t)col * a.lda + row) = f;
+    } else {
+      u32x2 o;
+      o[0] = f2bf(f[0]) | (f2bf(f[1]) << 16);
+      o[1] = f2bf(f[2]) | (f2bf(f[3]) << 16);
+      *reinterpret_cast<u32x2*>(a.act + (size_t)col * a.lda + row) = o;
     }
-    u32x2 o;
-    o[0] = h[0] | (h[1] << 16);
-    o[1] = h[2] | (h[3] << 16);
-    *reinterpret_cast<u32x2*>(a.act + (size_t)col * a.lda + row) = o;
   } else {  // EPI_QKV
     qkv_store(a, tile * 16 + (l >> 4) * 4, col, s);
   }
@@ -1086,7 +1087,8 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_kernel(AttnArgs a) {
       L += f * Ll[ww][h];
       acc += f * Om[ww][h][d];
     }
-    a.out[(size_t)c * a.ldo + (kvh * G + h) * D + d] = (uint16_t)f2bf(acc / L);
+    if (a.outf) a.outf[(size_t)c * a.ldo + (kvh * G + h) * D + d] = acc / L;
+    else a.out[(size_t)c * a.ldo + (kvh * G + h) * D + d] = (uint16_t)f2bf(acc / L);
   }
 }
 
@@ -1427,7 +1429,8 @@ __global__ __launch_bounds__(64 * G) void attn_prefill_kernel(AttnArgs a) {
     const float inv = 1.0f / l_i[i];
 #pragma unroll
     for (int t = 0; t < DT; ++t)
-      a.out[(size_t)row * a.ldo + (size_t)hq * D + t * 16 + r16] = (uint16_t)f2bf(o[t][i] * inv);
+      if (a.outf) a.outf[(size_t)row * a.ldo + (size_t)hq * D + t * 16 + r16] = o[t][i] * inv;
+      else a.out[(size_t)row * a.ldo + (size_t)hq * D + t * 16 + r16] = (uint16_t)f2bf(o[t][i] * inv);
   }
 }
 
@@ -1447,6 +1450,343 @@ void launch_attention_prefill(const AttnArgs& a, hipStream_t s) {
     launch_attn_prefill_d<64>(a, s);
   else
     launch_attn_prefill_d<128>(a, s);
+}
+
+// ---------------------------------------------------------------------------
+// Q8_0 weights  (ggml-common.h block_q8_0, ggml-quants.c)
+//
+// A Q8_0 GGUF stores each weight row as blocks of 32: f16 scale d + 32 int8 q,
+// w = q * d.  ggml's MUL_MAT quantises the f32 activation row to Q8_0 too
+// (vec_dot_type of Q8_0) and takes per block (d_w * d_x) * sum(q_w * q_x).
+// Here the weights are repacked into 1088-byte tiles (kernels.h) that feed
+// v_mfma_i32_16x16x32_i8 directly: one MFMA per 16 rows x one block, the int32
+// block sums scaled by d_w * d_x in f32.  Activations are quantised once per
+// GEMV by their producer-side kernel (norm or launch_quantize_q8) into rows whose
+// 64-k groups are permuted so a lane's 16-byte B fragment of both blocks is one
+// load.  Decode reads 1.0625 bytes per weight instead of 2.
+// ---------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+// permuted byte position of logical k in a Q8_0 activation row: within each 64-k group,
+// lane group g reads 16 bytes = k 8g..8g+7 (block 0) then k 32+8g..32+8g+7 (block 1)
+__device__ __forceinline__ int q8_perm(int k) {
+  return (k & ~63) | (((k >> 3) & 3) << 4) | (((k >> 5) & 1) << 3) | (k & 7);
+}
+
+// ggml quantize_row_q8_0_ref on one block (weights): ties away from zero
+__device__ __forceinline__ void q8_quant_ref(const float (&v)[32], uint16_t& dbits, int8_t (&q)[32]) {
+  float amax = 0.f;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(v[j]));
+  const float d = amax / 127.0f;
+  const float id = d != 0.f ? 1.0f / d : 0.0f;
+  dbits = __builtin_bit_cast(uint16_t, (_Float16)d);
+#pragma unroll
+  for (int j = 0; j < 32; ++j) q[j] = (int8_t)roundf(v[j] * id);
+}
+
+// place one block (row, block b) into its packed tile
+__device__ __forceinline__ void q8_place(uint8_t* dst, int P, int b, int KT2, uint16_t dbits, const int8_t (&q)[32]) {
+  uint8_t* tile = dst + ((size_t)(P >> 4) * KT2 + (b >> 1)) * Q8_TILE_BYTES;
+  const int r = P & 15, half = b & 1;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      w0 |= (uint32_t)(uint8_t)q[8 * g + j] << (8 * j);
+      w1 |= (uint32_t)(uint8_t)q[8 * g + 4 + j] << (8 * j);
+    }
+    uint32_t* p = reinterpret_cast<uint32_t*>(tile + 16 * (g * 16 + r) + 8 * half);
+    p[0] = w0;
+    p[1] = w1;
+  }
+  *reinterpret_cast<uint16_t*>(tile + 1024 + 16 * (r >> 2) + 8 * half + 2 * (r & 3)) = dbits;
+}
+
+__global__ void pack_q8_kernel(uint8_t* dst, const uint8_t* src, int N, int K, int mode, int offset) {
+  const int nb = K / 32;
+  const size_t total = (size_t)N * nb;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int row = (int)(i / nb), b = (int)(i % nb);
+    const uint8_t* blk = src + i * 34;
+    const uint16_t dbits = (uint16_t)(blk[0] | (blk[1] << 8));
+    int8_t q[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) q[j] = (int8_t)blk[2 + j];
+    q8_place(dst, packed_row(row, mode, offset), b, K / Q8_TILE_K, dbits, q);
+  }
+}
+
+// synthetic Q8_0 matrix: the quantisation of the bf16 synthetic matrix (synth.py values -> bf16 -> f32)
+__device__ __forceinline__ void q8_synth_block(uint64_t seed, uint64_t tid, size_t i0, float scale, uint16_t& dbits,
+                                               int8_t (&q)[32]) {
+  float v[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) v[j] = bf2f(f2bf(synth_value(seed, tid, i0 + j, scale)));
+  q8_quant_ref(v, dbits, q);
+}
+
+__global__ void synth_q8_packed_kernel(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, int mode,
+                                       int offset) {
+  const int nb = K / 32;
+  const size_t total = (size_t)N * nb;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int row = (int)(i / nb), b = (int)(i % nb);
+    uint16_t dbits;
+    int8_t q[32];
+    q8_synth_block(seed, tid, (size_t)row * K + 32 * b, scale, dbits, q);
+    q8_place(dst, packed_row(row, mode, offset), b, K / Q8_TILE_K, dbits, q);
+  }
+}
+
+__global__ void synth_q8_rowmajor_kernel(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale) {
+  const size_t total = (size_t)N * (K / 32);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    uint16_t dbits;
+    int8_t q[32];
+    q8_synth_block(seed, tid, i * 32, scale, dbits, q);
+    uint8_t* blk = dst + i * 34;
+    blk[0] = (uint8_t)dbits;
+    blk[1] = (uint8_t)(dbits >> 8);
+#pragma unroll
+    for (int j = 0; j < 32; ++j) blk[2 + j] = (uint8_t)q[j];
+  }
+}
+
+void launch_pack_q8(uint8_t* dst, const uint8_t* src, int N, int K, int mode, int offset, hipStream_t s) {
+  pack_q8_kernel<<<fill_grid((size_t)N * K / 32), 256, 0, s>>>(dst, src, N, K, mode, offset);
+}
+void launch_synth_q8_packed(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, int mode,
+                            int offset, hipStream_t s) {
+  synth_q8_packed_kernel<<<fill_grid((size_t)N * K / 32), 256, 0, s>>>(dst, N, K, seed, tid, scale, mode, offset);
+}
+void launch_synth_q8_rowmajor(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, hipStream_t s) {
+  synth_q8_rowmajor_kernel<<<fill_grid((size_t)N * K / 32), 256, 0, s>>>(dst, N, K, seed, tid, scale);
+}
+
+// GET_ROWS of a Q8_0 token_embd (dequantize_row_q8_0): x = q * f32(d); thread = one block
+__global__ __launch_bounds__(256) void embed_q8_kernel(float* x, const uint8_t* tok, const int* ids, int n) {
+  const int c = blockIdx.x;
+  const uint8_t* row = tok + (size_t)ids[c] * (n / 32) * 34;
+  for (int b = threadIdx.x; b < n / 32; b += blockDim.x) {
+    const uint8_t* blk = row + (size_t)b * 34;
+    const float d = (float)__builtin_bit_cast(_Float16, (uint16_t)(blk[0] | (blk[1] << 8)));
+    float* xo = x + (size_t)c * n + 32 * b;
+#pragma unroll
+    for (int j = 0; j < 32; j += 4)
+      *reinterpret_cast<f32x4*>(xo + j) = f32x4{(float)(int8_t)blk[2 + j] * d, (float)(int8_t)blk[3 + j] * d,
+                                               (float)(int8_t)blk[4 + j] * d, (float)(int8_t)blk[5 + j] * d};
+  }
+}
+
+void launch_embed_q8(float* x, const uint8_t* tok, const int* ids, int M, int n, hipStream_t s) {
+  embed_q8_kernel<<<M, 256, 0, s>>>(x, tok, ids, n);
+}
+
+// Activation quantisation (ggml quantize_row_q8_0, vec_dot_type of Q8_0): 8 aligned lanes hold the
+// 32 values of one block, 4 consecutive each (k = first of them).  d = amax/127, id = d ? 1/d : 0,
+// q = round-half-even(v * id) (ggml's AVX2/NEON rounding), d kept as its f16 value.
+__device__ __forceinline__ void q8_store_act(f32x4 v, int k, int8_t* qrow, float* drow) {
+  float amax = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+  amax = fmaxf(amax, __shfl_xor(amax, 1));
+  amax = fmaxf(amax, __shfl_xor(amax, 2));
+  amax = fmaxf(amax, __shfl_xor(amax, 4));
+  const float d = amax / 127.0f;
+  const float id = d != 0.f ? 1.0f / d : 0.0f;
+  uint32_t w = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w |= (uint32_t)(uint8_t)(int8_t)(int)__builtin_rintf(v[j] * id) << (8 * j);
+  *reinterpret_cast<uint32_t*>(qrow + q8_perm(k)) = w;
+  if ((k & 31) == 0) drow[k >> 5] = round_f16(d);
+}
+
+// RMS_NORM + MUL -> Q8_0 rows (norm_generic_kernel's arithmetic, then quantised)
+__global__ __launch_bounds__(256) void norm_q8_kernel(int8_t* xq, float* xd, const float* x, const float* w,
+                                                      const int* row_map, int n, float eps) {
+  const int c = blockIdx.x;
+  const int r = row_map ? row_map[c] : c;
+  const float* xr = x + (size_t)r * n;
+  double acc = 0.0;
+  for (int i = threadIdx.x * 4; i < n; i += 1024) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc += (double)(v[j] * v[j]);
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  __shared__ double part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  const double sum = part[0] + part[1] + part[2] + part[3];
+  const float scale = 1.0f / sqrtf((float)(sum / n) + eps);
+  for (int i = threadIdx.x * 4; i < n; i += 1024) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
+    const f32x4 g = *reinterpret_cast<const f32x4*>(w + i);
+    f32x4 y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = (v[j] * scale) * g[j];
+    q8_store_act(y, i, xq + (size_t)c * n, xd + (size_t)c * (n / 32));
+  }
+}
+
+__global__ __launch_bounds__(256) void quantize_q8_kernel(int8_t* xq, float* xd, const float* src, int ld, int n) {
+  const int c = blockIdx.x;
+  for (int i = threadIdx.x * 4; i < n; i += 1024)
+    q8_store_act(*reinterpret_cast<const f32x4*>(src + (size_t)c * ld + i), i, xq + (size_t)c * n,
+                 xd + (size_t)c * (n / 32));
+}
+
+void launch_rmsnorm_q8(int8_t* xq, float* xd, const float* x, const float* w, const int* row_map, int M, int n,
+                       float eps, hipStream_t s) {
+  norm_q8_kernel<<<M, 256, 0, s>>>(xq, xd, x, w, row_map, n, eps);
+}
+void launch_quantize_q8(int8_t* xq, float* xd, const float* src, int ld, int M, int n, hipStream_t s) {
+  quantize_q8_kernel<<<M, 256, 0, s>>>(xq, xd, src, ld, n);
+}
+
+// Q8_0 x Q8_0 MUL_MAT: mm_kernel's work split (KS waves over K, RT row tiles, NB column tiles of
+// 16 tokens, ring of U tiles per wave) over 1088-byte Q8 tiles; grid.y = groups of 16*NB tokens.
+template <int KS, int RT, int NB, int EPI, int U>
+__global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int KT = a.K / Q8_TILE_K;
+  const int tile0 = blockIdx.x * RT;
+  const int cb = blockIdx.y * 16 * NB;
+  const int kb = (KT * w) / KS, ke = (KT * (w + 1)) / KS;
+
+  __shared__ f32x4 red[KS][RT][NB][64];
+
+  const uint8_t* Wr[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) Wr[r] = reinterpret_cast<const uint8_t*>(a.W) + (size_t)(tile0 + r) * KT * Q8_TILE_BYTES;
+  const int8_t* Xq[NB];
+  const float* Xd[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    int col = cb + n * 16 + (lane & 15);
+    col = col < a.M ? col : a.M - 1;  // padded columns re-read a valid row (outputs dropped)
+    Xq[n] = a.xq + (size_t)col * a.K + (lane >> 4) * 16;
+    Xd[n] = a.xd + (size_t)col * (a.K / 32);
+  }
+
+  f32x4 acc[RT][NB];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  struct Frag {
+    u32x4 q[RT], d[RT];
+  };
+  auto load_w = [&](Frag& f, int kt) {
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const uint8_t* t = Wr[r] + (size_t)kt * Q8_TILE_BYTES;
+      f.q[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t) + lane);
+      f.d[r] = *reinterpret_cast<const u32x4*>(t + 1024 + 16 * (lane >> 4));
+    }
+  };
+  auto mma = [&](const Frag& f, int kt) {
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const u32x4 xb = *reinterpret_cast<const u32x4*>(Xq[n] + kt * Q8_TILE_K);
+      const f32x2 dx = *reinterpret_cast<const f32x2*>(Xd[n] + 2 * kt);
+      const long b0 = (long)(((unsigned long)xb[1] << 32) | xb[0]);
+      const long b1 = (long)(((unsigned long)xb[3] << 32) | xb[2]);
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const long a0 = (long)(((unsigned long)f.q[r][1] << 32) | f.q[r][0]);
+        const long a1 = (long)(((unsigned long)f.q[r][3] << 32) | f.q[r][2]);
+        const i32x4 p0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, b0, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        const i32x4 p1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, b1, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        const f16x8 dw = __builtin_bit_cast(f16x8, f.d[r]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[r][n][i] = fmaf((float)dw[i] * dx[0], (float)p0[i], acc[r][n][i]);
+          acc[r][n][i] = fmaf((float)dw[4 + i] * dx[1], (float)p1[i], acc[r][n][i]);
+        }
+      }
+    }
+  };
+
+  Frag ring[U];
+  int kt = kb;
+  const int nfull = (ke - kb) / U;
+  if (nfull > 0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) load_w(ring[u], kt + u);
+    for (int ch = 1; ch < nfull; ++ch) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        mma(ring[u], kt + u);
+        load_w(ring[u], kt + U + u);
+      }
+      kt += U;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) mma(ring[u], kt + u);
+    kt += U;
+  }
+  for (; kt < ke; ++kt) {
+    Frag f;
+    load_w(f, kt);
+    mma(f, kt);
+  }
+
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) red[w][r][n][lane] = acc[r][n];
+  __syncthreads();
+
+  constexpr int LU = (EPI == EPI_SWIGLU) ? 32 : 64;
+  constexpr int UNITS = RT * NB * LU;
+  for (int u = threadIdx.x; u < UNITS; u += 64 * KS) {
+    const int l = u % LU;
+    const int n = (u / LU) % NB;
+    const int r = (u / LU) / NB;
+    const int col = cb + n * 16 + (l & 15);
+    if (col >= a.M) continue;
+    f32x4 s = red[0][r][n][l];
+#pragma unroll
+    for (int ww = 1; ww < KS; ++ww) s += red[ww][r][n][l];
+    f32x4 up = s;
+    if constexpr (EPI == EPI_SWIGLU) {
+      up = red[0][r][n][l + 32];
+#pragma unroll
+      for (int ww = 1; ww < KS; ++ww) up += red[ww][r][n][l + 32];
+    }
+    epi_store<EPI>(a, tile0 + r, l, col, s, up);
+  }
+}
+
+// one column tile: 16 waves split K (as mm_kernel); two or four tiles: 8 waves (the B fragments and
+// block scales of every tile stay in registers: 16 waves would spill)
+template <int EPI>
+static int launch_mq8_epi(const MMArgs& a, hipStream_t s) {
+  const int ntiles = a.N / TILE_N;
+  if (a.M <= 16) {
+    mq8_kernel<16, 1, 1, EPI, 4><<<dim3(ntiles, 1), 1024, 0, s>>>(a);
+  } else if (a.M <= 32) {
+    mq8_kernel<8, 1, 2, EPI, 4><<<dim3(ntiles, 1), 512, 0, s>>>(a);
+  } else {
+    mq8_kernel<8, 1, 4, EPI, 2><<<dim3(ntiles, (a.M + 63) / 64), 512, 0, s>>>(a);
+  }
+  return 0;
+}
+
+int launch_mq8(int epi, const MMArgs& a, hipStream_t s) {
+  if (a.M < 1 || a.K % Q8_TILE_K || a.N % TILE_N || !a.xq || !a.xd) return -1;
+  if (epi == EPI_SWIGLU && !a.actf && !a.act) return -1;
+  switch (epi) {
+    case EPI_F32: return launch_mq8_epi<EPI_F32>(a, s);
+    case EPI_RESID: return launch_mq8_epi<EPI_RESID>(a, s);
+    case EPI_QKV: return launch_mq8_epi<EPI_QKV>(a, s);
+    case EPI_SWIGLU: return launch_mq8_epi<EPI_SWIGLU>(a, s);
+  }
+  return -1;
 }
 
 }  // namespace mx

@@ -49,7 +49,7 @@ class MxModelInfo(ctypes.Structure):
                [(n, ctypes.c_int32) for n in ("bos_id", "eos_id", "n_ctx", "n_seq_max", "layer_begin",
                                               "layer_end", "has_embed", "has_head")] + \
                [("weight_bytes", ctypes.c_uint64), ("persistent_decode", ctypes.c_int32),
-                ("persistent_grid", ctypes.c_int32)]
+                ("persistent_grid", ctypes.c_int32), ("weight_type", ctypes.c_int32)]
 
 
 class MxSampling(ctypes.Structure):

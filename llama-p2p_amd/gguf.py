@@ -29,6 +29,51 @@ _SCALAR = {
 # ggml tensor types used here
 GGML_F32, GGML_F16, GGML_Q4_0, GGML_Q8_0, GGML_Q4_K, GGML_Q6_K, GGML_BF16 = 0, 1, 2, 8, 12, 14, 30
 _TYPE_ELEM_BYTES = {GGML_F32: 4, GGML_F16: 2, GGML_BF16: 2}
+QK8_0 = 32          # ggml block_q8_0: f16 d + 32 x int8 (ggml-common.h)
+Q8_0_BLOCK = 34
+
+
+def type_nbytes(ggml_type: int, n: int) -> int:
+    if ggml_type == GGML_Q8_0:
+        if n % QK8_0:
+            raise ValueError("Q8_0 rows must be a multiple of 32")
+        return n // QK8_0 * Q8_0_BLOCK
+    return n * _TYPE_ELEM_BYTES[ggml_type]
+
+
+def _round_half_away(v: np.ndarray) -> np.ndarray:
+    """C roundf(): ties away from zero (numpy's round is ties-to-even).  v is f32; the
+    +-0.5 is added in f64, where it is exact, so no second rounding can creep in."""
+    v = v.astype(np.float64)
+    return np.trunc(v + np.copysign(0.5, v))
+
+
+def quantize_q8_0(x: np.ndarray) -> np.ndarray:
+    """ggml quantize_row_q8_0_ref (ggml-quants.c), row-wise over the last axis: per block of
+    32, d = amax/127 (f32), id = d ? 1/d : 0, q = roundf(x*id), d stored as f16.  This is what
+    llama.cpp's convert/quantize tools write for weights.  Returns uint8 [..., K/32*34]."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    K = x.shape[-1]
+    if K % QK8_0:
+        raise ValueError("Q8_0 rows must be a multiple of 32")
+    b = x.reshape(-1, K // QK8_0, QK8_0)
+    amax = np.abs(b).max(axis=-1)
+    d = (amax / np.float32(127)).astype(np.float32)
+    with np.errstate(divide="ignore"):
+        idv = np.where(d != 0, np.float32(1) / d, np.float32(0)).astype(np.float32)
+    q = _round_half_away(b * idv[..., None]).astype(np.int8)
+    out = np.empty(b.shape[:2] + (Q8_0_BLOCK,), dtype=np.uint8)
+    out[..., :2] = d.astype(np.float16).view(np.uint8).reshape(b.shape[:2] + (2,))
+    out[..., 2:] = q.view(np.uint8)
+    return out.reshape(x.shape[:-1] + (K // QK8_0 * Q8_0_BLOCK,))
+
+
+def dequantize_q8_0(blocks: np.ndarray, K: int) -> np.ndarray:
+    """ggml dequantize_row_q8_0: y = q * f32(d)."""
+    b = np.ascontiguousarray(blocks, dtype=np.uint8).reshape(-1, K // QK8_0, Q8_0_BLOCK)
+    d = b[..., :2].copy().view(np.float16).astype(np.float32)
+    q = b[..., 2:].view(np.int8).astype(np.float32)
+    return (q * d).reshape(blocks.shape[:-1] + (K,))
 
 
 class GGUFWriter:
@@ -57,7 +102,7 @@ class GGUFWriter:
         """shape_rowmajor is numpy order ([out, in]); GGUF stores ne reversed ([in, out])."""
         ne = tuple(int(x) for x in reversed(shape_rowmajor))
         n = int(np.prod(ne))
-        nbytes = n * _TYPE_ELEM_BYTES[ggml_type]
+        nbytes = type_nbytes(ggml_type, n)
         self.tensors.append((name, ne, ggml_type, nbytes))
 
     @staticmethod
@@ -159,9 +204,13 @@ class GGUFReader:
     def tensor(self, name: str) -> np.ndarray:
         info = self.tensors[name]
         t = info["type"]
-        dt = {GGML_F32: np.float32, GGML_F16: np.float16, GGML_BF16: np.uint16}[t]
         shape = tuple(reversed(info["ne"]))
         n = int(np.prod(shape))
+        if t == GGML_Q8_0:  # raw blocks, [rows][K/32*34] uint8
+            nb = type_nbytes(t, n)
+            return np.memmap(self.path, dtype=np.uint8, mode="r", offset=info["offset"],
+                             shape=(nb,)).reshape(shape[:-1] + (shape[-1] // QK8_0 * Q8_0_BLOCK,))
+        dt = {GGML_F32: np.float32, GGML_F16: np.float16, GGML_BF16: np.uint16}[t]
         return np.memmap(self.path, dtype=dt, mode="r", offset=info["offset"], shape=(n,)).reshape(shape)
 
 
@@ -227,14 +276,25 @@ def synthetic_spm_vocab(n_vocab: int):
     return toks[:n_vocab], scores[:n_vocab], types[:n_vocab]
 
 
-def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = None):
-    """Write a bf16 LLaMA GGUF with the synthetic weights of synth.py."""
+def synth_q8_0_tensor(arr_bf16: np.ndarray) -> np.ndarray:
+    """Q8_0 blocks of a synthetic bf16 matrix: what llama.cpp's quantize tool makes of a bf16
+    checkpoint (bf16 -> f32 -> quantize_row_q8_0_ref)."""
     from . import synth
+    return quantize_q8_0(synth.bf16_bits_to_f32(arr_bf16))
+
+
+def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = None, wtype: str = "bf16"):
+    """Write a LLaMA GGUF with the synthetic weights of synth.py: every matrix bf16, or (wtype
+    "q8_0") the Q8_0 quantisation of those bf16 matrices; norms f32 either way."""
+    from . import synth
+
+    if wtype not in ("bf16", "q8_0"):
+        raise ValueError("wtype must be 'bf16' or 'q8_0'")
 
     w = GGUFWriter(path)
     w.add_string("general.architecture", "llama")
     w.add_string("general.name", f"synthetic-{shape.name}-seed{seed}")
-    w.add_uint32("general.file_type", 32)  # MOSTLY_BF16
+    w.add_uint32("general.file_type", 32 if wtype == "bf16" else 7)  # MOSTLY_BF16 / MOSTLY_Q8_0
     w.add_uint32("llama.context_length", n_ctx_train or shape.n_ctx_train)
     w.add_uint32("llama.embedding_length", shape.n_embd)
     w.add_uint32("llama.block_count", shape.n_layer)
@@ -256,7 +316,11 @@ def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = Non
     w.add_bool("tokenizer.ggml.add_bos_token", True)
     arrays = []
     for name, kind, arr in synth.synth_tensors(shape, seed):
-        w.add_tensor_info(name, arr.shape, GGML_BF16 if kind == "bf16" else GGML_F32)
-        arrays.append(arr)
+        if kind == "bf16" and wtype == "q8_0":
+            w.add_tensor_info(name, arr.shape, GGML_Q8_0)
+            arrays.append(synth_q8_0_tensor(arr))
+        else:
+            w.add_tensor_info(name, arr.shape, GGML_BF16 if kind == "bf16" else GGML_F32)
+            arrays.append(arr)
     w.write(arrays)
     return path

@@ -25,6 +25,15 @@
  *   - SwiGLU: silu(g) = g/(1+expf(-g)) in f32, times up, rounded to bf16 for
  *     ffn_down                                                   a12
  *   - logits f32 for the requested rows; greedy = argmax, ties -> lowest id  a13, a14
+ *   - Q8_0 weights (a GGUF quantised with llama.cpp's Q8_0): MUL_MAT
+ *     quantises the f32 activation rows to Q8_0 (vec_dot_type of GGML_TYPE_Q8_0):
+ *     per block of 32, d = amax/127, id = d ? 1/d : 0, q = round-half-even(x*id) (the
+ *     rounding of ggml's AVX2 / NEON quantize_row_q8_0; the scalar _ref rounds ties away
+ *     from zero -- a measure-zero difference), d kept as f16; then
+ *     ggml_vec_dot_q8_0_q8_0: sum over blocks of (f32(d_w)*f32(d_x)) * sum_i(qw*qx).
+ *     GET_ROWS of a Q8_0 token_embd dequantises: x = q * f32(d).  Weight blocks come
+ *     from the caller (the bytes of the GGUF) or from orc_quantize_q8 (ggml
+ *     quantize_row_q8_0_ref: ties away from zero), never from the engine.
  * ORC_EXACT mode drops every bf16/f16 activation rounding (fp32 math over the
  * same bf16 weights): that is what tests cross-check against
  * transformers.LlamaForCausalLM (an independent implementation) to pin the
@@ -52,6 +61,7 @@ typedef struct {
 typedef struct {
     uint16_t *wq, *wk, *wv, *wo, *wg, *wu, *wd; /* bf16 */
     float *attn_norm, *ffn_norm;
+    uint8_t *q8[9]; /* Q8_0 blocks by L_* kind (NULL: the bf16 matrix is used) */
 } orc_layer;
 
 typedef struct {
@@ -59,6 +69,7 @@ typedef struct {
     int flags;
     int head_dim, n_embd_kv;
     uint16_t *tok_embd, *output; /* bf16 [V][h] */
+    uint8_t *tok_embd_q8, *output_q8; /* Q8_0 blocks or NULL */
     float *out_norm;
     orc_layer *layers;
 } orc_model;
@@ -176,7 +187,9 @@ void orc_free(orc_model *m) {
         orc_layer *L = &m->layers[l];
         free(L->wq); free(L->wk); free(L->wv); free(L->wo); free(L->wg); free(L->wu); free(L->wd);
         free(L->attn_norm); free(L->ffn_norm);
+        for (int k = 0; k < 9; k++) free(L->q8[k]);
     }
+    free(m->tok_embd_q8); free(m->output_q8);
     free(m->layers); free(m->tok_embd); free(m->output); free(m->out_norm); free(m);
 }
 
@@ -230,6 +243,145 @@ int orc_set_tensor(orc_model *m, int layer, int kind, const void *src) {
     case L_DOWN: memcpy(L->wd, src, h * ff * 2); return 0;
     }
     return -1;
+}
+
+/* ------------------------------------------------------------------ Q8_0 */
+#define QK8_0 32
+#define Q8_0_BLOCK 34
+
+/* ggml quantize_row_q8_0_ref: what the quantize tool writes for weights (ties away from zero) */
+static void quantize_row_q8_0_ref(const float *x, uint8_t *y, int n) {
+    for (int b = 0; b < n / QK8_0; b++) {
+        const float *xb = x + (size_t)b * QK8_0;
+        float amax = 0.f;
+        for (int j = 0; j < QK8_0; j++) amax = fmaxf(amax, fabsf(xb[j]));
+        const float d = amax / 127.0f;
+        const float id = d != 0.f ? 1.0f / d : 0.0f;
+        uint8_t *yb = y + (size_t)b * Q8_0_BLOCK;
+        uint16_t dh = f32_to_f16(d);
+        memcpy(yb, &dh, 2);
+        for (int j = 0; j < QK8_0; j++) yb[2 + j] = (uint8_t)(int8_t)roundf(xb[j] * id);
+    }
+}
+
+static size_t q8_bytes(size_t rows, size_t cols) { return rows * (cols / QK8_0) * Q8_0_BLOCK; }
+
+static uint8_t **q8_slot(orc_model *m, int layer, int kind, size_t *rows, size_t *cols, uint16_t **bf) {
+    size_t h = m->hp.n_embd, kv = m->n_embd_kv, ff = m->hp.n_ff, V = m->hp.n_vocab;
+    if (layer < 0) {
+        if (kind == K_TOK_EMBD) { *rows = V; *cols = h; *bf = m->tok_embd; return &m->tok_embd_q8; }
+        if (kind == K_OUTPUT) { *rows = V; *cols = h; *bf = m->output; return &m->output_q8; }
+        return NULL;
+    }
+    if (layer >= m->hp.n_layer) return NULL;
+    orc_layer *L = &m->layers[layer];
+    switch (kind) {
+    case L_Q: *rows = h; *cols = h; *bf = L->wq; break;
+    case L_K: *rows = kv; *cols = h; *bf = L->wk; break;
+    case L_V: *rows = kv; *cols = h; *bf = L->wv; break;
+    case L_O: *rows = h; *cols = h; *bf = L->wo; break;
+    case L_GATE: *rows = ff; *cols = h; *bf = L->wg; break;
+    case L_UP: *rows = ff; *cols = h; *bf = L->wu; break;
+    case L_DOWN: *rows = h; *cols = ff; *bf = L->wd; break;
+    default: return NULL;
+    }
+    return &L->q8[kind];
+}
+
+/* Make one matrix Q8_0 from caller bytes (GGUF block layout, rows x cols/32 blocks of 34 B). */
+int orc_set_tensor_q8(orc_model *m, int layer, int kind, const void *blocks) {
+    size_t rows, cols;
+    uint16_t *bf;
+    uint8_t **slot = q8_slot(m, layer, kind, &rows, &cols, &bf);
+    if (!slot || cols % QK8_0) return -1;
+    if (!*slot) *slot = (uint8_t *)malloc(q8_bytes(rows, cols));
+    memcpy(*slot, blocks, q8_bytes(rows, cols));
+    return 0;
+}
+
+/* Quantise every matrix (token_embd, output, and the seven per layer) from its bf16 values. */
+int orc_quantize_q8(orc_model *m) {
+    static const int kinds[] = {L_Q, L_K, L_V, L_O, L_GATE, L_UP, L_DOWN};
+    for (int l = -1; l < m->hp.n_layer; l++) {
+        int nk = l < 0 ? 2 : 7;
+        for (int i = 0; i < nk; i++) {
+            int kind = l < 0 ? (i ? K_OUTPUT : K_TOK_EMBD) : kinds[i];
+            size_t rows, cols;
+            uint16_t *bf;
+            uint8_t **slot = q8_slot(m, l, kind, &rows, &cols, &bf);
+            if (!slot || cols % QK8_0) return -1;
+            if (!*slot) *slot = (uint8_t *)malloc(q8_bytes(rows, cols));
+            uint8_t *dst = *slot;
+#pragma omp parallel for schedule(static)
+            for (size_t r = 0; r < rows; r++)
+                for (size_t b = 0; b < cols / QK8_0; b++) {
+                    float blk[QK8_0];
+                    for (int j = 0; j < QK8_0; j++) blk[j] = bf16_to_f32(bf[r * cols + b * QK8_0 + j]);
+                    quantize_row_q8_0_ref(blk, dst + (r * (cols / QK8_0) + b) * Q8_0_BLOCK, QK8_0);
+                }
+        }
+    }
+    return 0;
+}
+
+/* activation row -> Q8_0 (vec_dot_type of Q8_0): q int8, d = f32 of the f16 scale */
+static void quantize_act_q8_0(const float *x, int n, int8_t *q, float *d) {
+    for (int b = 0; b < n / QK8_0; b++) {
+        const float *xb = x + (size_t)b * QK8_0;
+        float amax = 0.f;
+        for (int j = 0; j < QK8_0; j++) amax = fmaxf(amax, fabsf(xb[j]));
+        const float dd = amax / 127.0f;
+        const float id = dd != 0.f ? 1.0f / dd : 0.0f;
+        d[b] = round_f16(dd);
+        for (int j = 0; j < QK8_0; j++) q[(size_t)b * QK8_0 + j] = (int8_t)nearbyintf(xb[j] * id);
+    }
+}
+
+/* ggml_vec_dot_q8_0_q8_0 */
+static float dot_q8_0(const uint8_t *w, const int8_t *q, const float *d, int n) {
+    float s = 0.f;
+    for (int b = 0; b < n / QK8_0; b++) {
+        const uint8_t *wb = w + (size_t)b * Q8_0_BLOCK;
+        uint16_t dh;
+        memcpy(&dh, wb, 2);
+        int sumi = 0;
+        for (int j = 0; j < QK8_0; j++) sumi += (int)(int8_t)wb[2 + j] * (int)q[(size_t)b * QK8_0 + j];
+        s += (f16_to_f32(dh) * d[b]) * (float)sumi;
+    }
+    return s;
+}
+
+/* Sensitivity probe for tests: a relative perturbation of up to q8_jitter (deterministic hash
+ * noise) on every activation before it is quantised.  0 = off (the restatement proper).  The
+ * Q8_0 forward is discontinuous in its inputs (x*id crossing a rounding boundary moves q by one
+ * step), so the tests bound the engine's deviation by the oracle's own under 1e-6 noise. */
+static float q8_jitter = 0.0f;
+void orc_set_q8_jitter(float eps) { q8_jitter = eps; }
+
+static void matmul_q8(float *y, const uint8_t *W, const float *x, int T, int n_in, int n_out) {
+    int8_t *xq = (int8_t *)malloc((size_t)T * n_in);
+    float *xd = (float *)malloc(sizeof(float) * (size_t)T * (n_in / QK8_0));
+    float *xj = q8_jitter != 0.0f ? (float *)malloc(sizeof(float) * n_in) : NULL;
+    for (int t = 0; t < T; t++) {
+        const float *xr = x + (size_t)t * n_in;
+        if (xj) {
+            for (int i = 0; i < n_in; i++) {
+                unsigned hsh = (unsigned)i * 2654435761u + (unsigned)t * 97u + (unsigned)n_out;
+                xj[i] = xr[i] * (1.0f + q8_jitter * (float)((int)(hsh % 2001u) - 1000) / 1000.0f);
+            }
+            xr = xj;
+        }
+        quantize_act_q8_0(xr, n_in, xq + (size_t)t * n_in, xd + (size_t)t * (n_in / QK8_0));
+    }
+    free(xj);
+    const size_t rb = (size_t)(n_in / QK8_0) * Q8_0_BLOCK;
+#pragma omp parallel for schedule(static)
+    for (int o = 0; o < n_out; o++)
+        for (int t = 0; t < T; t++)
+            y[(size_t)t * n_out + o] = dot_q8_0(W + (size_t)o * rb, xq + (size_t)t * n_in,
+                                                xd + (size_t)t * (n_in / QK8_0), n_in);
+    free(xq);
+    free(xd);
 }
 
 /* ------------------------------------------------------------------ context */
@@ -297,8 +449,8 @@ static float dot_bf16_f32(const uint16_t *w, const float *x, int n) {
 }
 
 /* y[t][o] = W[o] . x[t] for T rows; ggml converts x to bf16 first (unless exact). */
-static void matmul(float *y, const uint16_t *W, const float *x, int T, int n_in, int n_out, int exact,
-                   uint16_t *scratch /* T*n_in */) {
+static void matmul_bf16(float *y, const uint16_t *W, const float *x, int T, int n_in, int n_out, int exact,
+                        uint16_t *scratch /* T*n_in */) {
     if (!exact) {
         for (size_t i = 0; i < (size_t)T * n_in; i++) scratch[i] = f32_to_bf16(x[i]);
 #pragma omp parallel for schedule(static)
@@ -311,6 +463,12 @@ static void matmul(float *y, const uint16_t *W, const float *x, int T, int n_in,
             for (int t = 0; t < T; t++)
                 y[(size_t)t * n_out + o] = dot_bf16_f32(W + (size_t)o * n_in, x + (size_t)t * n_in, n_in);
     }
+}
+
+static void matmul(float *y, const uint16_t *W, const uint8_t *Wq8, const float *x, int T, int n_in, int n_out,
+                   int exact, uint16_t *scratch) {
+    if (Wq8) matmul_q8(y, Wq8, x, T, n_in, n_out);
+    else matmul_bf16(y, W, x, T, n_in, n_out, exact, scratch);
 }
 
 static void rope_rows(float *v, int n_heads, int d, const float *cs /* [d/2][2] at pos */) {
@@ -353,15 +511,25 @@ int orc_eval(orc_ctx *c, const int32_t *ids, int n, int pos0, float *logits, int
     uint16_t *scratch = (uint16_t *)malloc(sizeof(uint16_t) * T * mx);
     const float kq_scale = 1.0f / sqrtf((float)d);
 
-    for (int t = 0; t < T; t++)
-        for (int i = 0; i < h; i++) x[(size_t)t * h + i] = bf16_to_f32(m->tok_embd[(size_t)ids[t] * h + i]);
+    for (int t = 0; t < T; t++) {
+        if (m->tok_embd_q8) { /* GET_ROWS of Q8_0: dequantize_row_q8_0 */
+            const uint8_t *rw = m->tok_embd_q8 + (size_t)ids[t] * (h / QK8_0) * Q8_0_BLOCK;
+            for (int i = 0; i < h; i++) {
+                uint16_t dh;
+                memcpy(&dh, rw + (size_t)(i / QK8_0) * Q8_0_BLOCK, 2);
+                x[(size_t)t * h + i] = (float)(int8_t)rw[(size_t)(i / QK8_0) * Q8_0_BLOCK + 2 + i % QK8_0] * f16_to_f32(dh);
+            }
+        } else {
+            for (int i = 0; i < h; i++) x[(size_t)t * h + i] = bf16_to_f32(m->tok_embd[(size_t)ids[t] * h + i]);
+        }
+    }
 
     for (int l = 0; l < hp->n_layer; l++) {
         orc_layer *L = &m->layers[l];
         for (int t = 0; t < T; t++) rmsnorm(cur + (size_t)t * h, x + (size_t)t * h, L->attn_norm, h, hp->eps);
-        matmul(q, L->wq, cur, T, h, h, exact, scratch);
-        matmul(k, L->wk, cur, T, h, kvd, exact, scratch);
-        matmul(v, L->wv, cur, T, h, kvd, exact, scratch);
+        matmul(q, L->wq, L->q8[L_Q], cur, T, h, h, exact, scratch);
+        matmul(k, L->wk, L->q8[L_K], cur, T, h, kvd, exact, scratch);
+        matmul(v, L->wv, L->q8[L_V], cur, T, h, kvd, exact, scratch);
         for (int t = 0; t < T; t++) {
             const float *cs = c->rope_cs + (size_t)(pos0 + t) * (d / 2) * 2;
             rope_rows(q + (size_t)t * h, nh, d, cs);
@@ -431,23 +599,23 @@ int orc_eval(orc_ctx *c, const int32_t *ids, int n, int pos0, float *logits, int
                 free(s);
             }
         }
-        matmul(tmp, L->wo, att, T, h, h, exact, scratch);
+        matmul(tmp, L->wo, L->q8[L_O], att, T, h, h, exact, scratch);
         for (size_t i = 0; i < (size_t)T * h; i++) x[i] += tmp[i];
         /* ffn */
         for (int t = 0; t < T; t++) rmsnorm(cur + (size_t)t * h, x + (size_t)t * h, L->ffn_norm, h, hp->eps);
-        matmul(u, L->wu, cur, T, h, ff, exact, scratch);
-        matmul(g, L->wg, cur, T, h, ff, exact, scratch);
+        matmul(u, L->wu, L->q8[L_UP], cur, T, h, ff, exact, scratch);
+        matmul(g, L->wg, L->q8[L_GATE], cur, T, h, ff, exact, scratch);
         for (size_t i = 0; i < (size_t)T * ff; i++) {
             float gg = g[i];
             g[i] = (gg / (1.0f + expf(-gg))) * u[i];
         }
-        matmul(tmp, L->wd, g, T, ff, h, exact, scratch);
+        matmul(tmp, L->wd, L->q8[L_DOWN], g, T, ff, h, exact, scratch);
         for (size_t i = 0; i < (size_t)T * h; i++) x[i] += tmp[i];
     }
     int t0 = all_logits ? 0 : T - 1;
     int nt = T - t0;
     for (int t = 0; t < nt; t++) rmsnorm(cur + (size_t)t * h, x + (size_t)(t0 + t) * h, m->out_norm, h, hp->eps);
-    matmul(logits, m->output, cur, nt, h, V, exact, scratch);
+    matmul(logits, m->output, m->output_q8, cur, nt, h, V, exact, scratch);
 
     free(x); free(cur); free(q); free(k); free(v); free(att); free(g); free(u); free(tmp); free(scratch);
     return 0;

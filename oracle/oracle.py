@@ -48,6 +48,11 @@ def lib():
         L.orc_fill_synthetic.argtypes = [vp, u64]
         L.orc_set_tensor.argtypes = [vp, i32, i32, vp]
         L.orc_set_tensor.restype = i32
+        L.orc_set_tensor_q8.argtypes = [vp, i32, i32, vp]
+        L.orc_set_tensor_q8.restype = i32
+        L.orc_quantize_q8.argtypes = [vp]
+        L.orc_quantize_q8.restype = i32
+        L.orc_set_q8_jitter.argtypes = [ctypes.c_float]
         L.orc_ctx_create.restype = vp
         L.orc_ctx_create.argtypes = [vp, i32]
         L.orc_ctx_free.argtypes = [vp]
@@ -83,6 +88,17 @@ class OracleModel:
         rc = lib().orc_set_tensor(self._m, layer, kind, arr.ctypes.data)
         if rc:
             raise ValueError(f"orc_set_tensor({layer},{kind}) failed")
+
+    def set_tensor_q8(self, layer: int, kind: int, blocks: np.ndarray):
+        """Make one matrix Q8_0 from GGUF block bytes (uint8 [rows][cols/32*34])."""
+        blocks = np.ascontiguousarray(blocks, dtype=np.uint8)
+        if lib().orc_set_tensor_q8(self._m, layer, kind, blocks.ctypes.data):
+            raise ValueError(f"orc_set_tensor_q8({layer},{kind}) failed")
+
+    def quantize_q8(self):
+        """Every matrix -> Q8_0 of its bf16 values (ggml quantize_row_q8_0_ref)."""
+        if lib().orc_quantize_q8(self._m):
+            raise ValueError("orc_quantize_q8 failed")
 
     def context(self, n_ctx: int = 512) -> "OracleContext":
         return OracleContext(self, n_ctx)
@@ -133,6 +149,11 @@ class OracleContext:
             self.close()
         except Exception:
             pass
+
+
+def q8_jitter(eps: float):
+    """Relative activation noise before every Q8_0 quantisation (sensitivity probe; 0 = off)."""
+    lib().orc_set_q8_jitter(eps)
 
 
 def argmax_lowest(logits: np.ndarray) -> int:

@@ -1,0 +1,132 @@
+"""Q8_0 GGUF models on the GPU: mq8_kernel (v_mfma_i32_16x16x32_i8 over
+packed Q8 tiles, activations quantised to Q8_0 rows as ggml's vec_dot_type) against the CPU
+oracle's Q8_0 MUL_MAT, for every row regime (1, 17-32, 33-64 and > 64 rows), the device greedy
+loop, and the GGUF loader (C++ parser + pack_q8_kernel) against on-device synthesis.
+
+Tolerance: the bf16 one of tests/conftest.py, and a sharper one.  Both sides quantise the same
+f32 activations with the same arithmetic, but Q8_0 is discontinuous: an activation whose x/d sits
+near a rounding boundary moves a whole step under any f32 reordering, and on these random-weight
+models that reaches ~1% of max|logit| (the oracle alone moves 0.075 of 5.4 on test-h4096 under
+1e-6 relative input noise).  So the engine's deviation is bounded by 2x the oracle's own deviation
+under 1e-6 noise (oracle.q8_jitter), the same-arithmetic-up-to-ordering claim made measurable."""
+import numpy as np
+import pytest
+
+from conftest import assert_logits_close, assert_tokens_match, check_greedy_chain
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mx():
+    from llama_p2p_amd import engine
+
+    engine.lib()
+    return engine
+
+
+def _seq(shape, n, seed=7):
+    rng = np.random.default_rng(seed)
+    return np.concatenate([[1], rng.integers(3, shape.n_vocab, n - 1)]).astype(np.int32)
+
+
+def _oracle_q8(oracle_mod, shape, seed):
+    om = oracle_mod.OracleModel(shape, seed=seed)
+    om.quantize_q8()
+    return om
+
+
+def test_q8_gguf_equals_synthetic(mx, tmp_path):
+    """A Q8_0 GGUF (numpy quantiser + C++ parser + pack_q8_kernel) and the on-device Q8_0 synthesis
+    of the same model give bit-identical logits; the info reports the weight type."""
+    from llama_p2p_amd import gguf, synth
+
+    shape = synth.SHAPES["test-tiny"]
+    path = str(tmp_path / "tiny_q8.gguf")
+    gguf.write_synthetic_gguf(path, shape, seed=3, wtype="q8_0")
+    ids = _seq(shape, 24)
+    a = mx.Engine(path, n_ctx=64, n_seq_max=2)
+    b = mx.Engine("synthetic:test-tiny:seed=3:q8_0", n_ctx=64, n_seq_max=2)
+    assert a.info.weight_type == 8 and b.info.weight_type == 8
+    la, lb = a.forward_logits(ids), b.forward_logits(ids)
+    assert np.array_equal(la, lb)
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("name", ["test-tiny", "test-d128", "test-h4096"])
+def test_q8_prefill_and_decode_vs_oracle(mx, oracle_mod, name):
+    """100-row prefill (64-row logits chunks: NB=4 and NB=2 kernels), then 12 single-row decode
+    steps (NB=1), teacher-forced, against the oracle's Q8_0 forward."""
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES[name]
+    ids = _seq(shape, 112, seed=5)
+    eng = mx.Engine(f"synthetic:{name}:seed=0:q8_0", n_ctx=256, n_seq_max=2)
+    octx = _oracle_q8(oracle_mod, shape, 0).context(256)
+    got = eng.forward_logits(ids[:100], 0, slot=1)
+    ref = octx.eval(ids[:100], 0, all_logits=True)
+    assert_logits_close(got, ref, f"{name} q8 prefill")
+    assert_tokens_match(got, ref, f"{name} q8 prefill")
+    err = np.abs(got - ref).max()
+    oracle_mod.q8_jitter(1e-6)
+    try:
+        jit = _oracle_q8(oracle_mod, shape, 0).context(256).eval(ids[:100], 0, all_logits=True)
+    finally:
+        oracle_mod.q8_jitter(0.0)
+    self_dev = np.abs(jit - ref).max()
+    assert err <= 2 * self_dev + 1e-4 * np.abs(ref).max(), (err, self_dev)
+    gs, rs = [], []
+    for p in range(100, 112):
+        gs.append(eng.forward_logits(ids[p:p + 1], p, slot=1)[0])
+        rs.append(octx.eval(ids[p:p + 1], p)[0])
+    gs, rs = np.stack(gs), np.stack(rs)
+    assert_logits_close(gs, rs, f"{name} q8 decode")
+    assert_tokens_match(gs, rs, f"{name} q8 decode")
+    print(f"{name}: q8 prefill max|d| {err:.3g} (oracle under 1e-6 noise: {self_dev:.3g}), "
+          f"decode max|d| {np.abs(gs - rs).max():.3g} (max|ref| {np.abs(ref).max():.3g})")
+    eng.close()
+
+
+def test_q8_large_prefill_then_wide_rows(mx, oracle_mod):
+    """A 600-row prompt as ONE forward (grid.y = 10 column groups, no logits), then rows of 24
+    and 40 different sequences in one forward each."""
+    from llama_p2p_amd import synth
+
+    name = "test-d128"
+    shape = synth.SHAPES[name]
+    om = _oracle_q8(oracle_mod, shape, 0)
+    eng = mx.Engine(f"synthetic:{name}:seed=0:q8_0", n_ctx=640, n_seq_max=40)
+    ids = _seq(shape, 610, seed=9)
+    assert eng.forward_rows([0] * 600, list(range(600)), ids[:600], want_logits=False) is None
+    got = eng.forward_logits(ids[600:610], 600, slot=0)
+    ref = om.context(640).eval(ids, 0, all_logits=True)[600:]
+    assert_logits_close(got, ref, "q8 600-row prefill")
+    for M in (24, 40):
+        seqs = [_seq(shape, 7, seed=100 + M + i) for i in range(M)]
+        for i, sq in enumerate(seqs):
+            eng.forward_rows([i] * 6, list(range(6)), sq[:6], want_logits=False)
+        gw = eng.forward_rows(list(range(M)), [6] * M, [int(sq[6]) for sq in seqs])
+        for i, sq in enumerate(seqs):
+            assert_logits_close(gw[i:i + 1], om.context(16).eval(sq, 0), f"q8 M={M} row {i}")
+    eng.close()
+
+
+def test_q8_batch_greedy_loop_vs_oracle(mx, oracle_mod):
+    """device-resident greedy loop (graph replay + on-device argmax) on a Q8_0 model."""
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES["test-h4096"]
+    eng = mx.Engine("synthetic:test-h4096:seed=0:q8_0", n_ctx=128, n_seq_max=4)
+    M, P, G = 3, 10, 16
+    prompts = [_seq(shape, P, seed=30 + i) for i in range(M)]
+    first = [int(np.argmax(eng.forward_logits(p, 0, slot=i)[-1])) for i, p in enumerate(prompts)]
+    b = eng.batch(slots=list(range(M)), pos=[P] * M, ids=first, max_steps=G)
+    for _ in range(G):
+        b.step()
+    toks = b.tokens()
+    om = _oracle_q8(oracle_mod, shape, 0)
+    for i, p in enumerate(prompts):
+        assert check_greedy_chain(om.context(128), p, [first[i]] + toks[i].tolist(), f"q8 seq {i}") >= G
+    b.close()
+    eng.close()
