@@ -157,6 +157,7 @@ struct mx_engine {
   // Q8_0 model: layer matrices as packed Q8 tiles; token_embd / output may each
   // be Q8_0 (tok_embd8: GGUF blocks, row-major) or BF16
   bool wq8 = false, embd_q8 = false, out_q8 = false;
+  bool q8_ql = getenv("MX_NO_Q8_QL") == nullptr;  // Q8_0 GEMVs of <= 4 rows quantise their operand on load
   uint8_t* tok_embd8 = nullptr;
   int8_t* xq8 = nullptr;    // Q8_0 activation rows [PREFILL_ROWS][max(h, ff)]
   float* xqd = nullptr;     // their block scales
@@ -205,6 +206,9 @@ struct mx_engine {
   int enqueue_forward(int M, const int* ids, const int* pos, const int* slot, const void* x_in, void* x_out,
                       bool head, const int* rowmap, int n_out, bool argmax, int* ids_next, int* pos_next, int* hist,
                       int hist_stride, int* hist_count, int max_hist, hipStream_t s);
+  bool q8_on_load(int M) const {
+    return wq8 && q8_ql && mq8_can_quantize_on_load(M, n_embd, true) && mq8_can_quantize_on_load(M, n_ff, false);
+  }
   int enqueue_forward_q8(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap, int n_out,
                          bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count,
                          int max_hist, hipStream_t s);
@@ -563,13 +567,14 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
   // RMS_NORM applied on load by the consuming GEMV (M <= 16); the residual-stream writers
   // (embedding, attn_output, ffn_down, or ssq_kernel for a stage's x_in) leave per-tile partials
   const bool nol = !wide && !wq8 && norm_on_load && mm_can_norm_on_load(M, h);
+  const bool qql = q8_on_load(M);
   if (x_in) {
     HIPC(hipMemcpyAsync(x, x_in, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
-    if (nol) launch_ssq(x, M, h, ssq, s);
+    if (nol || qql) launch_ssq(x, M, h, ssq, s);
   } else {
     if (!has_embed) return fail(MX_ERR_STATE, "this stage has no token embedding: x_in required");
-    if (embd_q8) launch_embed_q8(x, tok_embd8, ids, M, h, s);
-    else launch_embed(x, tok_embd, ids, M, h, nol ? ssq : nullptr, s);
+    if (embd_q8) launch_embed_q8(x, tok_embd8, ids, M, h, (nol || qql) ? ssq : nullptr, s);
+    else launch_embed(x, tok_embd, ids, M, h, (nol || qql) ? ssq : nullptr, s);
   }
   if (wq8) return enqueue_forward_q8(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next, pos_next, hist,
                                      hist_stride, hist_count, max_hist, s);
@@ -739,13 +744,28 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
                                   int* hist_count, int max_hist, hipStream_t s) {
   const int h = n_embd, kv = n_embd_kv, ff = n_ff;
   if (head && n_out > MAX_ROWS) return fail(MX_ERR_ARG, "logits for at most 64 rows per forward");
+  // <= 4 rows: every GEMV quantises its operand on load (RMS_NORM from the ssq partials the
+  // residual writers leave); more rows: Q8_0 rows made once per GEMV by a norm / quantise launch
+  const bool ql = q8_on_load(M);
+  static const int no_ql_mask = getenv("MX_Q8_NO_QL_MASK") ? atoi(getenv("MX_Q8_NO_QL_MASK")) : 0;  // probe
+  int site = 0;  // 1 qkv, 2 attn_output, 4 gate/up, 8 down, 16 lm_head
+  auto operand = [&](MMArgs& m, const float* src, int K, const float* norm_w, int rows, const int* rmap) {
+    if (ql && !rmap && !(no_ql_mask & site)) {
+      m.xq = nullptr; m.xf = src; m.norm_w = norm_w; m.eps = eps; m.ssq = norm_w ? ssq : nullptr; m.np = K / 16;
+    } else {
+      if (norm_w) launch_rmsnorm_q8(xq8, xqd, src, norm_w, rmap, rows, K, eps, s);
+      else launch_quantize_q8(xq8, xqd, src, K, rows, K, s);
+      m.xq = xq8; m.xd = xqd;
+    }
+  };
   for (int li = 0; li < (int)layers.size(); li++) {
     const Layer& L = layers[li];
     _Float16* kc = kcache + layer_kv_stride * li;
     _Float16* vc = vcache + layer_kv_stride * li;
-    launch_rmsnorm_q8(xq8, xqd, x, L.attn_norm, nullptr, M, h, eps, s);
     MMArgs a{};
-    a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M; a.xq = xq8; a.xd = xqd;
+    a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M;
+    site = 1;
+    operand(a, x, h, L.attn_norm, M, nullptr);
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
     a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
     a.slot_stride = slot_stride;
@@ -757,25 +777,31 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     at.scale = 1.0f / sqrtf((float)head_dim);
     if (M > MAX_ROWS && rows_blocked) launch_attention_prefill(at, s);
     else launch_attention(at, s);
-    launch_quantize_q8(xq8, xqd, attn_f, h, M, h, s);
     MMArgs b{};
-    b.W = L.o; b.N = h; b.K = h; b.M = M; b.xq = xq8; b.xd = xqd; b.out = x; b.ldo = h;
+    b.W = L.o; b.N = h; b.K = h; b.M = M; b.out = x; b.ldo = h;
+    site = 2;
+    operand(b, attn_f, h, nullptr, M, nullptr);
+    b.ssq = ql ? ssq : nullptr; b.np = h / 16;  // partials of the new residual for gate/up's norm
     if (launch_mq8(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "q8 attn_output launch shape");
-    launch_rmsnorm_q8(xq8, xqd, x, L.ffn_norm, nullptr, M, h, eps, s);
     MMArgs c{};
-    c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.xq = xq8; c.xd = xqd; c.actf = act_f; c.lda = ff;
+    c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.actf = act_f; c.lda = ff;
+    site = 4;
+    operand(c, x, h, L.ffn_norm, M, nullptr);
     if (launch_mq8(EPI_SWIGLU, c, s)) return fail(MX_ERR_ARG, "q8 gate/up launch shape");
-    launch_quantize_q8(xq8, xqd, act_f, ff, M, ff, s);
     MMArgs d{};
-    d.W = L.down; d.N = h; d.K = ff; d.M = M; d.xq = xq8; d.xd = xqd; d.out = x; d.ldo = h;
+    d.W = L.down; d.N = h; d.K = ff; d.M = M; d.out = x; d.ldo = h;
+    site = 8;
+    operand(d, act_f, ff, nullptr, M, nullptr);
+    d.ssq = ql ? ssq : nullptr; d.np = h / 16;  // for the next layer's qkv (or lm_head) norm
     if (launch_mq8(EPI_RESID, d, s)) return fail(MX_ERR_ARG, "q8 ffn_down launch shape");
   }
   if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
   if (head) {
     if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
-    launch_rmsnorm_q8(xq8, xqd, x, out_norm, rowmap, n_out, h, eps, s);
     MMArgs g{};
-    g.W = output; g.N = n_vocab; g.K = h; g.M = n_out; g.xq = xq8; g.xd = xqd; g.out = logits; g.ldo = n_vocab;
+    g.W = output; g.N = n_vocab; g.K = h; g.M = n_out; g.out = logits; g.ldo = n_vocab;
+    site = 16;
+    operand(g, x, h, out_norm, n_out, (rowmap || n_out != M) ? rowmap : nullptr);
     if (launch_mq8(EPI_F32, g, s)) return fail(MX_ERR_ARG, "q8 lm_head launch shape");
     if (argmax)
       launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, ids_next, pos_next, hist, hist_stride,

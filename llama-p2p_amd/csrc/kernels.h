@@ -174,13 +174,18 @@ void launch_pack_q8(uint8_t* dst, const uint8_t* src_blocks, int N, int K, int m
 void launch_synth_q8_packed(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, int mode,
                             int row_offset, hipStream_t s);
 void launch_synth_q8_rowmajor(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, hipStream_t s);
-void launch_embed_q8(float* x, const uint8_t* tok_embd_blocks, const int* ids, int M, int n_embd, hipStream_t s);
+void launch_embed_q8(float* x, const uint8_t* tok_embd_blocks, const int* ids, int M, int n_embd, float* ssq,
+                     hipStream_t s);
 // RMS_NORM + MUL, quantised to Q8_0 activation rows (xq [M][n], xd [M][n/32])
 void launch_rmsnorm_q8(int8_t* xq, float* xd, const float* x, const float* w, const int* row_map, int M, int n,
                        float eps, hipStream_t s);
 void launch_quantize_q8(int8_t* xq, float* xd, const float* src, int ld, int M, int n, hipStream_t s);
-// Q8_0 x Q8_0 products for any M (column groups of <= 64 tokens on grid.y), same epilogues
+// Q8_0 x Q8_0 products for any M (column groups of <= 64 tokens on grid.y), same epilogues.
+// a.xq == nullptr: quantise on load from f32 rows a.xf ([M][K]; RMS_NORM + MUL first when norm_w,
+// scale from the ssq partials), for mq8_can_quantize_on_load(M, K, norm_w != nullptr).  EPI_RESID writes ssq
+// partials when a.ssq.
 int launch_mq8(int epi, const MMArgs& a, hipStream_t s);
+bool mq8_can_quantize_on_load(int M, int K, bool norm);
 
 void launch_argmax(const float* logits, int ldl, int M, int V, float* ws_val, int* ws_idx, int* tok_out,
                    int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count, int max_hist,

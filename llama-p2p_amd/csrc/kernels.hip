@@ -1567,22 +1567,33 @@ void launch_synth_q8_rowmajor(uint8_t* dst, int N, int K, uint64_t seed, uint64_
 }
 
 // GET_ROWS of a Q8_0 token_embd (dequantize_row_q8_0): x = q * f32(d); thread = one block
-__global__ __launch_bounds__(256) void embed_q8_kernel(float* x, const uint8_t* tok, const int* ids, int n) {
+// ssq (optional): the per-16-element-tile sums of squares quantise-on-load consumers reduce
+__global__ __launch_bounds__(256) void embed_q8_kernel(float* x, const uint8_t* tok, const int* ids, int n,
+                                                       float* ssq) {
   const int c = blockIdx.x;
   const uint8_t* row = tok + (size_t)ids[c] * (n / 32) * 34;
   for (int b = threadIdx.x; b < n / 32; b += blockDim.x) {
     const uint8_t* blk = row + (size_t)b * 34;
     const float d = (float)__builtin_bit_cast(_Float16, (uint16_t)(blk[0] | (blk[1] << 8)));
     float* xo = x + (size_t)c * n + 32 * b;
+    double q[2] = {0.0, 0.0};
 #pragma unroll
-    for (int j = 0; j < 32; j += 4)
-      *reinterpret_cast<f32x4*>(xo + j) = f32x4{(float)(int8_t)blk[2 + j] * d, (float)(int8_t)blk[3 + j] * d,
-                                               (float)(int8_t)blk[4 + j] * d, (float)(int8_t)blk[5 + j] * d};
+    for (int j = 0; j < 32; j += 4) {
+      const f32x4 v{(float)(int8_t)blk[2 + j] * d, (float)(int8_t)blk[3 + j] * d, (float)(int8_t)blk[4 + j] * d,
+                    (float)(int8_t)blk[5 + j] * d};
+      *reinterpret_cast<f32x4*>(xo + j) = v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) q[j >> 4] += (double)(v[i] * v[i]);
+    }
+    if (ssq) {
+      ssq[(size_t)c * (n / 16) + 2 * b] = (float)q[0];
+      ssq[(size_t)c * (n / 16) + 2 * b + 1] = (float)q[1];
+    }
   }
 }
 
-void launch_embed_q8(float* x, const uint8_t* tok, const int* ids, int M, int n, hipStream_t s) {
-  embed_q8_kernel<<<M, 256, 0, s>>>(x, tok, ids, n);
+void launch_embed_q8(float* x, const uint8_t* tok, const int* ids, int M, int n, float* ssq, hipStream_t s) {
+  embed_q8_kernel<<<M, 256, 0, s>>>(x, tok, ids, n, ssq);
 }
 
 // Activation quantisation (ggml quantize_row_q8_0, vec_dot_type of Q8_0): 8 aligned lanes hold the
@@ -1647,7 +1658,13 @@ void launch_quantize_q8(int8_t* xq, float* xd, const float* src, int ld, int M, 
 
 // Q8_0 x Q8_0 MUL_MAT: mm_kernel's work split (KS waves over K, RT row tiles, NB column tiles of
 // 16 tokens, ring of U tiles per wave) over 1088-byte Q8 tiles; grid.y = groups of 16*NB tokens.
-template <int KS, int RT, int NB, int EPI, int U>
+//
+// QP > 0 (quantise on load, QM <= 4 tokens, a.xq == nullptr): no activation launch.  Each wave
+// reads its K-slice of the f32 source rows (a.xf, row stride K) -- optionally RMS_NORM + MUL with
+// the scale from the residual writers' ssq partials, as mm_kernel's XS path -- into registers
+// BEFORE issuing its weight ring (QP float4 per lane and row: slice <= 256*QP), then quantises
+// them to Q8_0 (8 lanes per block) into a wave-private LDS image its B fragments are read from.
+template <int KS, int RT, int NB, int EPI, int U, int QP, int QM>
 __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -1657,18 +1674,28 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
   const int kb = (KT * w) / KS, ke = (KT * (w + 1)) / KS;
 
   __shared__ f32x4 red[KS][RT][NB][64];
+  extern __shared__ __attribute__((aligned(16))) uint8_t ql_dyn[];  // QP: per-wave Q8 images
 
   const uint8_t* Wr[RT];
 #pragma unroll
   for (int r = 0; r < RT; ++r) Wr[r] = reinterpret_cast<const uint8_t*>(a.W) + (size_t)(tile0 + r) * KT * Q8_TILE_BYTES;
   const int8_t* Xq[NB];
   const float* Xd[NB];
+  // QP image: rows of QB bytes (slice + 16 pad), then QM*QS floats of block scales
+  const int QB = (KT + KS - 1) / KS * Q8_TILE_K + 16, QS = (KT + KS - 1) / KS * 2;
+  uint8_t* qimg = ql_dyn + (size_t)w * QM * (QB + 4 * QS);
+  float* dimg = reinterpret_cast<float*>(qimg + QM * QB);
 #pragma unroll
   for (int n = 0; n < NB; ++n) {
     int col = cb + n * 16 + (lane & 15);
     col = col < a.M ? col : a.M - 1;  // padded columns re-read a valid row (outputs dropped)
-    Xq[n] = a.xq + (size_t)col * a.K + (lane >> 4) * 16;
-    Xd[n] = a.xd + (size_t)col * (a.K / 32);
+    if constexpr (QP > 0) {
+      Xq[n] = reinterpret_cast<const int8_t*>(qimg) + col * QB + (lane >> 4) * 16 - kb * Q8_TILE_K;
+      Xd[n] = dimg + col * QS - 2 * kb;
+    } else {
+      Xq[n] = a.xq + (size_t)col * a.K + (lane >> 4) * 16;
+      Xd[n] = a.xd + (size_t)col * (a.K / 32);
+    }
   }
 
   f32x4 acc[RT][NB];
@@ -1677,8 +1704,35 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
 #pragma unroll
     for (int n = 0; n < NB; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // ---- QP: this wave's source values and norm operands, loaded before the weight ring
+  constexpr int QPn = QP > 0 ? QP : 1, QMn = QP > 0 ? QM : 1;
+  f32x4 xv[QMn][QPn], gv[QPn], sv[QMn][2];
+  const int nk = (ke - kb) * Q8_TILE_K, kbase = kb * Q8_TILE_K;
+  if constexpr (QP > 0) {
+#pragma unroll
+    for (int p = 0; p < QP; ++p) {
+      const int i = lane * 4 + 256 * p;
+      if (i < nk) {
+        if (a.norm_w) gv[p] = *reinterpret_cast<const f32x4*>(a.norm_w + kbase + i);
+#pragma unroll
+        for (int c = 0; c < QM; ++c)
+          if (c < a.M) xv[c][p] = *reinterpret_cast<const f32x4*>(a.xf + (size_t)c * a.K + kbase + i);
+      }
+    }
+    if (a.norm_w)
+#pragma unroll
+      for (int c = 0; c < QM; ++c)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          if (c < a.M && lane * 4 + 256 * p < a.np)
+            sv[c][p] = *reinterpret_cast<const f32x4*>(a.ssq + (size_t)c * a.np + lane * 4 + 256 * p);
+  }
+
+  // one ring slot = one 64-k tile: RT weight tiles (int8 operands + scales) and, from global
+  // memory, the NB activation fragments + block scales, loaded together ahead of their use
   struct Frag {
-    u32x4 q[RT], d[RT];
+    u32x4 q[RT], d[RT], xb[NB];
+    f32x2 dx[NB];
   };
   auto load_w = [&](Frag& f, int kt) {
 #pragma unroll
@@ -1687,12 +1741,26 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
       f.q[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t) + lane);
       f.d[r] = *reinterpret_cast<const u32x4*>(t + 1024 + 16 * (lane >> 4));
     }
+    if constexpr (QP == 0) {
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        f.xb[n] = *reinterpret_cast<const u32x4*>(Xq[n] + kt * Q8_TILE_K);
+        f.dx[n] = *reinterpret_cast<const f32x2*>(Xd[n] + 2 * kt);
+      }
+    }
   };
   auto mma = [&](const Frag& f, int kt) {
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
-      const u32x4 xb = *reinterpret_cast<const u32x4*>(Xq[n] + kt * Q8_TILE_K);
-      const f32x2 dx = *reinterpret_cast<const f32x2*>(Xd[n] + 2 * kt);
+      u32x4 xb;
+      f32x2 dx;
+      if constexpr (QP > 0) {
+        xb = *reinterpret_cast<const u32x4*>(Xq[n] + kt * Q8_TILE_K);
+        dx = *reinterpret_cast<const f32x2*>(Xd[n] + 2 * kt);
+      } else {
+        xb = f.xb[n];
+        dx = f.dx[n];
+      }
       const long b0 = (long)(((unsigned long)xb[1] << 32) | xb[0]);
       const long b1 = (long)(((unsigned long)xb[3] << 32) | xb[2]);
 #pragma unroll
@@ -1717,6 +1785,39 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
   if (nfull > 0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) load_w(ring[u], kt + u);
+  }
+  if constexpr (QP > 0) {  // build the image while the ring is in flight
+#pragma unroll
+    for (int c = 0; c < QM; ++c) {
+      if (c >= a.M) break;
+      float sc = 1.0f;
+      if (a.norm_w) {
+        double sum = 0.0;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          if (lane * 4 + 256 * p < a.np)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) sum += (double)sv[c][p][j];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) sum += __shfl_xor(sum, o);
+        sc = 1.0f / sqrtf((float)(sum / a.K) + a.eps);
+      }
+#pragma unroll
+      for (int p = 0; p < QP; ++p) {
+        const int i = lane * 4 + 256 * p;
+        if (i < nk) {
+          f32x4 v = xv[c][p];
+          if (a.norm_w)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (v[j] * sc) * gv[p][j];
+          q8_store_act(v, i, reinterpret_cast<int8_t*>(qimg) + c * QB, dimg + c * QS);
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (nfull > 0) {
     for (int ch = 1; ch < nfull; ++ch) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1748,10 +1849,26 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
     const int n = (u / LU) % NB;
     const int r = (u / LU) / NB;
     const int col = cb + n * 16 + (l & 15);
-    if (col >= a.M) continue;
     f32x4 s = red[0][r][n][l];
 #pragma unroll
     for (int ww = 1; ww < KS; ++ww) s += red[ww][r][n][l];
+    if constexpr (EPI == EPI_RESID) {  // residual add + this tile's ssq partial (see mm_kernel)
+      double q = 0.0;
+      if (col < a.M) {
+        f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + (tile0 + r) * 16 + (l >> 4) * 4);
+        const f32x4 xv2 = *px + s;
+        *px = xv2;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q += (double)(xv2[i] * xv2[i]);
+      }
+      if (a.ssq) {
+        q += __shfl_xor(q, 16);
+        q += __shfl_xor(q, 32);
+        if (l < 16 && col < a.M) a.ssq[(size_t)col * a.np + tile0 + r] = (float)q;
+      }
+      continue;
+    }
+    if (col >= a.M) continue;
     f32x4 up = s;
     if constexpr (EPI == EPI_SWIGLU) {
       up = red[0][r][n][l + 32];
@@ -1762,24 +1879,80 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
   }
 }
 
+// quantise-on-load launch: 8 waves (the slice of K per wave <= 256*QP), QM row slots
+template <int EPI, int QP, int QM>
+static void launch_mq8_ql(const MMArgs& a, hipStream_t s) {
+  const int KT = a.K / Q8_TILE_K;
+  const int QB = (KT + 7) / 8 * Q8_TILE_K + 16, QS = (KT + 7) / 8 * 2;
+  const size_t lds = (size_t)8 * QM * (QB + 4 * QS);
+  static const int rt = getenv("MX_Q8_QL_RT") ? atoi(getenv("MX_Q8_QL_RT")) : 1;  // geometry probe
+  if (rt == 2 && (a.N / TILE_N) % 2 == 0)
+    mq8_kernel<8, 2, 1, EPI, 2, QP, QM><<<dim3(a.N / TILE_N / 2, 1), 512, lds, s>>>(a);
+  else
+    mq8_kernel<8, 1, 1, EPI, 4, QP, QM><<<dim3(a.N / TILE_N, 1), 512, lds, s>>>(a);
+}
+
+template <int EPI, int QP>
+static void launch_mq8_ql_m(const MMArgs& a, hipStream_t s) {
+  if (a.M == 1) launch_mq8_ql<EPI, QP, 1>(a, s);
+  else if (a.M == 2) launch_mq8_ql<EPI, QP, 2>(a, s);
+  else launch_mq8_ql<EPI, QP, 4>(a, s);
+}
+
+bool mq8_can_quantize_on_load(int M, int K, bool norm) {
+  const int slice = (K / Q8_TILE_K + 7) / 8 * Q8_TILE_K;
+  return M >= 1 && M <= XS_MAX_M && K % Q8_TILE_K == 0 && slice <= 2048 && (!norm || K / 16 <= 512);
+}
+
 // one column tile: 16 waves split K (as mm_kernel); two or four tiles: 8 waves (the B fragments and
 // block scales of every tile stay in registers: 16 waves would spill)
 template <int EPI>
 static int launch_mq8_epi(const MMArgs& a, hipStream_t s) {
   const int ntiles = a.N / TILE_N;
   if (a.M <= 16) {
-    mq8_kernel<16, 1, 1, EPI, 4><<<dim3(ntiles, 1), 1024, 0, s>>>(a);
+    static const int cfg = getenv("MX_Q8_CFG") ? atoi(getenv("MX_Q8_CFG")) : 1;  // geometry probe
+    switch (ntiles % 2 ? 1 : cfg) {  // 1 (default): 8 waves, best of tools/gpu/q8_probe.sh
+      case 0: mq8_kernel<16, 1, 1, EPI, 4, 0, 1><<<dim3(ntiles, 1), 1024, 0, s>>>(a); return 0;
+      case 2: mq8_kernel<16, 2, 1, EPI, 2, 0, 1><<<dim3(ntiles / 2, 1), 1024, 0, s>>>(a); return 0;
+      case 3: mq8_kernel<8, 2, 1, EPI, 4, 0, 1><<<dim3(ntiles / 2, 1), 512, 0, s>>>(a); return 0;
+      case 4: mq8_kernel<4, 1, 1, EPI, 8, 0, 1><<<dim3(ntiles, 1), 256, 0, s>>>(a); return 0;
+      case 5: mq8_kernel<16, 1, 1, EPI, 2, 0, 1><<<dim3(ntiles, 1), 1024, 0, s>>>(a); return 0;
+      case 6: mq8_kernel<8, 2, 1, EPI, 2, 0, 1><<<dim3(ntiles / 2, 1), 512, 0, s>>>(a); return 0;
+    }
+    mq8_kernel<8, 1, 1, EPI, 4, 0, 1><<<dim3(ntiles, 1), 512, 0, s>>>(a);
   } else if (a.M <= 32) {
-    mq8_kernel<8, 1, 2, EPI, 4><<<dim3(ntiles, 1), 512, 0, s>>>(a);
+    mq8_kernel<8, 1, 2, EPI, 4, 0, 1><<<dim3(ntiles, 1), 512, 0, s>>>(a);
   } else {
-    mq8_kernel<8, 1, 4, EPI, 2><<<dim3(ntiles, (a.M + 63) / 64), 512, 0, s>>>(a);
+    mq8_kernel<8, 1, 4, EPI, 2, 0, 1><<<dim3(ntiles, (a.M + 63) / 64), 512, 0, s>>>(a);
   }
   return 0;
 }
 
+template <int EPI>
+static int launch_mq8_ql_epi(const MMArgs& a, hipStream_t s) {
+  const int slice = (a.K / Q8_TILE_K + 7) / 8 * Q8_TILE_K;
+  if (slice <= 512) launch_mq8_ql_m<EPI, 2>(a, s);
+  else if (slice <= 1024) launch_mq8_ql_m<EPI, 4>(a, s);
+  else launch_mq8_ql_m<EPI, 8>(a, s);
+  return 0;
+}
+
 int launch_mq8(int epi, const MMArgs& a, hipStream_t s) {
-  if (a.M < 1 || a.K % Q8_TILE_K || a.N % TILE_N || !a.xq || !a.xd) return -1;
+  if (a.M < 1 || a.K % Q8_TILE_K || a.N % TILE_N) return -1;
   if (epi == EPI_SWIGLU && !a.actf && !a.act) return -1;
+  if (!a.xq) {  // quantise on load from a.xf (+ RMS_NORM when norm_w)
+    if (!a.xf || !mq8_can_quantize_on_load(a.M, a.K, a.norm_w != nullptr) ||
+        (a.norm_w && (!a.ssq || a.np * 16 != a.K)))
+      return -1;
+    switch (epi) {
+      case EPI_F32: return launch_mq8_ql_epi<EPI_F32>(a, s);
+      case EPI_RESID: return launch_mq8_ql_epi<EPI_RESID>(a, s);
+      case EPI_QKV: return launch_mq8_ql_epi<EPI_QKV>(a, s);
+      case EPI_SWIGLU: return launch_mq8_ql_epi<EPI_SWIGLU>(a, s);
+    }
+    return -1;
+  }
+  if (!a.xd) return -1;
   switch (epi) {
     case EPI_F32: return launch_mq8_epi<EPI_F32>(a, s);
     case EPI_RESID: return launch_mq8_epi<EPI_RESID>(a, s);

@@ -18,14 +18,15 @@ def main():
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--rows", default="1,32")
     ap.add_argument("--pos", type=int, default=255)
+    ap.add_argument("--q8", action="store_true", help="the Q8_0 quantisation of the model")
     args = ap.parse_args()
     os.environ["MX_PROF_POS"] = str(args.pos)
     from llama_p2p_amd.engine import Engine
 
-    eng = Engine(f"synthetic:{args.model}:seed=0", n_ctx=512, n_seq_max=64)
+    eng = Engine(f"synthetic:{args.model}:seed=0" + (":q8_0" if args.q8 else ""), n_ctx=512, n_seq_max=64)
     for M in [int(x) for x in args.rows.split(",")]:
         for k, name in KINDS.items():
-            if k in (5, 6) and M > 4:
+            if k in (5, 6) and (M > 4 or args.q8):
                 continue
             us, b = eng.profile_kernel(k, M, iters=3)
             print(f"M={M:<3d} {name:14s} {us:9.2f} us  {b / us / 1e3:8.1f} GB/s", flush=True)
