@@ -157,7 +157,12 @@ struct mx_engine {
   // Q8_0 model: layer matrices as packed Q8 tiles; token_embd / output may each
   // be Q8_0 (tok_embd8: GGUF blocks, row-major) or BF16
   bool wq8 = false, embd_q8 = false, out_q8 = false;
-  bool q8_ql = getenv("MX_NO_Q8_QL") == nullptr;  // Q8_0 GEMVs of <= 4 rows quantise their operand on load
+  bool q8_ql = getenv("MX_NO_Q8_QL") == nullptr;
+  // attention + attn_output fused (<= 4 rows, bf16), opt-in: measured slower than the two launches
+  // (profiles/round1_attn_o_trace.txt); ao_sync holds the counters of its in-launch hand-off
+  bool use_attn_o = getenv("MX_ATTN_O") != nullptr;
+  unsigned* ao_sync = nullptr;
+  unsigned long long* ao_trace = nullptr;  // MX_AO_TRACE: phase stamps of layer 1's attn_o launch  // Q8_0 GEMVs of <= 4 rows quantise their operand on load
   uint8_t* tok_embd8 = nullptr;
   int8_t* xq8 = nullptr;    // Q8_0 activation rows [PREFILL_ROWS][max(h, ff)]
   float* xqd = nullptr;     // their block scales
@@ -305,6 +310,8 @@ int mx_engine::init_common() {
   if (int rc = alloc((void**)&d_pos, (size_t)R * 4)) return rc;
   if (int rc = alloc((void**)&d_slot, (size_t)R * 4)) return rc;
   if (int rc = alloc((void**)&d_rowmap, (size_t)R * 4)) return rc;
+  if (int rc = alloc((void**)&ao_sync, 640 * 4)) return rc;
+  HIPC(hipMemsetAsync(ao_sync, 0, 640 * 4, stream));
   if (wq8) {
     const size_t kmax = std::max(n_embd, n_ff);
     if (int rc = alloc((void**)&xq8, (size_t)R * kmax)) return rc;
@@ -347,6 +354,15 @@ int mx_engine::init_pdk() {
 
 // a persistent-kernel barrier that timed out (grid not co-resident) leaves sync[1] != 0
 int mx_engine::check_pdk() {
+  if (ao_sync) {
+    unsigned to = 0;
+    HIPC(hipMemcpy(&to, ao_sync + 64, 4, hipMemcpyDeviceToHost));
+    if (to) {
+      use_attn_o = false;
+      HIPC(hipMemset(ao_sync, 0, 640 * 4));
+      return fail(MX_ERR_HIP, "attention+attn_output kernel: wait timed out (unset MX_ATTN_O)");
+    }
+  }
   if (!use_pdk) return 0;
   unsigned flag = 0;
   HIPC(hipMemcpy(&flag, pdk_sync + 32 * 33, 4, hipMemcpyDeviceToHost));  // pdk.hip sync_err()
@@ -629,10 +645,19 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     at.out = attn_out; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
     at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;
     at.scale = 1.0f / sqrtf((float)head_dim);
-    launch_attention(at, s);
     MMArgs b{};
     b.W = L.o; b.N = h; b.K = h; b.X = attn_out; b.ldx = h; b.M = M; b.out = x; b.ldo = h;
-    if (launch_mm(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "attn_output launch shape");
+    if (getenv("MX_AO_TRACE") && !ao_trace) {
+      if (int rc = alloc((void**)&ao_trace, 4096 * 8)) return rc;
+      HIPC(hipMemset(ao_trace, 0, 4096 * 8));
+    }
+    b.trace = (li == 1) ? ao_trace : nullptr;
+    if (use_attn_o && attn_o_supported(at, b)) {  // attn_output's weight stream overlaps attention
+      if (launch_attn_o(at, b, ao_sync, s)) return fail(MX_ERR_ARG, "attention+attn_output launch shape");
+    } else {
+      launch_attention(at, s);
+      if (launch_mm(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "attn_output launch shape");
+    }
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M;
     norm_operand(c, L.ffn_norm, false);
@@ -900,6 +925,21 @@ int mx_engine::forward_rows_chunk(int n, const int32_t* slots, const int32_t* po
   if (frc) return frc;
   if (head) HIPC(hipMemcpyAsync(logits_host, logits, (size_t)n_out * n_vocab * 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
+  if (ao_trace && n == 1) {  // diagnosis: per-work-group stamps relative to the earliest start (us)
+    std::vector<unsigned long long> t(1024);
+    HIPC(hipMemcpy(t.data(), ao_trace, 1024 * 8, hipMemcpyDeviceToHost));
+    unsigned long long t0 = ~0ull;
+    for (int g = 0; g < 256; g++) if (t[g * 4] && t[g * 4] < t0) t0 = t[g * 4];
+    double st_max = 0, flag_min = 1e9, flag_max = 0, end_max = 0, attn_max = 0;
+    for (int g = 0; g < 256; g++) {
+      const double a0 = (t[g * 4] - t0) / 100.0, f = (t[g * 4 + 2] - t0) / 100.0, e = (t[g * 4 + 3] - t0) / 100.0;
+      st_max = std::max(st_max, a0); flag_min = std::min(flag_min, f); flag_max = std::max(flag_max, f);
+      end_max = std::max(end_max, e);
+      if (g < 8) attn_max = std::max(attn_max, (t[g * 4 + 1] - t0) / 100.0);
+    }
+    fprintf(stderr, "attn_o: last start %.2f  attn done %.2f  flag seen %.2f..%.2f  end %.2f us\n", st_max, attn_max,
+            flag_min, flag_max, end_max);
+  }
   return check_pdk();
 }
 

@@ -65,6 +65,7 @@ struct MMArgs {
   int n_ctx, ctx_stride, n_head_kv;
   size_t slot_stride;          // elements per slot in kc/vc = n_head_kv*ctx_stride*head_dim
   size_t slab_stride;          // EPI_SLAB: floats between consecutive K-split partial slabs
+  unsigned long long* trace;   // attn_o_kernel phase stamps (diagnosis; nullptr normally)
 };
 
 struct AttnArgs {
@@ -157,6 +158,10 @@ int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, h
 void launch_resid_norm(uint16_t* y, int ldy, float* x, const float* slabs, int nslab, size_t slab_stride,
                        const float* w, int M, int n, float eps, hipStream_t s);  // X == nullptr path (RMS_NORM fused into the GEMV) is legal
 void launch_attention(const AttnArgs& a, hipStream_t s);
+// decode attention + attn_output (EPI_RESID, X = at.out) in one launch for <= 4 rows; sync: 640
+// zeroed uints of this engine (counters, timeout flag at [64], flag replicas); -1 if unsupported
+bool attn_o_supported(const AttnArgs& at, const MMArgs& a);
+int launch_attn_o(const AttnArgs& at, const MMArgs& a, unsigned* sync, hipStream_t s);
 // rows in blocks of 16 consecutive positions of one sequence each (prefill chunks): one
 // work-group per (kv head, block), the 16 queries share every K/V chunk
 void launch_attention_prefill(const AttnArgs& a, hipStream_t s);

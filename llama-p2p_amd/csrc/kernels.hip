@@ -906,12 +906,19 @@ bool mm_can_norm_on_load(int M, int K) {
 // [pos][d] (B operand of QK^T = contiguous 16 B per lane) and V transposed
 // [d][pos] (B operand of P.V = contiguous 16 B per lane).
 // ---------------------------------------------------------------------------
-template <int D, int G, int NW>
-__global__ __launch_bounds__(64 * NW) void attn_decode_kernel(AttnArgs a) {
+// sc1 (write-through, L1-bypassing) buffer accesses for data handed between work-groups of one
+// launch (cdna_hip_programming.md §6 Guideline 16, as pdk.hip)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sc_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7ffffff0, 0x00020000);
+}
+
+// One (kv head, row) of decode attention, by the NW waves of the calling work-group.  PUB: the
+// output is stored with sc1 stores for consumers in other work-groups of the same launch.
+template <int D, int G, int NW, bool PUB>
+__device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int c) {
   constexpr int CH = ATTN_CHUNK;
   constexpr int QK = D / 32;  // k-steps of QK^T
   constexpr int DT = D / 16;  // d tiles of P.V
-  const int kvh = blockIdx.x, c = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r16 = lane & 15, q4 = lane >> 4;
   const int pos = a.pos[c];
@@ -1087,9 +1094,23 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_kernel(AttnArgs a) {
       L += f * Ll[ww][h];
       acc += f * Om[ww][h][d];
     }
-    if (a.outf) a.outf[(size_t)c * a.ldo + (kvh * G + h) * D + d] = acc / L;
-    else a.out[(size_t)c * a.ldo + (kvh * G + h) * D + d] = (uint16_t)f2bf(acc / L);
+    if constexpr (PUB) {
+      const float v = acc / L;
+      const float v1 = __shfl_down(v, 1);  // d + 1 (d even: idx and D are even, lanes adjacent)
+      if ((d & 1) == 0)
+        __builtin_amdgcn_raw_buffer_store_b32(f2bf(v) | (f2bf(v1) << 16), sc_rsrc(a.out),
+                                              (unsigned)(((size_t)c * a.ldo + (kvh * G + h) * D + d) * 2), 0, 16);
+    } else if (a.outf) {
+      a.outf[(size_t)c * a.ldo + (kvh * G + h) * D + d] = acc / L;
+    } else {
+      a.out[(size_t)c * a.ldo + (kvh * G + h) * D + d] = (uint16_t)f2bf(acc / L);
+    }
   }
+}
+
+template <int D, int G, int NW>
+__global__ __launch_bounds__(64 * NW) void attn_decode_kernel(AttnArgs a) {
+  attn_decode_body<D, G, NW, false>(a, blockIdx.x, blockIdx.y);
 }
 
 #ifndef ATTN_WAVES
@@ -1111,6 +1132,169 @@ void launch_attention(const AttnArgs& a, hipStream_t s) {
     launch_attn_d<64>(a, s);
   else
     launch_attn_d<128>(a, s);
+}
+
+// ---------------------------------------------------------------------------
+// Attention + attn_output in one launch (<= 4 rows, bf16 weights; opt-in MX_ATTN_O=1 -- measured
+// 1.5 us/layer SLOWER than the two launches, profiles/round1_attn_o_trace.txt).  Every work-group owns one
+// 16-row tile of the attn_output GEMV (8 waves split K) and first issues ALL of its weight loads
+// (they do not depend on attention); work-groups 0 .. n_kv*M-1 also run decode attention for
+// one (kv head, row) and publish it (sc1 stores, drained, then one agent-scope counter add).
+// The GEMV waits on that counter, reads the attention output with sc1 loads and finishes with
+// the residual add.  So the weight stream of attn_output overlaps attention instead of
+// following it, and one launch ramp disappears.  The attention work-groups have the lowest
+// indices and are dispatched first, so the waits always end; each is bounded anyway (2 s, then
+// sync[2] is set and the host reports it).  The last work-group out resets the counters.
+// ---------------------------------------------------------------------------
+constexpr int AO_WAVES = 8;
+constexpr int AO_PREFETCH = 12;  // K-tiles per wave held in registers across the wait (of 16 at K = 4096)
+constexpr long long AO_TIMEOUT = 200000000;  // 100 MHz wall clock: 2 s
+
+// sync layout (uints, one 128-B line each): [0] arrivals, [32] exits, [64] timeout flag,
+// [96 + 32 j] done-flag replica j (AO_REPL of them; work-group g polls replica g % AO_REPL)
+constexpr int AO_REPL = 16;
+template <int D, int G>
+__global__ __launch_bounds__(64 * AO_WAVES) void attn_o_kernel(AttnArgs at, MMArgs a, unsigned* sync, int poll_ticks,
+                                                               int prefetch) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = blockIdx.x;
+  const int n_attn = at.n_head_kv * at.M;
+  const int KT = a.K / TILE_K;
+  const int kb = (KT * w) / AO_WAVES, ke = (KT * (w + 1)) / AO_WAVES;
+  __shared__ f32x4 red[AO_WAVES][64];
+  __shared__ unsigned ok_flag;
+  unsigned long long* trace = a.trace ? a.trace + (size_t)g * 4 : nullptr;  // diagnosis only
+  if (trace && threadIdx.x == 0) trace[0] = wall_clock64();
+
+  // 1. this wave's attn_output weights, all in flight before anything else
+  const u32x4* Wp = reinterpret_cast<const u32x4*>(a.W) + (size_t)g * KT * 64 + lane;
+  u32x4 ra[AO_PREFETCH];
+  const int npre = prefetch ? AO_PREFETCH : 0;
+#pragma unroll
+  for (int i = 0; i < AO_PREFETCH; ++i)
+    if (i < npre && kb + i < ke) ra[i] = __builtin_nontemporal_load(Wp + (size_t)(kb + i) * 64);
+
+  // 2. attention for one (kv head, row), published
+  if (g < n_attn) {
+    attn_decode_body<D, G, AO_WAVES, true>(at, g % at.n_head_kv, g / at.n_head_kv);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are done
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (trace) trace[1] = wall_clock64();
+      const unsigned old = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == (unsigned)n_attn - 1)  // the last attention work-group raises every replica
+        for (int j = 0; j < AO_REPL; ++j)
+          __hip_atomic_store(sync + 96 + 32 * j, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+
+  // 3. wait for all attention work-groups (bounded)
+  if (threadIdx.x == 0) {
+    const long long t0 = wall_clock64();
+    unsigned ok = 1;
+    unsigned* flag = sync + 96 + 32 * (g % AO_REPL);
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      const long long t1 = wall_clock64();
+      if (t1 - t0 > AO_TIMEOUT) {
+        __hip_atomic_store(sync + 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      while (wall_clock64() - t1 < poll_ticks) __builtin_amdgcn_s_sleep(2);  // few polls: one line, many CUs
+    }
+    ok_flag = ok;
+    if (trace) trace[2] = wall_clock64();
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no handed-over load moves above the poll
+
+  // 4. the GEMV: B fragments of the attention output (sc1 loads), prefetched tiles, then the rest
+  const int col = (lane & 15) < a.M ? (lane & 15) : a.M - 1;
+  const __amdgpu_buffer_rsrc_t xr = sc_rsrc(a.X);
+  const unsigned xoff = (unsigned)(((size_t)col * a.ldx + (lane >> 4) * 8) * 2);
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < AO_PREFETCH; ++i) {
+    if (i < npre && kb + i < ke) {
+      const u32x4 xb = __builtin_amdgcn_raw_buffer_load_b128(xr, xoff + (unsigned)(kb + i) * TILE_K * 2, 0, 16);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ra[i]), __builtin_bit_cast(bf16x8, xb),
+                                                    acc, 0, 0, 0);
+    }
+  }
+  for (int kt0 = kb + npre; kt0 < ke; kt0 += 4) {  // the rest, 4 tiles' loads in flight at a time
+    u32x4 wv[4], xb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (kt0 + j < ke) {
+        wv[j] = __builtin_nontemporal_load(Wp + (size_t)(kt0 + j) * 64);
+        xb[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, xoff + (unsigned)(kt0 + j) * TILE_K * 2, 0, 16);
+      }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (kt0 + j < ke)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wv[j]), __builtin_bit_cast(bf16x8, xb[j]),
+                                                      acc, 0, 0, 0);
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0) {  // residual add (one C-layout unit per lane) + this tile's ssq partial
+    f32x4 sacc = red[0][lane];
+#pragma unroll
+    for (int ww = 1; ww < AO_WAVES; ++ww) sacc += red[ww][lane];
+    const int cc = lane & 15;
+    double q = 0.0;
+    if (cc < a.M) {
+      f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)cc * a.ldo + g * 16 + (lane >> 4) * 4);
+      const f32x4 xv = *px + sacc;
+      *px = xv;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) q += (double)(xv[i] * xv[i]);
+    }
+    if (a.ssq) {
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      if (lane < 16 && cc < a.M) a.ssq[(size_t)cc * a.np + g] = (float)q;
+    }
+    // 5. leave; the last work-group out resets the counters for the next launch
+    if (lane == 0) {
+      if (trace) trace[3] = wall_clock64();
+      const unsigned old = __hip_atomic_fetch_add(sync + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == gridDim.x - 1) {
+        __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sync + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int j = 0; j < AO_REPL; ++j)
+          __hip_atomic_store(sync + 96 + 32 * j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  (void)ok_flag;
+}
+
+bool attn_o_supported(const AttnArgs& at, const MMArgs& a) {
+  const int G = at.n_head / at.n_head_kv;
+  return at.M >= 1 && at.M <= 4 && !at.slabs && !at.outf && (at.head_dim == 64 || at.head_dim == 128) &&
+         (G == 1 || G == 2 || G == 4 || G == 8) && a.M == at.M && a.N % TILE_N == 0 && a.K % TILE_K == 0 &&
+         a.N / TILE_N >= at.n_head_kv * at.M && a.X == at.out && a.K / TILE_K >= AO_WAVES;
+}
+
+template <int D>
+static void launch_attn_o_d(const AttnArgs& at, const MMArgs& a, unsigned* sync, hipStream_t s) {
+  const int grid = a.N / TILE_N;
+  static const int poll = getenv("MX_AO_POLL") ? atoi(getenv("MX_AO_POLL")) : 20;  // 100 MHz ticks
+  static const int pre = getenv("MX_AO_NOPREFETCH") ? 0 : 1;
+  switch (at.n_head / at.n_head_kv) {
+    case 1: attn_o_kernel<D, 1><<<grid, 64 * AO_WAVES, 0, s>>>(at, a, sync, poll, pre); break;
+    case 2: attn_o_kernel<D, 2><<<grid, 64 * AO_WAVES, 0, s>>>(at, a, sync, poll, pre); break;
+    case 4: attn_o_kernel<D, 4><<<grid, 64 * AO_WAVES, 0, s>>>(at, a, sync, poll, pre); break;
+    case 8: attn_o_kernel<D, 8><<<grid, 64 * AO_WAVES, 0, s>>>(at, a, sync, poll, pre); break;
+  }
+}
+
+int launch_attn_o(const AttnArgs& at, const MMArgs& a, unsigned* sync, hipStream_t s) {
+  if (!attn_o_supported(at, a) || !sync) return -1;
+  if (at.head_dim == 64) launch_attn_o_d<64>(at, a, sync, s);
+  else launch_attn_o_d<128>(at, a, sync, s);
+  return 0;
 }
 
 // ---------------------------------------------------------------------------

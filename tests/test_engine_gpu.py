@@ -358,3 +358,28 @@ def test_70b_geometry_all_paths(mx, oracle_mod):
     for i, sq in enumerate(seqs):
         assert_logits_close(gotw[i:i + 1], om.context(64).eval(sq, 0), f"h8192 wide row {i}")
     eng.close()
+
+
+def test_fused_attention_attn_output_vs_oracle(mx, oracle_mod):
+    """The opt-in attention + attn_output launch (MX_ATTN_O=1: in-launch hand-off with sc1 stores,
+    an agent-scope counter and flag replicas) gives the oracle's logits at 1 and 3 rows."""
+    from llama_p2p_amd import synth
+
+    name = "test-h4096"
+    shape = synth.SHAPES[name]
+    os.environ["MX_ATTN_O"] = "1"
+    try:
+        eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=128, n_seq_max=4)
+    finally:
+        del os.environ["MX_ATTN_O"]
+    om = oracle_mod.OracleModel(shape, seed=0)
+    seqs = [_seq(shape, 40, seed=90 + i) for i in range(3)]
+    for i, sq in enumerate(seqs):
+        eng.forward_rows([i] * 38, list(range(38)), sq[:38], want_logits=False)
+    got1 = eng.forward_logits(seqs[0][38:39], 38, slot=0)                          # 1 row
+    assert_logits_close(got1, om.context(64).eval(seqs[0][:39], 0)[-1:], "attn_o 1 row")
+    got3 = eng.forward_rows([0, 1, 2], [39, 38, 38], [int(seqs[0][39]), int(seqs[1][38]), int(seqs[2][38])])
+    refs = [om.context(64).eval(seqs[0][:40], 0)[-1], om.context(64).eval(seqs[1][:39], 0)[-1],
+            om.context(64).eval(seqs[2][:39], 0)[-1]]
+    assert_logits_close(got3, np.stack(refs), "attn_o 3 rows")
+    eng.close()
