@@ -2223,6 +2223,17 @@ static int launch_mq8_epi(const MMArgs& a, hipStream_t s) {
     }
     mq8_kernel<8, 1, 1, EPI, 4, 0, 1><<<dim3(ntiles, 1), 512, 0, s>>>(a);
   } else if (a.M <= 32) {
+    // per epilogue, from tools/gpu/q8_probe32.sh (Llama-3-8B, 32 rows): more row tiles per wave for
+    // the wide matrices (each B fragment loaded from L2 feeds RT MFMAs), one for the 4096-row ones
+    const int dflt = EPI == EPI_QKV ? 1 : (EPI == EPI_SWIGLU || EPI == EPI_F32) ? 3 : 0;
+    static const int cfg2e = getenv("MX_Q8_CFG2") ? atoi(getenv("MX_Q8_CFG2")) : -1;  // geometry probe
+    const int cfg2 = cfg2e >= 0 ? cfg2e : dflt;
+    switch (ntiles % 4 ? 0 : cfg2) {
+      case 1: mq8_kernel<8, 2, 2, EPI, 2, 0, 1><<<dim3(ntiles / 2, 1), 512, 0, s>>>(a); return 0;
+      case 2: mq8_kernel<8, 4, 2, EPI, 2, 0, 1><<<dim3(ntiles / 4, 1), 512, 0, s>>>(a); return 0;
+      case 3: mq8_kernel<4, 4, 2, EPI, 2, 0, 1><<<dim3(ntiles / 4, 1), 256, 0, s>>>(a); return 0;
+      case 4: mq8_kernel<16, 2, 2, EPI, 1, 0, 1><<<dim3(ntiles / 2, 1), 1024, 0, s>>>(a); return 0;
+    }
     mq8_kernel<8, 1, 2, EPI, 4, 0, 1><<<dim3(ntiles, 1), 512, 0, s>>>(a);
   } else {
     mq8_kernel<8, 1, 4, EPI, 2, 0, 1><<<dim3(ntiles, (a.M + 63) / 64), 512, 0, s>>>(a);
