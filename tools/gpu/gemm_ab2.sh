@@ -1,6 +1,6 @@
-# prefill GEMM scheduling variants (ab/*.so via MX_LIB), interleaved
+# prefill GEMM variants (ab/*.so via MX_LIB), interleaved
 for i in 1 2; do
-  for v in base iglp0 iglp1; do
+  for v in base prio; do
     echo "$v: $(MX_LIB=$PWD/ab/$v.so timeout -k 10 200 python3 tools/prefill_probe.py 2>&1 | tail -1)"
   done
 done
