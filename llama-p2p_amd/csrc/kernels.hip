@@ -1551,7 +1551,8 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(MMArgs a) {
     const uint8_t* Ab = lds + buf * 65536;
     const uint8_t* Bb = Ab + 32768;
     // all 24 fragments of the step are read up front, and iglp_opt(0) interleaves the ds_reads with
-    // the MFMAs (+3.6 % prefill over the default schedule, tools/gpu/gemm_ab2.sh)
+    // the MFMAs (+3.6 % prefill over the default schedule; s_setprio(1) around the MFMAs: -12 %;
+    // tools/gpu/gemm_ab2.sh)
     __builtin_amdgcn_iglp_opt(0);
     u32x4 af[2][4], bf[2][8];
 #pragma unroll
@@ -1569,6 +1570,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(MMArgs a) {
         for (int r = 0; r < 4; ++r)
           acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[kt][r]),
                                                               __builtin_bit_cast(bf16x8, bf[kt][j]), acc[r][j], 0, 0, 0);
+
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave is done reading buf before step st+2 is copied into it
     asm volatile("" ::: "memory");

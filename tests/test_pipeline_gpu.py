@@ -26,8 +26,9 @@ def _rows(prompts, base_slot=0):
     return (slots, pos, ids), st
 
 
+@pytest.mark.parametrize("wtype", ["bf16", "q8_0"])
 @pytest.mark.parametrize("splits", [[(0, 1), (1, 3)], [(0, 1), (1, 2), (2, 3)]])
-def test_stage_engines_match_full_model(splits):
+def test_stage_engines_match_full_model(splits, wtype):
     from llama_p2p_amd import synth
     from llama_p2p_amd.engine import Engine
     from llama_p2p_amd.pipeline import EngineAdapter
@@ -41,7 +42,8 @@ def test_stage_engines_match_full_model(splits):
     dev = torch.device("cuda", 0)
     torch.cuda.set_stream(torch.cuda.Stream())
 
-    full = Engine(f"synthetic:{name}:seed=0", n_ctx=128, n_seq_max=M)
+    path = f"synthetic:{name}:seed=0:{wtype}"  # Q8_0: stage x_in feeds the quantise-on-load GEMVs
+    full = Engine(path, n_ctx=128, n_seq_max=M)
     fa = EngineAdapter(full)
     for i in range(0, len(slots), 64):
         fa.stage_rows_tensors(slots[i:i + 64], pos[i:i + 64], ids[i:i + 64], None, None)
@@ -50,7 +52,7 @@ def test_stage_engines_match_full_model(splits):
         fb.step()
     ref = fb.tokens()
 
-    engs = [Engine(f"synthetic:{name}:seed=0", n_ctx=128, n_seq_max=M, layer_begin=lb, layer_end=le)
+    engs = [Engine(path, n_ctx=128, n_seq_max=M, layer_begin=lb, layer_end=le)
             for lb, le in splits]
     ads = [EngineAdapter(e) for e in engs]
     S = len(engs)
