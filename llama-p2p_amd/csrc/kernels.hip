@@ -697,14 +697,18 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
     const int rr = xrow[i] < a.M ? xrow[i] : a.M - 1;
     xsrc[i] = reinterpret_cast<const u32x4*>(a.X + (size_t)rr * a.ldx + (size_t)kb * TILE_K + xseg[i] * 8);
   }
-  u32x4 xr[PPT];
-  auto load_x = [&](int c) {
+  // activation chunks are loaded TWO chunks ahead into alternating register sets: the wait for
+  // chunk c+1's pieces (before its LDS store) then retires only loads issued before the weight
+  // refills of chunk c+1, so 2 chunks of weight loads stay in flight across every barrier (one
+  // chunk ahead, the wait drained the ring down to the current chunk's refills)
+  u32x4 xr[2][PPT];
+  auto load_x = [&](int set, int c) {
 #pragma unroll
-    for (int i = 0; i < PPT; ++i) xr[i] = xsrc[i][c * (KC / 8)];
+    for (int i = 0; i < PPT; ++i) xr[set][i] = xsrc[i][c * (KC / 8)];
   };
-  auto store_x = [&](int buf) {
+  auto store_x = [&](int set, int buf) {
 #pragma unroll
-    for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(&xs[buf][xrow[i]][xseg[i] * 8]) = xr[i];
+    for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(&xs[buf][xrow[i]][xseg[i] * 8]) = xr[set][i];
   };
 
   f32x4 acc[RTW][NB];
@@ -714,7 +718,8 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
     for (int n = 0; n < NB; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   u32x4 ra[U][RTW];
-  load_x(0);
+  load_x(0, 0);
+  load_x(1, nch > 1 ? 1 : 0);
 #pragma unroll
   for (int u = 0; u < KCT; ++u)
 #pragma unroll
@@ -726,15 +731,16 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
       for (int r = 0; r < RTW; ++r)
         ra[KCT + u][r] = __builtin_nontemporal_load(Wp[r] + (size_t)(kb + KCT + u) * 64);
   }
-  store_x(0);
+  store_x(0, 0);
   __syncthreads();
 
-  // one chunk: H = ring half (compile time), REFILL = load the chunk two ahead into that half
+  // one chunk: H = ring half = c & 1 (compile time), REFILL = load the chunk two ahead into that
+  // half; activation set H receives chunk c+2, set 1-H (chunk c+1) goes to LDS at the end
   auto chunk = [&](auto Hc, auto Rc, int c) {
     constexpr int H = decltype(Hc)::value;
     constexpr bool REFILL = decltype(Rc)::value;
     const int buf = c & 1;
-    load_x(c + 1 < nch ? c + 1 : c);  // the last chunk re-reads itself: loads stay unconditional
+    load_x(H, c + 2 < nch ? c + 2 : nch - 1);  // past the end: re-read the last chunk (unconditional)
 #pragma unroll
     for (int kk = 0; kk < KCT; ++kk) {
       u32x4 xb[NB];
@@ -753,7 +759,7 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
           ra[H * KCT + kk][r] = __builtin_nontemporal_load(Wp[r] + (size_t)(kb + (c + 2) * KCT + kk) * 64);
       }
     }
-    store_x(buf ^ 1);
+    store_x(1 - H, buf ^ 1);
     __syncthreads();
   };
   using I0 = std::integral_constant<int, 0>;
