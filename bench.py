@@ -262,6 +262,13 @@ def main():
     ap.add_argument("--force-pipeline", action="store_true", help="run the torch.distributed pipeline path even at N=1")
     args = ap.parse_args()
 
+    # stdout carries exactly the one JSON line: native libraries that write to fd 1 (the RCCL
+    # version banner at communicator init, HIP runtime notes) are sent to stderr, and Python's
+    # sys.stdout keeps the original descriptor
+    real_stdout = os.dup(1)
+    os.dup2(2, 1)
+    sys.stdout = os.fdopen(real_stdout, "w", buffering=1)
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 or args.gpus > 1 or args.force_pipeline:
         from llama_p2p_amd import pipeline
