@@ -490,29 +490,69 @@ int mx_engine::load_gguf(const std::string& path) {
   if ((int)f.get_num("llama.rope.dimension_count", n_embd / n_head) != n_embd / n_head)
     return fail(MX_ERR_MODEL, "partial RoPE (rope.dimension_count != head_dim) is not supported");
   if (le < 0 || le > n_layer) le = n_layer;
-  {  // matrix type: every layer matrix and the output BF16 (30), or all Q8_0 (8); token_embd either
-    const GGUFTensor* t0 = f.tensor("blk." + std::to_string(lb < 0 ? 0 : lb) + ".attn_q.weight");
-    if (!t0) return fail(MX_ERR_MODEL, "missing attn_q.weight");
-    if (t0->type != 30 && t0->type != 8)
-      return fail(MX_ERR_MODEL, "layer matrices must be BF16 (ggml type 30) or Q8_0 (type 8), got type " +
-                                    std::to_string(t0->type));
-    wq8 = out_q8 = t0->type == 8;
+  // Matrix types.  All BF16 -> the bf16 path; all Q8_0 -> the Q8_0 path (int8 MFMA on the blocks);
+  // any other mix of F32 / F16 / BF16 / Q4_0 / Q8_0 / Q4_K / Q5_K / Q6_K (Q4_K_M, Q5_K_M, ... files)
+  // -> every matrix is dequantised to bf16 at load (ggml's dequantize_row_*) and runs on the bf16 path.
+  bool deq = false;
+  size_t raw_max = 0;
+  {
+    const int b0 = lb < 0 ? 0 : lb, e0 = (le < 0 || le > n_layer) ? n_layer : le;
+    std::vector<std::string> mats;
+    static const char* kinds[] = {"attn_q", "attn_k", "attn_v", "attn_output", "ffn_gate", "ffn_up", "ffn_down"};
+    for (int l = b0; l < e0; l++)
+      for (const char* k : kinds) mats.push_back("blk." + std::to_string(l) + "." + k + ".weight");
+    if (e0 == n_layer) mats.push_back(f.tensor("output.weight") ? "output.weight" : "token_embd.weight");
+    int n8 = 0, n30 = 0;
+    for (const std::string& nm : mats) {
+      const GGUFTensor* t = f.tensor(nm);
+      if (!t) return fail(MX_ERR_MODEL, "missing tensor " + nm);
+      if (t->type != 30 && !ggml_block_elems(t->type))
+        return fail(MX_ERR_MODEL, "tensor " + nm + ": ggml type " + std::to_string(t->type) +
+                                      " is not supported (F32, F16, BF16, Q4_0, Q8_0, Q4_K, Q5_K, Q6_K are)");
+      n8 += t->type == 8;
+      n30 += t->type == 30;
+      raw_max = std::max(raw_max, (size_t)t->nbytes);
+    }
+    wq8 = out_q8 = n8 == (int)mats.size();
+    deq = !wq8 && n30 != (int)mats.size();
     embd_q8 = te->type == 8;
+    if (te->type != 30 && te->type != 8) {
+      if (!ggml_block_elems(te->type))
+        return fail(MX_ERR_MODEL, "token_embd.weight: ggml type " + std::to_string(te->type) + " is not supported");
+      raw_max = std::max(raw_max, (size_t)te->nbytes);
+    }
   }
   if (int rc = init_common()) return rc;
   const int h = n_embd, kv = n_embd_kv, ff = n_ff, V = n_vocab;
   const int mat_type = wq8 ? 8 : 30;
 
-  // staging buffer for the largest matrix
+  // staging buffer for the largest matrix (bf16), and for the raw blocks of dequantised tensors
   size_t stage_bytes = std::max({(size_t)V * h * 2, (size_t)ff * h * 2, (size_t)(h + 2 * kv) * h * 2});
   uint16_t* stage = nullptr;
+  uint8_t* stage_raw = nullptr;
   HIPC(hipMalloc((void**)&stage, stage_bytes));
+  if (raw_max && (deq || (te->type != 30 && te->type != 8))) {
+    if (hipMalloc((void**)&stage_raw, raw_max) != hipSuccess) {
+      hipFree(stage);
+      return fail(MX_ERR_HIP, "staging buffer");
+    }
+  }
+  // any supported type -> bf16 row-major in `stage`
+  auto to_bf16 = [&](const GGUFTensor* t, size_t n) -> int {
+    if (t->type == 30) {
+      HIPC(hipMemcpy(stage, f.data(*t), t->nbytes, hipMemcpyHostToDevice));
+      return 0;
+    }
+    HIPC(hipMemcpy(stage_raw, f.data(*t), t->nbytes, hipMemcpyHostToDevice));
+    if (launch_dequant_bf16(stage, stage_raw, t->type, n, stream)) return fail(MX_ERR_MODEL, "dequantise " + t->name);
+    return 0;
+  };
   auto get_mat = [&](const std::string& name, int rows, int cols, const GGUFTensor** out, int type) -> int {
     const GGUFTensor* t = f.tensor(name);
     if (!t) return fail(MX_ERR_MODEL, "missing tensor " + name);
     if (t->ne.size() != 2 || (int)t->ne[0] != cols || (int)t->ne[1] != rows)
       return fail(MX_ERR_MODEL, "tensor " + name + " has unexpected shape");
-    if (t->type != type)
+    if (t->type != type && !(deq && type == 30))
       return fail(MX_ERR_MODEL, "tensor " + name + ": expected ggml type " + std::to_string(type) +
                                     (type == 8 ? " (Q8_0, like the other matrices)" : " (BF16, like the other matrices)") +
                                     ", got type " + std::to_string(t->type));
@@ -523,9 +563,13 @@ int mx_engine::load_gguf(const std::string& path) {
                            int offset) -> int {
     const GGUFTensor* t = nullptr;
     if (int rc = get_mat(name, rows, cols, &t, mat_type)) return rc;
-    HIPC(hipMemcpy(stage, f.data(*t), t->nbytes, hipMemcpyHostToDevice));
-    if (wq8) launch_pack_q8((uint8_t*)dst, (const uint8_t*)stage, rows, cols, mode, offset, stream);
-    else launch_pack(dst, stage, rows, cols, mode, offset, stream);
+    if (wq8) {
+      HIPC(hipMemcpy(stage, f.data(*t), t->nbytes, hipMemcpyHostToDevice));
+      launch_pack_q8((uint8_t*)dst, (const uint8_t*)stage, rows, cols, mode, offset, stream);
+    } else {
+      if (int rc = to_bf16(t, (size_t)rows * cols)) return rc;
+      launch_pack(dst, stage, rows, cols, mode, offset, stream);
+    }
     HIPC(hipStreamSynchronize(stream));
     return 0;
   };
@@ -537,15 +581,29 @@ int mx_engine::load_gguf(const std::string& path) {
   };
   int rc = 0;
   if (has_embed) {
-    const GGUFTensor* t = nullptr;
-    if ((rc = get_mat("token_embd.weight", V, h, &t, embd_q8 ? 8 : 30))) goto out;
-    void** dst = embd_q8 ? (void**)&tok_embd8 : (void**)&tok_embd;
-    if ((rc = alloc(dst, t->nbytes))) goto out;
-    if (hipMemcpy(*dst, f.data(*t), t->nbytes, hipMemcpyHostToDevice) != hipSuccess) {
-      rc = fail(MX_ERR_HIP, "upload token_embd");
+    const GGUFTensor* t = f.tensor("token_embd.weight");
+    if (t->ne.size() != 2 || (int)t->ne[0] != h || (int)t->ne[1] != V) {
+      rc = fail(MX_ERR_MODEL, "tensor token_embd.weight has unexpected shape");
       goto out;
     }
-    weight_bytes += t->nbytes / V;
+    if (t->type == 30 || t->type == 8) {  // rows used as stored (Q8_0 rows dequantised per lookup)
+      void** dst = embd_q8 ? (void**)&tok_embd8 : (void**)&tok_embd;
+      if ((rc = alloc(dst, t->nbytes))) goto out;
+      if (hipMemcpy(*dst, f.data(*t), t->nbytes, hipMemcpyHostToDevice) != hipSuccess) {
+        rc = fail(MX_ERR_HIP, "upload token_embd");
+        goto out;
+      }
+      weight_bytes += t->nbytes / V;
+    } else {  // other block types: dequantised to a bf16 table once
+      if ((rc = alloc((void**)&tok_embd, (size_t)V * h * 2))) goto out;
+      if ((rc = to_bf16(t, (size_t)V * h))) goto out;
+      if (hipMemcpyAsync(tok_embd, stage, (size_t)V * h * 2, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
+          hipStreamSynchronize(stream) != hipSuccess) {
+        rc = fail(MX_ERR_HIP, "upload token_embd");
+        goto out;
+      }
+      weight_bytes += (size_t)h * 2;
+    }
   }
   if (has_head) {
     if ((rc = alloc((void**)&output, wq8 ? q8_matrix_bytes(V, h) : (size_t)V * h * 2))) goto out;
@@ -570,7 +628,9 @@ int mx_engine::load_gguf(const std::string& path) {
     if ((rc = upload_packed(p + "ffn_down.weight", h, ff, L.down, PACK_ROWS, 0))) goto out;
   }
 out:
+  hipStreamSynchronize(stream);
   hipFree(stage);
+  if (stage_raw) hipFree(stage_raw);
   return rc;
 }
 

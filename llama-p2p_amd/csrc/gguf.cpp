@@ -65,6 +65,7 @@ uint64_t type_bytes(int type, uint64_t n) {
     case 8: return n / 32 * 34;          // Q8_0
     case 2: return n / 32 * 18;          // Q4_0
     case 12: return n / 256 * 144;       // Q4_K
+    case 13: return n / 256 * 176;       // Q5_K
     case 14: return n / 256 * 210;       // Q6_K
   }
   return 0;

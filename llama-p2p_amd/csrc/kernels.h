@@ -179,6 +179,10 @@ void launch_pack_q8(uint8_t* dst, const uint8_t* src_blocks, int N, int K, int m
 void launch_synth_q8_packed(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, int mode,
                             int row_offset, hipStream_t s);
 void launch_synth_q8_rowmajor(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, hipStream_t s);
+// any GGUF matrix type (F32 0, F16 1, Q4_0 2, Q8_0 8, Q4_K 12, Q5_K 13, Q6_K 14) -> bf16 row-major,
+// n elements (ggml dequantize_row_*, then RNE to bf16); -1 for an unsupported type or ragged n
+int ggml_block_elems(int type);
+int launch_dequant_bf16(uint16_t* dst, const uint8_t* src, int type, size_t n, hipStream_t s);
 void launch_embed_q8(float* x, const uint8_t* tok_embd_blocks, const int* ids, int M, int n_embd, float* ssq,
                      hipStream_t s);
 // RMS_NORM + MUL, quantised to Q8_0 activation rows (xq [M][n], xd [M][n/32])

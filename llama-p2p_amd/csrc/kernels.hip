@@ -1876,6 +1876,103 @@ void launch_synth_q8_rowmajor(uint8_t* dst, int N, int K, uint64_t seed, uint64_
   synth_q8_rowmajor_kernel<<<fill_grid((size_t)N * K / 32), 256, 0, s>>>(dst, N, K, seed, tid, scale);
 }
 
+// ---------------------------------------------------------------------------
+// Any other GGUF block type -> bf16 at load (dequantize_row_* of ggml-quants.c in f32, one rounding
+// per operation as the C code -- contraction is off here -- then round-to-nearest-even to bf16).
+// Used when a file's layer matrices are not all BF16 or all Q8_0 (Q4_K_M, Q5_K_M, Q4_0, F16 ...):
+// the model then runs on the bf16 path.  gguf.py dequantize() is the same restatement.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float f16b(const uint8_t* p) {
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(p[0] | (p[1] << 8)));
+}
+__device__ __forceinline__ void scale_min_k4(int j, const uint8_t* q, int& sc, int& m) {
+  if (j < 4) {
+    sc = q[j] & 63;
+    m = q[j + 4] & 63;
+  } else {
+    sc = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
+    m = (q[j + 4] >> 4) | ((q[j] >> 6) << 4);
+  }
+}
+
+__global__ void dequant_bf16_kernel(uint16_t* dst, const uint8_t* src, int type, size_t nblocks) {
+#pragma clang fp contract(off)  // no fused multiply-subtract: one rounding per operation, as ggml's C
+  for (size_t b = blockIdx.x * (size_t)blockDim.x + threadIdx.x; b < nblocks; b += (size_t)gridDim.x * blockDim.x) {
+    if (type == 0 || type == 1) {  // F32 / F16: "blocks" of 32 values
+      uint16_t* y = dst + b * 32;
+      for (int j = 0; j < 32; ++j)
+        y[j] = (uint16_t)f2bf(type == 0 ? reinterpret_cast<const float*>(src)[b * 32 + j]
+                                        : (float)reinterpret_cast<const _Float16*>(src)[b * 32 + j]);
+    } else if (type == 2) {  // Q4_0
+      const uint8_t* x = src + b * 18;
+      const float d = f16b(x);
+      uint16_t* y = dst + b * 32;
+      for (int j = 0; j < 16; ++j) {
+        y[j] = (uint16_t)f2bf((float)((x[2 + j] & 15) - 8) * d);
+        y[j + 16] = (uint16_t)f2bf((float)((x[2 + j] >> 4) - 8) * d);
+      }
+    } else if (type == 8) {  // Q8_0
+      const uint8_t* x = src + b * 34;
+      const float d = f16b(x);
+      uint16_t* y = dst + b * 32;
+      for (int j = 0; j < 32; ++j) y[j] = (uint16_t)f2bf((float)(int8_t)x[2 + j] * d);
+    } else if (type == 12 || type == 13) {  // Q4_K, Q5_K
+      const bool q5 = type == 13;
+      const uint8_t* x = src + b * (q5 ? 176 : 144);
+      const float d = f16b(x), dmin = f16b(x + 2);
+      const uint8_t* scales = x + 4;
+      const uint8_t* qh = x + 16;
+      const uint8_t* q = x + (q5 ? 48 : 16);
+      uint16_t* y = dst + b * 256;
+      for (int g = 0; g < 4; ++g) {
+        int sc, m;
+        scale_min_k4(2 * g, scales, sc, m);
+        const float d1 = d * (float)sc, m1 = dmin * (float)m;
+        scale_min_k4(2 * g + 1, scales, sc, m);
+        const float d2 = d * (float)sc, m2 = dmin * (float)m;
+        for (int l = 0; l < 32; ++l) {
+          int lo = q[32 * g + l] & 15, hi = q[32 * g + l] >> 4;
+          if (q5) {
+            lo += (qh[l] & (1 << (2 * g))) ? 16 : 0;
+            hi += (qh[l] & (2 << (2 * g))) ? 16 : 0;
+          }
+          y[64 * g + l] = (uint16_t)f2bf(d1 * (float)lo - m1);
+          y[64 * g + 32 + l] = (uint16_t)f2bf(d2 * (float)hi - m2);
+        }
+      }
+    } else if (type == 14) {  // Q6_K
+      const uint8_t* x = src + b * 210;
+      const uint8_t* ql = x;
+      const uint8_t* qh = x + 128;
+      const int8_t* sc = reinterpret_cast<const int8_t*>(x + 192);
+      const float d = f16b(x + 208);
+      uint16_t* y = dst + b * 256;
+      for (int h = 0; h < 2; ++h)
+        for (int l = 0; l < 32; ++l) {
+          const int L0 = ql[64 * h + l], L1 = ql[64 * h + 32 + l], H = qh[32 * h + l];
+          const int qv[4] = {((L0 & 15) | (((H >> 0) & 3) << 4)) - 32, ((L1 & 15) | (((H >> 2) & 3) << 4)) - 32,
+                             ((L0 >> 4) | (((H >> 4) & 3) << 4)) - 32, ((L1 >> 4) | (((H >> 6) & 3) << 4)) - 32};
+          for (int i = 0; i < 4; ++i)
+            y[128 * h + 32 * i + l] = (uint16_t)f2bf((d * (float)sc[8 * h + l / 16 + 2 * i]) * (float)qv[i]);
+        }
+    }
+  }
+}
+int ggml_block_elems(int type) {
+  switch (type) {
+    case 0: case 1: case 2: case 8: return 32;
+    case 12: case 13: case 14: return 256;
+  }
+  return 0;
+}
+
+int launch_dequant_bf16(uint16_t* dst, const uint8_t* src, int type, size_t n, hipStream_t s) {
+  const int be = ggml_block_elems(type);
+  if (!be || n % be) return -1;
+  dequant_bf16_kernel<<<fill_grid(n / be), 256, 0, s>>>(dst, src, type, n / be);
+  return 0;
+}
+
 // GET_ROWS of a Q8_0 token_embd (dequantize_row_q8_0): x = q * f32(d); thread = one block
 // ssq (optional): the per-16-element-tile sums of squares quantise-on-load consumers reduce
 __global__ __launch_bounds__(256) void embed_q8_kernel(float* x, const uint8_t* tok, const int* ids, int n,

@@ -27,17 +27,22 @@ _SCALAR = {
 }
 
 # ggml tensor types used here
-GGML_F32, GGML_F16, GGML_Q4_0, GGML_Q8_0, GGML_Q4_K, GGML_Q6_K, GGML_BF16 = 0, 1, 2, 8, 12, 14, 30
+GGML_F32, GGML_F16, GGML_Q4_0, GGML_Q8_0, GGML_Q4_K, GGML_Q5_K, GGML_Q6_K, GGML_BF16 = 0, 1, 2, 8, 12, 13, 14, 30
+# block (elements, bytes) of the quantised types (ggml-common.h block_q4_0, block_q8_0, block_q4_K,
+# block_q5_K, block_q6_K; QK_K = 256)
+BLOCKS = {GGML_Q4_0: (32, 18), GGML_Q8_0: (32, 34), GGML_Q4_K: (256, 144), GGML_Q5_K: (256, 176),
+          GGML_Q6_K: (256, 210)}
 _TYPE_ELEM_BYTES = {GGML_F32: 4, GGML_F16: 2, GGML_BF16: 2}
 QK8_0 = 32          # ggml block_q8_0: f16 d + 32 x int8 (ggml-common.h)
 Q8_0_BLOCK = 34
 
 
 def type_nbytes(ggml_type: int, n: int) -> int:
-    if ggml_type == GGML_Q8_0:
-        if n % QK8_0:
-            raise ValueError("Q8_0 rows must be a multiple of 32")
-        return n // QK8_0 * Q8_0_BLOCK
+    if ggml_type in BLOCKS:
+        be, bb = BLOCKS[ggml_type]
+        if n % be:
+            raise ValueError(f"ggml type {ggml_type}: rows must be a multiple of {be}")
+        return n // be * bb
     return n * _TYPE_ELEM_BYTES[ggml_type]
 
 
@@ -74,6 +79,130 @@ def dequantize_q8_0(blocks: np.ndarray, K: int) -> np.ndarray:
     d = b[..., :2].copy().view(np.float16).astype(np.float32)
     q = b[..., 2:].view(np.int8).astype(np.float32)
     return (q * d).reshape(blocks.shape[:-1] + (K,))
+
+
+# --- the other block formats, restated from ggml-quants.c dequantize_row_* (all arithmetic in f32,
+# one rounding per operation, as the C code: products are NOT fused with the following subtraction)
+def _f16(b: np.ndarray) -> np.ndarray:
+    return np.ascontiguousarray(b).view(np.float16).astype(np.float32)[..., 0]
+
+
+def dequantize_q4_0(blocks: np.ndarray, K: int) -> np.ndarray:
+    """block_q4_0 {f16 d; u8 qs[16]}: y[j] = ((qs[j] & 15) - 8) * d, y[j+16] = ((qs[j] >> 4) - 8) * d."""
+    b = np.ascontiguousarray(blocks, dtype=np.uint8).reshape(-1, 18)
+    d = _f16(b[:, 0:2])[:, None]
+    qs = b[:, 2:18].astype(np.int32)
+    q = np.concatenate([(qs & 15) - 8, (qs >> 4) - 8], axis=1).astype(np.float32)
+    return (q * d).astype(np.float32).reshape(blocks.shape[:-1] + (K,))
+
+
+def _scale_min_k4(sc: np.ndarray):
+    """get_scale_min_k4 for j = 0..7 over the 12 packed 6-bit scale/min bytes -> (scale, min) [nb][8]."""
+    sc = sc.astype(np.int32)
+    s = np.empty(sc.shape[:-1] + (8,), np.int32)
+    m = np.empty_like(s)
+    s[..., :4] = sc[..., 0:4] & 63
+    m[..., :4] = sc[..., 4:8] & 63
+    s[..., 4:] = (sc[..., 8:12] & 0xF) | ((sc[..., 0:4] >> 6) << 4)
+    m[..., 4:] = (sc[..., 8:12] >> 4) | ((sc[..., 4:8] >> 6) << 4)
+    return s, m
+
+
+def dequantize_q4_k(blocks: np.ndarray, K: int) -> np.ndarray:
+    """block_q4_K {f16 d; f16 dmin; u8 scales[12]; u8 qs[128]}: per 64 values j, sub-blocks 2j/2j+1 with
+    (sc, m) from get_scale_min_k4: y = (d*sc) * q - (dmin*m), low nibbles then high nibbles."""
+    b = np.ascontiguousarray(blocks, dtype=np.uint8).reshape(-1, 144)
+    d, dmin = _f16(b[:, 0:2])[:, None], _f16(b[:, 2:4])[:, None]
+    sc, mn = _scale_min_k4(b[:, 4:16])
+    dl = (d * sc.astype(np.float32)).astype(np.float32)     # [nb][8]
+    ml = (dmin * mn.astype(np.float32)).astype(np.float32)
+    qs = b[:, 16:144].reshape(-1, 4, 32).astype(np.int32)   # 4 groups of 32 bytes (64 values each)
+    q = np.stack([qs & 15, qs >> 4], axis=2).reshape(-1, 8, 32).astype(np.float32)  # sub-block 2g, 2g+1
+    y = (dl[:, :, None] * q).astype(np.float32) - ml[:, :, None]
+    return y.astype(np.float32).reshape(blocks.shape[:-1] + (K,))
+
+
+def dequantize_q5_k(blocks: np.ndarray, K: int) -> np.ndarray:
+    """block_q5_K {f16 d; f16 dmin; u8 scales[12]; u8 qh[32]; u8 qs[128]}: as Q4_K with the 5th bit of
+    sub-block 2g from bit 2g of qh and of 2g+1 from bit 2g+1."""
+    b = np.ascontiguousarray(blocks, dtype=np.uint8).reshape(-1, 176)
+    d, dmin = _f16(b[:, 0:2])[:, None], _f16(b[:, 2:4])[:, None]
+    sc, mn = _scale_min_k4(b[:, 4:16])
+    dl = (d * sc.astype(np.float32)).astype(np.float32)
+    ml = (dmin * mn.astype(np.float32)).astype(np.float32)
+    qh = b[:, 16:48].astype(np.int32)                       # [nb][32]
+    qs = b[:, 48:176].reshape(-1, 4, 32).astype(np.int32)
+    q = np.empty((b.shape[0], 8, 32), np.float32)
+    for g in range(4):
+        q[:, 2 * g] = (qs[:, g] & 15) + np.where(qh & (1 << (2 * g)), 16, 0)
+        q[:, 2 * g + 1] = (qs[:, g] >> 4) + np.where(qh & (2 << (2 * g)), 16, 0)
+    y = (dl[:, :, None] * q).astype(np.float32) - ml[:, :, None]
+    return y.astype(np.float32).reshape(blocks.shape[:-1] + (K,))
+
+
+def dequantize_q6_k(blocks: np.ndarray, K: int) -> np.ndarray:
+    """block_q6_K {u8 ql[128]; u8 qh[64]; i8 scales[16]; f16 d}: two halves of 128 values; in half h,
+    for l < 32: q1..q4 from ql[64h+l], ql[64h+l+32] nibbles and the 2-bit pairs of qh[32h+l], minus 32;
+    y[128h + 32i + l] = d * sc[8h + l/16 + 2i] * q_(i+1)."""
+    b = np.ascontiguousarray(blocks, dtype=np.uint8).reshape(-1, 210)
+    ql = b[:, 0:128].astype(np.int32)
+    qh = b[:, 128:192].astype(np.int32)
+    sc = b[:, 192:208].view(np.int8).astype(np.float32)
+    d = _f16(b[:, 208:210])[:, None]
+    y = np.empty((b.shape[0], 256), np.float32)
+    l = np.arange(32)
+    for h in range(2):
+        L0, L1, H = ql[:, 64 * h + l], ql[:, 64 * h + 32 + l], qh[:, 32 * h + l]
+        qv = [(L0 & 15) | (((H >> 0) & 3) << 4), (L1 & 15) | (((H >> 2) & 3) << 4),
+              (L0 >> 4) | (((H >> 4) & 3) << 4), (L1 >> 4) | (((H >> 6) & 3) << 4)]
+        for i in range(4):
+            s = sc[:, 8 * h + l // 16 + 2 * i]
+            y[:, 128 * h + 32 * i + l] = ((d * s).astype(np.float32) * (qv[i] - 32).astype(np.float32)).astype(np.float32)
+    return y.reshape(blocks.shape[:-1] + (K,))
+
+
+def dequantize(ggml_type: int, data: np.ndarray, shape) -> np.ndarray:
+    """Any supported tensor -> f32 [rows][K] (GGUF order), as ggml's to_float does."""
+    K = shape[-1]
+    if ggml_type == GGML_F32:
+        return np.asarray(data, dtype=np.float32).reshape(shape)
+    if ggml_type == GGML_F16:
+        return np.asarray(data, dtype=np.float16).astype(np.float32).reshape(shape)
+    if ggml_type == GGML_BF16:
+        return (np.asarray(data, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32).reshape(shape)
+    fn = {GGML_Q4_0: dequantize_q4_0, GGML_Q8_0: dequantize_q8_0, GGML_Q4_K: dequantize_q4_k,
+          GGML_Q5_K: dequantize_q5_k, GGML_Q6_K: dequantize_q6_k}[ggml_type]
+    return fn(np.asarray(data), K).reshape(shape)
+
+
+def random_blocks(ggml_type: int, rows: int, K: int, rng, amp: float = 0.03) -> np.ndarray:
+    """Valid random blocks of a quantised type whose values are roughly zero-mean within +-amp (test
+    models: no quantiser needed to exercise a decoder)."""
+    be, bb = BLOCKS[ggml_type]
+    nb = rows * K // be
+    b = rng.integers(0, 256, size=(nb, bb), dtype=np.uint8)
+    if ggml_type == GGML_Q4_0:
+        b[:, 0:2] = np.full((nb, 1), amp / 8, np.float16).view(np.uint8)
+    elif ggml_type == GGML_Q8_0:
+        b[:, 0:2] = np.full((nb, 1), amp / 127, np.float16).view(np.uint8)
+    elif ggml_type in (GGML_Q4_K, GGML_Q5_K):
+        top = 15 if ggml_type == GGML_Q4_K else 31
+        # scales 32..63, mins ~ scale * (top/2) * d / dmin so every sub-block is centred
+        d = amp / (63 * top / 2)
+        dmin = 8 * d
+        s = rng.integers(32, 64, size=(nb, 8))
+        m = np.clip(np.rint(s * (top / 2) * d / dmin), 0, 63).astype(np.int64)
+        sc = np.zeros((nb, 12), np.int64)
+        sc[:, 0:4] = (s[:, 0:4] & 63) | ((s[:, 4:8] >> 4) << 6)
+        sc[:, 4:8] = (m[:, 0:4] & 63) | ((m[:, 4:8] >> 4) << 6)
+        sc[:, 8:12] = (s[:, 4:8] & 15) | ((m[:, 4:8] & 15) << 4)
+        b[:, 0:2] = np.full((nb, 1), d, np.float16).view(np.uint8)
+        b[:, 2:4] = np.full((nb, 1), dmin, np.float16).view(np.uint8)
+        b[:, 4:16] = sc.astype(np.uint8)
+    elif ggml_type == GGML_Q6_K:
+        b[:, 192:208] = rng.integers(8, 16, size=(nb, 16)).astype(np.int8).view(np.uint8)
+        b[:, 208:210] = np.full((nb, 1), amp / (16 * 32), np.float16).view(np.uint8)
+    return b.reshape(rows, K // be * bb)
 
 
 class GGUFWriter:
@@ -206,10 +335,11 @@ class GGUFReader:
         t = info["type"]
         shape = tuple(reversed(info["ne"]))
         n = int(np.prod(shape))
-        if t == GGML_Q8_0:  # raw blocks, [rows][K/32*34] uint8
+        if t in BLOCKS:  # raw blocks, [rows][K/block*bytes] uint8
+            be, bb = BLOCKS[t]
             nb = type_nbytes(t, n)
             return np.memmap(self.path, dtype=np.uint8, mode="r", offset=info["offset"],
-                             shape=(nb,)).reshape(shape[:-1] + (shape[-1] // QK8_0 * Q8_0_BLOCK,))
+                             shape=(nb,)).reshape(shape[:-1] + (shape[-1] // be * bb,))
         dt = {GGML_F32: np.float32, GGML_F16: np.float16, GGML_BF16: np.uint16}[t]
         return np.memmap(self.path, dtype=dt, mode="r", offset=info["offset"], shape=(n,)).reshape(shape)
 
@@ -283,18 +413,45 @@ def synth_q8_0_tensor(arr_bf16: np.ndarray) -> np.ndarray:
     return quantize_q8_0(synth.bf16_bits_to_f32(arr_bf16))
 
 
-def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = None, wtype: str = "bf16"):
+# per-tensor types of the mixed test files, after llama.cpp's ftype recipes (Q4_K_M: Q6_K for attn_v,
+# ffn_down and output; Q4_0: Q6_K output) -- the weights of these are random valid blocks, not
+# quantisations of the synthetic model
+MIXED = {
+    "q4_k_m": {"token_embd": GGML_Q4_K, "output": GGML_Q6_K, "attn_v": GGML_Q6_K, "ffn_down": GGML_Q6_K,
+               "*": GGML_Q4_K},
+    "q5_k_m": {"token_embd": GGML_Q5_K, "output": GGML_Q6_K, "attn_v": GGML_Q6_K, "ffn_down": GGML_Q6_K,
+               "*": GGML_Q5_K},
+    "q4_0": {"token_embd": GGML_Q4_0, "output": GGML_Q6_K, "*": GGML_Q4_0},
+    "f16": {"*": GGML_F16},
+}
+
+
+def _mixed_type(wtype: str, name: str) -> int:
+    m = MIXED[wtype]
+    for key, t in m.items():
+        if key != "*" and (name.startswith(key + ".") or f".{key}." in name):
+            return t
+    return m["*"]
+
+
+def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = None, wtype: str = "bf16",
+                         dequant_from: str = None):
     """Write a LLaMA GGUF with the synthetic weights of synth.py: every matrix bf16, or (wtype
-    "q8_0") the Q8_0 quantisation of those bf16 matrices; norms f32 either way."""
+    "q8_0") the Q8_0 quantisation of those bf16 matrices; norms f32 either way.  wtype "q4_k_m",
+    "q5_k_m", "q4_0", "f16": matrices in those per-tensor types (MIXED), with random valid blocks
+    (seeded) for the quantised ones and the synthetic values for f16.  dequant_from: a GGUF of the
+    same shape whose matrices are written here dequantised (dequantize(), then bf16 RNE) as BF16."""
     from . import synth
 
-    if wtype not in ("bf16", "q8_0"):
-        raise ValueError("wtype must be 'bf16' or 'q8_0'")
+    if wtype not in ("bf16", "q8_0") and wtype not in MIXED:
+        raise ValueError(f"unknown wtype {wtype!r}")
+    rng = np.random.default_rng(1000 + seed)
 
     w = GGUFWriter(path)
     w.add_string("general.architecture", "llama")
     w.add_string("general.name", f"synthetic-{shape.name}-seed{seed}")
-    w.add_uint32("general.file_type", 32 if wtype == "bf16" else 7)  # MOSTLY_BF16 / MOSTLY_Q8_0
+    w.add_uint32("general.file_type", {"bf16": 32, "q8_0": 7, "q4_k_m": 15, "q5_k_m": 17, "q4_0": 2,
+                                        "f16": 1}[wtype])  # llama_ftype
     w.add_uint32("llama.context_length", n_ctx_train or shape.n_ctx_train)
     w.add_uint32("llama.embedding_length", shape.n_embd)
     w.add_uint32("llama.block_count", shape.n_layer)
@@ -315,10 +472,23 @@ def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = Non
     w.add_uint32("tokenizer.ggml.unknown_token_id", 0)
     w.add_bool("tokenizer.ggml.add_bos_token", True)
     arrays = []
+    src = GGUFReader(dequant_from) if dequant_from else None
     for name, kind, arr in synth.synth_tensors(shape, seed):
-        if kind == "bf16" and wtype == "q8_0":
+        if kind == "bf16" and src is not None:
+            info = src.tensors[name]
+            y = dequantize(info["type"], src.tensor(name), arr.shape)
+            w.add_tensor_info(name, arr.shape, GGML_BF16)
+            arrays.append(synth.f32_to_bf16_bits(y))
+        elif kind == "bf16" and wtype == "q8_0":
             w.add_tensor_info(name, arr.shape, GGML_Q8_0)
             arrays.append(synth_q8_0_tensor(arr))
+        elif kind == "bf16" and wtype in MIXED:
+            t = _mixed_type(wtype, name)
+            w.add_tensor_info(name, arr.shape, t)
+            if t == GGML_F16:
+                arrays.append(synth.bf16_bits_to_f32(arr).astype(np.float16))
+            else:
+                arrays.append(random_blocks(t, arr.shape[0], arr.shape[1], rng))
         else:
             w.add_tensor_info(name, arr.shape, GGML_BF16 if kind == "bf16" else GGML_F32)
             arrays.append(arr)
