@@ -383,3 +383,26 @@ def test_fused_attention_attn_output_vs_oracle(mx, oracle_mod):
             om.context(64).eval(seqs[2][:39], 0)[-1]]
     assert_logits_close(got3, np.stack(refs), "attn_o 3 rows")
     eng.close()
+
+
+def test_long_context_prefill_and_decode(mx, oracle_mod):
+    """n_ctx 2048: a 1800-token prompt (GEMM prefill chunks, flash prefill attention over long K/V),
+    then decode steps at positions ~1800 (56 attention chunks per row) vs the oracle."""
+    from llama_p2p_amd import synth
+
+    name = "test-d128"
+    shape = synth.SHAPES[name]
+    ids = _seq(shape, 1806, seed=123)
+    eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=2048, n_seq_max=2)
+    assert eng.forward_rows([1] * 1800, list(range(1800)), ids[:1800], want_logits=False) is None
+    octx = oracle_mod.OracleModel(shape, seed=0).context(2048)
+    ref = octx.eval(ids[:1801], 0, all_logits=True)[1800:]
+    got = eng.forward_logits(ids[1800:1801], 1800, slot=1)
+    assert_logits_close(got, ref, "pos 1800")
+    gs, rs = [], []
+    for p in range(1801, 1806):
+        gs.append(eng.forward_logits(ids[p:p + 1], p, slot=1)[0])
+        rs.append(octx.eval(ids[p:p + 1], p)[0])
+    assert_logits_close(np.stack(gs), np.stack(rs), "decode at ~1800")
+    assert_tokens_match(np.stack(gs), np.stack(rs), "decode at ~1800")
+    eng.close()
