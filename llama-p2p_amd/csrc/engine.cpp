@@ -157,12 +157,17 @@ struct mx_engine {
   // Q8_0 model: layer matrices as packed Q8 tiles; token_embd / output may each
   // be Q8_0 (tok_embd8: GGUF blocks, row-major) or BF16
   bool wq8 = false, embd_q8 = false, out_q8 = false;
-  bool q8_ql = getenv("MX_NO_Q8_QL") == nullptr;
+  bool q8_ql = getenv("MX_NO_Q8_QL") == nullptr;  // Q8_0 GEMVs of <= 4 rows quantise their operand on load
   // attention + attn_output fused (<= 4 rows, bf16), opt-in: measured slower than the two launches
   // (profiles/round1_attn_o_trace.txt); ao_sync holds the counters of its in-launch hand-off
   bool use_attn_o = getenv("MX_ATTN_O") != nullptr;
   unsigned* ao_sync = nullptr;
-  unsigned long long* ao_trace = nullptr;  // MX_AO_TRACE: phase stamps of layer 1's attn_o launch  // Q8_0 GEMVs of <= 4 rows quantise their operand on load
+  unsigned long long* ao_trace = nullptr;  // MX_AO_TRACE: phase stamps of layer 1's attn_o launch
+  // attn_output's last work-group applies the ffn RMS_NORM instead of a norm launch -- opt-in
+  // (MX_FUSED_NORM=1): measured 4.6 us/layer SLOWER at batch 1 (every work-group's agent release
+  // writes back its L2 lines; the serial tail outlasts the launch it replaces); nrm_cnt: its counter
+  bool fuse_norm = getenv("MX_FUSED_NORM") != nullptr;
+  unsigned* nrm_cnt = nullptr;
   uint8_t* tok_embd8 = nullptr;
   int8_t* xq8 = nullptr;    // Q8_0 activation rows [PREFILL_ROWS][max(h, ff)]
   float* xqd = nullptr;     // their block scales
@@ -310,6 +315,8 @@ int mx_engine::init_common() {
   if (int rc = alloc((void**)&d_pos, (size_t)R * 4)) return rc;
   if (int rc = alloc((void**)&d_slot, (size_t)R * 4)) return rc;
   if (int rc = alloc((void**)&d_rowmap, (size_t)R * 4)) return rc;
+  if (int rc = alloc((void**)&nrm_cnt, 64 * 4)) return rc;
+  HIPC(hipMemsetAsync(nrm_cnt, 0, 64 * 4, stream));
   if (int rc = alloc((void**)&ao_sync, 640 * 4)) return rc;
   HIPC(hipMemsetAsync(ao_sync, 0, 640 * 4, stream));
   if (wq8) {
@@ -712,7 +719,11 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
       HIPC(hipMemset(ao_trace, 0, 4096 * 8));
     }
     b.trace = (li == 1) ? ao_trace : nullptr;
-    if (use_attn_o && attn_o_supported(at, b)) {  // attn_output's weight stream overlaps attention
+    const bool fused_ao = use_attn_o && attn_o_supported(at, b);
+    if (fuse_norm && !fused_ao) {  // the ffn RMS_NORM by attn_output's last work-group (M <= 16 here)
+      b.ssq = ssq; b.np = h / 16; b.eps = eps; b.nxt_y = xn; b.nxt_w = L.ffn_norm; b.nxt_cnt = nrm_cnt;
+    }
+    if (fused_ao) {  // attn_output's weight stream overlaps attention
       if (launch_attn_o(at, b, ao_sync, s)) return fail(MX_ERR_ARG, "attention+attn_output launch shape");
     } else {
       launch_attention(at, s);
@@ -720,7 +731,11 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     }
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M;
-    norm_operand(c, L.ffn_norm, false);
+    if (b.nxt_y) {  // attn_output's last work-group already wrote the normalised gate/up operand
+      c.X = xn; c.ldx = h;
+    } else {
+      norm_operand(c, L.ffn_norm, false);
+    }
     c.act = act; c.lda = ff;
     if (launch_mm(EPI_SWIGLU, c, s)) return fail(MX_ERR_ARG, "ffn gate/up launch shape");
     MMArgs d{};

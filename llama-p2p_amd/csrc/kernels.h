@@ -66,6 +66,12 @@ struct MMArgs {
   size_t slot_stride;          // elements per slot in kc/vc = n_head_kv*ctx_stride*head_dim
   size_t slab_stride;          // EPI_SLAB: floats between consecutive K-split partial slabs
   unsigned long long* trace;   // attn_o_kernel phase stamps (diagnosis; nullptr normally)
+  // EPI_RESID with nxt_y (mm_kernel, <= 16 rows): the last work-group to finish also applies the
+  // NEXT RMS_NORM + MUL(nxt_w) to the new residual rows (scale from the ssq partials this launch
+  // wrote, so ssq/np must be set) and writes bf16 nxt_y [M][N]; nxt_cnt: a zeroed arrival counter
+  uint16_t* nxt_y;
+  const float* nxt_w;
+  unsigned* nxt_cnt;
 };
 
 struct AttnArgs {

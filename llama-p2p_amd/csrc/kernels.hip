@@ -422,6 +422,59 @@ __device__ __forceinline__ void epi_store(const MMArgs& a, int tile, int l, int 
   }
 }
 
+// Last-arriver RMS_NORM after an EPI_RESID GEMV (<= 16 rows): every work-group publishes its
+// residual rows and ssq partials (plain stores, drained, agent-scope release, relaxed counter add:
+// cdna_hip_programming.md "In-launch split-K reduction" recipe); the work-group that draws the last
+// ticket acquires and writes nxt_y = bf16((x * 1/sqrt(mean + eps)) * nxt_w) for all M rows, with
+// the sum of squares from the partials in a fixed order (as the RMS_NORM-on-load path), then
+// resets the counter.  Replaces the separate norm launch and its kernel boundary -- but measured
+// slower at batch 1 (2.88 -> 3.03 ms/token, tools/gpu/fn_ab.sh), so it is opt-in (MX_FUSED_NORM=1).
+// `flag` is a word of the caller's LDS (no second __shared__ object).
+__device__ __forceinline__ void resid_then_norm(const MMArgs& a, unsigned* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(a.nxt_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = old == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(a.nxt_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float* scl = reinterpret_cast<float*>(flag) + 1;  // per-row scales (M <= 16) after the flag word
+  if (w == 0) {
+    for (int c = 0; c < a.M; ++c) {
+      double acc = 0.0;
+      for (int i = lane * 4; i < a.np; i += 256)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc += (double)a.ssq[(size_t)c * a.np + i + j];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) acc += __shfl_xor(acc, o);
+      if (lane == 0) scl[c] = 1.0f / sqrtf((float)(acc / a.N) + a.eps);
+    }
+  }
+  __syncthreads();
+  const int n4 = a.N / 4;
+  for (int u = threadIdx.x; u < a.M * n4; u += blockDim.x) {
+    const int c = u / n4, i = (u % n4) * 4;
+    const f32x4 xv = *reinterpret_cast<const f32x4*>(a.out + (size_t)c * a.ldo + i);
+    const f32x4 g = *reinterpret_cast<const f32x4*>(a.nxt_w + i);
+    const float sc = scl[c];
+    u32x2 o;
+    o[0] = f2bf((xv[0] * sc) * g[0]) | (f2bf((xv[1] * sc) * g[1]) << 16);
+    o[1] = f2bf((xv[2] * sc) * g[2]) | (f2bf((xv[3] * sc) * g[3]) << 16);
+    *reinterpret_cast<u32x2*>(a.nxt_y + (size_t)c * a.N + i) = o;
+  }
+}
+
 template <int KS, int RT, int NB, int EPI, int U, bool XS>
 __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
   const int lane = threadIdx.x & 63;
@@ -560,6 +613,9 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
       for (int ww = 1; ww < KS; ++ww) up += red[ww][r][n][l + 32];
     }
     epi_store<EPI>(a, tile0 + r, l, col, s, up);
+  }
+  if constexpr (EPI == EPI_RESID) {
+    if (a.nxt_y) resid_then_norm(a, reinterpret_cast<unsigned*>(&red[0][0][0][0]));
   }
 }
 

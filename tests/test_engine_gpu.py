@@ -406,3 +406,27 @@ def test_long_context_prefill_and_decode(mx, oracle_mod):
     assert_logits_close(np.stack(gs), np.stack(rs), "decode at ~1800")
     assert_tokens_match(np.stack(gs), np.stack(rs), "decode at ~1800")
     eng.close()
+
+
+def test_fused_ffn_norm_vs_oracle(mx, oracle_mod):
+    """Opt-in MX_FUSED_NORM=1: attn_output's last work-group writes the ffn RMS_NORM operand
+    (agent release/acquire hand-off) -- same logits as the oracle at 1 and 3 rows."""
+    from llama_p2p_amd import synth
+
+    name = "test-h4096"
+    shape = synth.SHAPES[name]
+    os.environ["MX_FUSED_NORM"] = "1"
+    try:
+        eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=128, n_seq_max=4)
+    finally:
+        del os.environ["MX_FUSED_NORM"]
+    om = oracle_mod.OracleModel(shape, seed=0)
+    seqs = [_seq(shape, 30, seed=140 + i) for i in range(3)]
+    for i, sq in enumerate(seqs):
+        eng.forward_rows([i] * 28, list(range(28)), sq[:28], want_logits=False)
+    got = eng.forward_rows([0, 1, 2], [28] * 3, [int(sq[28]) for sq in seqs])
+    for i, sq in enumerate(seqs):
+        assert_logits_close(got[i:i + 1], om.context(64).eval(sq[:29], 0)[-1:], f"fused norm row {i}")
+    g1 = eng.forward_logits(seqs[0][29:30], 29, slot=0)
+    assert_logits_close(g1, om.context(64).eval(seqs[0][:30], 0)[-1:], "fused norm batch 1")
+    eng.close()
