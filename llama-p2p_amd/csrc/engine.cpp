@@ -180,6 +180,9 @@ struct mx_engine {
   float *x = nullptr, *q = nullptr, *logits = nullptr;
   uint16_t *xn = nullptr, *act = nullptr, *attn_out = nullptr;
   float* am_val = nullptr;
+  bool use_dev_topk = getenv("MX_NO_DEV_TOPK") == nullptr;  // MX_NO_DEV_TOPK: all-host sampler (tests)
+  float *tk_ws_val = nullptr, *tk_val = nullptr;  // device top-k for the sampler chain
+  int *tk_ws_idx = nullptr, *tk_idx = nullptr;
   int *am_idx = nullptr, *d_tok = nullptr;
   int *d_ids = nullptr, *d_pos = nullptr, *d_slot = nullptr, *d_rowmap = nullptr;
   std::vector<void*> allocations;
@@ -238,6 +241,7 @@ struct mx_engine {
   int sched_step(std::vector<Request*>& rows);
   int prefill(Request* r, std::vector<float>& last_logits);
   int32_t sample_host(Request* r, const float* logits);
+  int32_t sample_chain(Request* r, std::vector<std::pair<float, int>>& c);  // c: top-k, sorted
   void finish(Request* r, int why);
 };
 
@@ -309,6 +313,12 @@ int mx_engine::init_common() {
   if (int rc = alloc((void**)&slabs, slab_stride * 8 * 4)) return rc;
   if (int rc = alloc((void**)&ssq, (size_t)R * (n_embd / 16) * 4)) return rc;
   if (int rc = alloc((void**)&am_val, (size_t)R * 64 * 4)) return rc;
+  if (has_head) {
+    if (int rc = alloc((void**)&tk_ws_val, (size_t)MAX_ROWS * 64 * TOPK_MAX * 4)) return rc;
+    if (int rc = alloc((void**)&tk_ws_idx, (size_t)MAX_ROWS * 64 * TOPK_MAX * 4)) return rc;
+    if (int rc = alloc((void**)&tk_val, (size_t)MAX_ROWS * TOPK_MAX * 4)) return rc;
+    if (int rc = alloc((void**)&tk_idx, (size_t)MAX_ROWS * TOPK_MAX * 4)) return rc;
+  }
   if (int rc = alloc((void**)&am_idx, (size_t)R * 64 * 4)) return rc;
   if (int rc = alloc((void**)&d_tok, (size_t)R * 4)) return rc;
   if (int rc = alloc((void**)&d_ids, (size_t)R * 4)) return rc;
@@ -1036,6 +1046,10 @@ void mx_engine::finish(Request* r, int why) {
 
 // llama.cpp default sampling chain (restricted to the parameters exposed in mx_sampling):
 // repetition penalty -> top_k -> top_p -> min_p -> temperature -> draw
+// llama.cpp's sampler chain as llama-cpp-python 0.3 builds it for create_completion: penalties ->
+// top_k -> top_p -> min_p -> temperature -> draw (greedy when temperature <= 0).  The candidates are
+// ordered by logit (ties: lower id first); only the top k are ever needed, so they are selected with
+// a partial sort here, or on the device (launch_topk) in the decode loop.
 int32_t mx_engine::sample_host(Request* r, const float* lg) {
   const mx_sampling& sp = r->samp;
   std::vector<std::pair<float, int>> c;
@@ -1050,15 +1064,19 @@ int32_t mx_engine::sample_host(Request* r, const float* lg) {
     for (auto& p : c)
       if (seen[p.second]) p.first = p.first <= 0 ? p.first * sp.repeat_penalty : p.first / sp.repeat_penalty;
   }
-  if (sp.temperature <= 0.f) {
-    auto best = std::max_element(c.begin(), c.end(), [](auto& a, auto& b) {
-      return a.first < b.first || (a.first == b.first && a.second > b.second);
-    });
-    return best->second;
-  }
-  std::sort(c.begin(), c.end(), [](auto& a, auto& b) { return a.first > b.first || (a.first == b.first && a.second < b.second); });
-  int k = sp.top_k > 0 ? std::min<int>(sp.top_k, n_vocab) : n_vocab;
+  auto before = [](const std::pair<float, int>& a, const std::pair<float, int>& b) {
+    return a.first > b.first || (a.first == b.first && a.second < b.second);
+  };
+  if (sp.temperature <= 0.f) return std::min_element(c.begin(), c.end(), before)->second;
+  const int k = sp.top_k > 0 ? std::min<int>(sp.top_k, n_vocab) : n_vocab;
+  std::partial_sort(c.begin(), c.begin() + k, c.end(), before);
   c.resize(k);
+  return sample_chain(r, c);
+}
+
+int32_t mx_engine::sample_chain(Request* r, std::vector<std::pair<float, int>>& c) {
+  const mx_sampling& sp = r->samp;
+  const int k = (int)c.size();
   std::vector<double> p(k);
   double mx = c[0].first, sum = 0;
   for (int i = 0; i < k; i++) sum += (p[i] = exp(c[i].first - mx));
@@ -1145,9 +1163,27 @@ int mx_engine::sched_step(std::vector<Request*>& rows) {
     return rc;
   }
   std::vector<int32_t> tok(M);
-  std::vector<float> lg;
+  std::vector<float> lg, tkv;
+  std::vector<int32_t> tki;
   HIPC(hipMemcpyAsync(tok.data(), d_tok, M * 4, hipMemcpyDeviceToHost, s));
-  if (!all_greedy) {
+  // sampling rows: the top-k candidates come from the device (k <= TOPK_MAX, no repeat penalty,
+  // which would reorder logits first); otherwise the whole logits rows go to the host
+  int K = 0;
+  bool dev_topk = !all_greedy && use_dev_topk;
+  for (int i = 0; i < M && dev_topk; i++) {
+    const mx_sampling& sp = rows[i]->samp;
+    if (sp.temperature <= 0.f && sp.repeat_penalty == 1.0f) continue;
+    if (sp.repeat_penalty != 1.0f || sp.top_k < 1 || sp.top_k > TOPK_MAX) dev_topk = false;
+    else K = std::max(K, std::min(sp.top_k, n_vocab));
+  }
+  if (dev_topk && K > 0) {
+    if (launch_topk(logits, n_vocab, M, n_vocab, K, tk_ws_val, tk_ws_idx, tk_val, tk_idx, s))
+      return fail(MX_ERR_HIP, "top-k launch");
+    tkv.resize((size_t)M * K);
+    tki.resize((size_t)M * K);
+    HIPC(hipMemcpyAsync(tkv.data(), tk_val, (size_t)M * K * 4, hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(tki.data(), tk_idx, (size_t)M * K * 4, hipMemcpyDeviceToHost, s));
+  } else if (!all_greedy) {
     lg.resize((size_t)M * n_vocab);
     HIPC(hipMemcpyAsync(lg.data(), logits, (size_t)M * n_vocab * 4, hipMemcpyDeviceToHost, s));
   }
@@ -1158,8 +1194,15 @@ int mx_engine::sched_step(std::vector<Request*>& rows) {
     Request* r = rows[i];
     r->pos++;
     int32_t t = tok[i];
-    if (!all_greedy && (r->samp.temperature > 0.f || r->samp.repeat_penalty != 1.0f))
-      t = sample_host(r, lg.data() + (size_t)i * n_vocab);
+    if (!all_greedy && (r->samp.temperature > 0.f || r->samp.repeat_penalty != 1.0f)) {
+      if (!tkv.empty()) {
+        std::vector<std::pair<float, int>> c(std::min(r->samp.top_k, n_vocab));
+        for (size_t j = 0; j < c.size(); j++) c[j] = {tkv[(size_t)i * K + j], tki[(size_t)i * K + j]};
+        t = sample_chain(r, c);
+      } else {
+        t = sample_host(r, lg.data() + (size_t)i * n_vocab);
+      }
+    }
     r->out.push_back(t);
     r->next_tok = t;
     if (t == eos && !r->samp.ignore_eos) finish(r, MX_FINISH_STOP);

@@ -202,6 +202,10 @@ void launch_quantize_q8(int8_t* xq, float* xd, const float* src, int ld, int M, 
 int launch_mq8(int epi, const MMArgs& a, hipStream_t s);
 bool mq8_can_quantize_on_load(int M, int K, bool norm);
 
+// top-k (k <= TOPK_MAX) candidates per logits row, value descending, ties by lower id; ws: M*64*k
+constexpr int TOPK_MAX = 64;
+int launch_topk(const float* logits, int ldl, int M, int V, int K, float* ws_val, int* ws_idx, float* out_val,
+                int* out_idx, hipStream_t s);
 void launch_argmax(const float* logits, int ldl, int M, int V, float* ws_val, int* ws_idx, int* tok_out,
                    int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count, int max_hist,
                    hipStream_t s);

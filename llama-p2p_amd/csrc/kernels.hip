@@ -1422,6 +1422,81 @@ __global__ void argmax_stage2(const float* ws_val, const int* ws_idx, int* tok_o
   }
 }
 
+// ---------------------------------------------------------------------------
+// top-k candidates of each logits row, for the sampler chain (llama.cpp top_k, then top_p / min_p /
+// temperature / draw on the host over k values instead of a sort of the whole vocabulary).  Order:
+// value descending, ties by lower id -- the host sampler's comparator.  Selection by K passes of
+// "largest element strictly after the previous pick in that order" (no mask, no sort).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool topk_after(float v, int i, float pv, int pi) {  // (v,i) comes after (pv,pi)
+  return v < pv || (v == pv && i > pi);
+}
+__device__ __forceinline__ bool topk_better(float v, int i, float bv, int bi) {
+  return v > bv || (v == bv && i < bi);
+}
+
+template <int NT>
+__device__ void topk_select(const float* val, const int* idx, int n, int K, float* ov, int* oi, float* sv, int* si) {
+  float pv = INFINITY;
+  int pi = -1;
+  for (int k = 0; k < K; ++k) {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int j = threadIdx.x; j < n; j += NT) {
+      const float v = val[j];
+      const int i = idx ? idx[j] : j;
+      if (topk_after(v, i, pv, pi) && topk_better(v, i, bv, bi)) bv = v, bi = i;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float v2 = __shfl_xor(bv, o);
+      const int i2 = __shfl_xor(bi, o);
+      if (topk_better(v2, i2, bv, bi)) bv = v2, bi = i2;
+    }
+    if ((threadIdx.x & 63) == 0) sv[threadIdx.x >> 6] = bv, si[threadIdx.x >> 6] = bi;
+    __syncthreads();
+    bv = sv[0];
+    bi = si[0];
+#pragma unroll
+    for (int w2 = 1; w2 < NT / 64; ++w2)
+      if (topk_better(sv[w2], si[w2], bv, bi)) bv = sv[w2], bi = si[w2];
+    __syncthreads();
+    if (threadIdx.x == 0) ov[k] = bv, oi[k] = bi;
+    pv = bv;
+    pi = bi;
+  }
+}
+
+// stage 1: block b of row c selects the top K of its slice; stage 2: one block per row merges
+__global__ __launch_bounds__(256) void topk_stage1(const float* logits, int ldl, int V, int K, float* cv, int* ci) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  const int c = blockIdx.y, b = blockIdx.x, nb = gridDim.x;
+  const int lo = (int)((long long)V * b / nb), hi = (int)((long long)V * (b + 1) / nb);
+  __shared__ int ids[4096];
+  __shared__ float vals[4096];
+  for (int j = threadIdx.x; j < hi - lo; j += 256) vals[j] = logits[(size_t)c * ldl + lo + j], ids[j] = lo + j;
+  __syncthreads();
+  topk_select<256>(vals, ids, hi - lo, K, cv + ((size_t)c * nb + b) * K, ci + ((size_t)c * nb + b) * K, sv, si);
+}
+
+__global__ __launch_bounds__(256) void topk_stage2(const float* cv, const int* ci, int n, int K, float* ov, int* oi) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  const int c = blockIdx.x;
+  topk_select<256>(cv + (size_t)c * n, ci + (size_t)c * n, n, K, ov + (size_t)c * K, oi + (size_t)c * K, sv, si);
+}
+
+int launch_topk(const float* logits, int ldl, int M, int V, int K, float* ws_val, int* ws_idx, float* out_val,
+                int* out_idx, hipStream_t s) {
+  if (K < 1 || K > TOPK_MAX || M < 1) return -1;
+  const int nb = std::min(64, std::max(1, (V + 2047) / 2048));
+  if ((V + nb - 1) / nb > 4096) return -1;
+  topk_stage1<<<dim3(nb, M), 256, 0, s>>>(logits, ldl, V, K, ws_val, ws_idx);
+  topk_stage2<<<M, 256, 0, s>>>(ws_val, ws_idx, nb * K, K, out_val, out_idx);
+  return 0;
+}
+
 void launch_argmax(const float* logits, int ldl, int M, int V, float* ws_val, int* ws_idx, int* tok_out,
                    int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count, int max_hist,
                    hipStream_t s) {

@@ -3,6 +3,8 @@ and Q8_0, with tokenizer metadata) -> ``Llama(model_path=...)`` (p2p:19) -> ``ll
 max_tokens=...)["choices"][0]["text"]`` (p2p:125).  Greedy output must follow the CPU oracle on
 the same tokenised prompt; the reference's own call (default sampling, max_tokens=100) must return
 a completion dict of the llama-cpp-python shape."""
+import os
+
 import numpy as np
 import pytest
 
@@ -43,3 +45,34 @@ def test_llama_dropin_greedy_vs_oracle(oracle_mod, tmp_path, wtype):
     res = llm(prompt, max_tokens=100)
     assert isinstance(res["choices"][0]["text"], str) and res["usage"]["completion_tokens"] <= 100
     llm.close()
+
+
+def test_sampling_device_topk_equals_host_chain():
+    """The decode loop's sampler takes its top-k candidates from the device (launch_topk); with fixed
+    seeds the completions must be identical to the all-host chain (an engine created with
+    MX_NO_DEV_TOPK=1: full logits rows, partial sort) -- same candidates, same order, same draws --
+    at the reference's default sampling and at other top-k / top-p / min-p / temperature settings,
+    for 1 and 3 concurrent requests."""
+    from llama_p2p_amd import engine
+
+    def run(host_only):
+        if host_only:
+            os.environ["MX_NO_DEV_TOPK"] = "1"
+        try:
+            eng = engine.Engine("synthetic:test-d128:seed=0", n_ctx=256, n_seq_max=4)
+        finally:
+            os.environ.pop("MX_NO_DEV_TOPK", None)
+        rng = np.random.default_rng(5)
+        prompts = [[1] + [int(t) for t in rng.integers(3, 2000, 12 + 5 * i)] for i in range(3)]
+        out = []
+        for kw in ({"temperature": 0.8, "top_k": 40, "top_p": 0.95, "min_p": 0.05},   # llama-cpp defaults
+                   {"top_k": 5, "temperature": 1.3}, {"top_k": 64, "top_p": 0.8, "min_p": 0.0, "temperature": 0.5}):
+            out.append(list(eng.generate(prompts[0], 24, seed=7, ignore_eos=True, **kw)[0]))
+            reqs = [eng.submit(p, 16, seed=11 + i, ignore_eos=True, **kw) for i, p in enumerate(prompts)]
+            out += [list(eng.wait(r)[0]) for r in reqs]
+        eng.close()
+        return out
+
+    dev, host = run(False), run(True)
+    assert dev == host
+    assert len({tuple(o) for o in dev}) > 3  # sampling actually varied the completions
