@@ -63,7 +63,13 @@ def partition_layers(n_layer: int, layer_cost: float, head_cost: float, n_stages
 
 
 class TorchComm:
-    """Point-to-point hand-offs over torch.distributed (nccl = RCCL on ROCm, or gloo)."""
+    """Point-to-point hand-offs over torch.distributed (nccl = RCCL on ROCm, or gloo).
+
+    ``exchange`` posts a set of sends and receives as ONE group
+    (``batch_isend_irecv`` = ncclGroupStart/End): RCCL's ncclSend may not complete
+    until the peer has posted the matching ncclRecv, so ops that must progress
+    together have to share a group (see ``Stage.decode_steps``).
+    """
 
     def __init__(self, rank: int, world: int):
         import torch.distributed as dist
@@ -78,6 +84,16 @@ class TorchComm:
 
     def recv(self, t, src: int):
         self.dist.recv(t, src)
+
+    def exchange(self, sends, recvs):
+        """sends = [(tensor, dst)], recvs = [(tensor, src)]; returns when all completed
+        (on nccl: the current stream waits for them)."""
+        P = self.dist.P2POp
+        ops = [P(self.dist.isend, t, d) for t, d in sends] + [P(self.dist.irecv, t, s) for t, s in recvs]
+        if not ops:
+            return
+        for w in self.dist.batch_isend_irecv(ops):
+            w.wait()
 
     def drain(self):
         for w in self._pending:
@@ -100,6 +116,7 @@ class Stage:
         self.batches = []
         self.x_in, self.x_out, self.tok = [], [], []
         self.pending_tokens = False  # stage 0 has not yet received the last step's tokens
+        self.deferred = []  # sends of the previous micro-step, posted with the next receive
 
     # -- prefill (untimed): prompt rows through every stage, 64 rows per hand-off
     def prefill(self, mb_rows: Sequence[Tuple[List[int], List[int], List[int]]], chunk: int = 64):
@@ -136,40 +153,49 @@ class Stage:
             self.x_out.append(torch.empty((M, self.n_embd), dtype=torch.float32, device=self.device))
 
     def decode_steps(self, n_steps: int, step0: int = 0):
-        """n_steps greedy tokens for every micro-batch, micro-batches interleaved."""
+        """n_steps greedy tokens for every micro-batch, micro-batches interleaved.
+
+        Per micro-step k a stage receives its input (x from stage r-1; on stage 0 the
+        tokens of micro-step k-S from the last stage), computes, and sends its output.
+        The send of micro-step k is deferred and posted in ONE group with the receive
+        of micro-step k+1.  Under rendezvous semantics (an RCCL send completes only
+        once its receive is posted) ungrouped ops deadlock as soon as S > 1: stage 0
+        would block sending x of micro-batch 1 while the last stage blocks sending the
+        tokens of micro-batch 0, each waiting for the other's next op.  Grouped, the
+        wait graph has no cycle (tests/test_pipeline_cpu.py runs the schedule over a
+        strict rendezvous transport)."""
         for st in range(step0, step0 + n_steps):
             for mb, b in enumerate(self.batches):
                 if self.world == 1:
                     b.step_tensors()
                     continue
                 if self.first:
-                    if self.pending_tokens:
-                        self.comm.recv(self.tok[mb], self.world - 1)  # tokens of the previous step
-                    b.step_tensors(None, self.x_out[mb])
-                    self.comm.send(self.x_out[mb], 1)
-                elif self.last:
-                    self.comm.recv(self.x_in[mb], self.rank - 1)
-                    b.step_tensors(self.x_in[mb], None)
-                    self.comm.send(self.tok[mb], 0)
+                    recvs = [(self.tok[mb], self.world - 1)] if self.pending_tokens else []
                 else:
-                    self.comm.recv(self.x_in[mb], self.rank - 1)
+                    recvs = [(self.x_in[mb], self.rank - 1)]
+                self.comm.exchange(self.deferred, recvs)
+                if self.first:
+                    b.step_tensors(None, self.x_out[mb])
+                    self.deferred = [(self.x_out[mb], 1)]
+                elif self.last:
+                    b.step_tensors(self.x_in[mb], None)
+                    self.deferred = [(self.tok[mb], 0)]
+                else:
                     b.step_tensors(self.x_in[mb], self.x_out[mb])
-                    self.comm.send(self.x_out[mb], self.rank + 1)
+                    self.deferred = [(self.x_out[mb], self.rank + 1)]
             self.pending_tokens = True
-            # isends of this step must finish before their buffers are refilled next step
-            if self.world > 1:
-                self.comm.drain()
 
     def finish(self):
-        """Drain the ring: stage 0 receives the tokens of the final step.  Must run
-        before any device-wide synchronize, or the last stage's pending send of
-        those tokens would never complete."""
-        if self.world > 1 and self.first and self.pending_tokens:
-            for mb in range(len(self.batches)):
-                self.comm.recv(self.tok[mb], self.world - 1)
-        self.pending_tokens = False
+        """Drain the ring: post the deferred send, and stage 0 receives the tokens of the
+        final step.  Must run before any device-wide synchronize, or the last stage's
+        send of those tokens would never complete."""
         if self.world > 1:
-            self.comm.drain()
+            recvs = []
+            if self.first and self.pending_tokens:
+                recvs = [(self.tok[mb], self.world - 1) for mb in range(len(self.batches))]
+            self.comm.exchange(self.deferred, recvs)
+            self.deferred = []
+        self.pending_tokens = False
 
     def tokens(self):
         return [b.tokens() for b in self.batches] if self.last else None

@@ -6,9 +6,17 @@ embedding, layers whose output depends on a per-(slot, layer) running state
 (standing in for the KV cache, so mis-routed micro-batches or slots change the
 tokens), and a greedy head.  The S-stage pipeline must produce exactly the
 tokens of the 1-stage run.  The stage partition is checked separately.
+
+RCCL's ncclSend may block until the peer posts the matching ncclRecv (gloo
+buffers sends, so the gloo runs cannot show a deadlock).  The same schedule is
+therefore also run over an in-process transport with strict rendezvous
+semantics: every op of a group completes only when each of its ops has been
+matched by the peer's op of the same direction, in order.
 """
+import collections
 import os
 import socket
+import threading
 
 import numpy as np
 import pytest
@@ -101,9 +109,10 @@ def _workload(S, M, seed=3):
     return mb_rows, mb_state
 
 
-def _run_stage(rank, world, parts, S, M, steps, q):
+def _run_stage(rank, world, parts, S, M, steps, q, comm=None):
     lb, le = parts[rank]
-    comm = TorchComm(rank, world) if world > 1 else None
+    if comm is None:
+        comm = TorchComm(rank, world) if world > 1 else None
     eng = ToyEngine(lb, le, S * M)
     st = Stage(eng, comm, rank, world, H, torch.device("cpu"), S)
     mb_rows, mb_state = _workload(S, M)
@@ -174,3 +183,97 @@ def test_partition_balances_bytes():
     assert p8[-1][1] - p8[-1][0] < p8[0][1] - p8[0][0]  # the head stage holds fewer layers
     with pytest.raises(ValueError):
         partition_layers(4, 1.0, 1.0, 5)
+
+
+class _Hub:
+    """Rendezvous matching of sends/receives per ordered (src, dst) pair."""
+
+    def __init__(self, timeout):
+        self.cv = threading.Condition()
+        self.sends = collections.defaultdict(collections.deque)
+        self.recvs = collections.defaultdict(collections.deque)
+        self.timeout = timeout
+
+    def group(self, rank, sends, recvs):
+        ops = []
+        with self.cv:
+            for t, d in sends:
+                ops.append([t, False])
+                self.sends[(rank, d)].append(ops[-1])
+            for t, s in recvs:
+                ops.append([t, False])
+                self.recvs[(s, rank)].append(ops[-1])
+            for key in list(self.sends):
+                qs, qr = self.sends[key], self.recvs[key]
+                while qs and qr:
+                    snd, rcv = qs.popleft(), qr.popleft()
+                    rcv[0].copy_(snd[0])
+                    snd[1] = rcv[1] = True
+            self.cv.notify_all()
+            if not self.cv.wait_for(lambda: all(o[1] for o in ops), timeout=self.timeout):
+                raise TimeoutError(f"rank {rank}: rendezvous deadlock")
+
+
+class RendezvousComm:
+    def __init__(self, hub, rank, grouped=True):
+        self.hub, self.rank, self.grouped = hub, rank, grouped
+
+    def exchange(self, sends, recvs):
+        if self.grouped:
+            self.hub.group(self.rank, sends, recvs)
+        else:  # every op alone, in the order the ungrouped schedule issued them
+            for snd in sends:
+                self.hub.group(self.rank, [snd], [])
+            for rcv in recvs:
+                self.hub.group(self.rank, [], [rcv])
+
+    def send(self, t, dst):
+        self.hub.group(self.rank, [(t, dst)], [])
+
+    def recv(self, t, src):
+        self.hub.group(self.rank, [], [(t, src)])
+
+    def drain(self):
+        pass
+
+
+def _run_rendezvous(world, grouped, timeout):
+    import queue
+
+    S, M, steps = world, 3, 6
+    parts = partition_layers(L, 1.0, 1.5, world)
+    hub = _Hub(timeout)
+    q, errs = queue.Queue(), []
+
+    def run(r):
+        try:
+            _run_stage(r, world, parts, S, M, steps, q, comm=RendezvousComm(hub, r, grouped))
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+            with hub.cv:  # wake the other ranks so they time out too
+                hub.cv.notify_all()
+
+    th = [threading.Thread(target=run, args=(r,), daemon=True) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=4 * timeout + 30)
+    return errs, (q.get() if not q.empty() else None)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_pipeline_schedule_under_rendezvous_transport(world):
+    import queue
+
+    qq = queue.Queue()
+    _run_stage(0, 1, [(0, L)], world, 3, 6, qq)
+    ref = qq.get()
+    errs, got = _run_rendezvous(world, grouped=True, timeout=20)
+    assert not errs, errs
+    assert np.array_equal(got, ref)
+
+
+def test_ungrouped_schedule_deadlocks_under_rendezvous():
+    # the transport is strict enough to catch the hazard: the same ops, each posted alone
+    errs, _ = _run_rendezvous(2, grouped=False, timeout=2)
+    assert errs and all(isinstance(e, TimeoutError) for e in errs)
