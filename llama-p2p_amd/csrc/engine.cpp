@@ -64,6 +64,8 @@ const Shape kShapes[] = {
     {"test-d128", 1024, 2, 8, 2, 2816, 2048, 500000.f, 1e-5f, 2048},
     {"test-h4096", 4096, 1, 32, 8, 2048, 1024, 500000.f, 1e-5f, 2048},
     {"test-h8192", 8192, 1, 64, 8, 2048, 1024, 500000.f, 1e-5f, 2048},
+    {"test-8b-ffn", 4096, 2, 32, 8, 14336, 1024, 500000.f, 1e-5f, 2048},
+    {"test-70b-ffn", 8192, 1, 64, 8, 28672, 1024, 500000.f, 1e-5f, 2048},
 };
 
 // synth.py tensor ids
@@ -127,6 +129,8 @@ struct mx_engine {
   // <= 16 rows: RMS_NORM applied while loading the GEMV's B operand, from per-tile sums of squares
   // written by the residual-stream producer (no norm launches); MX_NO_NORM_ON_LOAD=1 for A/B runs
   bool norm_on_load = getenv("MX_NO_NORM_ON_LOAD") == nullptr;
+  // gate/up as a row-tile-persistent GEMV with RMS_NORM on load (<= 4 rows); MX_NO_PERS=1 for A/B
+  bool use_pers = getenv("MX_NO_PERS") == nullptr;
   float* ssq = nullptr;  // [MAX_ROWS][n_embd/16] per-tile sums of squares of x
   // rows of the next forward belong to distinct sequences (decode): no row attends to another row's
   // new K/V, so the wide path lets the attention kernel finish q/k/v from the split-K slabs
@@ -729,6 +733,9 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
       HIPC(hipMemset(ao_trace, 0, 4096 * 8));
     }
     b.trace = (li == 1) ? ao_trace : nullptr;
+    if (use_pers && nol && mm_pers_supported(EPI_SWIGLU, M, 2 * ff, h)) {  // partials for gate/up's norm on load
+      b.ssq = ssq; b.np = h / 16;
+    }
     const bool fused_ao = use_attn_o && attn_o_supported(at, b);
     if (fuse_norm && !fused_ao) {  // the ffn RMS_NORM by attn_output's last work-group (M <= 16 here)
       b.ssq = ssq; b.np = h / 16; b.eps = eps; b.nxt_y = xn; b.nxt_w = L.ffn_norm; b.nxt_cnt = nrm_cnt;
@@ -737,21 +744,27 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
       if (launch_attn_o(at, b, ao_sync, s)) return fail(MX_ERR_ARG, "attention+attn_output launch shape");
     } else {
       launch_attention(at, s);
-      if (launch_mm(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "attn_output launch shape");
+      if ((!b.nxt_y && mm_pers_supported(EPI_RESID, M, h, h) ? launch_mm_pers(EPI_RESID, b, s) : -1) != 0 &&
+          launch_mm(EPI_RESID, b, s))
+        return fail(MX_ERR_ARG, "attn_output launch shape");
     }
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M;
+    const bool pers_gu = use_pers && nol && !b.nxt_y && mm_pers_supported(EPI_SWIGLU, M, 2 * ff, h);
     if (b.nxt_y) {  // attn_output's last work-group already wrote the normalised gate/up operand
       c.X = xn; c.ldx = h;
     } else {
-      norm_operand(c, L.ffn_norm, false);
+      norm_operand(c, L.ffn_norm, pers_gu);
     }
     c.act = act; c.lda = ff;
-    if (launch_mm(EPI_SWIGLU, c, s)) return fail(MX_ERR_ARG, "ffn gate/up launch shape");
+    if ((pers_gu ? launch_mm_pers(EPI_SWIGLU, c, s) : -1) != 0 && launch_mm(EPI_SWIGLU, c, s))
+      return fail(MX_ERR_ARG, "ffn gate/up launch shape");
     MMArgs d{};
     d.W = L.down; d.N = h; d.K = ff; d.X = act; d.ldx = ff; d.M = M; d.out = x; d.ldo = h;
     d.ssq = nol ? ssq : nullptr; d.np = h / 16;
-    if (launch_mm(EPI_RESID, d, s)) return fail(MX_ERR_ARG, "ffn_down launch shape");
+    if ((mm_pers_supported(EPI_RESID, M, h, ff) ? launch_mm_pers(EPI_RESID, d, s) : -1) != 0 &&
+        launch_mm(EPI_RESID, d, s))
+      return fail(MX_ERR_ARG, "ffn_down launch shape");
   }
   if (x_out) {
     HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));

@@ -155,6 +155,9 @@ void launch_rmsnorm(uint16_t* y, int ldy, const float* x, const float* w, const 
                     float eps, hipStream_t s);
 int launch_mm(int epi, const MMArgs& a, hipStream_t s);
 bool mm_can_norm_on_load(int M, int K);
+// <= 16 rows, row-tile-persistent gate/up: -1 if the shape has no instantiation
+bool mm_pers_supported(int epi, int M, int N, int K);
+int launch_mm_pers(int epi, const MMArgs& a, hipStream_t s);
 // 17..64 rows: activation chunks shared through LDS.  EPI_QKV / EPI_RESID run split-K into
 // `slabs` ([ksplit][MAX_ROWS][N] floats, slab_stride apart); returns the split used (the caller
 // folds RESID partials with launch_resid_norm; QKV partials are finished inside), or -1.

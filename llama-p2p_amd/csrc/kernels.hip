@@ -312,18 +312,20 @@ void launch_rmsnorm(uint16_t* y, int ldy, const float* x, const float* w, const 
 // this lane's 4 partials of ssq (whole wave = all np <= 512 of them, 2 pieces) and 4 values of
 // x and of w per 256-k piece of the wave's K-slice (nk <= 512: 2 pieces).
 constexpr int XS_MAX_M = 4;
+template <int MM = XS_MAX_M>
 struct XsRegs {
-  f32x4 q[XS_MAX_M][2], x[XS_MAX_M][2], g[2];
+  f32x4 q[MM][2], x[MM][2], g[2];
 };
 
-__device__ __forceinline__ void xs_load(XsRegs& r, const MMArgs& a, int kbase, int nk, int lane) {
+template <int MM>
+__device__ __forceinline__ void xs_load(XsRegs<MM>& r, const MMArgs& a, int kbase, int nk, int lane) {
   const int i0 = lane * 4;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     const int i = i0 + 256 * p;
     if (i < nk) r.g[p] = *reinterpret_cast<const f32x4*>(a.norm_w + kbase + i);
 #pragma unroll
-    for (int c = 0; c < XS_MAX_M; ++c) {
+    for (int c = 0; c < MM; ++c) {
       if (c < a.M) {
         if (i < a.np) r.q[c][p] = *reinterpret_cast<const f32x4*>(a.ssq + (size_t)c * a.np + i);
         if (i < nk) r.x[c][p] = *reinterpret_cast<const f32x4*>(a.xf + (size_t)c * a.K + kbase + i);
@@ -334,11 +336,12 @@ __device__ __forceinline__ void xs_load(XsRegs& r, const MMArgs& a, int kbase, i
 
 // scale per column from the partials (fixed-order lane sum, then a fixed xor tree: every lane
 // agrees), then xs[c][k - kbase] = bf16((x * scale) * w): this wave's LDS image (only it reads it)
-__device__ __forceinline__ void xs_build(const XsRegs& r, const MMArgs& a, uint16_t* xs, int pitch, int nk,
+template <int MM>
+__device__ __forceinline__ void xs_build(const XsRegs<MM>& r, const MMArgs& a, uint16_t* xs, int pitch, int nk,
                                          int lane) {
   const int i0 = lane * 4;
 #pragma unroll
-  for (int c = 0; c < XS_MAX_M; ++c) {
+  for (int c = 0; c < MM; ++c) {
     if (c >= a.M) break;
     double acc = 0.0;
 #pragma unroll
@@ -519,7 +522,7 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
                                                              __builtin_bit_cast(bf16x8, xb[n]), acc[r][n], 0, 0, 0);
   };
 
-  XsRegs xr;
+  XsRegs<> xr;
   if constexpr (XS) xs_load(xr, a, kb * TILE_K, (ke - kb) * TILE_K, lane);
   u32x4 ra[U][RT];
   int kt = kb;
@@ -643,6 +646,182 @@ static int launch_mm_cfg(const MMArgs& a, hipStream_t s) {
     else return -1;
   }
   return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Row-tile-persistent GEMV (<= 16 tokens; <= 4 with RMS_NORM on load).
+//
+// mm_kernel gives each work-group ONE 16-row tile, so a large N (gate/up: 1792 tiles) runs
+// 7 rounds of work-groups and every round pays the ramp (first loads in flight) and, with
+// RMS_NORM on load, the per-work-group norm prologue -- which is why gate/up kept a separate
+// norm launch.  Here a grid of G work-groups walks tiles blockIdx.x, +G, +2G, ...: each wave's
+// weight ring runs unbroken across tile seams (the next tile's first loads are issued while
+// this tile's last MFMAs retire), the B fragments (the same for every tile) are loaded once
+// into registers, and the RMS_NORM-on-load image is built once per work-group.  Partial tiles
+// meet in a double-buffered LDS array behind a raw s_barrier that waits only for the LDS
+// writes (a __syncthreads would also drain the ring); wave 0 finishes tile i while the other
+// waves stream tile i+1.  Same epilogues (F32 / RESID + ssq partials / SWIGLU) and the same
+// summation order per tile (K-slices in wave order) as mm_kernel, so results are bit-identical.
+// ---------------------------------------------------------------------------
+// XL (XS only): B fragments read from the LDS image at each MFMA instead of held in registers,
+// so the kernel fits 64 VGPRs and two 16-wave work-groups share a CU (WPE = waves per SIMD).
+template <int KS, int NKW, int TPW, int EPI, int U, bool XS, bool XL = false, int WPE = 4, int XM = XS_MAX_M>
+__global__ __launch_bounds__(64 * KS, WPE) void mm_pers_kernel(MMArgs a) {
+  static_assert(NKW % U == 0 || (U % NKW == 0 && U / NKW <= TPW), "ring depth vs per-wave K-slice");
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  constexpr int KT = KS * NKW;
+  const int kb = w * NKW;
+  const int G = gridDim.x;
+
+  __shared__ f32x4 red[2][KS][64];
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs_dyn[];
+
+  const u32x4* Wb = reinterpret_cast<const u32x4*>(a.W) + lane;
+  auto wp = [&](int i, int k) { return Wb + ((size_t)(blockIdx.x + i * G) * KT + kb + k) * 64; };
+
+  const int col_raw = lane & 15;
+  const int col = col_raw < a.M ? col_raw : a.M - 1;
+  constexpr int xs_pitch = NKW * TILE_K + 8;
+  uint16_t* xsw = xs_dyn + (size_t)w * XS_MAX_M * xs_pitch;
+
+  XsRegs<XM> xr;
+  if constexpr (XS) xs_load(xr, a, kb * TILE_K, NKW * TILE_K, lane);
+  u32x4 ra[U];
+#pragma unroll
+  for (int f = 0; f < U; ++f) ra[f] = __builtin_nontemporal_load(wp(f / NKW, f % NKW));
+  u32x4 xb[NKW];
+  if constexpr (XS) {
+    xs_build(xr, a, xsw, xs_pitch, NKW * TILE_K, lane);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
+    __builtin_amdgcn_wave_barrier();
+    const u32x4* xp = reinterpret_cast<const u32x4*>(xsw + col * xs_pitch + (lane >> 4) * 8);
+    if constexpr (!XL) {
+#pragma unroll
+      for (int k = 0; k < NKW; ++k) xb[k] = xp[k * 4];
+    }
+  } else {
+    const u32x4* xp = reinterpret_cast<const u32x4*>(a.X + (size_t)col * a.ldx + (lane >> 4) * 8);
+#pragma unroll
+    for (int k = 0; k < NKW; ++k) xb[k] = xp[(kb + k) * 4];
+  }
+
+  constexpr int LU = (EPI == EPI_SWIGLU) ? 32 : 64;
+  auto finish = [&](int i) {  // after the barrier of tile i: wave 0 sums the KS partials, epilogue
+    if (w != 0) return;
+    const int tile = blockIdx.x + i * G;
+    f32x4 (*rb)[64] = red[i & 1];
+    const int l = lane;
+    if constexpr (EPI == EPI_RESID) {
+      f32x4 s = rb[0][l];
+#pragma unroll
+      for (int ww = 1; ww < KS; ++ww) s += rb[ww][l];
+      double q = 0.0;
+      if (col_raw < a.M) {
+        f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col_raw * a.ldo + tile * 16 + (l >> 4) * 4);
+        const f32x4 xv = *px + s;
+        *px = xv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q += (double)(xv[j] * xv[j]);
+      }
+      if (a.ssq) {
+        q += __shfl_xor(q, 16);
+        q += __shfl_xor(q, 32);
+        if (l < 16 && col_raw < a.M) a.ssq[(size_t)col_raw * a.np + tile] = (float)q;
+      }
+    } else {
+      if (l >= LU || col_raw >= a.M) return;
+      // partial unroll: fully unrolled, hipcc hoists all 2*KS LDS reads and spills the ring / B
+      // registers around the epilogue (the reloads then wait for the whole ring)
+      f32x4 s = rb[0][l];
+      f32x4 up = (EPI == EPI_SWIGLU) ? rb[0][l + 32] : s;
+#pragma unroll 3
+      for (int ww = 1; ww < KS; ++ww) {
+        s += rb[ww][l];
+        if constexpr (EPI == EPI_SWIGLU) up += rb[ww][l + 32];
+      }
+      epi_store<EPI>(a, tile, l, col_raw, s, up);
+    }
+  };
+  auto publish = [&](int i, f32x4 acc) {
+    red[i & 1][w][lane] = acc;
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only: the ring stays in flight
+    __builtin_amdgcn_s_barrier();
+    finish(i);
+  };
+
+  // fully unrolled over the TPW tiles: a loop back-edge makes hipcc rename the ring registers
+  // with moves that wait for the loads (vmcnt(0) at the loop header), draining the ring
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < NKW; ++k) {
+      const int f = i * NKW + k;  // flat ring position (compile-time after unrolling)
+      u32x4 bk;
+      if constexpr (XL) bk = reinterpret_cast<const u32x4*>(xsw + col * xs_pitch + (lane >> 4) * 8)[k * 4];
+      else bk = xb[k];
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ra[f % U]),
+                                                    __builtin_bit_cast(bf16x8, bk), acc, 0, 0, 0);
+      if ((f + U) / NKW < TPW) ra[f % U] = __builtin_nontemporal_load(wp((f + U) / NKW, (f + U) % NKW));
+    }
+    publish(i, acc);
+  }
+}
+
+// grid = N / (16 * TPW) work-groups (every one walks exactly TPW tiles)
+template <int KS, int NKW, int TPW, int EPI, int U, bool XL = false>
+static int launch_pers_cfg(const MMArgs& a, hipStream_t s) {
+  const int ntiles = a.N / TILE_N;
+  if (ntiles % TPW || a.K != KS * NKW * TILE_K) return -1;
+  const int grid = ntiles / TPW;
+  if (a.X == nullptr) {
+    if (a.M > XS_MAX_M || !a.xf || !a.norm_w || !a.ssq || a.np * 16 != a.K || a.np > 512 || NKW * TILE_K > 512)
+      return -1;
+    const size_t lds = (size_t)KS * XS_MAX_M * (NKW * TILE_K + 8) * 2;
+    if constexpr (XL) {  // one row (XsRegs for one column: fits 64 VGPRs)
+      if (a.M != 1) return -1;
+      mm_pers_kernel<KS, NKW, TPW, EPI, U, true, true, 8, 1><<<grid, 64 * KS, lds, s>>>(a);
+    } else {
+      mm_pers_kernel<KS, NKW, TPW, EPI, U, true><<<grid, 64 * KS, lds, s>>>(a);
+    }
+  } else {
+    mm_pers_kernel<KS, NKW, TPW, EPI, U, false><<<grid, 64 * KS, 0, s>>>(a);
+  }
+  return 0;
+}
+
+// Row-tile-persistent gate/up for <= 16 tokens; -1 when the shape has no instantiation (callers
+// fall back to launch_mm).  Llama-3-8B (K 4096, 1792 tiles = 256 x 7) and Llama-3-70B (K 8192,
+// 3584 tiles = 256 x 14) are instantiated: one work-group per CU.
+static const bool pers_resid = getenv("MX_NO_PERS_RESID") == nullptr;  // attn_output / ffn_down too
+
+bool mm_pers_supported(int epi, int M, int N, int K) {
+  if (M < 1 || M > 16) return false;
+  if (epi == EPI_SWIGLU) return (K == 4096 && N == 1792 * TILE_N) || (K == 8192 && N == 3584 * TILE_N);
+  if (epi == EPI_RESID && pers_resid) return N == 4096 && (K == 4096 || K == 14336);
+  return false;
+}
+
+int launch_mm_pers(int epi, const MMArgs& a, hipStream_t s) {
+  if (!mm_pers_supported(epi, a.M, a.N, a.K)) return -1;
+  static const int uenv = getenv("MX_PERS_U") ? atoi(getenv("MX_PERS_U")) : 8;
+  const int ntiles = a.N / TILE_N;
+  static const int tenv = getenv("MX_PERS_TPW") ? atoi(getenv("MX_PERS_TPW")) : 0;
+  if (a.K == 4096 && ntiles == 1792 && a.X == nullptr && tenv) {  // A/B: 2 work-groups per CU
+    if (tenv == 4) return launch_pers_cfg<16, 8, 4, EPI_SWIGLU, 4, true>(a, s);
+    if (tenv == 2) return launch_pers_cfg<16, 8, 2, EPI_SWIGLU, 4, true>(a, s);
+    if (tenv == 7) return launch_pers_cfg<16, 8, 7, EPI_SWIGLU, 4, true>(a, s);
+    if (tenv == 1) return launch_pers_cfg<16, 8, 1, EPI_SWIGLU, 4, true>(a, s);
+  }
+  if (a.K == 4096 && ntiles == 1792)
+    return uenv == 4    ? launch_pers_cfg<16, 8, 7, EPI_SWIGLU, 4>(a, s)
+           : uenv == 16 ? launch_pers_cfg<16, 8, 7, EPI_SWIGLU, 16>(a, s)
+                        : launch_pers_cfg<16, 8, 7, EPI_SWIGLU, 8>(a, s);
+  if (a.K == 8192 && ntiles == 3584) return launch_pers_cfg<16, 16, 14, EPI_SWIGLU, 4>(a, s);
+  if (epi == EPI_RESID && a.K == 4096) return launch_pers_cfg<16, 8, 1, EPI_RESID, 8>(a, s);
+  if (epi == EPI_RESID && a.K == 14336) return launch_pers_cfg<16, 28, 1, EPI_RESID, 14>(a, s);
+  return -1;
 }
 
 // Work-group geometry per (epilogue, token-column tiles), from tools/gemv_sweep.hip on MI355X
@@ -974,6 +1153,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t sc_rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7ffffff0, 0x00020000);
 }
 
+#ifndef ATTN_PREFETCH
+// 1: the first K/V chunk is issued right behind q (one round trip instead of two) -- measured
+// SLOWER at batch 1 (2.772 -> 2.810 ms/token, interleaved A/B tools/gpu/ab_b1q.sh), so off
+#define ATTN_PREFETCH 0
+#endif
 // One (kv head, row) of decode attention, by the NW waves of the calling work-group.  PUB: the
 // output is stored with sc1 stores for consumers in other work-groups of the same launch.
 template <int D, int G, int NW, bool PUB>
@@ -1033,20 +1217,40 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
   f16x8 qa[QK];
   const float* qrow = fin ? qs + (r16 < G ? r16 : 0) * D
                           : a.q + (size_t)c * a.n_head * D + (size_t)(kvh * G + (r16 < G ? r16 : 0)) * D;
+  f32x4 qv[QK][2];
 #pragma unroll
   for (int kk = 0; kk < QK; ++kk) {
-    f32x4 v0 = *reinterpret_cast<const f32x4*>(qrow + kk * 32 + 8 * q4);
-    f32x4 v1 = *reinterpret_cast<const f32x4*>(qrow + kk * 32 + 8 * q4 + 4);
-    const bool live = r16 < G;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      qa[kk][j] = live ? (_Float16)v0[j] : (_Float16)0.f;
-      qa[kk][4 + j] = live ? (_Float16)v1[j] : (_Float16)0.f;
-    }
+    qv[kk][0] = *reinterpret_cast<const f32x4*>(qrow + kk * 32 + 8 * q4);
+    qv[kk][1] = *reinterpret_cast<const f32x4*>(qrow + kk * 32 + 8 * q4 + 4);
   }
 
   const _Float16* Kb = a.kc + (size_t)slot * a.slot_stride + (size_t)kvh * a.ctx_stride * D;
   const _Float16* Vb = a.vc + (size_t)slot * a.slot_stride + (size_t)kvh * D * a.ctx_stride;
+  // this wave's first K/V chunk is issued right behind q (not after q's f16 conversion, which waits
+  // for q): one memory round trip instead of two (rows of a step are distinct sequences or, in
+  // prefill, their K/V was stored by an earlier launch; the wide path's own position comes from LDS)
+  f16x8 kf0[2][QK], vf0[DT];
+  const bool pre = ATTN_PREFETCH && !fin && w * CH < ctx;
+  if (pre) {
+    const int p0 = w * CH, pb = p0 + 8 * q4;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int kk = 0; kk < QK; ++kk)
+        kf0[t][kk] = *reinterpret_cast<const f16x8*>(Kb + (size_t)(p0 + 16 * t + r16) * D + 8 * q4 + kk * 32);
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+      vf0[t] = *reinterpret_cast<const f16x8*>(Vb + (size_t)(t * 16 + r16) * a.ctx_stride + pb);
+  }
+#pragma unroll
+  for (int kk = 0; kk < QK; ++kk) {
+    const bool live = r16 < G;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      qa[kk][j] = live ? (_Float16)qv[kk][0][j] : (_Float16)0.f;
+      qa[kk][4 + j] = live ? (_Float16)qv[kk][1][j] : (_Float16)0.f;
+    }
+  }
 
   float m_i[4], l_i[4];
 #pragma unroll
@@ -1062,15 +1266,24 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
     const int p0 = ch * CH;
     // issue this chunk's K and V fragment loads together: one memory round trip per chunk
     f16x8 kf[2][QK], vf[DT];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int kk = 0; kk < QK; ++kk)
-        kf[t][kk] = *reinterpret_cast<const f16x8*>(Kb + (size_t)(p0 + 16 * t + r16) * D + 8 * q4 + kk * 32);
     const int pb = p0 + 8 * q4;  // first position of this lane's P.V B fragment
+    if (pre && ch == w) {
 #pragma unroll
-    for (int t = 0; t < DT; ++t)
-      vf[t] = *reinterpret_cast<const f16x8*>(Vb + (size_t)(t * 16 + r16) * a.ctx_stride + pb);
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int kk = 0; kk < QK; ++kk) kf[t][kk] = kf0[t][kk];
+#pragma unroll
+      for (int t = 0; t < DT; ++t) vf[t] = vf0[t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int kk = 0; kk < QK; ++kk)
+          kf[t][kk] = *reinterpret_cast<const f16x8*>(Kb + (size_t)(p0 + 16 * t + r16) * D + 8 * q4 + kk * 32);
+#pragma unroll
+      for (int t = 0; t < DT; ++t)
+        vf[t] = *reinterpret_cast<const f16x8*>(Vb + (size_t)(t * 16 + r16) * a.ctx_stride + pb);
+    }
     if (fin) {  // this position's K/V: the values just finished in LDS (the cache lines may be in flight)
 #pragma unroll
       for (int t = 0; t < 2; ++t)

@@ -89,6 +89,9 @@ SHAPES = {
     "test-h4096": LlamaShape("test-h4096", 4096, 1, 32, 8, 2048, 1024, 500000.0, 1e-5),
     # Llama-3-70B hidden geometry (h 8192, 64 q / 8 kv heads: GQA group 8), one layer
     "test-h8192": LlamaShape("test-h8192", 8192, 1, 64, 8, 2048, 1024, 500000.0, 1e-5),
+    # full Llama-3-8B / -70B FFN width (the row-tile-persistent gate/up instantiations), small vocab
+    "test-8b-ffn": LlamaShape("test-8b-ffn", 4096, 2, 32, 8, 14336, 1024, 500000.0, 1e-5),
+    "test-70b-ffn": LlamaShape("test-70b-ffn", 8192, 1, 64, 8, 28672, 1024, 500000.0, 1e-5),
 }
 
 _M64 = (1 << 64) - 1

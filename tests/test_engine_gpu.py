@@ -430,3 +430,43 @@ def test_fused_ffn_norm_vs_oracle(mx, oracle_mod):
     g1 = eng.forward_logits(seqs[0][29:30], 29, slot=0)
     assert_logits_close(g1, om.context(64).eval(seqs[0][:30], 0)[-1:], "fused norm batch 1")
     eng.close()
+
+
+@pytest.mark.parametrize("name", ["test-8b-ffn", "test-70b-ffn"])
+def test_persistent_gate_up_vs_oracle(mx, oracle_mod, name):
+    """<= 4-row decode with gate/up as the row-tile-persistent GEMV (RMS_NORM on load, one
+    work-group per CU walking 7 / 14 tiles): at the full Llama-3-8B / -70B FFN width, 1 and 3
+    rows against the oracle, and against the same engine with MX_NO_PERS=1 (norm launch +
+    one-tile-per-work-group GEMV)."""
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES[name]
+    eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=64, n_seq_max=4)
+    os.environ["MX_NO_PERS"] = "1"
+    try:
+        base = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=64, n_seq_max=4)
+    finally:
+        del os.environ["MX_NO_PERS"]
+    om = oracle_mod.OracleModel(shape, seed=0)
+    seqs = [_seq(shape, 12, seed=170 + i) for i in range(3)]
+    for e in (eng, base):
+        for i, sq in enumerate(seqs):
+            e.forward_rows([i] * 10, list(range(10)), sq[:10], want_logits=False)
+    ctxs = [om.context(64) for _ in seqs]
+    for i, sq in enumerate(seqs):
+        ctxs[i].eval(sq[:10], 0)
+    # 3 rows at position 10, then batch 1 at 11 (slot 0)
+    got3 = eng.forward_rows([0, 1, 2], [10] * 3, [int(sq[10]) for sq in seqs])
+    b3 = base.forward_rows([0, 1, 2], [10] * 3, [int(sq[10]) for sq in seqs])
+    ref3 = np.concatenate([ctxs[i].eval(sq[10:11], 10)[-1:] for i, sq in enumerate(seqs)])
+    assert_logits_close(got3, ref3, f"{name} 3 rows")
+    assert_logits_close(got3, b3, f"{name} 3 rows vs MX_NO_PERS")
+    g1 = eng.forward_logits(seqs[0][11:12], 11, slot=0)
+    b1 = base.forward_logits(seqs[0][11:12], 11, slot=0)
+    r1 = ctxs[0].eval(seqs[0][11:12], 11)[-1:]
+    assert_logits_close(g1, r1, f"{name} batch 1")
+    assert_logits_close(g1, b1, f"{name} batch 1 vs MX_NO_PERS")
+    print(f"{name}: max|d| vs oracle {np.abs(g1 - r1).max():.3g} (max|ref| {np.abs(r1).max():.3g}), "
+          f"vs MX_NO_PERS {np.abs(g1 - b1).max():.3g}")
+    eng.close()
+    base.close()
