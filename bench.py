@@ -148,6 +148,12 @@ def run_single(args):
         res["batch1"] = {"tok_s": round(1.0 / d1, 2), "ms_per_token": round(d1 * 1e3, 3),
                          "hbm_frac": round(b1_bytes / d1 / 1e9 / HBM_PEAK_GBS, 4),
                          "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / b1_bytes, 1)}
+        # its dominant kernel: gate/up with the ffn RMS_NORM on load (row-tile-persistent GEMV)
+        us1, wb1 = eng.profile_kernel(6, 1, iters=3)
+        kb1 = wb1 + shape.n_embd * 4 + shape.n_ff * 2
+        res["batch1"]["gate_up"] = {"kernel": "mm_pers_kernel<EPI_SWIGLU, norm on load>", "us_per_launch": round(us1, 2),
+                                    "bytes_per_launch": int(kb1), "achieved_gbs": round(kb1 / us1 / 1e3, 1),
+                                    "frac": round(kb1 / us1 / 1e3 / HBM_PEAK_GBS, 4)}
         b1.close()
     b.close()
     if args.prefill_prompts > 0:
@@ -217,6 +223,43 @@ def q8_bench(args):
     return out
 
 
+def tiny_bench(args):
+    """BASELINE.json config 2: TinyLlama-1.1B on one MI355X -- batch-1 greedy decode of 128 tokens
+    on a fixed prompt (BOS + 31 ids uniform in [3, 32000) from seed 1) and batched
+    prefill of 32 prompts x 128 tokens, against the HBM and MFMA rooflines."""
+    import numpy as np
+
+    from llama_p2p_amd import synth
+    from llama_p2p_amd.engine import Engine
+
+    name = "tinyllama-1.1b"
+    shape = synth.SHAPES[name]
+    eng = Engine(f"synthetic:{name}:seed=0", n_ctx=512, n_seq_max=32)
+    rng = np.random.default_rng(1)
+    prompt = [1] + [int(t) for t in rng.integers(3, shape.n_vocab, 31)]
+    n_gen = args.tiny_tokens
+    eng.forward_rows([0] * 31, list(range(31)), prompt[:31], want_logits=False)
+    b = eng.batch(slots=[0], pos=[31], ids=[prompt[31]], max_steps=n_gen + 4)
+    for _ in range(4):
+        b.step()
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(n_gen):
+        b.step()
+    eng.sync()
+    d1 = (time.perf_counter() - t0) / n_gen
+    b.close()
+    by = eng.info.weight_bytes + (36 + n_gen / 2) * shape.kv_bytes_per_pos() + shape.n_vocab * 4
+    out = {"model": f"{name} bf16 (synthetic weights, seed 0)",
+           "batch1": {"tok_s": round(1.0 / d1, 1), "ms_per_token": round(d1 * 1e3, 4), "tokens": n_gen,
+                      "hbm_frac": round(by / d1 / 1e9 / HBM_PEAK_GBS, 4),
+                      "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / by, 1)}}
+    if args.prefill_prompts > 0:
+        out["prefill"] = prefill_bench(eng, shape, args.prefill_prompts, args.prefill_len)
+    eng.close()
+    return out
+
+
 def prefill_bench(eng, shape, n_prompts: int, plen: int):
     """Batched prefill: n_prompts prompts of plen tokens (seed 3) pushed through the
     engine's GEMM path (chunks of up to PREFILL_ROWS = 4096 rows) with no lm_head (logits of prompt tokens are not needed), timed on the
@@ -259,6 +302,8 @@ def main():
     ap.add_argument("--prefill-prompts", type=int, default=32)
     ap.add_argument("--prefill-len", type=int, default=128)
     ap.add_argument("--q8-steps", type=int, default=32, help="Q8_0 decode steps (0: skip the Q8_0 section)")
+    ap.add_argument("--tiny-tokens", type=int, default=128,
+                    help="TinyLlama-1.1B batch-1 tokens (config 2; 0: skip the section)")
     ap.add_argument("--force-pipeline", action="store_true", help="run the torch.distributed pipeline path even at N=1")
     args = ap.parse_args()
 
@@ -296,6 +341,11 @@ def main():
             line["q8_0"] = q8_bench(args)
         except Exception as ex:  # report, never hide
             line["q8_0"] = {"error": repr(ex)}
+    if args.tiny_tokens > 0:
+        try:
+            line["tinyllama"] = tiny_bench(args)
+        except Exception as ex:  # report, never hide
+            line["tinyllama"] = {"error": repr(ex)}
     if not args.no_cpu_baseline:
         try:
             line["cpu_baseline"] = cpu_baseline(args.model)

@@ -66,6 +66,7 @@ const Shape kShapes[] = {
     {"test-h8192", 8192, 1, 64, 8, 2048, 1024, 500000.f, 1e-5f, 2048},
     {"test-8b-ffn", 4096, 2, 32, 8, 14336, 1024, 500000.f, 1e-5f, 2048},
     {"test-70b-ffn", 8192, 1, 64, 8, 28672, 1024, 500000.f, 1e-5f, 2048},
+    {"test-tiny-ffn", 2048, 1, 32, 4, 5632, 32000, 10000.f, 1e-5f, 2048},
 };
 
 // synth.py tensor ids
@@ -131,6 +132,9 @@ struct mx_engine {
   bool norm_on_load = getenv("MX_NO_NORM_ON_LOAD") == nullptr;
   // gate/up as a row-tile-persistent GEMV with RMS_NORM on load (<= 4 rows); MX_NO_PERS=1 for A/B
   bool use_pers = getenv("MX_NO_PERS") == nullptr;
+  // one-token qkv as split-K slabs finished by the attention kernel (opt-in, MX_QKV_SPLIT=1): qkv
+  // 11.0 -> 10.2 us but attention +1.05 us (the finish), net neutral at batch 1 (tools/gpu/qkv_split.sh)
+  bool use_qkv_split = getenv("MX_QKV_SPLIT") != nullptr;
   float* ssq = nullptr;  // [MAX_ROWS][n_embd/16] per-tile sums of squares of x
   // rows of the next forward belong to distinct sequences (decode): no row attends to another row's
   // new K/V, so the wide path lets the attention kernel finish q/k/v from the split-K slabs
@@ -720,8 +724,14 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
     a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
     a.slot_stride = slot_stride;
-    if (launch_mm(EPI_QKV, a, s)) return fail(MX_ERR_ARG, "qkv launch shape");
+    // one token: qkv as two split-K halves (balanced over the CUs), finished inside attention
+    const int qsplit = (use_qkv_split && nol && rows_distinct && !use_attn_o) ? launch_qkv_split(a, slabs, slab_stride, s) : -1;
+    if (qsplit < 0 && launch_mm(EPI_QKV, a, s)) return fail(MX_ERR_ARG, "qkv launch shape");
     AttnArgs at{};
+    if (qsplit > 0) {
+      at.slabs = slabs; at.nslab = qsplit; at.slab_stride = slab_stride; at.rope_cs = rope_cs; at.kc_w = kc;
+      at.vc_w = vc;
+    }
     at.q = q; at.kc = kc; at.vc = vc; at.pos = pos; at.slot = slot;
     at.out = attn_out; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
     at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;
@@ -773,13 +783,16 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
     MMArgs g{};
     g.W = output; g.N = n_vocab; g.K = h; g.M = n_out; g.out = logits; g.ldo = n_vocab;
+    // lm_head as a row-tile-persistent GEMV with the output RMS_NORM on load (no norm launch)
+    const bool pers_head = use_pers && nol && !rowmap && n_out == M && mm_pers_supported(EPI_F32, M, n_vocab, h);
     if (!rowmap && n_out == M) {
-      norm_operand(g, out_norm, false);
+      norm_operand(g, out_norm, pers_head);
     } else {
       launch_rmsnorm(xn, h, x, out_norm, rowmap, n_out, h, eps, s);
       g.X = xn; g.ldx = h;
     }
-    if (launch_mm(EPI_F32, g, s)) return fail(MX_ERR_ARG, "lm_head launch shape");
+    if ((pers_head ? launch_mm_pers(EPI_F32, g, s) : -1) != 0 && launch_mm(EPI_F32, g, s))
+      return fail(MX_ERR_ARG, "lm_head launch shape");
     if (argmax)
       launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, ids_next, pos_next, hist, hist_stride,
                     hist_count, max_hist, s);
@@ -1740,7 +1753,8 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
         a.ssq = e->ssq; a.np = h / 16;
         a.act = e->act; a.lda = ff;
         per = (size_t)2 * ff * h * 2;
-        return launch_mm(EPI_SWIGLU, a, s);
+        return (e->use_pers && mm_pers_supported(EPI_SWIGLU, M, a.N, a.K)) ? launch_mm_pers(EPI_SWIGLU, a, s)
+                                                                            : launch_mm(EPI_SWIGLU, a, s);
       case 7: {  // attention at the positions set below (ctx = pos + 1)
         AttnArgs at{};
         at.q = e->q; at.kc = e->kcache + e->layer_kv_stride * li; at.vc = e->vcache + e->layer_kv_stride * li;

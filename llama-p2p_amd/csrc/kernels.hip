@@ -665,31 +665,43 @@ static int launch_mm_cfg(const MMArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------------------
 // XL (XS only): B fragments read from the LDS image at each MFMA instead of held in registers,
 // so the kernel fits 64 VGPRs and two 16-wave work-groups share a CU (WPE = waves per SIMD).
-template <int KS, int NKW, int TPW, int EPI, int U, bool XS, bool XL = false, int WPE = 4, int XM = XS_MAX_M>
+// KZ > 1 (EPI_SLAB): grid.y = KZ work-groups split K; partial tile sums go to slab blockIdx.y
+// (a.out + kz * a.slab_stride, [col][ldo]) for a consumer that adds them in slab order.
+template <int KS, int NKW, int TPW, int EPI, int U, bool XS, bool XL = false, int WPE = 4, int XM = XS_MAX_M,
+          int KZ = 1>
 __global__ __launch_bounds__(64 * KS, WPE) void mm_pers_kernel(MMArgs a) {
   static_assert(NKW % U == 0 || (U % NKW == 0 && U / NKW <= TPW), "ring depth vs per-wave K-slice");
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  constexpr int KT = KS * NKW;
-  const int kb = w * NKW;
+  constexpr int KT = KS * NKW * KZ;
+  const int kz = KZ > 1 ? (int)blockIdx.y : 0;
+  const int kb = kz * KS * NKW + w * NKW;
   const int G = gridDim.x;
 
   __shared__ f32x4 red[2][KS][64];
   extern __shared__ __attribute__((aligned(16))) uint16_t xs_dyn[];
 
-  const u32x4* Wb = reinterpret_cast<const u32x4*>(a.W) + lane;
-  auto wp = [&](int i, int k) { return Wb + ((size_t)(blockIdx.x + i * G) * KT + kb + k) * 64; };
+  // weights through a buffer resource sized to the matrix: the last tiles of a work-group may lie
+  // past the end when TPW does not divide the tile count -- those loads return zeros and fetch
+  // nothing, so every refill stays unconditional (no branch for hipcc's waitcnt merge)
+  const int ntiles = a.N / TILE_N;
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.W), (short)0, (int)((size_t)ntiles * KT * 1024), 0x00020000);
+  auto wld = [&](int i, int k) -> u32x4 {
+    const unsigned off = ((unsigned)(blockIdx.x + i * G) * KT + kb + k) * 1024u + lane * 16u;
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, off, 0, 2 /* nt */));
+  };
 
   const int col_raw = lane & 15;
   const int col = col_raw < a.M ? col_raw : a.M - 1;
   constexpr int xs_pitch = NKW * TILE_K + 8;
-  uint16_t* xsw = xs_dyn + (size_t)w * XS_MAX_M * xs_pitch;
+  uint16_t* xsw = xs_dyn + (size_t)w * XM * xs_pitch;
 
   XsRegs<XM> xr;
-  if constexpr (XS) xs_load(xr, a, kb * TILE_K, NKW * TILE_K, lane);
+  if constexpr (XS) xs_load(xr, a, kb * TILE_K, NKW * TILE_K, lane);  // scale from all K/16 partials
   u32x4 ra[U];
 #pragma unroll
-  for (int f = 0; f < U; ++f) ra[f] = __builtin_nontemporal_load(wp(f / NKW, f % NKW));
+  for (int f = 0; f < U; ++f) ra[f] = wld(f / NKW, f % NKW);
   u32x4 xb[NKW];
   if constexpr (XS) {
     xs_build(xr, a, xsw, xs_pitch, NKW * TILE_K, lane);
@@ -708,8 +720,8 @@ __global__ __launch_bounds__(64 * KS, WPE) void mm_pers_kernel(MMArgs a) {
 
   constexpr int LU = (EPI == EPI_SWIGLU) ? 32 : 64;
   auto finish = [&](int i) {  // after the barrier of tile i: wave 0 sums the KS partials, epilogue
-    if (w != 0) return;
     const int tile = blockIdx.x + i * G;
+    if (w != 0 || tile >= ntiles) return;
     f32x4 (*rb)[64] = red[i & 1];
     const int l = lane;
     if constexpr (EPI == EPI_RESID) {
@@ -729,6 +741,12 @@ __global__ __launch_bounds__(64 * KS, WPE) void mm_pers_kernel(MMArgs a) {
         q += __shfl_xor(q, 32);
         if (l < 16 && col_raw < a.M) a.ssq[(size_t)col_raw * a.np + tile] = (float)q;
       }
+    } else if constexpr (EPI == EPI_SLAB) {
+      if (col_raw >= a.M) return;
+      f32x4 s = rb[0][l];
+#pragma unroll 3
+      for (int ww = 1; ww < KS; ++ww) s += rb[ww][l];
+      *reinterpret_cast<f32x4*>(a.out + kz * a.slab_stride + (size_t)col_raw * a.ldo + tile * 16 + (l >> 4) * 4) = s;
     } else {
       if (l >= LU || col_raw >= a.M) return;
       // partial unroll: fully unrolled, hipcc hoists all 2*KS LDS reads and spills the ring / B
@@ -763,7 +781,7 @@ __global__ __launch_bounds__(64 * KS, WPE) void mm_pers_kernel(MMArgs a) {
       else bk = xb[k];
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ra[f % U]),
                                                     __builtin_bit_cast(bf16x8, bk), acc, 0, 0, 0);
-      if ((f + U) / NKW < TPW) ra[f % U] = __builtin_nontemporal_load(wp((f + U) / NKW, (f + U) % NKW));
+      if ((f + U) / NKW < TPW) ra[f % U] = wld((f + U) / NKW, (f + U) % NKW);
     }
     publish(i, acc);
   }
@@ -773,8 +791,8 @@ __global__ __launch_bounds__(64 * KS, WPE) void mm_pers_kernel(MMArgs a) {
 template <int KS, int NKW, int TPW, int EPI, int U, bool XL = false>
 static int launch_pers_cfg(const MMArgs& a, hipStream_t s) {
   const int ntiles = a.N / TILE_N;
-  if (ntiles % TPW || a.K != KS * NKW * TILE_K) return -1;
-  const int grid = ntiles / TPW;
+  if (a.K != KS * NKW * TILE_K || (size_t)ntiles * a.K * 32 >= (1ull << 31)) return -1;
+  const int grid = (ntiles + TPW - 1) / TPW;  // the last tiles of some work-groups are phantoms
   if (a.X == nullptr) {
     if (a.M > XS_MAX_M || !a.xf || !a.norm_w || !a.ssq || a.np * 16 != a.K || a.np > 512 || NKW * TILE_K > 512)
       return -1;
@@ -791,36 +809,62 @@ static int launch_pers_cfg(const MMArgs& a, hipStream_t s) {
   return 0;
 }
 
-// Row-tile-persistent gate/up for <= 16 tokens; -1 when the shape has no instantiation (callers
-// fall back to launch_mm).  Llama-3-8B (K 4096, 1792 tiles = 256 x 7) and Llama-3-70B (K 8192,
-// 3584 tiles = 256 x 14) are instantiated: one work-group per CU.
+// qkv of ONE token as KZ = 2 split-K halves with RMS_NORM on load: 2 x (h + 2 kv) / 16 work-groups
+// of 8 waves (Llama-3-8B: 768 = 3 per CU, 70B: 1280 = 5 per CU) instead of 384 / 640 whole tiles
+// (1.5 / 2.5 per CU: the CUs holding one more tile set the time).  Partial q/k/v go to slabs that
+// the attention kernel sums (slab order), ropes and stores into the KV cache (its `fin` path), so
+// the rows must be distinct sequences.  Returns the slab count, or -1 (nothing launched).
+int launch_qkv_split(const MMArgs& a0, float* slabs, size_t slab_stride, hipStream_t s) {
+  if (a0.M != 1 || a0.X != nullptr || !a0.xf || !a0.norm_w || !a0.ssq || a0.np * 16 != a0.K) return -1;
+  if (a0.N % TILE_N) return -1;
+  MMArgs a = a0;
+  a.out = slabs; a.ldo = a0.N; a.slab_stride = slab_stride;
+  const dim3 grid(a.N / TILE_N, 2);
+  if (a.K == 4096) {
+    const size_t lds = (size_t)8 * 1 * (8 * TILE_K + 8) * 2;
+    mm_pers_kernel<8, 8, 1, EPI_SLAB, 4, true, false, 6, 1, 2><<<grid, 512, lds, s>>>(a);
+    return 2;
+  }
+  if (a.K == 8192) {
+    const size_t lds = (size_t)8 * 1 * (16 * TILE_K + 8) * 2;
+    mm_pers_kernel<8, 16, 1, EPI_SLAB, 4, true, true, 6, 1, 2><<<grid, 512, lds, s>>>(a);
+    return 2;
+  }
+  return -1;
+}
+
+// Row-tile-persistent GEMVs for <= 16 tokens; -1 when the shape has no instantiation (callers
+// fall back to launch_mm).  gate/up: Llama-3-8B (K 4096, 1792 tiles = 256 x 7), -70B (K 8192,
+// 3584 = 256 x 14), TinyLlama (K 2048, 704 tiles = 235 groups x <= 3); attn_output / ffn_down of
+// h 4096 (one tile per group, whole K-slice in flight); lm_head (<= 32 / 8 tiles per group).
 static const bool pers_resid = getenv("MX_NO_PERS_RESID") == nullptr;  // attn_output / ffn_down too
+// lm_head with the output norm on load: correct but neutral at batch 1 (8B 2.804 vs 2.809 ms,
+// TinyLlama 0.750 vs 0.751; tools/gpu/pers_ab4.sh), so opt-in (MX_PERS_HEAD=1)
+static const bool pers_head = getenv("MX_PERS_HEAD") != nullptr;
 
 bool mm_pers_supported(int epi, int M, int N, int K) {
   if (M < 1 || M > 16) return false;
-  if (epi == EPI_SWIGLU) return (K == 4096 && N == 1792 * TILE_N) || (K == 8192 && N == 3584 * TILE_N);
+  const int nt = N / TILE_N;
+  if (epi == EPI_SWIGLU) return (K == 4096 && nt == 1792) || (K == 8192 && nt == 3584) || (K == 2048 && nt == 704);
   if (epi == EPI_RESID && pers_resid) return N == 4096 && (K == 4096 || K == 14336);
+  if (epi == EPI_F32 && pers_head) return (K == 4096 && nt <= 256 * 32) || (K == 2048 && nt <= 256 * 8);
   return false;
 }
 
 int launch_mm_pers(int epi, const MMArgs& a, hipStream_t s) {
   if (!mm_pers_supported(epi, a.M, a.N, a.K)) return -1;
-  static const int uenv = getenv("MX_PERS_U") ? atoi(getenv("MX_PERS_U")) : 8;
   const int ntiles = a.N / TILE_N;
-  static const int tenv = getenv("MX_PERS_TPW") ? atoi(getenv("MX_PERS_TPW")) : 0;
-  if (a.K == 4096 && ntiles == 1792 && a.X == nullptr && tenv) {  // A/B: 2 work-groups per CU
-    if (tenv == 4) return launch_pers_cfg<16, 8, 4, EPI_SWIGLU, 4, true>(a, s);
-    if (tenv == 2) return launch_pers_cfg<16, 8, 2, EPI_SWIGLU, 4, true>(a, s);
-    if (tenv == 7) return launch_pers_cfg<16, 8, 7, EPI_SWIGLU, 4, true>(a, s);
-    if (tenv == 1) return launch_pers_cfg<16, 8, 1, EPI_SWIGLU, 4, true>(a, s);
+  if (epi == EPI_SWIGLU) {
+    if (a.K == 4096 && ntiles == 1792) return launch_pers_cfg<16, 8, 7, EPI_SWIGLU, 8>(a, s);
+    if (a.K == 8192 && ntiles == 3584) return launch_pers_cfg<16, 16, 14, EPI_SWIGLU, 4>(a, s);
+    if (a.K == 2048 && ntiles == 704) return launch_pers_cfg<16, 4, 3, EPI_SWIGLU, 4>(a, s);
+  } else if (epi == EPI_RESID) {
+    if (a.K == 4096) return launch_pers_cfg<16, 8, 1, EPI_RESID, 8>(a, s);
+    if (a.K == 14336) return launch_pers_cfg<16, 28, 1, EPI_RESID, 14>(a, s);
+  } else if (epi == EPI_F32) {
+    if (a.K == 4096) return launch_pers_cfg<16, 8, 32, EPI_F32, 8>(a, s);  // 8B: 251 groups
+    if (a.K == 2048) return launch_pers_cfg<16, 4, 8, EPI_F32, 4>(a, s);   // TinyLlama: 250 groups
   }
-  if (a.K == 4096 && ntiles == 1792)
-    return uenv == 4    ? launch_pers_cfg<16, 8, 7, EPI_SWIGLU, 4>(a, s)
-           : uenv == 16 ? launch_pers_cfg<16, 8, 7, EPI_SWIGLU, 16>(a, s)
-                        : launch_pers_cfg<16, 8, 7, EPI_SWIGLU, 8>(a, s);
-  if (a.K == 8192 && ntiles == 3584) return launch_pers_cfg<16, 16, 14, EPI_SWIGLU, 4>(a, s);
-  if (epi == EPI_RESID && a.K == 4096) return launch_pers_cfg<16, 8, 1, EPI_RESID, 8>(a, s);
-  if (epi == EPI_RESID && a.K == 14336) return launch_pers_cfg<16, 28, 1, EPI_RESID, 14>(a, s);
   return -1;
 }
 

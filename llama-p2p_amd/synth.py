@@ -92,6 +92,8 @@ SHAPES = {
     # full Llama-3-8B / -70B FFN width (the row-tile-persistent gate/up instantiations), small vocab
     "test-8b-ffn": LlamaShape("test-8b-ffn", 4096, 2, 32, 8, 14336, 1024, 500000.0, 1e-5),
     "test-70b-ffn": LlamaShape("test-70b-ffn", 8192, 1, 64, 8, 28672, 1024, 500000.0, 1e-5),
+    # TinyLlama-1.1B hidden/FFN/vocab geometry, one layer (gate/up 704 tiles: 235 groups x <= 3)
+    "test-tiny-ffn": LlamaShape("test-tiny-ffn", 2048, 1, 32, 4, 5632, 32000, 10000.0, 1e-5),
 }
 
 _M64 = (1 << 64) - 1

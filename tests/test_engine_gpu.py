@@ -432,12 +432,12 @@ def test_fused_ffn_norm_vs_oracle(mx, oracle_mod):
     eng.close()
 
 
-@pytest.mark.parametrize("name", ["test-8b-ffn", "test-70b-ffn"])
+@pytest.mark.parametrize("name", ["test-8b-ffn", "test-70b-ffn", "test-tiny-ffn"])
 def test_persistent_gate_up_vs_oracle(mx, oracle_mod, name):
-    """<= 4-row decode with gate/up as the row-tile-persistent GEMV (RMS_NORM on load, one
-    work-group per CU walking 7 / 14 tiles): at the full Llama-3-8B / -70B FFN width, 1 and 3
-    rows against the oracle, and against the same engine with MX_NO_PERS=1 (norm launch +
-    one-tile-per-work-group GEMV)."""
+    """<= 4-row decode with gate/up (and lm_head) as row-tile-persistent GEMVs with RMS_NORM on
+    load: at the full Llama-3-8B / -70B / TinyLlama FFN width (7 / 14 / <= 3 tiles per work-group,
+    TinyLlama's last group holding a phantom tile past the matrix end), 1 and 3 rows against the
+    oracle, and against the same engine with MX_NO_PERS=1 (norm launches + one tile per group)."""
     from llama_p2p_amd import synth
 
     shape = synth.SHAPES[name]
