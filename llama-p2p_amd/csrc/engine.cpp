@@ -176,6 +176,8 @@ struct mx_engine {
   // writes back its L2 lines; the serial tail outlasts the launch it replaces); nrm_cnt: its counter
   bool fuse_norm = getenv("MX_FUSED_NORM") != nullptr;
   unsigned* nrm_cnt = nullptr;
+  float* kz_part = nullptr;    // split-K persistent RESID GEMVs: partial tiles [512][2][64] f32x4
+  unsigned* kz_cnt = nullptr;  // and their zeroed per-tile arrival counters [512]
   uint8_t* tok_embd8 = nullptr;
   int8_t* xq8 = nullptr;    // Q8_0 activation rows [PREFILL_ROWS][max(h, ff)]
   float* xqd = nullptr;     // their block scales
@@ -335,6 +337,9 @@ int mx_engine::init_common() {
   if (int rc = alloc((void**)&d_rowmap, (size_t)R * 4)) return rc;
   if (int rc = alloc((void**)&nrm_cnt, 64 * 4)) return rc;
   HIPC(hipMemsetAsync(nrm_cnt, 0, 64 * 4, stream));
+  if (int rc = alloc((void**)&kz_part, (size_t)512 * 2 * 64 * 16)) return rc;
+  if (int rc = alloc((void**)&kz_cnt, 512 * 4)) return rc;
+  HIPC(hipMemsetAsync(kz_cnt, 0, 512 * 4, stream));
   if (int rc = alloc((void**)&ao_sync, 640 * 4)) return rc;
   HIPC(hipMemsetAsync(ao_sync, 0, 640 * 4, stream));
   if (wq8) {
@@ -746,6 +751,9 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     if (use_pers && nol && mm_pers_supported(EPI_SWIGLU, M, 2 * ff, h)) {  // partials for gate/up's norm on load
       b.ssq = ssq; b.np = h / 16;
     }
+    if (h / 16 <= 512) {
+      b.kz_part = kz_part; b.kz_cnt = kz_cnt;
+    }
     const bool fused_ao = use_attn_o && attn_o_supported(at, b);
     if (fuse_norm && !fused_ao) {  // the ffn RMS_NORM by attn_output's last work-group (M <= 16 here)
       b.ssq = ssq; b.np = h / 16; b.eps = eps; b.nxt_y = xn; b.nxt_w = L.ffn_norm; b.nxt_cnt = nrm_cnt;
@@ -772,6 +780,9 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     MMArgs d{};
     d.W = L.down; d.N = h; d.K = ff; d.X = act; d.ldx = ff; d.M = M; d.out = x; d.ldo = h;
     d.ssq = nol ? ssq : nullptr; d.np = h / 16;
+    if (h / 16 <= 512) {
+      d.kz_part = kz_part; d.kz_cnt = kz_cnt;
+    }
     if ((mm_pers_supported(EPI_RESID, M, h, ff) ? launch_mm_pers(EPI_RESID, d, s) : -1) != 0 &&
         launch_mm(EPI_RESID, d, s))
       return fail(MX_ERR_ARG, "ffn_down launch shape");

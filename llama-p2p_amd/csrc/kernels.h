@@ -72,6 +72,10 @@ struct MMArgs {
   uint16_t* nxt_y;
   const float* nxt_w;
   unsigned* nxt_cnt;
+  // row-tile-persistent EPI_RESID split over K by 2 work-groups (mm_pers_kernel KZ = 2): partial
+  // tiles [N/16][2][64] f32x4 and zeroed per-tile arrival counters [N/16] (the 2nd arriver folds)
+  float* kz_part;
+  unsigned* kz_cnt;
 };
 
 struct AttnArgs {

@@ -728,6 +728,22 @@ __global__ __launch_bounds__(64 * KS, WPE) void mm_pers_kernel(MMArgs a) {
       f32x4 s = rb[0][l];
 #pragma unroll
       for (int ww = 1; ww < KS; ++ww) s += rb[ww][l];
+      if constexpr (KZ > 1) {
+        // in-launch split-K fold (cdna_hip_programming.md "In-launch split-K reduction"): publish
+        // this half, count in; the second arriver adds both halves in kz order (deterministic)
+        f32x4* part = reinterpret_cast<f32x4*>(a.kz_part) + (size_t)tile * KZ * 64;
+        part[kz * 64 + l] = s;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        unsigned old = 0;
+        if (l == 0) old = __hip_atomic_fetch_add(a.kz_cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        old = __shfl(old, 0);
+        if (old != KZ - 1) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (l == 0) __hip_atomic_store(a.kz_cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s = part[l];
+#pragma unroll
+        for (int z = 1; z < KZ; ++z) s += part[z * 64 + l];
+      }
       double q = 0.0;
       if (col_raw < a.M) {
         f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col_raw * a.ldo + tile * 16 + (l >> 4) * 4);
@@ -788,11 +804,18 @@ __global__ __launch_bounds__(64 * KS, WPE) void mm_pers_kernel(MMArgs a) {
 }
 
 // grid = N / (16 * TPW) work-groups (every one walks exactly TPW tiles)
-template <int KS, int NKW, int TPW, int EPI, int U, bool XL = false>
+template <int KS, int NKW, int TPW, int EPI, int U, bool XL = false, int KZ = 1>
 static int launch_pers_cfg(const MMArgs& a, hipStream_t s) {
   const int ntiles = a.N / TILE_N;
-  if (a.K != KS * NKW * TILE_K || (size_t)ntiles * a.K * 32 >= (1ull << 31)) return -1;
-  const int grid = (ntiles + TPW - 1) / TPW;  // the last tiles of some work-groups are phantoms
+  if (a.K != KS * NKW * TILE_K * KZ || (size_t)ntiles * a.K * 32 >= (1ull << 31)) return -1;
+  const int gx = (ntiles + TPW - 1) / TPW;  // the last tiles of some work-groups are phantoms
+  if constexpr (KZ > 1) {
+    static_assert(EPI == EPI_RESID, "split-K persistent GEMV: residual epilogue only");
+    if (a.X == nullptr) return -1;
+    mm_pers_kernel<KS, NKW, TPW, EPI, U, false, false, 4, XS_MAX_M, KZ><<<dim3(gx, KZ), 64 * KS, 0, s>>>(a);
+    return 0;
+  }
+  const int grid = gx;
   if (a.X == nullptr) {
     if (a.M > XS_MAX_M || !a.xf || !a.norm_w || !a.ssq || a.np * 16 != a.K || a.np > 512 || NKW * TILE_K > 512)
       return -1;
@@ -841,12 +864,17 @@ static const bool pers_resid = getenv("MX_NO_PERS_RESID") == nullptr;  // attn_o
 // lm_head with the output norm on load: correct but neutral at batch 1 (8B 2.804 vs 2.809 ms,
 // TinyLlama 0.750 vs 0.751; tools/gpu/pers_ab4.sh), so opt-in (MX_PERS_HEAD=1)
 static const bool pers_head = getenv("MX_PERS_HEAD") != nullptr;
+// TinyLlama attn_output / ffn_down (128 tiles) split over K by 2 work-groups with the in-launch
+// fold: correct, but the release/acquire hand-off costs ~4.5 us per launch (batch-1 0.755 ->
+// 0.95 ms/token, tools/gpu/tiny_kz.sh), so opt-in (MX_PERS_KZ=1)
+static const bool pers_kz = getenv("MX_PERS_KZ") != nullptr;
 
 bool mm_pers_supported(int epi, int M, int N, int K) {
   if (M < 1 || M > 16) return false;
   const int nt = N / TILE_N;
   if (epi == EPI_SWIGLU) return (K == 4096 && nt == 1792) || (K == 8192 && nt == 3584) || (K == 2048 && nt == 704);
-  if (epi == EPI_RESID && pers_resid) return N == 4096 && (K == 4096 || K == 14336);
+  if (epi == EPI_RESID && pers_resid)
+    return (N == 4096 && (K == 4096 || K == 14336)) || (pers_kz && N == 2048 && (K == 2048 || K == 5632));
   if (epi == EPI_F32 && pers_head) return (K == 4096 && nt <= 256 * 32) || (K == 2048 && nt <= 256 * 8);
   return false;
 }
@@ -861,6 +889,10 @@ int launch_mm_pers(int epi, const MMArgs& a, hipStream_t s) {
   } else if (epi == EPI_RESID) {
     if (a.K == 4096) return launch_pers_cfg<16, 8, 1, EPI_RESID, 8>(a, s);
     if (a.K == 14336) return launch_pers_cfg<16, 28, 1, EPI_RESID, 14>(a, s);
+    if (a.N == 2048 && a.kz_part && a.kz_cnt) {  // TinyLlama: 128 tiles, K split over 2 groups -> 256
+      if (a.K == 2048) return launch_pers_cfg<16, 2, 1, EPI_RESID, 2, false, 2>(a, s);
+      if (a.K == 5632) return launch_pers_cfg<8, 11, 1, EPI_RESID, 11, false, 2>(a, s);
+    }
   } else if (epi == EPI_F32) {
     if (a.K == 4096) return launch_pers_cfg<16, 8, 32, EPI_F32, 8>(a, s);  // 8B: 251 groups
     if (a.K == 2048) return launch_pers_cfg<16, 4, 8, EPI_F32, 4>(a, s);   // TinyLlama: 250 groups
