@@ -260,6 +260,20 @@ def tiny_bench(args):
     return out
 
 
+def copy_peak(gib: int = 4, iters: int = 10):
+    """Measured HBM copy ceiling: the engine's streaming copy kernel (16 B per lane,
+    mx_probe_copy) over two gib-GiB buffers, (read + write) bytes / HIP-event time on its stream.
+    Reported next to the 8 TB/s spec that the roofline fractions use."""
+    from llama_p2p_amd import engine
+
+    gbs = engine.probe_copy(0, gib, iters)
+    rd = engine.probe_copy(0, gib, iters, read_only=True)
+    return {"gbs": round(gbs, 1), "frac_of_spec": round(gbs / HBM_PEAK_GBS, 4),
+            "read_gbs": round(rd, 1), "read_frac_of_spec": round(rd / HBM_PEAK_GBS, 4),
+            "method": f"mx_probe_copy / mx_probe_read: 16-B/lane streaming kernels, {gib} GiB x {iters}, "
+                      "(read + write) or read bytes / HIP-event time"}
+
+
 def prefill_bench(eng, shape, n_prompts: int, plen: int):
     """Batched prefill: n_prompts prompts of plen tokens (seed 3) pushed through the
     engine's GEMM path (chunks of up to PREFILL_ROWS = 4096 rows) with no lm_head (logits of prompt tokens are not needed), timed on the
@@ -305,7 +319,11 @@ def main():
     ap.add_argument("--tiny-tokens", type=int, default=128,
                     help="TinyLlama-1.1B batch-1 tokens (config 2; 0: skip the section)")
     ap.add_argument("--force-pipeline", action="store_true", help="run the torch.distributed pipeline path even at N=1")
+    ap.add_argument("--copy-peak-only", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.copy_peak_only:
+        print(json.dumps(copy_peak()), flush=True)
+        return
 
     # stdout carries exactly the one JSON line: native libraries that write to fd 1 (the RCCL
     # version banner at communicator init, HIP runtime notes) are sent to stderr, and Python's
@@ -321,6 +339,10 @@ def main():
         return pipeline.bench_main(args, METRIC, make_prompts)
 
     res = run_single(args)
+    try:
+        copy = copy_peak()
+    except Exception as ex:  # report, never hide
+        copy = {"error": repr(ex)}
     line = {
         "metric": METRIC, "value": round(res["tok_s"], 2), "unit": "tokens/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(res["ms_per_step"], 4),
@@ -346,6 +368,10 @@ def main():
             line["tinyllama"] = tiny_bench(args)
         except Exception as ex:  # report, never hide
             line["tinyllama"] = {"error": repr(ex)}
+    line["hbm_copy_peak"] = copy
+    if "gbs" in copy:
+        line["roofline"]["frac_of_copy_peak"] = round(line["roofline"]["achieved"] / copy["gbs"], 4)
+        line["roofline"]["frac_of_read_peak"] = round(line["roofline"]["achieved"] / copy["read_gbs"], 4)
     if not args.no_cpu_baseline:
         try:
             line["cpu_baseline"] = cpu_baseline(args.model)

@@ -141,6 +141,13 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us_per_l
 
 int mx_sync(mx_engine* e);
 
+/* Measured HBM copy ceiling on `device` (no engine): a 16-byte-per-lane streaming copy kernel over
+ * two `bytes`-sized buffers, `iters` passes timed with HIP events; *gbs = (read + write) bytes / s.
+ * Benchmark support (SURVEY.md §8d "also report a measured copy-kernel peak"), not a reference API. */
+int mx_probe_copy(int device, size_t bytes, int iters, double* gbs);
+/* Read-only variant (a GEMV's traffic is ~99.5 % reads): *gbs = bytes read / s. */
+int mx_probe_read(int device, size_t bytes, int iters, double* gbs);
+
 /* Request-path counters (mx_submit/mx_wait).  reused_prompt_tokens: prompt positions whose K/V were
  * kept from the slot's previous request (longest common prefix, as llama-cpp-python's generate). */
 typedef struct {

@@ -1677,6 +1677,57 @@ int mx_sync(mx_engine* e) {
   return e->check_pdk();
 }
 
+static int probe_hbm(int device, size_t bytes, int iters, bool read_only, double* gbs);
+
+int mx_probe_copy(int device, size_t bytes, int iters, double* gbs) { return probe_hbm(device, bytes, iters, false, gbs); }
+
+int mx_probe_read(int device, size_t bytes, int iters, double* gbs) { return probe_hbm(device, bytes, iters, true, gbs); }
+
+}  // extern "C"
+
+static int probe_hbm(int device, size_t bytes, int iters, bool read_only, double* gbs) {
+  const size_t n16 = bytes / 16 / 1024 * 1024;  // whole 1024-word chunks (the kernel's unit)
+  if (n16 == 0 || iters < 1 || !gbs) return fail(MX_ERR_ARG, "bad arguments");
+  HIPC(hipSetDevice(device));
+  uint4 *src = nullptr, *dst = nullptr;
+  HIPC(hipMalloc(&src, n16 * 16));
+  if (hipMalloc(&dst, n16 * 16) != hipSuccess) {
+    hipFree(src);
+    return fail(MX_ERR_HIP, "copy probe: out of device memory");
+  }
+  hipStream_t s;
+  hipEvent_t t0, t1;
+  hipError_t err = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  if (err == hipSuccess) err = hipEventCreate(&t0);
+  if (err == hipSuccess) err = hipEventCreate(&t1);
+  float ms = 0.f;
+  if (err == hipSuccess) {
+    hipMemsetAsync(src, 1, n16 * 16, s);
+    auto run = [&] {
+      if (read_only)
+        mx::launch_read_probe(src, dst, n16, s);  // dst: sink, written only on a sentinel fold
+      else
+        mx::launch_copy_probe(src, dst, n16, s);
+    };
+    for (int i = 0; i < 2; i++) run();  // warm
+    hipEventRecord(t0, s);
+    for (int i = 0; i < iters; i++) run();
+    hipEventRecord(t1, s);
+    err = hipEventSynchronize(t1);
+    if (err == hipSuccess) err = hipEventElapsedTime(&ms, t0, t1);
+    hipEventDestroy(t0);
+    hipEventDestroy(t1);
+    hipStreamDestroy(s);
+  }
+  hipFree(src);
+  hipFree(dst);
+  if (err != hipSuccess) return fail(MX_ERR_HIP, std::string("copy probe: ") + hipGetErrorString(err));
+  *gbs = (read_only ? 1.0 : 2.0) * (double)n16 * 16 * iters / (ms * 1e-3) / 1e9;
+  return MX_OK;
+}
+
+extern "C" {
+
 int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, double* bytes) {
   if (!e || M < 1 || M > MAX_ROWS || iters < 1) return fail(MX_ERR_ARG, "bad arguments");
   std::lock_guard<std::mutex> lk(e->gpu_mu);

@@ -219,4 +219,11 @@ void launch_argmax(const float* logits, int ldl, int M, int V, float* ws_val, in
                    int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count, int max_hist,
                    hipStream_t s);
 
+// HBM copy ceiling probe: dst = src over n16 16-byte words (n16 % 1024 == 0), 16 B per lane,
+// four independent loads in flight per lane, grid-stride over 8 work-groups per CU
+void launch_copy_probe(const uint4* src, uint4* dst, size_t n16, hipStream_t s);
+// read-only variant (the GEMVs' traffic is ~99.5 % reads): XOR-folds src, writes one word per lane
+// only when the fold hits a sentinel (never for the probe's fill)
+void launch_read_probe(const uint4* src, uint4* sink, size_t n16, hipStream_t s);
+
 }  // namespace mx

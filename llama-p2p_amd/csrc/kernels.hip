@@ -2801,3 +2801,45 @@ int launch_mq8(int epi, const MMArgs& a, hipStream_t s) {
 }
 
 }  // namespace mx
+
+namespace mx {
+
+// Copy-ceiling probe (bench.py hbm_copy_peak): the float4-copy measurement of
+// MI355X_MICROARCH.md, so the decode kernels' HBM fractions can be read against what a plain
+// streaming kernel reaches on the same box.  Each 256-lane group owns 1024 consecutive 16-B words
+// per pass (lane i moves words i, i+256, i+512, i+768: coalesced, four loads in flight).
+__global__ __launch_bounds__(256) void copy_probe_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                         size_t n16) {
+  const size_t stride = (size_t)gridDim.x * 1024;
+  for (size_t i = (size_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += stride) {
+    const uint4 a = src[i], b = src[i + 256], c = src[i + 512], d = src[i + 768];
+    dst[i] = a;
+    dst[i + 256] = b;
+    dst[i + 512] = c;
+    dst[i + 768] = d;
+  }
+}
+
+void launch_copy_probe(const uint4* src, uint4* dst, size_t n16, hipStream_t s) {
+  copy_probe_kernel<<<2048, 256, 0, s>>>(src, dst, n16);  // 256 CUs x 8 groups
+}
+
+__global__ __launch_bounds__(256) void read_probe_kernel(const uint4* __restrict__ src, uint4* __restrict__ sink,
+                                                         size_t n16) {
+  const size_t stride = (size_t)gridDim.x * 1024;
+  uint4 x = {0u, 0u, 0u, 0u};
+  for (size_t i = (size_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += stride) {
+    const uint4 a = src[i], b = src[i + 256], c = src[i + 512], d = src[i + 768];
+    x.x ^= a.x ^ b.x ^ c.x ^ d.x;
+    x.y ^= a.y ^ b.y ^ c.y ^ d.y;
+    x.z ^= a.z ^ b.z ^ c.z ^ d.z;
+    x.w ^= a.w ^ b.w ^ c.w ^ d.w;
+  }
+  if (x.x == 0x9e3779b9u && x.y == 0x7f4a7c15u) sink[(size_t)blockIdx.x * 256 + threadIdx.x] = x;
+}
+
+void launch_read_probe(const uint4* src, uint4* sink, size_t n16, hipStream_t s) {
+  read_probe_kernel<<<2048, 256, 0, s>>>(src, sink, n16);
+}
+
+}  // namespace mx

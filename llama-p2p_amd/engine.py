@@ -27,6 +27,7 @@ EXPORTS = [
     "mx_engine_info", "mx_forward_logits", "mx_forward_rows", "mx_submit", "mx_wait", "mx_batch_create",
     "mx_batch_step", "mx_batch_ids_device", "mx_batch_bind_ids", "mx_batch_tokens", "mx_batch_destroy", "mx_stage_rows",
     "mx_profile_kernel", "mx_sync", "mx_debug_pdk_trace", "mx_device_count", "mx_engine_stats",
+    "mx_probe_copy", "mx_probe_read",
 ]
 
 
@@ -94,6 +95,8 @@ def lib() -> ctypes.CDLL:
         L.mx_stage_rows.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp]
         L.mx_profile_kernel.argtypes = [vp, i32, i32, i32, P(ctypes.c_double), P(ctypes.c_double)]
         L.mx_sync.argtypes = [vp]
+        L.mx_probe_copy.argtypes = [i32, ctypes.c_size_t, i32, P(ctypes.c_double)]
+        L.mx_probe_read.argtypes = [i32, ctypes.c_size_t, i32, P(ctypes.c_double)]
         L.mx_debug_pdk_trace.argtypes = [vp, i32, i32, vp, i32, P(i32), P(i32)]
         L.mx_device_count.argtypes = [P(i32)]
         L.mx_engine_stats.argtypes = [vp, P(MxStats)]
@@ -114,6 +117,15 @@ def device_count() -> int:
     n = ctypes.c_int32()
     _check(lib().mx_device_count(ctypes.byref(n)))
     return n.value
+
+
+def probe_copy(device: int = 0, gib: int = 4, iters: int = 10, read_only: bool = False) -> float:
+    """Measured HBM ceiling in GB/s of a streaming copy kernel ((read + write) bytes / s) or, with
+    read_only, of a streaming read kernel (bytes read / s)."""
+    gbs = ctypes.c_double()
+    fn = lib().mx_probe_read if read_only else lib().mx_probe_copy
+    _check(fn(device, gib << 30, iters, ctypes.byref(gbs)))
+    return gbs.value
 
 
 def _check(rc: int):
