@@ -470,3 +470,15 @@ def test_persistent_gate_up_vs_oracle(mx, oracle_mod, name):
           f"vs MX_NO_PERS {np.abs(g1 - b1).max():.3g}")
     eng.close()
     base.close()
+
+
+def test_hbm_probes_plausible(mx):
+    """The bench's measured HBM ceilings (mx_probe_read / mx_probe_copy): finite, below the 8 TB/s
+    spec, and a read-only stream is not slower than a copy's read + write stream."""
+    rd = mx.probe_copy(0, 1, 4, read_only=True)
+    cp = mx.probe_copy(0, 1, 4)
+    assert 1000.0 < rd < 8400.0, rd
+    assert 1000.0 < cp < 8400.0, cp
+    assert rd > 0.8 * cp
+    with pytest.raises(mx.MxError):
+        mx._check(mx.lib().mx_probe_read(0, 0, 1, None))  # zero bytes: argument error, no launch
