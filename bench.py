@@ -55,10 +55,20 @@ def measured_traffic(label: str):
         return None
 
 
-def cpu_baseline(shape_name: str, n_prompt: int = 4, n_decode: int = 6):
-    """The CPU oracle (C/OpenMP restatement of llama.cpp's CPU forward, bf16
-    weights, f32 accumulation) doing what the reference does: batch-1 greedy
-    decode, timed on this host's cores.  Bounded sample: n_decode tokens."""
+def tiny_prompt(vocab: int = 32000):
+    """SURVEY §8d config 1/2 fixed prompt: BOS + 31 ids uniform in [3, vocab) from seed 1."""
+    import numpy as np
+
+    rng = np.random.default_rng(1)
+    return np.array([1] + [int(t) for t in rng.integers(3, vocab, 31)], np.int32)
+
+
+def cpu_baseline(shape_name: str, n_prompt: int = 16, n_decode: int = 24, tiny_tokens: int = 128):
+    """The CPU oracle (C/OpenMP restatement of llama.cpp's CPU forward: bf16 weights, f32
+    accumulation) doing what the reference does -- one request at a time, batch-1 greedy decode
+    (its lock serialises every request, p2p:121) -- timed on this host's cores.  Bounded samples:
+    the bench model (n_decode tokens after an n_prompt-token prompt), and BASELINE config 1
+    (TinyLlama-1.1B, 128 greedy tokens on the fixed prompt, whole generate() call timed)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from llama_p2p_amd import synth
@@ -66,7 +76,7 @@ def cpu_baseline(shape_name: str, n_prompt: int = 4, n_decode: int = 6):
     shape = synth.SHAPES[shape_name]
     t0 = time.time()
     m = O.OracleModel(shape, seed=0)
-    ctx = m.context(64)
+    ctx = m.context(128)
     t_gen = time.time() - t0
     prompt = make_prompts(shape.n_vocab, 1, seed=5, lo=n_prompt, hi=n_prompt)[0]
     lg = ctx.eval(prompt, 0)
@@ -79,9 +89,23 @@ def cpu_baseline(shape_name: str, n_prompt: int = 4, n_decode: int = 6):
     cores = O.lib().orc_num_threads()
     ctx.close()
     m.close()
-    return {"value": round(n_decode / dt, 3), "unit": "tokens/s", "cores": cores, "kind": "port",
-            "sample": f"{shape_name} bf16, batch 1 (the reference's serial path), {n_prompt}-token prompt then "
-                      f"{n_decode} greedy decode tokens timed; weight synthesis {t_gen:.1f}s untimed"}
+    out = {"value": round(n_decode / dt, 3), "unit": "tokens/s", "cores": cores, "kind": "port",
+           "sample": f"{shape_name} bf16, batch 1 (the reference serialises requests, p2p:121), {n_prompt}-token "
+                     f"prompt then {n_decode} greedy decode tokens timed; weight synthesis {t_gen:.1f}s untimed"}
+    if tiny_tokens > 0:
+        ts = synth.SHAPES["tinyllama-1.1b"]
+        tm = O.OracleModel(ts, seed=0)
+        tc = tm.context(512)
+        t2 = time.time()
+        toks = tc.generate_greedy(tiny_prompt(ts.n_vocab), tiny_tokens)
+        d2 = time.time() - t2
+        tc.close()
+        tm.close()
+        out["config1"] = {"value": round(tiny_tokens / d2, 2), "unit": "tokens/s", "cores": cores, "kind": "port",
+                          "seconds": round(d2, 3), "first_tokens": [int(t) for t in toks[:8]],
+                          "sample": f"BASELINE config 1: tinyllama-1.1b bf16, {tiny_tokens} greedy tokens on the "
+                                    "fixed prompt (BOS + 31 ids, seed 1), prompt eval + decode timed"}
+    return out
 
 
 def run_single(args):
@@ -101,8 +125,7 @@ def run_single(args):
         slots += [i] * (len(p) - 1)
         pos += list(range(len(p) - 1))
         ids += [int(t) for t in p[:-1]]
-    for i in range(0, len(slots), 64):
-        eng.stage_rows(slots[i:i + 64], pos[i:i + 64], ids[i:i + 64])
+    eng.forward_rows(slots, pos, ids, want_logits=False)  # GEMM prefill chunks
     b = eng.batch(slots=list(range(M)), pos=[len(p) - 1 for p in prompts], ids=[int(p[-1]) for p in prompts],
                   max_steps=args.warmup + args.steps)
     for _ in range(args.warmup):
@@ -260,17 +283,68 @@ def tiny_bench(args):
     return out
 
 
-def copy_peak(gib: int = 4, iters: int = 10):
-    """Measured HBM copy ceiling: the engine's streaming copy kernel (16 B per lane,
-    mx_probe_copy) over two gib-GiB buffers, (read + write) bytes / HIP-event time on its stream.
-    Reported next to the 8 TB/s spec that the roofline fractions use."""
+def big_bench(args):
+    """BASELINE config 5's model on ONE MI355X (141 GB of bf16 weights fit in 288 GB): Llama-3-70B
+    synthetic, batch-1 and M-sequence greedy decode tok/s against the HBM roofline, and its gate/up
+    GEMV (the dominant kernel) at both widths.  The 8-stage pipeline itself needs the 8-GPU node."""
+    from llama_p2p_amd import synth
+    from llama_p2p_amd.engine import Engine
+
+    name = "llama3-70b"
+    shape = synth.SHAPES[name]
+    M = args.seqs
+    t0 = time.time()
+    eng = Engine(f"synthetic:{name}:seed=0", n_ctx=512, n_seq_max=M)
+    t_load = time.time() - t0
+    prompts = make_prompts(shape.n_vocab, M, lo=16, hi=64)
+    slots, pos, ids = [], [], []
+    for i, p in enumerate(prompts):
+        slots += [i] * (len(p) - 1)
+        pos += list(range(len(p) - 1))
+        ids += [int(t) for t in p[:-1]]
+    eng.forward_rows(slots, pos, ids, want_logits=False)
+    out = {"model": f"{name} bf16 (synthetic weights, seed 0)", "weight_bytes": int(eng.info.weight_bytes),
+           "load_s": round(t_load, 1)}
+    steps = args.big_steps
+    for m in (1, M):
+        b = eng.batch(slots=list(range(m)), pos=[len(p) - 1 for p in prompts[:m]], ids=[int(p[-1]) for p in prompts[:m]],
+                      max_steps=steps + 2)
+        for _ in range(2):
+            b.step()
+        eng.sync()
+        t1 = time.perf_counter()
+        for _ in range(steps):
+            b.step()
+        eng.sync()
+        dt = (time.perf_counter() - t1) / steps
+        b.close()
+        ctx_sum = sum(len(p) + 2 + steps / 2 for p in prompts[:m])
+        by = eng.info.weight_bytes + ctx_sum * shape.kv_bytes_per_pos() + m * shape.n_vocab * 4
+        out[f"decode_M{m}"] = {"tok_s": round(m / dt, 2), "ms_per_step": round(dt * 1e3, 3),
+                               "hbm_frac": round(by / dt / 1e9 / HBM_PEAK_GBS, 4),
+                               "roofline_tok_s": round(m * HBM_PEAK_GBS * 1e9 / by, 1)}
+        us, wbytes = eng.profile_kernel(2 if m > 1 else 6, m, iters=2)
+        kb = wbytes + m * shape.n_embd * 2 + m * shape.n_ff * 2
+        out[f"gate_up_M{m}"] = {"us_per_launch": round(us, 2), "bytes_per_launch": int(kb),
+                                "achieved_gbs": round(kb / us / 1e3, 1), "frac": round(kb / us / 1e3 / HBM_PEAK_GBS, 4)}
+        if m == M:
+            break
+    eng.close()
+    return out
+
+
+def hbm_probe(gib: int = 4, iters: int = 8):
+    """Measured HBM streaming rates: the best of the engine's streaming probe
+    variants (16 B per lane; 4/8/16 loads in flight x 1024-4096 work-groups x non-temporal or not)
+    over gib-GiB buffers, bytes / HIP-event time.  Reported next to the 8 TB/s spec that the
+    roofline fractions use; a reference stream, not a hard ceiling."""
     from llama_p2p_amd import engine
 
-    gbs = engine.probe_copy(0, gib, iters)
-    rd = engine.probe_copy(0, gib, iters, read_only=True)
-    return {"gbs": round(gbs, 1), "frac_of_spec": round(gbs / HBM_PEAK_GBS, 4),
-            "read_gbs": round(rd, 1), "read_frac_of_spec": round(rd / HBM_PEAK_GBS, 4),
-            "method": f"mx_probe_copy / mx_probe_read: 16-B/lane streaming kernels, {gib} GiB x {iters}, "
+    cp, cdesc = engine.probe_copy(0, gib, iters)
+    rd, rdesc = engine.probe_copy(0, gib, iters, read_only=True)
+    return {"copy_gbs": round(cp, 1), "copy_frac_of_spec": round(cp / HBM_PEAK_GBS, 4), "copy_variant": cdesc,
+            "read_gbs": round(rd, 1), "read_frac_of_spec": round(rd / HBM_PEAK_GBS, 4), "read_variant": rdesc,
+            "method": f"mx_probe_copy / mx_probe_read: best of {gib} GiB x {iters} passes per variant, "
                       "(read + write) or read bytes / HIP-event time"}
 
 
@@ -303,6 +377,33 @@ def prefill_bench(eng, shape, n_prompts: int, plen: int):
             "sample": f"{n_prompts} prompts x {plen} tokens, 4096-row GEMM chunks, no lm_head"}
 
 
+class Sections:
+    """Runs the bench sections in order with wall-clock timings on stderr.  The headline section
+    raises on failure; optional ones report their error in the line, and are skipped once the
+    run has used its time budget (so the default run always ends inside the driver's limit)."""
+
+    def __init__(self, budget_s: float):
+        self.t0 = time.time()
+        self.budget = budget_s
+        self.seconds = {}
+
+    def run(self, name, fn, optional=True):
+        if optional and time.time() - self.t0 > self.budget:
+            print(f"[bench] {name}: skipped (time budget {self.budget:.0f}s used)", file=sys.stderr, flush=True)
+            return {"skipped": f"time budget of {self.budget:.0f}s used"}
+        t = time.time()
+        print(f"[bench] {name} ...", file=sys.stderr, flush=True)
+        try:
+            res = fn()
+        except Exception as ex:  # report, never hide
+            if not optional:
+                raise
+            res = {"error": repr(ex)}
+        self.seconds[name] = round(time.time() - t, 1)
+        print(f"[bench] {name}: {self.seconds[name]}s", file=sys.stderr, flush=True)
+        return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -318,11 +419,14 @@ def main():
     ap.add_argument("--q8-steps", type=int, default=32, help="Q8_0 decode steps (0: skip the Q8_0 section)")
     ap.add_argument("--tiny-tokens", type=int, default=128,
                     help="TinyLlama-1.1B batch-1 tokens (config 2; 0: skip the section)")
+    ap.add_argument("--big-steps", type=int, default=8, help="Llama-3-70B decode steps (0: skip the section)")
+    ap.add_argument("--budget", type=float, default=360.0,
+                    help="seconds after which optional sections are skipped")
     ap.add_argument("--force-pipeline", action="store_true", help="run the torch.distributed pipeline path even at N=1")
-    ap.add_argument("--copy-peak-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--probe-only", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
-    if args.copy_peak_only:
-        print(json.dumps(copy_peak()), flush=True)
+    if args.probe_only:
+        print(json.dumps(hbm_probe()), flush=True)
         return
 
     # stdout carries exactly the one JSON line: native libraries that write to fd 1 (the RCCL
@@ -338,11 +442,8 @@ def main():
 
         return pipeline.bench_main(args, METRIC, make_prompts)
 
-    res = run_single(args)
-    try:
-        copy = copy_peak()
-    except Exception as ex:  # report, never hide
-        copy = {"error": repr(ex)}
+    sec = Sections(args.budget)
+    res = sec.run("decode", lambda: run_single(args), optional=False)
     line = {
         "metric": METRIC, "value": round(res["tok_s"], 2), "unit": "tokens/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(res["ms_per_step"], 4),
@@ -354,29 +455,19 @@ def main():
         "step_hbm_gbs": round(res["step_gbs"], 1), "step_hbm_frac": round(res["step_gbs"] / HBM_PEAK_GBS, 4),
         "roofline": res["roofline"],
     }
-    if "batch1" in res:
-        line["batch1"] = res["batch1"]
-    if "prefill" in res:
-        line["prefill"] = res["prefill"]
-    if args.q8_steps > 0:
-        try:
-            line["q8_0"] = q8_bench(args)
-        except Exception as ex:  # report, never hide
-            line["q8_0"] = {"error": repr(ex)}
-    if args.tiny_tokens > 0:
-        try:
-            line["tinyllama"] = tiny_bench(args)
-        except Exception as ex:  # report, never hide
-            line["tinyllama"] = {"error": repr(ex)}
-    line["hbm_copy_peak"] = copy
-    if "gbs" in copy:
-        line["roofline"]["frac_of_copy_peak"] = round(line["roofline"]["achieved"] / copy["gbs"], 4)
-        line["roofline"]["frac_of_read_peak"] = round(line["roofline"]["achieved"] / copy["read_gbs"], 4)
+    for k in ("batch1", "prefill"):
+        if k in res:
+            line[k] = res[k]
     if not args.no_cpu_baseline:
-        try:
-            line["cpu_baseline"] = cpu_baseline(args.model)
-        except Exception as ex:  # report, never hide
-            line["cpu_baseline"] = {"error": repr(ex)}
+        line["cpu_baseline"] = sec.run("cpu_baseline", lambda: cpu_baseline(args.model))
+    if args.tiny_tokens > 0:
+        line["tinyllama"] = sec.run("tinyllama", lambda: tiny_bench(args))
+    line["hbm_probe"] = sec.run("hbm_probe", hbm_probe)
+    if args.q8_steps > 0:
+        line["q8_0"] = sec.run("q8_0", lambda: q8_bench(args))
+    if args.big_steps > 0:
+        line["llama3_70b"] = sec.run("llama3_70b", lambda: big_bench(args))
+    line["section_seconds"] = sec.seconds
     print(json.dumps(line), flush=True)
 
 

@@ -68,8 +68,6 @@ typedef struct {
   int32_t n_ctx, n_seq_max;
   int32_t layer_begin, layer_end, has_embed, has_head;
   uint64_t weight_bytes; /* device bytes of the weights this stage streams per decode step */
-  int32_t persistent_decode; /* 1: steps of <= 4 tokens run as one persistent kernel (opt-in: MX_PDK=1) */
-  int32_t persistent_grid;   /* its work-groups (one per CU) */
   int32_t weight_type;       /* ggml type of the layer matrices: 30 BF16, 8 Q8_0 */
 } mx_model_info;
 
@@ -82,6 +80,8 @@ typedef struct {
   int32_t repeat_last_n;/* 64 */
   uint64_t seed;
   int32_t ignore_eos;
+  float frequency_penalty; /* 0.0 = off: logit -= count * frequency_penalty (llama.cpp penalties sampler) */
+  float presence_penalty;  /* 0.0 = off: logit -= (count > 0) * presence_penalty */
 } mx_sampling;
 
 void mx_opts_default(mx_opts* o);
@@ -91,6 +91,9 @@ const char* mx_last_error(void);
 /* model_path: a GGUF file (bf16 LLaMA) or "synthetic:<shape>[:seed=N]" */
 int mx_engine_create(const char* model_path, const mx_opts* opts, mx_engine** out);
 void mx_engine_destroy(mx_engine* e);
+/* Parse a GGUF container without touching a GPU (header, metadata, tensor table, bounds of every
+ * tensor against the file): 0, or MX_ERR_MODEL with the reason in mx_last_error(). */
+int mx_gguf_check(const char* path);
 int mx_engine_info(const mx_engine* e, mx_model_info* out);
 
 /* Parity hook: evaluate n tokens of sequence `slot` at positions pos0..pos0+n-1
@@ -102,11 +105,26 @@ int mx_forward_logits(mx_engine* e, int slot, const int32_t* ids, int n, int pos
 int mx_forward_rows(mx_engine* e, int n, const int32_t* slots, const int32_t* pos, const int32_t* ids,
                     float* logits_out);
 
+/* Parity hook for the sampler: rows forward as mx_forward_rows (n <= 64), then the device top-k
+ * kernel (the sampler chain's candidate selection): vals/idx [n][k], value descending, ties -> lower
+ * id; k <= 64. */
+int mx_forward_topk(mx_engine* e, int n, const int32_t* slots, const int32_t* pos, const int32_t* ids, int k,
+                    float* vals, int32_t* idx);
+
 /* Request API (what Llama.__call__ uses).  Tokens are generated by the
  * scheduler thread, micro-batched with every other active request. */
 int mx_submit(mx_engine* e, const int32_t* ids, int n, const mx_sampling* s, int max_tokens, uint64_t* req);
-/* Blocks until the request finishes; copies up to cap generated ids. */
+/* Blocks until the request finishes; copies up to cap generated ids and releases the request.
+ * If more than cap ids were generated, nothing is released: *n_out is set and MX_ERR_ARG returned,
+ * so the caller can retry with a larger buffer. */
 int mx_wait(mx_engine* e, uint64_t req, int32_t* out_ids, int cap, int* n_out, int* finish);
+/* Incremental read (streaming / stop strings): blocks until the request holds more than n_have
+ * generated ids or has finished; copies the first min(cap, n) ids, *n_out = n, *done = finished.
+ * The request stays registered (mx_wait releases it). */
+int mx_poll(mx_engine* e, uint64_t req, int n_have, int32_t* out_ids, int cap, int* n_out, int* done);
+/* Ask the scheduler to end a request after its current step (finish reason STOP), e.g. when the
+ * caller found a stop string.  The request still has to be released with mx_wait. */
+int mx_cancel(mx_engine* e, uint64_t req);
 
 /* Device-resident decode batch (benchmark, pipeline stages).  Rows are M
  * sequences in KV slots `slots`, next token ids[i] at position pos[i].
@@ -141,12 +159,13 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us_per_l
 
 int mx_sync(mx_engine* e);
 
-/* Measured HBM copy ceiling on `device` (no engine): a 16-byte-per-lane streaming copy kernel over
- * two `bytes`-sized buffers, `iters` passes timed with HIP events; *gbs = (read + write) bytes / s.
- * Benchmark support (SURVEY.md §8d "also report a measured copy-kernel peak"), not a reference API. */
-int mx_probe_copy(int device, size_t bytes, int iters, double* gbs);
-/* Read-only variant (a GEMV's traffic is ~99.5 % reads): *gbs = bytes read / s. */
-int mx_probe_read(int device, size_t bytes, int iters, double* gbs);
+/* HBM streaming probes on `device` (no engine): the best of a sweep of 16-byte-per-lane streaming
+ * kernels (loads in flight per lane x grid x non-temporal) over `bytes`-sized buffers, `iters`
+ * passes each timed with HIP events.  copy: *gbs = (read + write) bytes / s; read: bytes read / s.
+ * desc (optional) receives the winning variant.  Benchmark support (SURVEY.md §8d "also report a
+ * measured copy-kernel peak"), not a reference API. */
+int mx_probe_copy(int device, size_t bytes, int iters, double* gbs, char* desc, int desc_len);
+int mx_probe_read(int device, size_t bytes, int iters, double* gbs, char* desc, int desc_len);
 
 /* Request-path counters (mx_submit/mx_wait).  reused_prompt_tokens: prompt positions whose K/V were
  * kept from the slot's previous request (longest common prefix, as llama-cpp-python's generate). */
@@ -157,10 +176,6 @@ int mx_engine_stats(mx_engine* e, mx_stats* out);
 
 /* Number of visible HIP devices (serving: one engine replica per GPU). */
 int mx_device_count(int32_t* n);
-
-/* Diagnostics: one persistent-decode-kernel step of M rows with per-phase wall-clock stamps
- * (100 MHz): out[grid][nphase][3] = {start, B image built, work end}; returns grid and nphase. */
-int mx_debug_pdk_trace(mx_engine* e, int M, int pos, uint64_t* out, int cap, int* grid, int* nphase);
 
 #ifdef __cplusplus
 }

@@ -57,18 +57,23 @@ double scalar(Cursor& c, int t) {
   throw std::runtime_error("GGUF: bad scalar type " + std::to_string(t));
 }
 
+// bytes of n elements of a ggml type (n < 2^56 checked by the caller, so nothing here overflows);
+// 0 for an unsupported type or a count that is not a whole number of blocks
 uint64_t type_bytes(int type, uint64_t n) {
+  uint64_t blk = 1, bb = 0;
   switch (type) {
-    case 0: return n * 4;                // F32
-    case 1: return n * 2;                // F16
-    case 30: return n * 2;               // BF16
-    case 8: return n / 32 * 34;          // Q8_0
-    case 2: return n / 32 * 18;          // Q4_0
-    case 12: return n / 256 * 144;       // Q4_K
-    case 13: return n / 256 * 176;       // Q5_K
-    case 14: return n / 256 * 210;       // Q6_K
+    case 0: bb = 4; break;                   // F32
+    case 1: bb = 2; break;                   // F16
+    case 30: bb = 2; break;                  // BF16
+    case 8: blk = 32, bb = 34; break;        // Q8_0
+    case 2: blk = 32, bb = 18; break;        // Q4_0
+    case 12: blk = 256, bb = 144; break;     // Q4_K
+    case 13: blk = 256, bb = 176; break;     // Q5_K
+    case 14: blk = 256, bb = 210; break;     // Q6_K
+    default: return 0;
   }
-  return 0;
+  if (n % blk) return 0;
+  return n / blk * bb;
 }
 }  // namespace
 
@@ -103,6 +108,10 @@ std::string GGUFFile::open(const std::string& path) {
       } else if (v.type == T_ARRAY) {
         v.arr_type = (int)c.rd<uint32_t>();
         uint64_t n = c.rd<uint64_t>();
+        // every element takes at least 1 byte (8 for a string's length): a count beyond what the
+        // file holds is truncation, reported before any allocation of that size
+        const uint64_t left = (uint64_t)(c.end - c.p);
+        if (n > (v.arr_type == T_STRING ? left / 8 : left)) throw std::runtime_error("GGUF: truncated array " + key);
         if (v.arr_type == T_STRING) {
           v.arr_str.reserve(n);
           for (uint64_t j = 0; j < n; j++) v.arr_str.push_back(c.str());
@@ -124,20 +133,30 @@ std::string GGUFFile::open(const std::string& path) {
       uint64_t n = 1;
       for (uint32_t d = 0; d < nd; d++) {
         t.ne.push_back(c.rd<uint64_t>());
-        n *= t.ne.back();
+        if (__builtin_mul_overflow(n, t.ne.back(), &n) || n >= (1ull << 56))
+          return "GGUF: tensor " + t.name + " has an element count that overflows";
       }
       t.type = (int)c.rd<uint32_t>();
       t.offset = c.rd<uint64_t>();
       t.nbytes = type_bytes(t.type, n);
+      if (t.nbytes == 0 && n != 0)
+        return "GGUF: tensor " + t.name + " has unsupported type " + std::to_string(t.type) +
+               " (or a ragged block count)";
       infos.push_back(t);
     }
-    uint64_t al = (uint64_t)get_num("general.alignment", 32);
-    uint64_t hdr = (uint64_t)(c.p - base_);
-    uint64_t data_start = (hdr + al - 1) / al * al;
+    const double al_num = get_num("general.alignment", 32);
+    if (!(al_num >= 1 && al_num <= 65536)) return "GGUF: general.alignment out of range";
+    const uint64_t al = (uint64_t)al_num;
+    if (al & (al - 1)) return "GGUF: general.alignment " + std::to_string(al) + " is not a power of two";
+    const uint64_t hdr = (uint64_t)(c.p - base_);
+    const uint64_t data_start = (hdr + al - 1) / al * al;
+    if (data_start > file_size) return "GGUF: data section starts past end of file";
     for (auto& t : infos) {
+      // offset and size are checked against the bytes after data_start without forming sums that wrap
+      const uint64_t room = file_size - data_start;
+      if (t.offset > room || t.nbytes > room - t.offset)
+        return "GGUF: tensor " + t.name + " extends past end of file";
       t.offset += data_start;
-      if (t.nbytes == 0) return "GGUF: tensor " + t.name + " has unsupported type " + std::to_string(t.type);
-      if (t.offset + t.nbytes > file_size) return "GGUF: tensor " + t.name + " extends past end of file";
       tensors[t.name] = t;
     }
   } catch (const std::exception& e) {

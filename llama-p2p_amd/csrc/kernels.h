@@ -65,17 +65,6 @@ struct MMArgs {
   int n_ctx, ctx_stride, n_head_kv;
   size_t slot_stride;          // elements per slot in kc/vc = n_head_kv*ctx_stride*head_dim
   size_t slab_stride;          // EPI_SLAB: floats between consecutive K-split partial slabs
-  unsigned long long* trace;   // attn_o_kernel phase stamps (diagnosis; nullptr normally)
-  // EPI_RESID with nxt_y (mm_kernel, <= 16 rows): the last work-group to finish also applies the
-  // NEXT RMS_NORM + MUL(nxt_w) to the new residual rows (scale from the ssq partials this launch
-  // wrote, so ssq/np must be set) and writes bf16 nxt_y [M][N]; nxt_cnt: a zeroed arrival counter
-  uint16_t* nxt_y;
-  const float* nxt_w;
-  unsigned* nxt_cnt;
-  // row-tile-persistent EPI_RESID split over K by 2 work-groups (mm_pers_kernel KZ = 2): partial
-  // tiles [N/16][2][64] f32x4 and zeroed per-tile arrival counters [N/16] (the 2nd arriver folds)
-  float* kz_part;
-  unsigned* kz_cnt;
 };
 
 struct AttnArgs {
@@ -98,48 +87,6 @@ struct AttnArgs {
   const float* rope_cs;  // [n_ctx][head_dim/2][2]
   _Float16 *kc_w, *vc_w; // writable views of kc / vc
 };
-
-// Persistent decode kernel (pdk.hip): one launch runs every layer + lm_head for <= PDK_MAX_M tokens
-constexpr int PDK_WAVES = 8;    // waves per work-group (one work-group per CU: 2 waves per SIMD, 256 VGPRs each)
-constexpr int PDK_MAX_M = 4;
-constexpr int PDK_MAX_XT = 4;   // residual tiles kept in LDS per work-group
-constexpr int PDK_SYNC_BYTES = 34 * 128;  // barrier counter tree + flags + timeout word
-
-struct PdkLayer {
-  const uint16_t *qkv, *o, *gu, *down;  // packed tiles
-  const float *attn_norm, *ffn_norm;
-  _Float16 *kc, *vc;                     // this layer's K / V^T cache
-};
-
-struct PdkArgs {
-  int M, n_layer, h, kv, ff, n_head, n_head_kv, head_dim, n_vocab;
-  float eps, attn_scale;
-  const PdkLayer* layers;  // device array [n_layer]
-  const uint16_t* output;
-  const float* out_norm;
-  const int* pos;          // [M]
-  const int* slot;         // [M]
-  float* x;                // residual stream [M][h] (embedded before the launch)
-  float* ssq;              // [M][h/16] per-tile sums of squares of x
-  float* q;                // [M][h]
-  float* kvs;              // [M][2*kv] this step's post-RoPE K and V (attention reads them here)
-  uint16_t* attn_out;      // [M][h] bf16
-  uint16_t* act;           // [M][ff] bf16
-  float* logits;           // [M][n_vocab]
-  const float* rope_cs;
-  int n_ctx, ctx_stride;
-  size_t slot_stride;
-  unsigned* sync;          // PDK_SYNC_BYTES: barrier counters, flags, timeout word (zeroed by launch_pdk)
-  int img_pitch;           // pdk_pitch(h, ff)
-  bool head;               // run lm_head after the last layer
-  unsigned long long* trace;  // optional [grid][n_phase][3] wall-clock (100 MHz) stamps: start, B image built, work end
-};
-
-int pdk_pitch(int h, int ff);
-size_t pdk_lds_bytes(int M, int h, int ff, int n_head, int n_head_kv, int head_dim);
-bool pdk_supported(int M, int h, int ff, int n_head, int n_head_kv, int head_dim, int n_vocab, int grid);
-int pdk_occupancy(int head_dim, int group, size_t lds);  // resident work-groups per CU
-int launch_pdk(const PdkArgs& a, int grid, hipStream_t s);
 
 // packing / synthetic weights.  mode: PACK_ROWS (logical row r -> packed row r + offset),
 // PACK_GATE / PACK_UP (ffn_gate / ffn_up rows interleaved by 8-row halves of each tile)
@@ -173,10 +120,6 @@ int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, h
 void launch_resid_norm(uint16_t* y, int ldy, float* x, const float* slabs, int nslab, size_t slab_stride,
                        const float* w, int M, int n, float eps, hipStream_t s);  // X == nullptr path (RMS_NORM fused into the GEMV) is legal
 void launch_attention(const AttnArgs& a, hipStream_t s);
-// decode attention + attn_output (EPI_RESID, X = at.out) in one launch for <= 4 rows; sync: 640
-// zeroed uints of this engine (counters, timeout flag at [64], flag replicas); -1 if unsupported
-bool attn_o_supported(const AttnArgs& at, const MMArgs& a);
-int launch_attn_o(const AttnArgs& at, const MMArgs& a, unsigned* sync, hipStream_t s);
 // rows in blocks of 16 consecutive positions of one sequence each (prefill chunks): one
 // work-group per (kv head, block), the 16 queries share every K/V chunk
 void launch_attention_prefill(const AttnArgs& a, hipStream_t s);
@@ -219,11 +162,10 @@ void launch_argmax(const float* logits, int ldl, int M, int V, float* ws_val, in
                    int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count, int max_hist,
                    hipStream_t s);
 
-// HBM copy ceiling probe: dst = src over n16 16-byte words (n16 % 1024 == 0), 16 B per lane,
-// four independent loads in flight per lane, grid-stride over 8 work-groups per CU
-void launch_copy_probe(const uint4* src, uint4* dst, size_t n16, hipStream_t s);
-// read-only variant (the GEMVs' traffic is ~99.5 % reads): XOR-folds src, writes one word per lane
-// only when the fold hits a sentinel (never for the probe's fill)
-void launch_read_probe(const uint4* src, uint4* sink, size_t n16, hipStream_t s);
+// HBM streaming probes: variant v of probe_variants() (loads in flight, grid, non-temporal) of a
+// read-only (XOR fold) or copy stream over n16 16-byte words (n16 % 4096 == 0); desc describes it
+int probe_variants();
+int launch_probe(int v, bool read_only, const uint4* src, uint4* dst, size_t n16, hipStream_t s, char* desc,
+                 int desc_len);
 
 }  // namespace mx

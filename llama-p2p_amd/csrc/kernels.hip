@@ -20,6 +20,7 @@
 #include "kernels.h"
 
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -425,59 +426,6 @@ __device__ __forceinline__ void epi_store(const MMArgs& a, int tile, int l, int 
   }
 }
 
-// Last-arriver RMS_NORM after an EPI_RESID GEMV (<= 16 rows): every work-group publishes its
-// residual rows and ssq partials (plain stores, drained, agent-scope release, relaxed counter add:
-// cdna_hip_programming.md "In-launch split-K reduction" recipe); the work-group that draws the last
-// ticket acquires and writes nxt_y = bf16((x * 1/sqrt(mean + eps)) * nxt_w) for all M rows, with
-// the sum of squares from the partials in a fixed order (as the RMS_NORM-on-load path), then
-// resets the counter.  Replaces the separate norm launch and its kernel boundary -- but measured
-// slower at batch 1 (2.88 -> 3.03 ms/token, tools/gpu/fn_ab.sh), so it is opt-in (MX_FUSED_NORM=1).
-// `flag` is a word of the caller's LDS (no second __shared__ object).
-__device__ __forceinline__ void resid_then_norm(const MMArgs& a, unsigned* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(a.nxt_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag[0] = old == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!flag[0]) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(a.nxt_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float* scl = reinterpret_cast<float*>(flag) + 1;  // per-row scales (M <= 16) after the flag word
-  if (w == 0) {
-    for (int c = 0; c < a.M; ++c) {
-      double acc = 0.0;
-      for (int i = lane * 4; i < a.np; i += 256)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc += (double)a.ssq[(size_t)c * a.np + i + j];
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) acc += __shfl_xor(acc, o);
-      if (lane == 0) scl[c] = 1.0f / sqrtf((float)(acc / a.N) + a.eps);
-    }
-  }
-  __syncthreads();
-  const int n4 = a.N / 4;
-  for (int u = threadIdx.x; u < a.M * n4; u += blockDim.x) {
-    const int c = u / n4, i = (u % n4) * 4;
-    const f32x4 xv = *reinterpret_cast<const f32x4*>(a.out + (size_t)c * a.ldo + i);
-    const f32x4 g = *reinterpret_cast<const f32x4*>(a.nxt_w + i);
-    const float sc = scl[c];
-    u32x2 o;
-    o[0] = f2bf((xv[0] * sc) * g[0]) | (f2bf((xv[1] * sc) * g[1]) << 16);
-    o[1] = f2bf((xv[2] * sc) * g[2]) | (f2bf((xv[3] * sc) * g[3]) << 16);
-    *reinterpret_cast<u32x2*>(a.nxt_y + (size_t)c * a.N + i) = o;
-  }
-}
-
 template <int KS, int RT, int NB, int EPI, int U, bool XS>
 __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
   const int lane = threadIdx.x & 63;
@@ -617,9 +565,6 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
     }
     epi_store<EPI>(a, tile0 + r, l, col, s, up);
   }
-  if constexpr (EPI == EPI_RESID) {
-    if (a.nxt_y) resid_then_norm(a, reinterpret_cast<unsigned*>(&red[0][0][0][0]));
-  }
 }
 
 template <int KS, int RT, int EPI, int U>
@@ -663,19 +608,14 @@ static int launch_mm_cfg(const MMArgs& a, hipStream_t s) {
 // waves stream tile i+1.  Same epilogues (F32 / RESID + ssq partials / SWIGLU) and the same
 // summation order per tile (K-slices in wave order) as mm_kernel, so results are bit-identical.
 // ---------------------------------------------------------------------------
-// XL (XS only): B fragments read from the LDS image at each MFMA instead of held in registers,
-// so the kernel fits 64 VGPRs and two 16-wave work-groups share a CU (WPE = waves per SIMD).
-// KZ > 1 (EPI_SLAB): grid.y = KZ work-groups split K; partial tile sums go to slab blockIdx.y
-// (a.out + kz * a.slab_stride, [col][ldo]) for a consumer that adds them in slab order.
-template <int KS, int NKW, int TPW, int EPI, int U, bool XS, bool XL = false, int WPE = 4, int XM = XS_MAX_M,
-          int KZ = 1>
-__global__ __launch_bounds__(64 * KS, WPE) void mm_pers_kernel(MMArgs a) {
+template <int KS, int NKW, int TPW, int EPI, int U, bool XS>
+__global__ __launch_bounds__(64 * KS) void mm_pers_kernel(MMArgs a) {
   static_assert(NKW % U == 0 || (U % NKW == 0 && U / NKW <= TPW), "ring depth vs per-wave K-slice");
+  constexpr int XM = XS_MAX_M;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  constexpr int KT = KS * NKW * KZ;
-  const int kz = KZ > 1 ? (int)blockIdx.y : 0;
-  const int kb = kz * KS * NKW + w * NKW;
+  constexpr int KT = KS * NKW;
+  const int kb = w * NKW;
   const int G = gridDim.x;
 
   __shared__ f32x4 red[2][KS][64];
@@ -708,10 +648,8 @@ __global__ __launch_bounds__(64 * KS, WPE) void mm_pers_kernel(MMArgs a) {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
     __builtin_amdgcn_wave_barrier();
     const u32x4* xp = reinterpret_cast<const u32x4*>(xsw + col * xs_pitch + (lane >> 4) * 8);
-    if constexpr (!XL) {
 #pragma unroll
-      for (int k = 0; k < NKW; ++k) xb[k] = xp[k * 4];
-    }
+    for (int k = 0; k < NKW; ++k) xb[k] = xp[k * 4];
   } else {
     const u32x4* xp = reinterpret_cast<const u32x4*>(a.X + (size_t)col * a.ldx + (lane >> 4) * 8);
 #pragma unroll
@@ -728,22 +666,6 @@ __global__ __launch_bounds__(64 * KS, WPE) void mm_pers_kernel(MMArgs a) {
       f32x4 s = rb[0][l];
 #pragma unroll
       for (int ww = 1; ww < KS; ++ww) s += rb[ww][l];
-      if constexpr (KZ > 1) {
-        // in-launch split-K fold (cdna_hip_programming.md "In-launch split-K reduction"): publish
-        // this half, count in; the second arriver adds both halves in kz order (deterministic)
-        f32x4* part = reinterpret_cast<f32x4*>(a.kz_part) + (size_t)tile * KZ * 64;
-        part[kz * 64 + l] = s;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        unsigned old = 0;
-        if (l == 0) old = __hip_atomic_fetch_add(a.kz_cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        old = __shfl(old, 0);
-        if (old != KZ - 1) return;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        if (l == 0) __hip_atomic_store(a.kz_cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s = part[l];
-#pragma unroll
-        for (int z = 1; z < KZ; ++z) s += part[z * 64 + l];
-      }
       double q = 0.0;
       if (col_raw < a.M) {
         f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col_raw * a.ldo + tile * 16 + (l >> 4) * 4);
@@ -757,12 +679,6 @@ __global__ __launch_bounds__(64 * KS, WPE) void mm_pers_kernel(MMArgs a) {
         q += __shfl_xor(q, 32);
         if (l < 16 && col_raw < a.M) a.ssq[(size_t)col_raw * a.np + tile] = (float)q;
       }
-    } else if constexpr (EPI == EPI_SLAB) {
-      if (col_raw >= a.M) return;
-      f32x4 s = rb[0][l];
-#pragma unroll 3
-      for (int ww = 1; ww < KS; ++ww) s += rb[ww][l];
-      *reinterpret_cast<f32x4*>(a.out + kz * a.slab_stride + (size_t)col_raw * a.ldo + tile * 16 + (l >> 4) * 4) = s;
     } else {
       if (l >= LU || col_raw >= a.M) return;
       // partial unroll: fully unrolled, hipcc hoists all 2*KS LDS reads and spills the ring / B
@@ -792,11 +708,8 @@ __global__ __launch_bounds__(64 * KS, WPE) void mm_pers_kernel(MMArgs a) {
 #pragma unroll
     for (int k = 0; k < NKW; ++k) {
       const int f = i * NKW + k;  // flat ring position (compile-time after unrolling)
-      u32x4 bk;
-      if constexpr (XL) bk = reinterpret_cast<const u32x4*>(xsw + col * xs_pitch + (lane >> 4) * 8)[k * 4];
-      else bk = xb[k];
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ra[f % U]),
-                                                    __builtin_bit_cast(bf16x8, bk), acc, 0, 0, 0);
+                                                    __builtin_bit_cast(bf16x8, xb[k]), acc, 0, 0, 0);
       if ((f + U) / NKW < TPW) ra[f % U] = wld((f + U) / NKW, (f + U) % NKW);
     }
     publish(i, acc);
@@ -804,56 +717,20 @@ __global__ __launch_bounds__(64 * KS, WPE) void mm_pers_kernel(MMArgs a) {
 }
 
 // grid = N / (16 * TPW) work-groups (every one walks exactly TPW tiles)
-template <int KS, int NKW, int TPW, int EPI, int U, bool XL = false, int KZ = 1>
+template <int KS, int NKW, int TPW, int EPI, int U>
 static int launch_pers_cfg(const MMArgs& a, hipStream_t s) {
   const int ntiles = a.N / TILE_N;
-  if (a.K != KS * NKW * TILE_K * KZ || (size_t)ntiles * a.K * 32 >= (1ull << 31)) return -1;
-  const int gx = (ntiles + TPW - 1) / TPW;  // the last tiles of some work-groups are phantoms
-  if constexpr (KZ > 1) {
-    static_assert(EPI == EPI_RESID, "split-K persistent GEMV: residual epilogue only");
-    if (a.X == nullptr) return -1;
-    mm_pers_kernel<KS, NKW, TPW, EPI, U, false, false, 4, XS_MAX_M, KZ><<<dim3(gx, KZ), 64 * KS, 0, s>>>(a);
-    return 0;
-  }
-  const int grid = gx;
+  if (a.K != KS * NKW * TILE_K || (size_t)ntiles * a.K * 32 >= (1ull << 31)) return -1;
+  const int grid = (ntiles + TPW - 1) / TPW;  // the last tiles of some work-groups are phantoms
   if (a.X == nullptr) {
     if (a.M > XS_MAX_M || !a.xf || !a.norm_w || !a.ssq || a.np * 16 != a.K || a.np > 512 || NKW * TILE_K > 512)
       return -1;
     const size_t lds = (size_t)KS * XS_MAX_M * (NKW * TILE_K + 8) * 2;
-    if constexpr (XL) {  // one row (XsRegs for one column: fits 64 VGPRs)
-      if (a.M != 1) return -1;
-      mm_pers_kernel<KS, NKW, TPW, EPI, U, true, true, 8, 1><<<grid, 64 * KS, lds, s>>>(a);
-    } else {
-      mm_pers_kernel<KS, NKW, TPW, EPI, U, true><<<grid, 64 * KS, lds, s>>>(a);
-    }
+    mm_pers_kernel<KS, NKW, TPW, EPI, U, true><<<grid, 64 * KS, lds, s>>>(a);
   } else {
     mm_pers_kernel<KS, NKW, TPW, EPI, U, false><<<grid, 64 * KS, 0, s>>>(a);
   }
   return 0;
-}
-
-// qkv of ONE token as KZ = 2 split-K halves with RMS_NORM on load: 2 x (h + 2 kv) / 16 work-groups
-// of 8 waves (Llama-3-8B: 768 = 3 per CU, 70B: 1280 = 5 per CU) instead of 384 / 640 whole tiles
-// (1.5 / 2.5 per CU: the CUs holding one more tile set the time).  Partial q/k/v go to slabs that
-// the attention kernel sums (slab order), ropes and stores into the KV cache (its `fin` path), so
-// the rows must be distinct sequences.  Returns the slab count, or -1 (nothing launched).
-int launch_qkv_split(const MMArgs& a0, float* slabs, size_t slab_stride, hipStream_t s) {
-  if (a0.M != 1 || a0.X != nullptr || !a0.xf || !a0.norm_w || !a0.ssq || a0.np * 16 != a0.K) return -1;
-  if (a0.N % TILE_N) return -1;
-  MMArgs a = a0;
-  a.out = slabs; a.ldo = a0.N; a.slab_stride = slab_stride;
-  const dim3 grid(a.N / TILE_N, 2);
-  if (a.K == 4096) {
-    const size_t lds = (size_t)8 * 1 * (8 * TILE_K + 8) * 2;
-    mm_pers_kernel<8, 8, 1, EPI_SLAB, 4, true, false, 6, 1, 2><<<grid, 512, lds, s>>>(a);
-    return 2;
-  }
-  if (a.K == 8192) {
-    const size_t lds = (size_t)8 * 1 * (16 * TILE_K + 8) * 2;
-    mm_pers_kernel<8, 16, 1, EPI_SLAB, 4, true, true, 6, 1, 2><<<grid, 512, lds, s>>>(a);
-    return 2;
-  }
-  return -1;
 }
 
 // Row-tile-persistent GEMVs for <= 16 tokens; -1 when the shape has no instantiation (callers
@@ -864,17 +741,13 @@ static const bool pers_resid = getenv("MX_NO_PERS_RESID") == nullptr;  // attn_o
 // lm_head with the output norm on load: correct but neutral at batch 1 (8B 2.804 vs 2.809 ms,
 // TinyLlama 0.750 vs 0.751; tools/gpu/pers_ab4.sh), so opt-in (MX_PERS_HEAD=1)
 static const bool pers_head = getenv("MX_PERS_HEAD") != nullptr;
-// TinyLlama attn_output / ffn_down (128 tiles) split over K by 2 work-groups with the in-launch
-// fold: correct, but the release/acquire hand-off costs ~4.5 us per launch (batch-1 0.755 ->
-// 0.95 ms/token, tools/gpu/tiny_kz.sh), so opt-in (MX_PERS_KZ=1)
-static const bool pers_kz = getenv("MX_PERS_KZ") != nullptr;
 
 bool mm_pers_supported(int epi, int M, int N, int K) {
   if (M < 1 || M > 16) return false;
   const int nt = N / TILE_N;
   if (epi == EPI_SWIGLU) return (K == 4096 && nt == 1792) || (K == 8192 && nt == 3584) || (K == 2048 && nt == 704);
   if (epi == EPI_RESID && pers_resid)
-    return (N == 4096 && (K == 4096 || K == 14336)) || (pers_kz && N == 2048 && (K == 2048 || K == 5632));
+    return N == 4096 && (K == 4096 || K == 14336);
   if (epi == EPI_F32 && pers_head) return (K == 4096 && nt <= 256 * 32) || (K == 2048 && nt <= 256 * 8);
   return false;
 }
@@ -889,10 +762,6 @@ int launch_mm_pers(int epi, const MMArgs& a, hipStream_t s) {
   } else if (epi == EPI_RESID) {
     if (a.K == 4096) return launch_pers_cfg<16, 8, 1, EPI_RESID, 8>(a, s);
     if (a.K == 14336) return launch_pers_cfg<16, 28, 1, EPI_RESID, 14>(a, s);
-    if (a.N == 2048 && a.kz_part && a.kz_cnt) {  // TinyLlama: 128 tiles, K split over 2 groups -> 256
-      if (a.K == 2048) return launch_pers_cfg<16, 2, 1, EPI_RESID, 2, false, 2>(a, s);
-      if (a.K == 5632) return launch_pers_cfg<8, 11, 1, EPI_RESID, 11, false, 2>(a, s);
-    }
   } else if (epi == EPI_F32) {
     if (a.K == 4096) return launch_pers_cfg<16, 8, 32, EPI_F32, 8>(a, s);  // 8B: 251 groups
     if (a.K == 2048) return launch_pers_cfg<16, 4, 8, EPI_F32, 4>(a, s);   // TinyLlama: 250 groups
@@ -1223,20 +1092,13 @@ bool mm_can_norm_on_load(int M, int K) {
 // [pos][d] (B operand of QK^T = contiguous 16 B per lane) and V transposed
 // [d][pos] (B operand of P.V = contiguous 16 B per lane).
 // ---------------------------------------------------------------------------
-// sc1 (write-through, L1-bypassing) buffer accesses for data handed between work-groups of one
-// launch (cdna_hip_programming.md §6 Guideline 16, as pdk.hip)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sc_rsrc(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7ffffff0, 0x00020000);
-}
-
 #ifndef ATTN_PREFETCH
 // 1: the first K/V chunk is issued right behind q (one round trip instead of two) -- measured
 // SLOWER at batch 1 (2.772 -> 2.810 ms/token, interleaved A/B tools/gpu/ab_b1q.sh), so off
 #define ATTN_PREFETCH 0
 #endif
-// One (kv head, row) of decode attention, by the NW waves of the calling work-group.  PUB: the
-// output is stored with sc1 stores for consumers in other work-groups of the same launch.
-template <int D, int G, int NW, bool PUB>
+// One (kv head, row) of decode attention, by the NW waves of the calling work-group.
+template <int D, int G, int NW>
 __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int c) {
   constexpr int CH = ATTN_CHUNK;
   constexpr int QK = D / 32;  // k-steps of QK^T
@@ -1445,13 +1307,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
       L += f * Ll[ww][h];
       acc += f * Om[ww][h][d];
     }
-    if constexpr (PUB) {
-      const float v = acc / L;
-      const float v1 = __shfl_down(v, 1);  // d + 1 (d even: idx and D are even, lanes adjacent)
-      if ((d & 1) == 0)
-        __builtin_amdgcn_raw_buffer_store_b32(f2bf(v) | (f2bf(v1) << 16), sc_rsrc(a.out),
-                                              (unsigned)(((size_t)c * a.ldo + (kvh * G + h) * D + d) * 2), 0, 16);
-    } else if (a.outf) {
+    if (a.outf) {
       a.outf[(size_t)c * a.ldo + (kvh * G + h) * D + d] = acc / L;
     } else {
       a.out[(size_t)c * a.ldo + (kvh * G + h) * D + d] = (uint16_t)f2bf(acc / L);
@@ -1461,7 +1317,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
 
 template <int D, int G, int NW>
 __global__ __launch_bounds__(64 * NW) void attn_decode_kernel(AttnArgs a) {
-  attn_decode_body<D, G, NW, false>(a, blockIdx.x, blockIdx.y);
+  attn_decode_body<D, G, NW>(a, blockIdx.x, blockIdx.y);
 }
 
 #ifndef ATTN_WAVES
@@ -1483,169 +1339,6 @@ void launch_attention(const AttnArgs& a, hipStream_t s) {
     launch_attn_d<64>(a, s);
   else
     launch_attn_d<128>(a, s);
-}
-
-// ---------------------------------------------------------------------------
-// Attention + attn_output in one launch (<= 4 rows, bf16 weights; opt-in MX_ATTN_O=1 -- measured
-// 1.5 us/layer SLOWER than the two launches, profiles/round1_attn_o_trace.txt).  Every work-group owns one
-// 16-row tile of the attn_output GEMV (8 waves split K) and first issues ALL of its weight loads
-// (they do not depend on attention); work-groups 0 .. n_kv*M-1 also run decode attention for
-// one (kv head, row) and publish it (sc1 stores, drained, then one agent-scope counter add).
-// The GEMV waits on that counter, reads the attention output with sc1 loads and finishes with
-// the residual add.  So the weight stream of attn_output overlaps attention instead of
-// following it, and one launch ramp disappears.  The attention work-groups have the lowest
-// indices and are dispatched first, so the waits always end; each is bounded anyway (2 s, then
-// sync[2] is set and the host reports it).  The last work-group out resets the counters.
-// ---------------------------------------------------------------------------
-constexpr int AO_WAVES = 8;
-constexpr int AO_PREFETCH = 12;  // K-tiles per wave held in registers across the wait (of 16 at K = 4096)
-constexpr long long AO_TIMEOUT = 200000000;  // 100 MHz wall clock: 2 s
-
-// sync layout (uints, one 128-B line each): [0] arrivals, [32] exits, [64] timeout flag,
-// [96 + 32 j] done-flag replica j (AO_REPL of them; work-group g polls replica g % AO_REPL)
-constexpr int AO_REPL = 16;
-template <int D, int G>
-__global__ __launch_bounds__(64 * AO_WAVES) void attn_o_kernel(AttnArgs at, MMArgs a, unsigned* sync, int poll_ticks,
-                                                               int prefetch) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int g = blockIdx.x;
-  const int n_attn = at.n_head_kv * at.M;
-  const int KT = a.K / TILE_K;
-  const int kb = (KT * w) / AO_WAVES, ke = (KT * (w + 1)) / AO_WAVES;
-  __shared__ f32x4 red[AO_WAVES][64];
-  __shared__ unsigned ok_flag;
-  unsigned long long* trace = a.trace ? a.trace + (size_t)g * 4 : nullptr;  // diagnosis only
-  if (trace && threadIdx.x == 0) trace[0] = wall_clock64();
-
-  // 1. this wave's attn_output weights, all in flight before anything else
-  const u32x4* Wp = reinterpret_cast<const u32x4*>(a.W) + (size_t)g * KT * 64 + lane;
-  u32x4 ra[AO_PREFETCH];
-  const int npre = prefetch ? AO_PREFETCH : 0;
-#pragma unroll
-  for (int i = 0; i < AO_PREFETCH; ++i)
-    if (i < npre && kb + i < ke) ra[i] = __builtin_nontemporal_load(Wp + (size_t)(kb + i) * 64);
-
-  // 2. attention for one (kv head, row), published
-  if (g < n_attn) {
-    attn_decode_body<D, G, AO_WAVES, true>(at, g % at.n_head_kv, g / at.n_head_kv);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are done
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      if (trace) trace[1] = wall_clock64();
-      const unsigned old = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (old == (unsigned)n_attn - 1)  // the last attention work-group raises every replica
-        for (int j = 0; j < AO_REPL; ++j)
-          __hip_atomic_store(sync + 96 + 32 * j, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-
-  // 3. wait for all attention work-groups (bounded)
-  if (threadIdx.x == 0) {
-    const long long t0 = wall_clock64();
-    unsigned ok = 1;
-    unsigned* flag = sync + 96 + 32 * (g % AO_REPL);
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-      const long long t1 = wall_clock64();
-      if (t1 - t0 > AO_TIMEOUT) {
-        __hip_atomic_store(sync + 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-      while (wall_clock64() - t1 < poll_ticks) __builtin_amdgcn_s_sleep(2);  // few polls: one line, many CUs
-    }
-    ok_flag = ok;
-    if (trace) trace[2] = wall_clock64();
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no handed-over load moves above the poll
-
-  // 4. the GEMV: B fragments of the attention output (sc1 loads), prefetched tiles, then the rest
-  const int col = (lane & 15) < a.M ? (lane & 15) : a.M - 1;
-  const __amdgpu_buffer_rsrc_t xr = sc_rsrc(a.X);
-  const unsigned xoff = (unsigned)(((size_t)col * a.ldx + (lane >> 4) * 8) * 2);
-  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < AO_PREFETCH; ++i) {
-    if (i < npre && kb + i < ke) {
-      const u32x4 xb = __builtin_amdgcn_raw_buffer_load_b128(xr, xoff + (unsigned)(kb + i) * TILE_K * 2, 0, 16);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ra[i]), __builtin_bit_cast(bf16x8, xb),
-                                                    acc, 0, 0, 0);
-    }
-  }
-  for (int kt0 = kb + npre; kt0 < ke; kt0 += 4) {  // the rest, 4 tiles' loads in flight at a time
-    u32x4 wv[4], xb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (kt0 + j < ke) {
-        wv[j] = __builtin_nontemporal_load(Wp + (size_t)(kt0 + j) * 64);
-        xb[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, xoff + (unsigned)(kt0 + j) * TILE_K * 2, 0, 16);
-      }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (kt0 + j < ke)
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wv[j]), __builtin_bit_cast(bf16x8, xb[j]),
-                                                      acc, 0, 0, 0);
-  }
-  red[w][lane] = acc;
-  __syncthreads();
-  if (w == 0) {  // residual add (one C-layout unit per lane) + this tile's ssq partial
-    f32x4 sacc = red[0][lane];
-#pragma unroll
-    for (int ww = 1; ww < AO_WAVES; ++ww) sacc += red[ww][lane];
-    const int cc = lane & 15;
-    double q = 0.0;
-    if (cc < a.M) {
-      f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)cc * a.ldo + g * 16 + (lane >> 4) * 4);
-      const f32x4 xv = *px + sacc;
-      *px = xv;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) q += (double)(xv[i] * xv[i]);
-    }
-    if (a.ssq) {
-      q += __shfl_xor(q, 16);
-      q += __shfl_xor(q, 32);
-      if (lane < 16 && cc < a.M) a.ssq[(size_t)cc * a.np + g] = (float)q;
-    }
-    // 5. leave; the last work-group out resets the counters for the next launch
-    if (lane == 0) {
-      if (trace) trace[3] = wall_clock64();
-      const unsigned old = __hip_atomic_fetch_add(sync + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (old == gridDim.x - 1) {
-        __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(sync + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int j = 0; j < AO_REPL; ++j)
-          __hip_atomic_store(sync + 96 + 32 * j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  (void)ok_flag;
-}
-
-bool attn_o_supported(const AttnArgs& at, const MMArgs& a) {
-  const int G = at.n_head / at.n_head_kv;
-  return at.M >= 1 && at.M <= 4 && !at.slabs && !at.outf && (at.head_dim == 64 || at.head_dim == 128) &&
-         (G == 1 || G == 2 || G == 4 || G == 8) && a.M == at.M && a.N % TILE_N == 0 && a.K % TILE_K == 0 &&
-         a.N / TILE_N >= at.n_head_kv * at.M && a.X == at.out && a.K / TILE_K >= AO_WAVES;
-}
-
-template <int D>
-static void launch_attn_o_d(const AttnArgs& at, const MMArgs& a, unsigned* sync, hipStream_t s) {
-  const int grid = a.N / TILE_N;
-  static const int poll = getenv("MX_AO_POLL") ? atoi(getenv("MX_AO_POLL")) : 20;  // 100 MHz ticks
-  static const int pre = getenv("MX_AO_NOPREFETCH") ? 0 : 1;
-  switch (at.n_head / at.n_head_kv) {
-    case 1: attn_o_kernel<D, 1><<<grid, 64 * AO_WAVES, 0, s>>>(at, a, sync, poll, pre); break;
-    case 2: attn_o_kernel<D, 2><<<grid, 64 * AO_WAVES, 0, s>>>(at, a, sync, poll, pre); break;
-    case 4: attn_o_kernel<D, 4><<<grid, 64 * AO_WAVES, 0, s>>>(at, a, sync, poll, pre); break;
-    case 8: attn_o_kernel<D, 8><<<grid, 64 * AO_WAVES, 0, s>>>(at, a, sync, poll, pre); break;
-  }
-}
-
-int launch_attn_o(const AttnArgs& at, const MMArgs& a, unsigned* sync, hipStream_t s) {
-  if (!attn_o_supported(at, a) || !sync) return -1;
-  if (at.head_dim == 64) launch_attn_o_d<64>(at, a, sync, s);
-  else launch_attn_o_d<128>(at, a, sync, s);
-  return 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1800,125 +1493,18 @@ namespace mx {
 
 // ---------------------------------------------------------------------------
 // Prefill GEMM (> 64 rows): out = X[M][K] . W[N][K]^T with the decode epilogues, bf16 MFMA
-// 16x16x32, f32 accumulation.  (SURVEY §8a a7, a11, a12 at prefill; §8d prefill FLOPs)
-//
-// Block = 8 waves, tile 256 weight rows x 256 tokens; wave (wn, wm) = 64 rows (4 packed row
-// tiles) x 128 tokens (8 column tiles): 32 MFMAs per 32-deep k-step.  The packed weight tiles are
-// already A fragments, so each wave streams its own straight from global memory one 64-deep
-// chunk ahead (no LDS, no transpose); the block's 256 token rows go through LDS in 64-deep chunks
-// (double buffer, one barrier per chunk) and every wave reads its B fragments there.  Blocks are
-// ordered token-block fastest, so the blocks resident at once share each weight tile through
-// L2 / Infinity Cache instead of re-reading it from HBM.
-// ---------------------------------------------------------------------------
-constexpr int GB_N = 256, GB_M = 256, GKC = 64, GPITCH = GKC + 8;
-
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm_kernel(MMArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t xs[2][GB_M][GPITCH];
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wn = w & 3, wm = w >> 2;
-  const int nmb = (a.M + GB_M - 1) / GB_M;
-  const int mb = blockIdx.x % nmb, nb = blockIdx.x / nmb;
-  const int KT = a.K / TILE_K, NC = a.K / GKC;
-  const int tile0 = nb * (GB_N / 16) + wn * 4;
-  const int m0 = mb * GB_M;
-  const int r16 = lane & 15, q4 = lane >> 4;
-
-  // token-row staging: piece p = tid + 512 i: row p / 8, 16-B segment p % 8 of the 128-B chunk row
-  const u32x4* xsrc[4];
-  int xrow[4], xseg[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int p = threadIdx.x + 512 * i;
-    xrow[i] = p >> 3;
-    xseg[i] = p & 7;
-    const int row = min(m0 + xrow[i], a.M - 1);  // rows past M re-read the last row (outputs dropped)
-    xsrc[i] = reinterpret_cast<const u32x4*>(a.X + (size_t)row * a.ldx + xseg[i] * 8);
-  }
-  u32x4 xr[4];
-  auto load_x = [&](int c) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) xr[i] = xsrc[i][c * (GKC / 8)];
-  };
-  auto store_x = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(&xs[buf][xrow[i]][xseg[i] * 8]) = xr[i];
-  };
-  const u32x4* Wp = reinterpret_cast<const u32x4*>(a.W) + (size_t)tile0 * KT * 64 + lane;
-  u32x4 wa[2][4], wb[2][4];  // A fragments: this chunk's two k-steps, next chunk's
-  auto load_w = [&](u32x4 (&dst)[2][4], int c) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dst[ks][r] = Wp[((size_t)r * KT + c * 2 + ks) * 64];
-  };
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  load_x(0);
-  load_w(wa, 0);
-  store_x(0);
-  __syncthreads();
-  for (int c = 0; c < NC; ++c) {
-    const int buf = c & 1;
-    const bool more = c + 1 < NC;
-    if (more) {
-      load_x(c + 1);
-      load_w(wb, c + 1);
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const u32x4 b = *reinterpret_cast<const u32x4*>(&xs[buf][wm * 128 + j * 16 + r16][ks * 32 + q4 * 8]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wa[ks][r]),
-                                                              __builtin_bit_cast(bf16x8, b), acc[r][j], 0, 0, 0);
-      }
-    }
-    if (more) {
-      store_x(buf ^ 1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) wa[ks][r] = wb[ks][r];
-    }
-    __syncthreads();
-  }
-
-  // epilogue: lane holds rows 16*tile + 4*(lane>>4) + i of token column (lane & 15) per 16x16 tile
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const f32x4 s = acc[r][j];
-      f32x4 up = s;
-      if constexpr (EPI == EPI_SWIGLU) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(s[i], 32);
-      }
-      const int col = m0 + wm * 128 + j * 16 + r16;
-      if (col >= a.M || (EPI == EPI_SWIGLU && lane >= 32)) continue;
-      epi_store<EPI>(a, tile0 + r, lane, col, s, up);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Prefill GEMM v2: both operands staged global -> LDS by LDS-DMA (global_load_lds, 16 B per lane)
+// 16x16x32, f32 accumulation (SURVEY §8a a7, a11, a12 at prefill; §8d prefill FLOPs).  Block = 8
+// waves, tile 256 weight rows x 256 tokens; wave (wn, wm) = 64 rows (4 packed row tiles) x 128
+// tokens (8 column tiles).  Both operands staged global -> LDS by LDS-DMA (global_load_lds, 16 B per lane)
 // into two 64 KiB buffers, one 64-deep K-step ahead, raw barriers with counted vmcnt so the DMA
 // of step s+1 stays in flight while step s is multiplied (cdna_hip_programming.md §5).
 // The packed weight tiles are lane-linear 1 KiB A fragments, so a wave-instruction copies one
 // tile verbatim; token rows are gathered per lane into the same lane-linear B-fragment images
 // (lane l = token l&15, k 8(l>>4)..+8 of a 32-deep k-tile), so every ds_read_b128 is
 // conflict-free without a swizzle.  Blocks are remapped so the token blocks of one weight block
-// run on one XCD (shared L2).  Same epilogues as gemm_kernel.
+// run on one XCD (shared L2).
 // ---------------------------------------------------------------------------
+constexpr int GB_N = 256, GB_M = 256, GKC = 64;
 typedef __attribute__((address_space(1))) const void gvoid;
 typedef __attribute__((address_space(3))) void lvoid;
 
@@ -2024,21 +1610,11 @@ bool gemm_supported(int N, int K) { return N % GB_N == 0 && K % GKC == 0; }
 int launch_gemm(int epi, const MMArgs& a, hipStream_t s) {
   if (a.M < 1 || !a.X || !gemm_supported(a.N, a.K)) return -1;
   const int grid = (a.N / GB_N) * ((a.M + GB_M - 1) / GB_M);
-  static const bool v1 = getenv("MX_GEMM_V1") != nullptr;  // A/B against the register-staged kernel
-  if (!v1) {
-    switch (epi) {
-      case EPI_F32: gemm2_kernel<EPI_F32><<<grid, 512, 0, s>>>(a); return 0;
-      case EPI_RESID: gemm2_kernel<EPI_RESID><<<grid, 512, 0, s>>>(a); return 0;
-      case EPI_QKV: gemm2_kernel<EPI_QKV><<<grid, 512, 0, s>>>(a); return 0;
-      case EPI_SWIGLU: gemm2_kernel<EPI_SWIGLU><<<grid, 512, 0, s>>>(a); return 0;
-    }
-    return -1;
-  }
   switch (epi) {
-    case EPI_F32: gemm_kernel<EPI_F32><<<grid, 512, 0, s>>>(a); return 0;
-    case EPI_RESID: gemm_kernel<EPI_RESID><<<grid, 512, 0, s>>>(a); return 0;
-    case EPI_QKV: gemm_kernel<EPI_QKV><<<grid, 512, 0, s>>>(a); return 0;
-    case EPI_SWIGLU: gemm_kernel<EPI_SWIGLU><<<grid, 512, 0, s>>>(a); return 0;
+    case EPI_F32: gemm2_kernel<EPI_F32><<<grid, 512, 0, s>>>(a); return 0;
+    case EPI_RESID: gemm2_kernel<EPI_RESID><<<grid, 512, 0, s>>>(a); return 0;
+    case EPI_QKV: gemm2_kernel<EPI_QKV><<<grid, 512, 0, s>>>(a); return 0;
+    case EPI_SWIGLU: gemm2_kernel<EPI_SWIGLU><<<grid, 512, 0, s>>>(a); return 0;
   }
   return -1;
 }
@@ -2804,42 +2380,68 @@ int launch_mq8(int epi, const MMArgs& a, hipStream_t s) {
 
 namespace mx {
 
-// Copy-ceiling probe (bench.py hbm_copy_peak): the float4-copy measurement of
-// MI355X_MICROARCH.md, so the decode kernels' HBM fractions can be read against what a plain
-// streaming kernel reaches on the same box.  Each 256-lane group owns 1024 consecutive 16-B words
-// per pass (lane i moves words i, i+256, i+512, i+768: coalesced, four loads in flight).
-__global__ __launch_bounds__(256) void copy_probe_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+// HBM streaming probes (bench.py hbm_probe): what a plain streaming kernel reaches on this box, so
+// the decode kernels' fractions of the 8 TB/s spec can also be read against a measured stream.
+// Each work-group owns 256*U consecutive 16-B words per pass (lane i moves words i, i+256, ...:
+// coalesced, U loads in flight per lane), grid-stride; NT = non-temporal loads (what the GEMVs
+// use for their once-read weights).  The host sweeps (U, grid, NT) and keeps the best.
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void copy_probe_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
                                                          size_t n16) {
-  const size_t stride = (size_t)gridDim.x * 1024;
-  for (size_t i = (size_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += stride) {
-    const uint4 a = src[i], b = src[i + 256], c = src[i + 512], d = src[i + 768];
-    dst[i] = a;
-    dst[i + 256] = b;
-    dst[i + 512] = c;
-    dst[i + 768] = d;
+  const size_t stride = (size_t)gridDim.x * 256 * U;
+  for (size_t i = (size_t)blockIdx.x * 256 * U + threadIdx.x; i < n16; i += stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(src + i + 256 * u) : src[i + 256 * u];
+#pragma unroll
+    for (int u = 0; u < U; ++u) __builtin_nontemporal_store(v[u], dst + i + 256 * u);
   }
 }
 
-void launch_copy_probe(const uint4* src, uint4* dst, size_t n16, hipStream_t s) {
-  copy_probe_kernel<<<2048, 256, 0, s>>>(src, dst, n16);  // 256 CUs x 8 groups
-}
-
-__global__ __launch_bounds__(256) void read_probe_kernel(const uint4* __restrict__ src, uint4* __restrict__ sink,
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void read_probe_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ sink,
                                                          size_t n16) {
-  const size_t stride = (size_t)gridDim.x * 1024;
-  uint4 x = {0u, 0u, 0u, 0u};
-  for (size_t i = (size_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += stride) {
-    const uint4 a = src[i], b = src[i + 256], c = src[i + 512], d = src[i + 768];
-    x.x ^= a.x ^ b.x ^ c.x ^ d.x;
-    x.y ^= a.y ^ b.y ^ c.y ^ d.y;
-    x.z ^= a.z ^ b.z ^ c.z ^ d.z;
-    x.w ^= a.w ^ b.w ^ c.w ^ d.w;
+  const size_t stride = (size_t)gridDim.x * 256 * U;
+  u32x4 x = {0u, 0u, 0u, 0u};
+  for (size_t i = (size_t)blockIdx.x * 256 * U + threadIdx.x; i < n16; i += stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(src + i + 256 * u) : src[i + 256 * u];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x ^= v[u];
   }
-  if (x.x == 0x9e3779b9u && x.y == 0x7f4a7c15u) sink[(size_t)blockIdx.x * 256 + threadIdx.x] = x;
+  // sink written only when the fold hits a sentinel (never for the probe's fill): keeps the loads live
+  if (x[0] == 0x9e3779b9u && x[1] == 0x7f4a7c15u) sink[(size_t)blockIdx.x * 256 + threadIdx.x] = x;
 }
 
-void launch_read_probe(const uint4* src, uint4* sink, size_t n16, hipStream_t s) {
-  read_probe_kernel<<<2048, 256, 0, s>>>(src, sink, n16);
+template <int U, bool NT>
+static void probe_launch(bool read_only, const uint4* src, uint4* dst, size_t n16, int grid, hipStream_t s) {
+  const u32x4* sv = reinterpret_cast<const u32x4*>(src);
+  u32x4* dv = reinterpret_cast<u32x4*>(dst);
+  if (read_only) read_probe_kernel<U, NT><<<grid, 256, 0, s>>>(sv, dv, n16);
+  else copy_probe_kernel<U, NT><<<grid, 256, 0, s>>>(sv, dv, n16);
+}
+
+int probe_variants() { return 3 * 2 * 3; }
+
+// variant v: U in {4, 8, 16} x NT in {0, 1} x grid in {1024, 2048, 4096}; n16 % (256 * 16) == 0
+int launch_probe(int v, bool read_only, const uint4* src, uint4* dst, size_t n16, hipStream_t s, char* desc,
+                 int desc_len) {
+  if (v < 0 || v >= probe_variants() || n16 % (256 * 16)) return -1;
+  const int grids[3] = {1024, 2048, 4096};
+  const int grid = grids[v % 3], nt = (v / 3) % 2, ui = v / 6;
+  const int U = 4 << ui;
+  if (desc) snprintf(desc, desc_len, "%d work-groups x 256 lanes, %d x 16-B loads in flight per lane%s", grid, U,
+                     nt ? ", non-temporal" : "");
+  switch (ui * 2 + nt) {
+    case 0: probe_launch<4, false>(read_only, src, dst, n16, grid, s); break;
+    case 1: probe_launch<4, true>(read_only, src, dst, n16, grid, s); break;
+    case 2: probe_launch<8, false>(read_only, src, dst, n16, grid, s); break;
+    case 3: probe_launch<8, true>(read_only, src, dst, n16, grid, s); break;
+    case 4: probe_launch<16, false>(read_only, src, dst, n16, grid, s); break;
+    case 5: probe_launch<16, true>(read_only, src, dst, n16, grid, s); break;
+  }
+  return 0;
 }
 
 }  // namespace mx

@@ -23,10 +23,10 @@ FINISH_LENGTH, FINISH_STOP, FINISH_ERROR = 0, 1, 2
 
 # every symbol include/mx_engine.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "mx_opts_default", "mx_sampling_default", "mx_last_error", "mx_engine_create", "mx_engine_destroy",
-    "mx_engine_info", "mx_forward_logits", "mx_forward_rows", "mx_submit", "mx_wait", "mx_batch_create",
+    "mx_opts_default", "mx_sampling_default", "mx_last_error", "mx_engine_create", "mx_engine_destroy", "mx_gguf_check",
+    "mx_engine_info", "mx_forward_logits", "mx_forward_rows", "mx_forward_topk", "mx_submit", "mx_wait", "mx_poll", "mx_cancel", "mx_batch_create",
     "mx_batch_step", "mx_batch_ids_device", "mx_batch_bind_ids", "mx_batch_tokens", "mx_batch_destroy", "mx_stage_rows",
-    "mx_profile_kernel", "mx_sync", "mx_debug_pdk_trace", "mx_device_count", "mx_engine_stats",
+    "mx_profile_kernel", "mx_sync", "mx_device_count", "mx_engine_stats",
     "mx_probe_copy", "mx_probe_read",
 ]
 
@@ -49,14 +49,14 @@ class MxModelInfo(ctypes.Structure):
                [("eps", ctypes.c_float), ("rope_base", ctypes.c_float)] + \
                [(n, ctypes.c_int32) for n in ("bos_id", "eos_id", "n_ctx", "n_seq_max", "layer_begin",
                                               "layer_end", "has_embed", "has_head")] + \
-               [("weight_bytes", ctypes.c_uint64), ("persistent_decode", ctypes.c_int32),
-                ("persistent_grid", ctypes.c_int32), ("weight_type", ctypes.c_int32)]
+               [("weight_bytes", ctypes.c_uint64), ("weight_type", ctypes.c_int32)]
 
 
 class MxSampling(ctypes.Structure):
     _fields_ = [("temperature", ctypes.c_float), ("top_k", ctypes.c_int32), ("top_p", ctypes.c_float),
                 ("min_p", ctypes.c_float), ("repeat_penalty", ctypes.c_float), ("repeat_last_n", ctypes.c_int32),
-                ("seed", ctypes.c_uint64), ("ignore_eos", ctypes.c_int32)]
+                ("seed", ctypes.c_uint64), ("ignore_eos", ctypes.c_int32),
+                ("frequency_penalty", ctypes.c_float), ("presence_penalty", ctypes.c_float)]
 
 
 _lib = None
@@ -80,11 +80,15 @@ def lib() -> ctypes.CDLL:
         L.mx_last_error.restype = ctypes.c_char_p
         L.mx_engine_create.argtypes = [ctypes.c_char_p, P(MxOpts), P(vp)]
         L.mx_engine_destroy.argtypes = [vp]
+        L.mx_gguf_check.argtypes = [ctypes.c_char_p]
         L.mx_engine_info.argtypes = [vp, P(MxModelInfo)]
         L.mx_forward_logits.argtypes = [vp, i32, vp, i32, i32, vp]
         L.mx_forward_rows.argtypes = [vp, i32, vp, vp, vp, vp]
+        L.mx_forward_topk.argtypes = [vp, i32, vp, vp, vp, i32, vp, vp]
         L.mx_submit.argtypes = [vp, vp, i32, P(MxSampling), i32, P(u64)]
         L.mx_wait.argtypes = [vp, u64, vp, i32, P(i32), P(i32)]
+        L.mx_poll.argtypes = [vp, u64, i32, vp, i32, P(i32), P(i32)]
+        L.mx_cancel.argtypes = [vp, u64]
         L.mx_batch_create.argtypes = [vp, i32, vp, vp, vp, i32, P(vp)]
         L.mx_batch_step.argtypes = [vp, vp, vp, vp, vp]
         L.mx_batch_ids_device.argtypes = [vp]
@@ -95,9 +99,8 @@ def lib() -> ctypes.CDLL:
         L.mx_stage_rows.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp]
         L.mx_profile_kernel.argtypes = [vp, i32, i32, i32, P(ctypes.c_double), P(ctypes.c_double)]
         L.mx_sync.argtypes = [vp]
-        L.mx_probe_copy.argtypes = [i32, ctypes.c_size_t, i32, P(ctypes.c_double)]
-        L.mx_probe_read.argtypes = [i32, ctypes.c_size_t, i32, P(ctypes.c_double)]
-        L.mx_debug_pdk_trace.argtypes = [vp, i32, i32, vp, i32, P(i32), P(i32)]
+        L.mx_probe_copy.argtypes = [i32, ctypes.c_size_t, i32, P(ctypes.c_double), ctypes.c_char_p, i32]
+        L.mx_probe_read.argtypes = [i32, ctypes.c_size_t, i32, P(ctypes.c_double), ctypes.c_char_p, i32]
         L.mx_device_count.argtypes = [P(i32)]
         L.mx_engine_stats.argtypes = [vp, P(MxStats)]
         for name in EXPORTS:
@@ -119,13 +122,19 @@ def device_count() -> int:
     return n.value
 
 
-def probe_copy(device: int = 0, gib: int = 4, iters: int = 10, read_only: bool = False) -> float:
-    """Measured HBM ceiling in GB/s of a streaming copy kernel ((read + write) bytes / s) or, with
-    read_only, of a streaming read kernel (bytes read / s)."""
+def gguf_check(path: str):
+    """Validate a GGUF container (no GPU needed); raises MxError(MX_ERR_MODEL) with the reason."""
+    _check(lib().mx_gguf_check(path.encode()))
+
+
+def probe_copy(device: int = 0, gib: int = 4, iters: int = 10, read_only: bool = False):
+    """Best streaming rate in GB/s over the probe variants: (read + write) bytes / s of a copy or,
+    with read_only, bytes read / s.  Returns (gbs, description of the winning variant)."""
     gbs = ctypes.c_double()
+    desc = ctypes.create_string_buffer(160)
     fn = lib().mx_probe_read if read_only else lib().mx_probe_copy
-    _check(fn(device, gib << 30, iters, ctypes.byref(gbs)))
-    return gbs.value
+    _check(fn(device, gib << 30, iters, ctypes.byref(gbs), desc, len(desc)))
+    return gbs.value, desc.value.decode()
 
 
 def _check(rc: int):
@@ -173,6 +182,15 @@ class Engine:
                                      out.ctypes.data if out is not None else None))
         return out
 
+    def forward_topk(self, slots, pos, ids, k: int):
+        """Rows forward (<= 64) + the device top-k kernel: (values [n][k], ids [n][k])."""
+        slots, pos, ids = _i32(slots), _i32(pos), _i32(ids)
+        vals = np.empty((len(ids), k), dtype=np.float32)
+        idx = np.empty((len(ids), k), dtype=np.int32)
+        _check(lib().mx_forward_topk(self._h, len(ids), slots.ctypes.data, pos.ctypes.data, ids.ctypes.data, k,
+                                     vals.ctypes.data, idx.ctypes.data))
+        return vals, idx
+
     def stage_rows(self, slots, pos, ids, x_in: int = 0, x_out: int = 0, want_logits: bool = False,
                    stream: int = 0) -> Optional[np.ndarray]:
         slots, pos = _i32(slots), _i32(pos)
@@ -189,23 +207,45 @@ class Engine:
     # -- request API ---------------------------------------------------------
     def submit(self, ids: Sequence[int], max_tokens: int, temperature: float = 0.0, top_k: int = 40,
                top_p: float = 0.95, min_p: float = 0.05, repeat_penalty: float = 1.0, repeat_last_n: int = 64,
-               seed: Optional[int] = None, ignore_eos: bool = False) -> int:
+               seed: Optional[int] = None, ignore_eos: bool = False, frequency_penalty: float = 0.0,
+               presence_penalty: float = 0.0) -> int:
         ids = _i32(ids)
         s = MxSampling()
         lib().mx_sampling_default(ctypes.byref(s))
         s.temperature, s.top_k, s.top_p, s.min_p = temperature, top_k, top_p, min_p
         s.repeat_penalty, s.repeat_last_n, s.ignore_eos = repeat_penalty, repeat_last_n, int(ignore_eos)
+        s.frequency_penalty, s.presence_penalty = frequency_penalty, presence_penalty
         if seed is not None and seed >= 0:
             s.seed = seed
         req = ctypes.c_uint64()
         _check(lib().mx_submit(self._h, ids.ctypes.data, len(ids), ctypes.byref(s), max_tokens, ctypes.byref(req)))
         return req.value
 
-    def wait(self, req: int, cap: int = 8192):
-        out = np.empty(cap, dtype=np.int32)
+    def wait(self, req: int, cap: Optional[int] = None):
+        """Block until the request finishes; (generated ids, finish reason).  The buffer holds the
+        whole context by default; a request that generated more is kept and re-read larger."""
+        cap = cap or self.n_ctx
         n, fin = ctypes.c_int32(), ctypes.c_int32()
-        _check(lib().mx_wait(self._h, req, out.ctypes.data, cap, ctypes.byref(n), ctypes.byref(fin)))
-        return out[: min(n.value, cap)].tolist(), fin.value
+        while True:
+            out = np.empty(cap, dtype=np.int32)
+            rc = lib().mx_wait(self._h, req, out.ctypes.data, cap, ctypes.byref(n), ctypes.byref(fin))
+            if rc == MX_ERR_ARG and n.value > cap:
+                cap = n.value
+                continue
+            _check(rc)
+            return out[: min(n.value, cap)].tolist(), fin.value
+
+    def poll(self, req: int, n_have: int = 0):
+        """Block until the request holds more than n_have ids or finishes: (ids so far, done)."""
+        cap = self.n_ctx
+        out = np.empty(cap, dtype=np.int32)
+        n, done = ctypes.c_int32(), ctypes.c_int32()
+        _check(lib().mx_poll(self._h, req, n_have, out.ctypes.data, cap, ctypes.byref(n), ctypes.byref(done)))
+        return out[: min(n.value, cap)].tolist(), bool(done.value)
+
+    def cancel(self, req: int):
+        """End the request after its current step (finish reason STOP); release it with wait()."""
+        _check(lib().mx_cancel(self._h, req))
 
     def generate(self, ids, max_tokens: int, **kw):
         return self.wait(self.submit(ids, max_tokens, **kw))
@@ -218,15 +258,6 @@ class Engine:
         us, nb = ctypes.c_double(), ctypes.c_double()
         _check(lib().mx_profile_kernel(self._h, kind, M, iters, ctypes.byref(us), ctypes.byref(nb)))
         return us.value, nb.value
-
-    def pdk_trace(self, M: int = 1, pos: int = 100):
-        """One persistent-decode-kernel step with per-phase wall-clock stamps (100 MHz ticks):
-        returns uint64 [grid, nphase, 3] = (start, image built, work end) per work-group and phase."""
-        cap = 512 * (5 * self.info.n_layer + 1) * 3
-        buf = np.zeros(cap, dtype=np.uint64)
-        g, n = ctypes.c_int32(), ctypes.c_int32()
-        _check(lib().mx_debug_pdk_trace(self._h, M, pos, buf.ctypes.data, cap, ctypes.byref(g), ctypes.byref(n)))
-        return buf[:g.value * n.value * 3].reshape(g.value, n.value, 3)
 
     def stats(self) -> dict:
         st = MxStats()

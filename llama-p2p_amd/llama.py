@@ -96,6 +96,8 @@ class Llama:
             raise NotImplementedError("stream=True is not supported (the reference never streams)")
         if logprobs is not None:
             raise NotImplementedError("logprobs are not supported")
+        if typical_p != 1.0:
+            raise NotImplementedError("typical_p != 1.0 is not supported (llama-cpp-python's default 1.0 is)")
         created = int(time.time())
         cid = f"cmpl-{uuid.uuid4()}"
         if isinstance(prompt, str):
@@ -108,15 +110,26 @@ class Llama:
             max_tokens = self._n_ctx - len(prompt_tokens)
         max_tokens = min(max_tokens, self._n_ctx - len(prompt_tokens))
         sd = seed if seed is not None else self._seed
-        toks, finish = self._engine.generate(prompt_tokens, max_tokens, temperature=temperature, top_k=top_k,
-                                             top_p=top_p, min_p=min_p, repeat_penalty=repeat_penalty,
-                                             seed=None if sd == LLAMA_DEFAULT_SEED else sd)
+        req = self._engine.submit(prompt_tokens, max_tokens, temperature=temperature, top_k=top_k, top_p=top_p,
+                                  min_p=min_p, repeat_penalty=repeat_penalty, frequency_penalty=frequency_penalty,
+                                  presence_penalty=presence_penalty, seed=None if sd == LLAMA_DEFAULT_SEED else sd)
+        stops = [s for s in ([stop] if isinstance(stop, str) else list(stop or [])) if s]
+        if stops:  # stop strings end generation as soon as one appears (llama-cpp-python's check per token)
+            n = 0
+            while True:
+                toks, done = self._engine.poll(req, n)
+                n = len(toks)
+                text = self.detokenize(toks, prev_tokens=prompt_tokens).decode("utf-8", errors="ignore")
+                if done or any(s in text for s in stops):
+                    break
+            if not done:
+                self._engine.cancel(req)
+        toks, finish = self._engine.wait(req)
         finish_reason = "stop" if finish == _engine.FINISH_STOP else "length"
         if toks and self.tokenizer_.is_eog(toks[-1]) and finish == _engine.FINISH_STOP:
             toks = toks[:-1]
         text = self.detokenize(toks, prev_tokens=prompt_tokens).decode("utf-8", errors="ignore")
-        stops = [stop] if isinstance(stop, str) else list(stop or [])
-        cut = min((text.find(s) for s in stops if s and s in text), default=-1)
+        cut = min((text.find(s) for s in stops if s in text), default=-1)
         if cut >= 0:
             text = text[:cut]
             finish_reason = "stop"

@@ -6,7 +6,7 @@ machine or on the GPU box and there is no network, so every benchmark and test
 uses *synthetic* weights of the exact LLaMA shapes.  The generator below is the
 single definition of those weights.  It is integer-only up to one float32
 multiply, so the numpy version here, the engine's HIP kernel
-(csrc/kernels_misc.hip: ``synth_value``) and the CPU oracle
+(csrc/kernels.hip: ``synth_value``) and the CPU oracle
 (oracle/llama_oracle.c: ``orc_synth_value``) produce bit-identical bf16 values.
 
     z  = seed*0x9E3779B97F4A7C15 + tensor_id*0xD1B54A32D192ED03 + index   (mod 2^64)
@@ -94,6 +94,9 @@ SHAPES = {
     "test-70b-ffn": LlamaShape("test-70b-ffn", 8192, 1, 64, 8, 28672, 1024, 500000.0, 1e-5),
     # TinyLlama-1.1B hidden/FFN/vocab geometry, one layer (gate/up 704 tiles: 235 groups x <= 3)
     "test-tiny-ffn": LlamaShape("test-tiny-ffn", 2048, 1, 32, 4, 5632, 32000, 10000.0, 1e-5),
+    # Llama-3-8B layers (2 of 32) with the full 128256-token vocabulary: the bench's lm_head / argmax /
+    # top-k instantiations at the real width
+    "test-8b-v128k": LlamaShape("test-8b-v128k", 4096, 2, 32, 8, 14336, 128256, 500000.0, 1e-5, 8192),
 }
 
 _M64 = (1 << 64) - 1

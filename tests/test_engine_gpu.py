@@ -188,54 +188,6 @@ def test_wide_decode_batch_vs_oracle(mx, oracle_mod):
     eng.close()
 
 
-def test_persistent_decode_vs_kernels_and_oracle(mx, oracle_mod):
-    """<= 4-token steps on the Llama-3-8B hidden geometry run as ONE persistent kernel (pdk.hip:
-    grid barriers, sc1 hand-offs, weight ring across phases).  Its logits must match the oracle
-    and the per-op kernel path (MX_NO_PDK=1) within the bf16 tolerance, for 1..4 rows of
-    different slots/positions, and its greedy graph loop must follow the oracle."""
-    from llama_p2p_amd import synth
-
-    name = "test-h4096"
-    shape = synth.SHAPES[name]
-    os.environ["MX_PDK"] = "1"  # opt-in this round
-    try:
-        eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=128, n_seq_max=4)
-    finally:
-        del os.environ["MX_PDK"]
-    assert eng.info.persistent_decode == 1, "persistent decode kernel not enabled on this device"
-    ref_eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=128, n_seq_max=4)
-    assert ref_eng.info.persistent_decode == 0
-    seqs = [_seq(shape, 40, seed=90 + i) for i in range(4)]
-    for e in (eng, ref_eng):
-        for i, s in enumerate(seqs):
-            e.forward_logits(s[:30 + i], 0, slot=i)  # prefill (> 4 rows: kernel path in both)
-    om = oracle_mod.OracleModel(shape, seed=0)
-    for M in (1, 2, 3, 4):
-        slots = list(range(M))
-        pos = [30 + i for i in range(M)]
-        ids = [int(seqs[i][30 + i]) for i in range(M)]
-        got = eng.forward_rows(slots, pos, ids)
-        alt = ref_eng.forward_rows(slots, pos, ids)
-        for i in range(M):
-            ref = om.context(128).eval(seqs[i][:31 + i], 0, all_logits=True)[-1]
-            assert_logits_close(got[i:i + 1], ref[None], f"pdk M={M} row {i}")
-            assert_logits_close(got[i:i + 1], alt[i:i + 1], f"pdk vs kernels M={M} row {i}")
-    # device greedy loop (graph replay of the persistent kernel), 2 sequences
-    G = 16
-    first = [int(np.argmax(eng.forward_rows([i], [31 + i], [int(seqs[i][31 + i])])[0])) for i in range(2)]
-    b = eng.batch(slots=[0, 1], pos=[32, 33], ids=first, max_steps=G)
-    for _ in range(G):
-        b.step()
-    toks = b.tokens()
-    exact = 0
-    for i in range(2):
-        exact += check_greedy_chain(om.context(128), seqs[i][:32 + i], [first[i]] + toks[i].tolist(), f"pdk seq {i}")
-    assert exact >= 0.9 * 2 * (G + 1)
-    b.close()
-    eng.close()
-    ref_eng.close()
-
-
 @pytest.mark.parametrize("name,n_prompt", [("test-tiny", 700), ("test-d128", 300), ("test-h4096", 300)])
 def test_gemm_prefill_vs_oracle(mx, oracle_mod, name, n_prompt):
     """Prompts of > 64 tokens without logits run as 512-row chunks of MFMA GEMMs (prefill path);
@@ -360,31 +312,6 @@ def test_70b_geometry_all_paths(mx, oracle_mod):
     eng.close()
 
 
-def test_fused_attention_attn_output_vs_oracle(mx, oracle_mod):
-    """The opt-in attention + attn_output launch (MX_ATTN_O=1: in-launch hand-off with sc1 stores,
-    an agent-scope counter and flag replicas) gives the oracle's logits at 1 and 3 rows."""
-    from llama_p2p_amd import synth
-
-    name = "test-h4096"
-    shape = synth.SHAPES[name]
-    os.environ["MX_ATTN_O"] = "1"
-    try:
-        eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=128, n_seq_max=4)
-    finally:
-        del os.environ["MX_ATTN_O"]
-    om = oracle_mod.OracleModel(shape, seed=0)
-    seqs = [_seq(shape, 40, seed=90 + i) for i in range(3)]
-    for i, sq in enumerate(seqs):
-        eng.forward_rows([i] * 38, list(range(38)), sq[:38], want_logits=False)
-    got1 = eng.forward_logits(seqs[0][38:39], 38, slot=0)                          # 1 row
-    assert_logits_close(got1, om.context(64).eval(seqs[0][:39], 0)[-1:], "attn_o 1 row")
-    got3 = eng.forward_rows([0, 1, 2], [39, 38, 38], [int(seqs[0][39]), int(seqs[1][38]), int(seqs[2][38])])
-    refs = [om.context(64).eval(seqs[0][:40], 0)[-1], om.context(64).eval(seqs[1][:39], 0)[-1],
-            om.context(64).eval(seqs[2][:39], 0)[-1]]
-    assert_logits_close(got3, np.stack(refs), "attn_o 3 rows")
-    eng.close()
-
-
 def test_long_context_prefill_and_decode(mx, oracle_mod):
     """n_ctx 2048: a 1800-token prompt (GEMM prefill chunks, flash prefill attention over long K/V),
     then decode steps at positions ~1800 (56 attention chunks per row) vs the oracle."""
@@ -405,30 +332,6 @@ def test_long_context_prefill_and_decode(mx, oracle_mod):
         rs.append(octx.eval(ids[p:p + 1], p)[0])
     assert_logits_close(np.stack(gs), np.stack(rs), "decode at ~1800")
     assert_tokens_match(np.stack(gs), np.stack(rs), "decode at ~1800")
-    eng.close()
-
-
-def test_fused_ffn_norm_vs_oracle(mx, oracle_mod):
-    """Opt-in MX_FUSED_NORM=1: attn_output's last work-group writes the ffn RMS_NORM operand
-    (agent release/acquire hand-off) -- same logits as the oracle at 1 and 3 rows."""
-    from llama_p2p_amd import synth
-
-    name = "test-h4096"
-    shape = synth.SHAPES[name]
-    os.environ["MX_FUSED_NORM"] = "1"
-    try:
-        eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=128, n_seq_max=4)
-    finally:
-        del os.environ["MX_FUSED_NORM"]
-    om = oracle_mod.OracleModel(shape, seed=0)
-    seqs = [_seq(shape, 30, seed=140 + i) for i in range(3)]
-    for i, sq in enumerate(seqs):
-        eng.forward_rows([i] * 28, list(range(28)), sq[:28], want_logits=False)
-    got = eng.forward_rows([0, 1, 2], [28] * 3, [int(sq[28]) for sq in seqs])
-    for i, sq in enumerate(seqs):
-        assert_logits_close(got[i:i + 1], om.context(64).eval(sq[:29], 0)[-1:], f"fused norm row {i}")
-    g1 = eng.forward_logits(seqs[0][29:30], 29, slot=0)
-    assert_logits_close(g1, om.context(64).eval(seqs[0][:30], 0)[-1:], "fused norm batch 1")
     eng.close()
 
 
@@ -473,12 +376,13 @@ def test_persistent_gate_up_vs_oracle(mx, oracle_mod, name):
 
 
 def test_hbm_probes_plausible(mx):
-    """The bench's measured HBM ceilings (mx_probe_read / mx_probe_copy): finite, below the 8 TB/s
-    spec, and a read-only stream is not slower than a copy's read + write stream."""
-    rd = mx.probe_copy(0, 1, 4, read_only=True)
-    cp = mx.probe_copy(0, 1, 4)
+    """The bench's measured HBM streaming rates (mx_probe_read / mx_probe_copy, best of the variant
+    sweep): finite, below the 8 TB/s spec, and a read-only stream is not slower than a copy."""
+    rd, rdesc = mx.probe_copy(0, 1, 4, read_only=True)
+    cp, cdesc = mx.probe_copy(0, 1, 4)
     assert 1000.0 < rd < 8400.0, rd
     assert 1000.0 < cp < 8400.0, cp
     assert rd > 0.8 * cp
+    assert "work-groups" in rdesc and "work-groups" in cdesc
     with pytest.raises(mx.MxError):
-        mx._check(mx.lib().mx_probe_read(0, 0, 1, None))  # zero bytes: argument error, no launch
+        mx._check(mx.lib().mx_probe_read(0, 0, 1, None, None, 0))  # zero bytes: argument error, no launch

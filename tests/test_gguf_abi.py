@@ -79,3 +79,96 @@ def test_engine_fails_loudly_without_gpu_or_model():
         pytest.skip("GPU present: covered by the gpu tests")
     with pytest.raises(engine.MxError):
         engine.Engine("synthetic:test-tiny")
+
+
+# ---- crafted headers: the C parser must reject them with MX_ERR_MODEL, never crash or over-read
+def _gguf_bytes(kvs, tensors, data=b"", pad_to=32):
+    """kvs: [(key, type, payload_bytes)]; tensors: [(name, ne, ggml_type, offset)]."""
+    import struct
+
+    def s(x):
+        b = x.encode()
+        return struct.pack("<Q", len(b)) + b
+
+    out = b"GGUF" + struct.pack("<IQQ", 3, len(tensors), len(kvs))
+    for k, t, payload in kvs:
+        out += s(k) + struct.pack("<I", t) + payload
+    for name, ne, typ, off in tensors:
+        out += s(name) + struct.pack("<I", len(ne)) + b"".join(struct.pack("<Q", n) for n in ne)
+        out += struct.pack("<IQ", typ, off)
+    out += b"\0" * ((-len(out)) % pad_to)
+    return out + data
+
+
+def _check_rejects(tmp_path, blob, what):
+    from llama_p2p_amd import engine
+
+    p = tmp_path / "crafted.gguf"
+    p.write_bytes(blob)
+    with pytest.raises(engine.MxError) as ei:
+        engine.gguf_check(str(p))
+    assert ei.value.code == engine.MX_ERR_MODEL, what
+    return str(ei.value)
+
+
+def test_gguf_check_accepts_valid_file(tmp_path):
+    import struct
+
+    from llama_p2p_amd import engine
+
+    p = tmp_path / "ok.gguf"
+    p.write_bytes(_gguf_bytes([("general.alignment", 4, struct.pack("<I", 32))], [("w", [32, 2], 0, 0)],
+                              data=b"\0" * 256))
+    engine.gguf_check(str(p))  # no exception
+
+
+def test_gguf_check_rejects_crafted_headers(tmp_path):
+    import struct
+
+    u32 = lambda v: struct.pack("<I", v)  # noqa: E731
+    data = b"\0" * 256
+    # general.alignment = 0 (was a division by zero) and a non-power-of-two alignment
+    msg = _check_rejects(tmp_path, _gguf_bytes([("general.alignment", 4, u32(0))], [("w", [32], 0, 0)], data), "al 0")
+    assert "alignment" in msg
+    _check_rejects(tmp_path, _gguf_bytes([("general.alignment", 4, u32(24))], [("w", [32], 0, 0)], data), "al 24")
+    # an offset that wraps offset + size past 2^64 (passed the old bounds check)
+    _check_rejects(tmp_path, _gguf_bytes([], [("w", [32], 0, 2 ** 64 - 16)], data), "wrapping offset")
+    # tensor past the end of the file
+    _check_rejects(tmp_path, _gguf_bytes([], [("w", [1024], 0, 0)], data), "past end")
+    # element count overflowing 64 bits
+    _check_rejects(tmp_path, _gguf_bytes([], [("w", [2 ** 40, 2 ** 40], 0, 0)], data), "ne overflow")
+    # ragged block count for a block type (Q8_0 rows of 33 elements)
+    _check_rejects(tmp_path, _gguf_bytes([], [("w", [33], 8, 0)], data), "ragged q8_0")
+    # unknown ggml type
+    _check_rejects(tmp_path, _gguf_bytes([], [("w", [32], 99, 0)], data), "unknown type")
+    # array whose count exceeds the bytes left (would have reserved 2^60 elements)
+    arr = u32(4) + struct.pack("<Q", 2 ** 60)
+    _check_rejects(tmp_path, _gguf_bytes([("a", 9, arr)], [], data), "huge array")
+    # string longer than the file
+    _check_rejects(tmp_path, b"GGUF" + struct.pack("<IQQ", 3, 0, 1) + struct.pack("<Q", 2 ** 62), "huge string")
+
+
+def test_gguf_check_survives_truncation_fuzz(tmp_path):
+    """Every prefix of a valid file and random byte flips: an error or success, never a crash."""
+    from llama_p2p_amd import engine, gguf, synth
+
+    p = str(tmp_path / "t.gguf")
+    gguf.write_synthetic_gguf(p, synth.SHAPES["test-tiny"], seed=1)
+    blob = open(p, "rb").read()
+    hdr_end = 4096
+    q = tmp_path / "f.gguf"
+    for cut in list(range(0, 200, 7)) + [hdr_end // 2, hdr_end]:
+        q.write_bytes(blob[:cut])
+        with pytest.raises(engine.MxError):
+            engine.gguf_check(str(q))
+    rng = np.random.default_rng(0)
+    head = bytearray(blob[:hdr_end])
+    for _ in range(200):
+        b = bytearray(head)
+        for i in rng.integers(8, hdr_end, 4):
+            b[i] = int(rng.integers(0, 256))
+        q.write_bytes(bytes(b) + blob[hdr_end:hdr_end + 1024])
+        try:
+            engine.gguf_check(str(q))
+        except engine.MxError as ex:
+            assert ex.code == engine.MX_ERR_MODEL
