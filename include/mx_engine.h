@@ -114,6 +114,11 @@ int mx_forward_topk(mx_engine* e, int n, const int32_t* slots, const int32_t* po
 /* Request API (what Llama.__call__ uses).  Tokens are generated by the
  * scheduler thread, micro-batched with every other active request. */
 int mx_submit(mx_engine* e, const int32_t* ids, int n, const mx_sampling* s, int max_tokens, uint64_t* req);
+/* n_req requests submitted atomically (all validated first, then queued under one lock): the
+ * scheduler admits them in one round -- one batched prefill, one decode batch.  s: n_req sampling
+ * settings (NULL: defaults); reqs receives the ids. */
+int mx_submit_batch(mx_engine* e, int n_req, const int32_t* const* ids, const int32_t* lens, const mx_sampling* s,
+                    const int32_t* max_tokens, uint64_t* reqs);
 /* Blocks until the request finishes; copies up to cap generated ids and releases the request.
  * If more than cap ids were generated, nothing is released: *n_out is set and MX_ERR_ARG returned,
  * so the caller can retry with a larger buffer. */

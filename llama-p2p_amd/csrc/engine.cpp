@@ -70,6 +70,9 @@ const Shape kShapes[] = {
     {"test-8b-v128k", 4096, 2, 32, 8, 14336, 128256, 500000.f, 1e-5f, 8192},
 };
 
+// decode steps the scheduler runs on the device between host syncs when every active row is greedy
+constexpr int SCHED_KMAX = 8;
+
 // synth.py tensor ids
 constexpr uint64_t TID_TOK_EMBD = 1, TID_OUT_NORM = 2, TID_OUTPUT = 3;
 enum { L_ATTN_NORM, L_Q, L_K, L_V, L_O, L_FFN_NORM, L_GATE, L_UP, L_DOWN };
@@ -226,7 +229,9 @@ struct mx_engine {
                          void* x_out, float* logits_host, hipStream_t s, bool last_row_only = false);
   void scheduler_loop();
   int sched_step(std::vector<Request*>& rows);
-  int prefill(Request* r, std::vector<float>& last_logits);
+  int prefill_batch(std::vector<Request*>& reqs);
+  int* sched_hist = nullptr;        // [MAX_ROWS][SCHED_KMAX] tokens of a multi-step greedy run
+  int* sched_hist_count = nullptr;  // [MAX_ROWS]
   int32_t sample_host(Request* r, const float* logits);
   int32_t sample_chain(Request* r, std::vector<std::pair<float, int>>& c);  // c: top-k, sorted
   void finish(Request* r, int why);
@@ -241,6 +246,7 @@ mx_engine::~mx_engine() {
   if (worker.joinable()) worker.join();
   for (auto& kv : sched_graphs) hipGraphExecDestroy(kv.second);
   if (stream) hipStreamSynchronize(stream);
+
   for (void* p : allocations) hipFree(p);
   if (stream) hipStreamDestroy(stream);
 }
@@ -265,7 +271,8 @@ int mx_engine::init_common() {
   const int nl = le - lb;
   layers.resize(nl);
 
-  // KV cache per layer and slot: K [kv head][pos][dim], V transposed [kv head][dim][pos], f16
+  // KV cache per layer and slot: K and V [kv head][ctx_stride * head_dim] f16 in 1 KiB MFMA B-operand
+  // tiles (kernels.hip kv_k_off / kv_v_off)
   slot_stride = (size_t)n_head_kv * ctx_stride * head_dim;
   layer_kv_stride = slot_stride * n_seq_max;
   if (int rc = alloc((void**)&kcache, layer_kv_stride * nl * sizeof(_Float16))) return rc;
@@ -312,6 +319,8 @@ int mx_engine::init_common() {
   if (int rc = alloc((void**)&d_pos, (size_t)R * 4)) return rc;
   if (int rc = alloc((void**)&d_slot, (size_t)R * 4)) return rc;
   if (int rc = alloc((void**)&d_rowmap, (size_t)R * 4)) return rc;
+  if (int rc = alloc((void**)&sched_hist, (size_t)MAX_ROWS * SCHED_KMAX * 4)) return rc;
+  if (int rc = alloc((void**)&sched_hist_count, (size_t)MAX_ROWS * 4)) return rc;
   if (wq8) {
     const size_t kmax = std::max(n_embd, n_ff);
     if (int rc = alloc((void**)&xq8, (size_t)R * kmax)) return rc;
@@ -1019,45 +1028,127 @@ int32_t mx_engine::sample_chain(Request* r, std::vector<std::pair<float, int>>& 
   return c.back().second;
 }
 
-int mx_engine::prefill(Request* r, std::vector<float>& last) {
-  const int n = (int)r->prompt.size();
-  const int chunk = gemm_ok() ? PREFILL_ROWS : MAX_ROWS;
-  std::vector<int32_t> slots(chunk, r->slot), pos(chunk);
-  last.resize(n_vocab);
-  for (int i = r->reuse; i < n; i += chunk) {
-    int m = std::min(chunk, n - i);
-    for (int j = 0; j < m; j++) pos[j] = i + j;
-    const bool lastc = i + m == n;  // logits of the prompt's last token only
-    if (int rc = forward_rows_chunk(m, slots.data(), pos.data(), r->prompt.data() + i, nullptr, nullptr,
-                                    lastc ? last.data() : nullptr, stream, true))
-      return rc;
+// Prefill of every newly admitted request together (llama.cpp's eval of the prompt, SURVEY §3.2,
+// for all of them in as few forwards as the GEMM chunk allows): their remaining prompt rows back
+// to back, each segment padded to a multiple of 16 rows with throw-away positions past the prompt
+// when that stays inside n_ctx (so the rows form 16-position blocks of one sequence and the flash
+// prefill attention runs; the pad K/V is overwritten by the first decode steps before anything
+// reads it), lm_head only on each request's last prompt row, and the first token by the device
+// argmax (ties -> lowest id) or, for sampling requests, the host sampler chain.
+int mx_engine::prefill_batch(std::vector<Request*>& reqs) {
+  std::vector<int32_t> slots, pos, ids;
+  std::vector<int> end_row(reqs.size());
+  for (size_t q = 0; q < reqs.size(); q++) {
+    Request* r = reqs[q];
+    const int n = (int)r->prompt.size();
+    for (int p = r->reuse; p < n; p++) {
+      slots.push_back(r->slot);
+      pos.push_back(p);
+      ids.push_back(r->prompt[p]);
+    }
+    end_row[q] = (int)slots.size() - 1;
+    const int pad = (16 - (n - r->reuse) % 16) % 16;
+    if (n + pad <= n_ctx)
+      for (int p = n; p < n + pad; p++) {
+        slots.push_back(r->slot);
+        pos.push_back(p);
+        ids.push_back(r->prompt[n - 1]);
+      }
+    r->pos = n;
   }
-  r->pos = n;
+  const int chunk = gemm_ok() ? PREFILL_ROWS : MAX_ROWS;
+  const int total = (int)slots.size();
+  std::vector<int32_t> tok(reqs.size());
+  bool any_sampling = false;
+  for (Request* r : reqs) any_sampling |= r->samp.temperature > 0.f || has_penalties(r->samp);
+  std::vector<float> lg;
+  size_t q0 = 0;  // first request whose last row is not yet evaluated
+  for (int i = 0; i < total;) {
+    // chunk [i, e): at most `chunk` rows and at most MAX_ROWS request ends (logits rows)
+    int e = std::min(total, i + chunk);
+    size_t q1 = q0;
+    while (q1 < reqs.size() && end_row[q1] < e && (int)(q1 - q0) < MAX_ROWS) q1++;
+    if ((int)(q1 - q0) == MAX_ROWS && q1 < reqs.size() && end_row[q1] < e) e = end_row[q1 - 1] + 1;
+    const int m = e - i, n_out = (int)(q1 - q0);
+    std::vector<int32_t> rowmap(n_out);
+    for (int k = 0; k < n_out; k++) rowmap[k] = end_row[q0 + k] - i;
+    hipStream_t st = stream;
+    HIPC(hipMemcpyAsync(d_ids, ids.data() + i, m * 4, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_pos, pos.data() + i, m * 4, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_slot, slots.data() + i, m * 4, hipMemcpyHostToDevice, st));
+    if (n_out) HIPC(hipMemcpyAsync(d_rowmap, rowmap.data(), n_out * 4, hipMemcpyHostToDevice, st));
+    rows_distinct = false;
+    rows_blocked = true;
+    for (int k = 0; k < m && rows_blocked; k++)
+      if (k % 16 && (slots[i + k] != slots[i + k - k % 16] || pos[i + k] != pos[i + k - k % 16] + k % 16))
+        rows_blocked = false;
+    const int frc = enqueue_forward(m, d_ids, d_pos, d_slot, nullptr, nullptr, n_out > 0, n_out ? d_rowmap : nullptr,
+                                    n_out, false, nullptr, nullptr, nullptr, 0, nullptr, 0, st);
+    rows_blocked = false;
+    if (frc) return frc;
+    if (n_out) {
+      launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, nullptr, nullptr, nullptr, 0, nullptr, 0, st);
+      HIPC(hipMemcpyAsync(tok.data() + q0, d_tok, n_out * 4, hipMemcpyDeviceToHost, st));
+      if (any_sampling) {
+        lg.resize((size_t)n_out * n_vocab);
+        HIPC(hipMemcpyAsync(lg.data(), logits, lg.size() * 4, hipMemcpyDeviceToHost, st));
+      }
+    }
+    HIPC(hipStreamSynchronize(st));
+    std::lock_guard<std::mutex> lk(mu);
+    for (int k = 0; k < n_out; k++) {
+      Request* r = reqs[q0 + k];
+      int32_t t = tok[q0 + k];
+      if (r->samp.temperature > 0.f || has_penalties(r->samp)) t = sample_host(r, lg.data() + (size_t)k * n_vocab);
+      r->out.push_back(t);
+      r->next_tok = t;
+    }
+    q0 = q1;
+    i = e;
+  }
   return 0;
 }
 
+// One scheduler round over the active rows.  All greedy (no penalties): K decode steps replayed
+// back to back on the device (the captured step feeds its argmax into the next step's ids and
+// positions and appends it to a history), one sync, then the K tokens of every row are applied in
+// order (a row that finishes early ignores the rest).  Otherwise one step, with the sampler chain
+// on the host (top-k candidates from the device when possible).
 int mx_engine::sched_step(std::vector<Request*>& rows) {
   const int M = (int)rows.size();
   std::vector<int32_t> ids(M), pos(M), slots(M);
   bool all_greedy = true;
+  int room = SCHED_KMAX, need = 1;
   for (int i = 0; i < M; i++) {
     ids[i] = rows[i]->next_tok;
     pos[i] = rows[i]->pos;
     slots[i] = rows[i]->slot;
     if (rows[i]->samp.temperature > 0.f || has_penalties(rows[i]->samp)) all_greedy = false;
+    room = std::min(room, n_ctx - rows[i]->pos);
+    need = std::max(need, rows[i]->max_tokens - (int)rows[i]->out.size());
+  }
+  int K = 1;
+  if (all_greedy) {
+    K = std::max(1, std::min(room, need));
+    std::lock_guard<std::mutex> lk(mu);
+    if (!pending.empty() && !free_slots.empty()) K = 1;  // admit waiting requests at the next round
   }
   hipStream_t s = stream;
   HIPC(hipMemcpyAsync(d_ids, ids.data(), M * 4, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(d_pos, pos.data(), M * 4, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(d_slot, slots.data(), M * 4, hipMemcpyHostToDevice, s));
+  HIPC(hipMemsetAsync(sched_hist_count, 0, M * 4, s));
   rows_distinct = true;  // one row per active request, each its own slot
   struct Reset { bool& f; ~Reset() { f = false; } } reset_distinct{rows_distinct};
+  auto step = [&]() -> int {
+    return enqueue_forward(M, d_ids, d_pos, d_slot, nullptr, nullptr, true, nullptr, M, true, d_ids, d_pos,
+                           sched_hist, SCHED_KMAX, sched_hist_count, SCHED_KMAX, s);
+  };
   auto it = sched_graphs.find(M);
   if (use_graphs && it == sched_graphs.end()) {
     hipGraph_t g;
     HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue_forward(M, d_ids, d_pos, d_slot, nullptr, nullptr, true, nullptr, M, true, nullptr, nullptr,
-                             nullptr, 0, nullptr, 0, s);
+    int rc = step();
     hipError_t ce = hipStreamEndCapture(s, &g);
     if (rc) return rc;
     if (ce != hipSuccess) return fail(MX_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(ce));
@@ -1066,33 +1157,31 @@ int mx_engine::sched_step(std::vector<Request*>& rows) {
     hipGraphDestroy(g);
     it = sched_graphs.emplace(M, ex).first;
   }
-  if (use_graphs) {
-    HIPC(hipGraphLaunch(it->second, s));
-  } else if (int rc = enqueue_forward(M, d_ids, d_pos, d_slot, nullptr, nullptr, true, nullptr, M, true, nullptr,
-                                      nullptr, nullptr, 0, nullptr, 0, s)) {
-    return rc;
+  for (int k = 0; k < K; k++) {
+    if (use_graphs) HIPC(hipGraphLaunch(it->second, s));
+    else if (int rc = step()) return rc;
   }
-  std::vector<int32_t> tok(M);
+  std::vector<int32_t> hist((size_t)M * SCHED_KMAX);
   std::vector<float> lg, tkv;
   std::vector<int32_t> tki;
-  HIPC(hipMemcpyAsync(tok.data(), d_tok, M * 4, hipMemcpyDeviceToHost, s));
-  // sampling rows: the top-k candidates come from the device (k <= TOPK_MAX, no repeat penalty,
-  // which would reorder logits first); otherwise the whole logits rows go to the host
-  int K = 0;
+  HIPC(hipMemcpyAsync(hist.data(), sched_hist, hist.size() * 4, hipMemcpyDeviceToHost, s));
+  // sampling rows: the top-k candidates come from the device (k <= TOPK_MAX, no penalties, which
+  // would reorder logits first); otherwise the whole logits rows go to the host
+  int TK = 0;
   bool dev_topk = !all_greedy && use_dev_topk;
   for (int i = 0; i < M && dev_topk; i++) {
     const mx_sampling& sp = rows[i]->samp;
     if (sp.temperature <= 0.f && !has_penalties(sp)) continue;
     if (has_penalties(sp) || sp.top_k < 1 || sp.top_k > TOPK_MAX) dev_topk = false;
-    else K = std::max(K, std::min(sp.top_k, n_vocab));
+    else TK = std::max(TK, std::min(sp.top_k, n_vocab));
   }
-  if (dev_topk && K > 0) {
-    if (launch_topk(logits, n_vocab, M, n_vocab, K, tk_ws_val, tk_ws_idx, tk_val, tk_idx, s))
+  if (dev_topk && TK > 0) {
+    if (launch_topk(logits, n_vocab, M, n_vocab, TK, tk_ws_val, tk_ws_idx, tk_val, tk_idx, s))
       return fail(MX_ERR_HIP, "top-k launch");
-    tkv.resize((size_t)M * K);
-    tki.resize((size_t)M * K);
-    HIPC(hipMemcpyAsync(tkv.data(), tk_val, (size_t)M * K * 4, hipMemcpyDeviceToHost, s));
-    HIPC(hipMemcpyAsync(tki.data(), tk_idx, (size_t)M * K * 4, hipMemcpyDeviceToHost, s));
+    tkv.resize((size_t)M * TK);
+    tki.resize((size_t)M * TK);
+    HIPC(hipMemcpyAsync(tkv.data(), tk_val, (size_t)M * TK * 4, hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(tki.data(), tk_idx, (size_t)M * TK * 4, hipMemcpyDeviceToHost, s));
   } else if (!all_greedy) {
     lg.resize((size_t)M * n_vocab);
     HIPC(hipMemcpyAsync(lg.data(), logits, (size_t)M * n_vocab * 4, hipMemcpyDeviceToHost, s));
@@ -1101,21 +1190,23 @@ int mx_engine::sched_step(std::vector<Request*>& rows) {
   std::lock_guard<std::mutex> lk(mu);
   for (int i = 0; i < M; i++) {
     Request* r = rows[i];
-    r->pos++;
-    int32_t t = tok[i];
-    if (!all_greedy && (r->samp.temperature > 0.f || has_penalties(r->samp))) {
-      if (!tkv.empty()) {
-        std::vector<std::pair<float, int>> c(std::min(r->samp.top_k, n_vocab));
-        for (size_t j = 0; j < c.size(); j++) c[j] = {tkv[(size_t)i * K + j], tki[(size_t)i * K + j]};
-        t = sample_chain(r, c);
-      } else {
-        t = sample_host(r, lg.data() + (size_t)i * n_vocab);
+    for (int k = 0; k < K && !r->done; k++) {
+      r->pos++;
+      int32_t t = hist[(size_t)i * SCHED_KMAX + k];
+      if (r->samp.temperature > 0.f || has_penalties(r->samp)) {
+        if (!tkv.empty()) {
+          std::vector<std::pair<float, int>> c(std::min(r->samp.top_k, n_vocab));
+          for (size_t j = 0; j < c.size(); j++) c[j] = {tkv[(size_t)i * TK + j], tki[(size_t)i * TK + j]};
+          t = sample_chain(r, c);
+        } else {
+          t = sample_host(r, lg.data() + (size_t)i * n_vocab);
+        }
       }
+      r->out.push_back(t);
+      r->next_tok = t;
+      if ((t == eos && !r->samp.ignore_eos) || r->cancel) finish(r, MX_FINISH_STOP);
+      else if ((int)r->out.size() >= r->max_tokens || r->pos >= n_ctx) finish(r, MX_FINISH_LENGTH);
     }
-    r->out.push_back(t);
-    r->next_tok = t;
-    if ((t == eos && !r->samp.ignore_eos) || r->cancel) finish(r, MX_FINISH_STOP);
-    else if ((int)r->out.size() >= r->max_tokens || r->pos >= n_ctx) finish(r, MX_FINISH_LENGTH);
   }
   return 0;
 }
@@ -1162,21 +1253,20 @@ void mx_engine::scheduler_loop() {
       }
     }
     std::lock_guard<std::mutex> glk(gpu_mu);
-    for (Request* r : admit) {
-      std::vector<float> last;
-      int rc = prefill(r, last);
+    if (!admit.empty()) {
+      const int rc = prefill_batch(admit);
       std::lock_guard<std::mutex> lk(mu);
-      if (rc) {
-        r->error = g_err;
-        finish(r, MX_FINISH_ERROR);
-        continue;
+      for (Request* r : admit) {
+        if (rc) {
+          r->error = g_err;
+          finish(r, MX_FINISH_ERROR);
+          continue;
+        }
+        const int32_t t = r->out.back();
+        if ((t == eos && !r->samp.ignore_eos) || r->cancel) finish(r, MX_FINISH_STOP);
+        else if ((int)r->out.size() >= r->max_tokens || r->pos >= n_ctx) finish(r, MX_FINISH_LENGTH);
+        else active.push_back(r);
       }
-      int32_t t = sample_host(r, last.data());
-      r->out.push_back(t);
-      r->next_tok = t;
-      if ((t == eos && !r->samp.ignore_eos) || r->cancel) finish(r, MX_FINISH_STOP);
-      else if ((int)r->out.size() >= r->max_tokens || r->pos >= n_ctx) finish(r, MX_FINISH_LENGTH);
-      else active.push_back(r);
     }
     std::vector<Request*> rows;
     {
@@ -1349,9 +1439,9 @@ int mx_stage_rows(mx_engine* e, int n, const int32_t* slots, const int32_t* pos,
   return e->forward_rows_chunk(n, slots, pos, ids, x_in, x_out, logits_out, s);
 }
 
-int mx_submit(mx_engine* e, const int32_t* ids, int n, const mx_sampling* s, int max_tokens, uint64_t* req) {
-  if (!e || !ids || n < 1 || !req) return fail(MX_ERR_ARG, "bad arguments");
-  if (!e->has_embed || !e->has_head) return fail(MX_ERR_STATE, "mx_submit needs a full-model engine");
+static int make_request(mx_engine* e, const int32_t* ids, int n, const mx_sampling* s, int max_tokens,
+                        std::unique_ptr<Request>* out) {
+  if (!ids || n < 1) return fail(MX_ERR_ARG, "bad arguments");
   if (n >= e->n_ctx) return fail(MX_ERR_CTX, "Requested tokens (" + std::to_string(n) + ") exceed context window of " +
                                                  std::to_string(e->n_ctx));
   for (int i = 0; i < n; i++)
@@ -1362,13 +1452,29 @@ int mx_submit(mx_engine* e, const int32_t* ids, int n, const mx_sampling* s, int
   if (s) r->samp = *s;
   r->max_tokens = max_tokens <= 0 ? e->n_ctx - n : std::min(max_tokens, e->n_ctx - n);
   r->rng.seed(r->samp.seed == 0xFFFFFFFFull ? std::random_device{}() : r->samp.seed);
+  *out = std::move(r);
+  return 0;
+}
+
+// all-or-nothing: every request is validated first, then all are queued under one lock, so the
+// scheduler admits them in the same round (one batched prefill, one decode batch)
+int mx_submit_batch(mx_engine* e, int n_req, const int32_t* const* ids, const int32_t* lens, const mx_sampling* s,
+                    const int32_t* max_tokens, uint64_t* reqs) {
+  if (!e || n_req < 1 || !ids || !lens || !max_tokens || !reqs) return fail(MX_ERR_ARG, "bad arguments");
+  if (!e->has_embed || !e->has_head) return fail(MX_ERR_STATE, "mx_submit needs a full-model engine");
+  std::vector<std::unique_ptr<Request>> rs(n_req);
+  for (int i = 0; i < n_req; i++)
+    if (int rc = make_request(e, ids[i], lens[i], s ? s + i : nullptr, max_tokens[i], &rs[i])) return rc;
   {
     std::lock_guard<std::mutex> lk(e->mu);
     if (e->stop) return fail(MX_ERR_STATE, "engine shutting down");
-    r->id = e->next_id++;
-    *req = r->id;
-    e->pending.push_back(r.get());
-    e->requests[r->id] = std::move(r);
+    for (int i = 0; i < n_req; i++) {
+      Request* r = rs[i].get();
+      r->id = e->next_id++;
+      reqs[i] = r->id;
+      e->pending.push_back(r);
+      e->requests[r->id] = std::move(rs[i]);
+    }
     if (!e->worker_started) {
       e->worker_started = true;
       e->worker = std::thread([e] { e->scheduler_loop(); });
@@ -1376,6 +1482,12 @@ int mx_submit(mx_engine* e, const int32_t* ids, int n, const mx_sampling* s, int
   }
   e->cv.notify_all();
   return 0;
+}
+
+int mx_submit(mx_engine* e, const int32_t* ids, int n, const mx_sampling* s, int max_tokens, uint64_t* req) {
+  if (!e || !ids || n < 1 || !req) return fail(MX_ERR_ARG, "bad arguments");
+  const int32_t len = n;
+  return mx_submit_batch(e, 1, &ids, &len, s, &max_tokens, req);
 }
 
 int mx_wait(mx_engine* e, uint64_t req, int32_t* out_ids, int cap, int* n_out, int* finish) {
@@ -1765,6 +1877,40 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
   HIPC(hipEventElapsedTime(&ms, t0, t1));
   hipEventDestroy(t0);
   hipEventDestroy(t1);
+  if (kind == 7 && getenv("MX_ATTN_TRACE")) {  // diagnosis: phase stamps of one launch (layer 0)
+    const size_t n = (size_t)M * e->n_head_kv * 8 * 8;
+    unsigned long long* tr = nullptr;
+    HIPC(hipMalloc((void**)&tr, n * 8));
+    HIPC(hipMemsetAsync(tr, 0, n * 8, s));
+    AttnArgs at{};
+    at.q = e->q; at.kc = e->kcache; at.vc = e->vcache; at.pos = e->d_pos; at.slot = e->d_slot; at.out = e->attn_out;
+    at.ldo = h; at.M = M; at.n_head = e->n_head; at.n_head_kv = e->n_head_kv; at.head_dim = e->head_dim;
+    at.n_ctx = e->n_ctx; at.ctx_stride = e->ctx_stride; at.slot_stride = e->slot_stride;
+    at.scale = 1.0f / sqrtf((float)e->head_dim); at.trace = tr;
+    launch_attention(at, s);
+    HIPC(hipStreamSynchronize(s));
+    std::vector<unsigned long long> t(n);
+    HIPC(hipMemcpy(t.data(), tr, n * 8, hipMemcpyDeviceToHost));
+    hipFree(tr);
+    unsigned long long t0m = ~0ull, tend = 0;
+    double ph[5] = {0, 0, 0, 0, 0};
+    int cnt = 0;
+    double chunks = 0;
+    for (size_t g = 0; g < n / 8; g++) {
+      const unsigned long long* p = &t[g * 8];
+      if (!p[0]) continue;
+      t0m = std::min(t0m, p[0]);
+      tend = std::max(tend, p[5]);
+      for (int k = 0; k < 5; k++)
+        if (p[k + 1] >= p[k] && p[k]) ph[k] += (double)(p[k + 1] - p[k]) / 100.0;
+      chunks += (double)p[7];
+      cnt++;
+    }
+    fprintf(stderr, "attn trace M=%d pos=%d: waves %d, span %.2f us (first start -> last end); mean per wave: "
+                    "q %.2f | first K/V %.2f | chunks %.2f (%.2f chunks) | merge wait %.2f | store %.2f us\n",
+            M, prof_pos, cnt, (tend - t0m) / 100.0, ph[0] / cnt, ph[1] / cnt, ph[2] / cnt, chunks / cnt, ph[3] / cnt,
+            ph[4] / cnt);
+  }
   if (us) *us = ms * 1000.0 / launches;
   if (bytes) *bytes = (double)per;
   return 0;

@@ -60,8 +60,8 @@ struct MMArgs {
   const int* pos;              // [M]
   const int* slot;             // [M]
   const float* rope_cs;        // [n_ctx][head_dim/2][2]
-  _Float16* kc;                // K cache of this layer: [slots][n_head_kv][ctx_stride][head_dim]
-  _Float16* vc;                // V cache of this layer, transposed: [slots][n_head_kv][head_dim][ctx_stride]
+  _Float16* kc;                // K cache of this layer: [slots][n_head_kv][ctx_stride * head_dim] (tiled)
+  _Float16* vc;                // V cache of this layer: [slots][n_head_kv][ctx_stride * head_dim] (tiled)
   int n_ctx, ctx_stride, n_head_kv;
   size_t slot_stride;          // elements per slot in kc/vc = n_head_kv*ctx_stride*head_dim
   size_t slab_stride;          // EPI_SLAB: floats between consecutive K-split partial slabs
@@ -69,8 +69,8 @@ struct MMArgs {
 
 struct AttnArgs {
   const float* q;        // [M][n_head*head_dim] f32 (post-RoPE)
-  const _Float16* kc;    // [slots][n_head_kv][ctx_stride][head_dim]
-  const _Float16* vc;    // [slots][n_head_kv][head_dim][ctx_stride]  (transposed)
+  const _Float16* kc;    // [slots][n_head_kv][ctx_stride * head_dim], 1 KiB B-operand tiles (kernels.hip)
+  const _Float16* vc;    // [slots][n_head_kv][ctx_stride * head_dim], 1 KiB B-operand tiles
   const int* pos;        // [M]  query position; attends to [0, pos]
   const int* slot;       // [M]
   uint16_t* out;         // bf16 [M][ldo] (src1 of attn_output)
@@ -86,7 +86,11 @@ struct AttnArgs {
   size_t slab_stride;
   const float* rope_cs;  // [n_ctx][head_dim/2][2]
   _Float16 *kc_w, *vc_w; // writable views of kc / vc
+  // diagnosis only (mx_profile_kernel with MX_ATTN_TRACE): per (row, kv head, wave) 8 wall-clock
+  // stamps (100 MHz) at the kernel's phases; nullptr normally
+  unsigned long long* trace;
 };
+
 
 // packing / synthetic weights.  mode: PACK_ROWS (logical row r -> packed row r + offset),
 // PACK_GATE / PACK_UP (ffn_gate / ffn_up rows interleaved by 8-row halves of each tile)

@@ -367,8 +367,23 @@ __device__ __forceinline__ void xs_build(const XsRegs<MM>& r, const MMArgs& a, u
   }
 }
 
+// KV cache layout.  Each (slot, kv head) owns ctx_stride * D f16 of K and as many of V, stored as
+// 1 KiB tiles in the lane order of the MFMA B operand that reads them, so every wave-instruction
+// of the attention kernels loads one contiguous 1 KiB (llama.cpp keeps K [pos][d] and V transposed
+// [d][pos] for the same reason on the CPU):
+//   K: tile (pos/16, d/32) = 16 positions x 32 dims, lane = pos%16 + 16*((d%32)/8), element d%8
+//      (the B operand of QK^T, v_mfma_f32_16x16x32_f16: k = dims, n = positions)
+//   V: tile (pos/32, d/16) = 32 positions x 16 dims, lane = d%16 + 16*((pos%32)/8), element pos%8
+//      (the B operand of P.V: k = positions, n = dims)
+__device__ __forceinline__ size_t kv_k_off(int pos, int d, int D) {
+  return (((size_t)(pos >> 4) * (D >> 5) + (d >> 5)) * 64 + (pos & 15) + 16 * ((d & 31) >> 3)) * 8 + (d & 7);
+}
+__device__ __forceinline__ size_t kv_v_off(int pos, int d, int D) {
+  return (((size_t)(pos >> 5) * (D >> 4) + (d >> 4)) * 64 + (d & 15) + 16 * ((pos & 31) >> 3)) * 8 + (pos & 7);
+}
+
 // q/k/v rows [row, row+4) of token column `col`: RoPE (mode NORM, adjacent pairs) on q and k,
-// q -> f32 buffer, k -> f16 K cache [pos][d], v -> f16 V cache transposed [d][pos].
+// q -> f32 buffer, k / v -> the f16 K / V caches (layout above).
 __device__ __forceinline__ void qkv_store(const MMArgs& a, int row, int col, f32x4 s) {
   const int d = a.head_dim;
   const int pos = a.pos[col];
@@ -386,14 +401,14 @@ __device__ __forceinline__ void qkv_store(const MMArgs& a, int row, int col, f32
     if (is_q) {
       *reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + row) = o;
     } else {
-      _Float16* kp = a.kc + (size_t)a.slot[col] * a.slot_stride + ((size_t)(rl / d) * a.ctx_stride + pos) * d + dd;
+      _Float16* kp = a.kc + (size_t)a.slot[col] * a.slot_stride + (size_t)(rl / d) * a.ctx_stride * d + kv_k_off(pos, dd, d);
       *reinterpret_cast<f16x4*>(kp) = f16x4{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
     }
   } else {
     const int rl = row - a.n_q - a.n_kv;
-    _Float16* vt = a.vc + (size_t)a.slot[col] * a.slot_stride + ((size_t)(rl / d) * d + rl % d) * a.ctx_stride + pos;
+    _Float16* vh = a.vc + (size_t)a.slot[col] * a.slot_stride + (size_t)(rl / d) * a.ctx_stride * d;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) vt[(size_t)i * a.ctx_stride] = (_Float16)s[i];
+    for (int i = 0; i < 4; ++i) vh[kv_v_off(pos, rl % d + i, d)] = (_Float16)s[i];
   }
 }
 
@@ -1092,19 +1107,48 @@ bool mm_can_norm_on_load(int M, int K) {
 // [pos][d] (B operand of QK^T = contiguous 16 B per lane) and V transposed
 // [d][pos] (B operand of P.V = contiguous 16 B per lane).
 // ---------------------------------------------------------------------------
-#ifndef ATTN_PREFETCH
-// 1: the first K/V chunk is issued right behind q (one round trip instead of two) -- measured
-// SLOWER at batch 1 (2.772 -> 2.810 ms/token, interleaved A/B tools/gpu/ab_b1q.sh), so off
-#define ATTN_PREFETCH 0
-#endif
-// One (kv head, row) of decode attention, by the NW waves of the calling work-group.
-template <int D, int G, int NW>
+// Reductions over the 16 lanes of a DPP row (the 16 positions of one C-layout row): rotations
+// within the row, so every lane ends with the result.  One VOP2-DPP instruction per step (the
+// builtin route adds a move and an fmax canonicalisation per step, and __shfl_xor is a chain of
+// ds_bpermute round trips); "s_nop 1" covers the VALU-write -> DPP-read hazard of the previous step.
+#define MX_ROW_STEP(op, v, n)                                                                        \
+  asm volatile("s_nop 1\n\t" op "_dpp %0, %1, %1 row_ror:" #n " row_mask:0xf bank_mask:0xf" : "=v"(v) \
+               : "v"(v))
+__device__ __forceinline__ float row16_max(float v) {
+  MX_ROW_STEP("v_max_f32", v, 8);
+  MX_ROW_STEP("v_max_f32", v, 4);
+  MX_ROW_STEP("v_max_f32", v, 2);
+  MX_ROW_STEP("v_max_f32", v, 1);
+  return v;
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  MX_ROW_STEP("v_add_f32", v, 8);
+  MX_ROW_STEP("v_add_f32", v, 4);
+  MX_ROW_STEP("v_add_f32", v, 2);
+  MX_ROW_STEP("v_add_f32", v, 1);
+  return v;
+}
+#undef MX_ROW_STEP
+constexpr float LOG2E = 1.4426950408889634f;
+
+// One (kv head, row) of decode attention, by the NW waves of the calling work-group.  Wave w takes
+// chunks w, w + NW, ... and issues each chunk's K/V loads when it reaches it (issuing two chunks
+// ahead measured slower: 18.6 vs 11.1 us at 32 rows, profiles/round2_attention.txt).  FIN: q/k/v
+// still as the wide path's split-K slabs (finished here, see below).  Everything that only the
+// chunk holding `pos` (FIN) or the partial last chunk needs sits behind a wave-uniform branch, so
+// the full chunks run the bare MFMA + softmax stream.
+template <int D, int G, int NW, bool FIN>
 __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int c) {
   constexpr int CH = ATTN_CHUNK;
   constexpr int QK = D / 32;  // k-steps of QK^T
   constexpr int DT = D / 16;  // d tiles of P.V
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r16 = lane & 15, q4 = lane >> 4;
+  unsigned long long* tr = a.trace ? a.trace + (((size_t)c * a.n_head_kv + kvh) * NW + w) * 8 : nullptr;
+  auto stamp = [&](int k) {
+    if (tr && lane == 0) tr[k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   const int pos = a.pos[c];
   const int ctx = min(pos + 1, a.n_ctx);
   const int slot = a.slot[c];
@@ -1114,11 +1158,29 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
   __shared__ float Mm[NW][G], Ll[NW][G];
   __shared__ __attribute__((aligned(16))) float qs[G * D + 2 * D];  // finished q rows, then this position's K, V
 
+  const _Float16* Kb = a.kc + (size_t)slot * a.slot_stride + (size_t)kvh * a.ctx_stride * D;
+  const _Float16* Vb = a.vc + (size_t)slot * a.slot_stride + (size_t)kvh * a.ctx_stride * D;
+  struct KV {
+    f16x8 k[2][QK], v[DT];
+  };
+  auto load = [&](KV& f, int ch) {
+    const int p0 = ch * CH;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int kk = 0; kk < QK; ++kk)
+        f.k[t][kk] = *reinterpret_cast<const f16x8*>(Kb + (((size_t)(p0 / 16 + t) * QK + kk) * 64 + lane) * 8);
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+      f.v[t] = *reinterpret_cast<const f16x8*>(Vb + (((size_t)(p0 / 32) * DT + t) * 64 + lane) * 8);
+  };
+  KV A;
+
   // wide path: q/k/v of this (kv head, token) are still split-K partial slabs -- sum them in slab
   // order (bit-identical to qkv_finish_kernel), RoPE q and k, write this position's K and V into
   // the caches for later steps, and keep all of it in LDS for this step
-  const bool fin = a.slabs != nullptr;
-  if (fin) {
+  constexpr bool fin = FIN;
+  if constexpr (FIN) {
     const int nq = a.n_head * D, nkv = a.n_head_kv * D, N = nq + 2 * nkv;
     for (int u = threadIdx.x; u < (G * D + 2 * D) / 4; u += 64 * NW) {
       const int i = u * 4;  // qs index
@@ -1139,12 +1201,12 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
       if (i >= G * D && pos < a.n_ctx) {
         const size_t sb = (size_t)slot * a.slot_stride;
         if (i < G * D + D) {
-          _Float16* kp = a.kc_w + sb + ((size_t)kvh * a.ctx_stride + pos) * D + dd;
+          _Float16* kp = a.kc_w + sb + (size_t)kvh * a.ctx_stride * D + kv_k_off(pos, dd, D);
           *reinterpret_cast<f16x4*>(kp) = f16x4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
         } else {
-          _Float16* vt = a.vc_w + sb + ((size_t)kvh * D + dd) * a.ctx_stride + pos;
+          _Float16* vh = a.vc_w + sb + (size_t)kvh * a.ctx_stride * D;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) vt[(size_t)j * a.ctx_stride] = (_Float16)v[j];
+          for (int j = 0; j < 4; ++j) vh[kv_v_off(pos, dd + j, D)] = (_Float16)v[j];
         }
       }
     }
@@ -1153,40 +1215,19 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
 
   // A operand of QK^T: rows = heads of the group (rows >= G are zero)
   f16x8 qa[QK];
-  const float* qrow = fin ? qs + (r16 < G ? r16 : 0) * D
-                          : a.q + (size_t)c * a.n_head * D + (size_t)(kvh * G + (r16 < G ? r16 : 0)) * D;
-  f32x4 qv[QK][2];
-#pragma unroll
-  for (int kk = 0; kk < QK; ++kk) {
-    qv[kk][0] = *reinterpret_cast<const f32x4*>(qrow + kk * 32 + 8 * q4);
-    qv[kk][1] = *reinterpret_cast<const f32x4*>(qrow + kk * 32 + 8 * q4 + 4);
-  }
-
-  const _Float16* Kb = a.kc + (size_t)slot * a.slot_stride + (size_t)kvh * a.ctx_stride * D;
-  const _Float16* Vb = a.vc + (size_t)slot * a.slot_stride + (size_t)kvh * D * a.ctx_stride;
-  // this wave's first K/V chunk is issued right behind q (not after q's f16 conversion, which waits
-  // for q): one memory round trip instead of two (rows of a step are distinct sequences or, in
-  // prefill, their K/V was stored by an earlier launch; the wide path's own position comes from LDS)
-  f16x8 kf0[2][QK], vf0[DT];
-  const bool pre = ATTN_PREFETCH && !fin && w * CH < ctx;
-  if (pre) {
-    const int p0 = w * CH, pb = p0 + 8 * q4;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int kk = 0; kk < QK; ++kk)
-        kf0[t][kk] = *reinterpret_cast<const f16x8*>(Kb + (size_t)(p0 + 16 * t + r16) * D + 8 * q4 + kk * 32);
-#pragma unroll
-    for (int t = 0; t < DT; ++t)
-      vf0[t] = *reinterpret_cast<const f16x8*>(Vb + (size_t)(t * 16 + r16) * a.ctx_stride + pb);
-  }
-#pragma unroll
-  for (int kk = 0; kk < QK; ++kk) {
+  {
+    const float* qrow = fin ? qs + (r16 < G ? r16 : 0) * D
+                            : a.q + (size_t)c * a.n_head * D + (size_t)(kvh * G + (r16 < G ? r16 : 0)) * D;
     const bool live = r16 < G;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      qa[kk][j] = live ? (_Float16)qv[kk][0][j] : (_Float16)0.f;
-      qa[kk][4 + j] = live ? (_Float16)qv[kk][1][j] : (_Float16)0.f;
+    for (int kk = 0; kk < QK; ++kk) {
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(qrow + kk * 32 + 8 * q4);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(qrow + kk * 32 + 8 * q4 + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        qa[kk][j] = live ? (_Float16)v0[j] : (_Float16)0.f;
+        qa[kk][4 + j] = live ? (_Float16)v1[j] : (_Float16)0.f;
+      }
     }
   }
 
@@ -1199,66 +1240,52 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
   f32x4 o[DT];
 #pragma unroll
   for (int t = 0; t < DT; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int ch = w; ch * CH < ctx; ch += NW) {
+  if (tr) {
+    __builtin_amdgcn_s_waitcnt(0);
+    stamp(1);  // q in registers
+  }
+  int nch = 0;
+  auto compute = [&](KV& f, int ch) {
     const int p0 = ch * CH;
-    // issue this chunk's K and V fragment loads together: one memory round trip per chunk
-    f16x8 kf[2][QK], vf[DT];
     const int pb = p0 + 8 * q4;  // first position of this lane's P.V B fragment
-    if (pre && ch == w) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int kk = 0; kk < QK; ++kk) kf[t][kk] = kf0[t][kk];
-#pragma unroll
-      for (int t = 0; t < DT; ++t) vf[t] = vf0[t];
-    } else {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int kk = 0; kk < QK; ++kk)
-          kf[t][kk] = *reinterpret_cast<const f16x8*>(Kb + (size_t)(p0 + 16 * t + r16) * D + 8 * q4 + kk * 32);
-#pragma unroll
-      for (int t = 0; t < DT; ++t)
-        vf[t] = *reinterpret_cast<const f16x8*>(Vb + (size_t)(t * 16 + r16) * a.ctx_stride + pb);
-    }
-    if (fin) {  // this position's K/V: the values just finished in LDS (the cache lines may be in flight)
+    if (FIN && pos >= p0 && pos < p0 + CH) {  // this position's K/V from LDS (its stores may be in flight)
 #pragma unroll
       for (int t = 0; t < 2; ++t)
         if (p0 + 16 * t + r16 == pos)
 #pragma unroll
           for (int kk = 0; kk < QK; ++kk)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) kf[t][kk][j] = (_Float16)qs[G * D + 8 * q4 + kk * 32 + j];
+            for (int j = 0; j < 8; ++j) f.k[t][kk][j] = (_Float16)qs[G * D + 8 * q4 + kk * 32 + j];
       if (pos >= pb && pos < pb + 8)
 #pragma unroll
-        for (int t = 0; t < DT; ++t) vf[t][pos - pb] = (_Float16)qs[G * D + D + t * 16 + r16];
+        for (int t = 0; t < DT; ++t) f.v[t][pos - pb] = (_Float16)qs[G * D + D + t * 16 + r16];
     }
+    if (tr && nch == 0) {
+      __builtin_amdgcn_s_waitcnt(0);
+      stamp(2);  // first chunk's K/V landed
+    }
+    nch++;
     // S[head][pos] for two 16-position tiles
-    f32x4 s[2];
+    f32x4 sc[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < QK; ++kk) s[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qa[kk], kf[t][kk], s[t], 0, 0, 0);
+      for (int kk = 0; kk < QK; ++kk) sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qa[kk], f.k[t][kk], sc[t], 0, 0, 0);
     }
-    // online softmax: C layout rows = heads 4*q4+i, cols = positions (lane r16)
+    // online softmax in the log2 domain (scores pre-multiplied by log2 e, v_exp_f32 = 2^x):
+    // C layout rows = heads 4*q4+i, cols = positions (lane r16)
     float e[2][4];
+    const float sl2 = a.scale * LOG2E;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float v0 = (p0 + r16 < ctx) ? s[0][i] * a.scale : -INFINITY;
-      float v1 = (p0 + 16 + r16 < ctx) ? s[1][i] * a.scale : -INFINITY;
-      float mx = fmaxf(v0, v1);
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
-      const float m_new = fmaxf(m_i[i], mx);
-      const float alpha = expf(m_i[i] - m_new);  // 0 on the first chunk (m_i = -inf)
-      e[0][i] = expf(v0 - m_new);
-      e[1][i] = expf(v1 - m_new);
-      float ls = e[0][i] + e[1][i];
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) ls += __shfl_xor(ls, off);
-      l_i[i] = l_i[i] * alpha + ls;
+      const float v0 = (p0 + r16 < ctx) ? sc[0][i] * sl2 : -INFINITY;
+      const float v1 = (p0 + 16 + r16 < ctx) ? sc[1][i] * sl2 : -INFINITY;
+      const float m_new = fmaxf(m_i[i], row16_max(fmaxf(v0, v1)));
+      const float alpha = __builtin_amdgcn_exp2f(m_i[i] - m_new);  // 0 on the first chunk (m_i = -inf)
+      e[0][i] = __builtin_amdgcn_exp2f(v0 - m_new);
+      e[1][i] = __builtin_amdgcn_exp2f(v1 - m_new);
+      l_i[i] = l_i[i] * alpha + row16_sum(e[0][i] + e[1][i]);
       m_i[i] = m_new;
 #pragma unroll
       for (int t = 0; t < DT; ++t) o[t][i] *= alpha;
@@ -1271,15 +1298,22 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
     __builtin_amdgcn_wave_barrier();
     const f16x8 pa = *reinterpret_cast<const f16x8*>(&Ps[w][r16][8 * q4]);
+    if (p0 + CH > ctx) {  // the partial last chunk: never-written positions must not reach P.V
 #pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      f16x8 vb = vf[t];
+      for (int t = 0; t < DT; ++t)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) vb[j] = (pb + j < ctx) ? vb[j] : (_Float16)0.f;
-      o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa, vb, o[t], 0, 0, 0);
+        for (int j = 0; j < 8; ++j) f.v[t][j] = (pb + j < ctx) ? f.v[t][j] : (_Float16)0.f;
     }
+#pragma unroll
+    for (int t = 0; t < DT; ++t) o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa, f.v[t], o[t], 0, 0, 0);
     __builtin_amdgcn_wave_barrier();  // Ps[w] is rewritten next chunk only after every lane read it
+  };
+  for (int ch = w; ch * CH < ctx; ch += NW) {
+    load(A, ch);
+    compute(A, ch);
   }
+  stamp(3);  // chunk loop done
+  if (tr && lane == 0) tr[7] = nch;
 
   // merge the NW wave partials
 #pragma unroll
@@ -1295,6 +1329,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
     }
   }
   __syncthreads();
+  stamp(4);  // partials in LDS
   for (int idx = threadIdx.x; idx < G * D; idx += 64 * NW) {
     const int h = idx / D, d = idx % D;
     float M = -INFINITY;
@@ -1303,7 +1338,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
     float L = 0.f, acc = 0.f;
 #pragma unroll
     for (int ww = 0; ww < NW; ++ww) {
-      const float f = (Mm[ww][h] == -INFINITY) ? 0.f : expf(Mm[ww][h] - M);
+      const float f = (Mm[ww][h] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(Mm[ww][h] - M);
       L += f * Ll[ww][h];
       acc += f * Om[ww][h][d];
     }
@@ -1313,25 +1348,35 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
       a.out[(size_t)c * a.ldo + (kvh * G + h) * D + d] = (uint16_t)f2bf(acc / L);
     }
   }
+  if (tr) {
+    __builtin_amdgcn_s_waitcnt(0);
+    stamp(5);  // outputs stored
+  }
 }
 
-template <int D, int G, int NW>
+template <int D, int G, int NW, bool FIN>
 __global__ __launch_bounds__(64 * NW) void attn_decode_kernel(AttnArgs a) {
-  attn_decode_body<D, G, NW>(a, blockIdx.x, blockIdx.y);
+  attn_decode_body<D, G, NW, FIN>(a, blockIdx.x, blockIdx.y);
 }
 
 #ifndef ATTN_WAVES
 #define ATTN_WAVES 8  // 16 waves measured slower (merge of 16 partials; tools/gpu/ab_lib.sh)
 #endif
-template <int D>
-static void launch_attn_d(const AttnArgs& a, hipStream_t s) {
+template <int D, bool FIN>
+static void launch_attn_df(const AttnArgs& a, hipStream_t s) {
   dim3 grid(a.n_head_kv, a.M);
   switch (a.n_head / a.n_head_kv) {
-    case 1: attn_decode_kernel<D, 1, ATTN_WAVES><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
-    case 2: attn_decode_kernel<D, 2, ATTN_WAVES><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
-    case 4: attn_decode_kernel<D, 4, ATTN_WAVES><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
-    case 8: attn_decode_kernel<D, 8, ATTN_WAVES><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
+    case 1: attn_decode_kernel<D, 1, ATTN_WAVES, FIN><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
+    case 2: attn_decode_kernel<D, 2, ATTN_WAVES, FIN><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
+    case 4: attn_decode_kernel<D, 4, ATTN_WAVES, FIN><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
+    case 8: attn_decode_kernel<D, 8, ATTN_WAVES, FIN><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
   }
+}
+
+template <int D>
+static void launch_attn_d(const AttnArgs& a, hipStream_t s) {
+  if (a.slabs) launch_attn_df<D, true>(a, s);
+  else launch_attn_df<D, false>(a, s);
 }
 
 void launch_attention(const AttnArgs& a, hipStream_t s) {
@@ -1661,7 +1706,7 @@ __global__ __launch_bounds__(64 * G) void attn_prefill_kernel(AttnArgs a) {
     }
   }
   const _Float16* Kb = a.kc + (size_t)slot * a.slot_stride + (size_t)kvh * a.ctx_stride * D;
-  const _Float16* Vb = a.vc + (size_t)slot * a.slot_stride + (size_t)kvh * D * a.ctx_stride;
+  const _Float16* Vb = a.vc + (size_t)slot * a.slot_stride + (size_t)kvh * a.ctx_stride * D;
   float m_i[4], l_i[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -1678,11 +1723,11 @@ __global__ __launch_bounds__(64 * G) void attn_prefill_kernel(AttnArgs a) {
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int kk = 0; kk < QK; ++kk)
-        kf[t][kk] = *reinterpret_cast<const f16x8*>(Kb + (size_t)(p0 + 16 * t + r16) * D + 8 * q4 + kk * 32);
+        kf[t][kk] = *reinterpret_cast<const f16x8*>(Kb + (((size_t)(p0 / 16 + t) * QK + kk) * 64 + lane) * 8);
     const int pb = p0 + 8 * q4;
 #pragma unroll
     for (int t = 0; t < DT; ++t)
-      vf[t] = *reinterpret_cast<const f16x8*>(Vb + (size_t)(t * 16 + r16) * a.ctx_stride + pb);
+      vf[t] = *reinterpret_cast<const f16x8*>(Vb + (((size_t)(p0 / 32) * DT + t) * 64 + lane) * 8);
     f32x4 s[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -1697,16 +1742,12 @@ __global__ __launch_bounds__(64 * G) void attn_prefill_kernel(AttnArgs a) {
       const int qp = pos0 + 4 * q4 + i;
       const float v0 = (p0 + r16 <= qp) ? s[0][i] * a.scale : -INFINITY;
       const float v1 = (p0 + 16 + r16 <= qp) ? s[1][i] * a.scale : -INFINITY;
-      float mx = fmaxf(v0, v1);
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+      const float mx = row16_max(fmaxf(v0, v1));
       const float m_new = fmaxf(m_i[i], mx);
       const float alpha = (m_new == -INFINITY) ? 1.f : expf(m_i[i] - m_new);
       e[0][i] = (m_new == -INFINITY) ? 0.f : expf(v0 - m_new);
       e[1][i] = (m_new == -INFINITY) ? 0.f : expf(v1 - m_new);
-      float ls = e[0][i] + e[1][i];
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) ls += __shfl_xor(ls, off);
+      const float ls = row16_sum(e[0][i] + e[1][i]);
       l_i[i] = l_i[i] * alpha + ls;
       m_i[i] = m_new;
 #pragma unroll

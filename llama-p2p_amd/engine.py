@@ -24,7 +24,7 @@ FINISH_LENGTH, FINISH_STOP, FINISH_ERROR = 0, 1, 2
 # every symbol include/mx_engine.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "mx_opts_default", "mx_sampling_default", "mx_last_error", "mx_engine_create", "mx_engine_destroy", "mx_gguf_check",
-    "mx_engine_info", "mx_forward_logits", "mx_forward_rows", "mx_forward_topk", "mx_submit", "mx_wait", "mx_poll", "mx_cancel", "mx_batch_create",
+    "mx_engine_info", "mx_forward_logits", "mx_forward_rows", "mx_forward_topk", "mx_submit", "mx_wait", "mx_submit_batch", "mx_poll", "mx_cancel", "mx_batch_create",
     "mx_batch_step", "mx_batch_ids_device", "mx_batch_bind_ids", "mx_batch_tokens", "mx_batch_destroy", "mx_stage_rows",
     "mx_profile_kernel", "mx_sync", "mx_device_count", "mx_engine_stats",
     "mx_probe_copy", "mx_probe_read",
@@ -87,6 +87,7 @@ def lib() -> ctypes.CDLL:
         L.mx_forward_topk.argtypes = [vp, i32, vp, vp, vp, i32, vp, vp]
         L.mx_submit.argtypes = [vp, vp, i32, P(MxSampling), i32, P(u64)]
         L.mx_wait.argtypes = [vp, u64, vp, i32, P(i32), P(i32)]
+        L.mx_submit_batch.argtypes = [vp, i32, vp, vp, vp, vp, P(u64)]
         L.mx_poll.argtypes = [vp, u64, i32, vp, i32, P(i32), P(i32)]
         L.mx_cancel.argtypes = [vp, u64]
         L.mx_batch_create.argtypes = [vp, i32, vp, vp, vp, i32, P(vp)]
@@ -220,6 +221,29 @@ class Engine:
         req = ctypes.c_uint64()
         _check(lib().mx_submit(self._h, ids.ctypes.data, len(ids), ctypes.byref(s), max_tokens, ctypes.byref(req)))
         return req.value
+
+    def submit_many(self, prompts, max_tokens: int, seeds=None, **kw):
+        """Several requests queued atomically (one scheduler round admits them all); same sampling
+        keywords as submit(), one seed per prompt.  Returns the request ids."""
+        n = len(prompts)
+        arrs = [_i32(p) for p in prompts]
+        ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
+        lens = _i32([len(a) for a in arrs])
+        mts = _i32([max_tokens] * n)
+        samp = (MxSampling * n)()
+        for i in range(n):
+            lib().mx_sampling_default(ctypes.byref(samp[i]))
+            s = samp[i]
+            s.temperature, s.top_k = kw.get("temperature", 0.0), kw.get("top_k", 40)
+            s.top_p, s.min_p = kw.get("top_p", 0.95), kw.get("min_p", 0.05)
+            s.repeat_penalty, s.repeat_last_n = kw.get("repeat_penalty", 1.0), kw.get("repeat_last_n", 64)
+            s.ignore_eos = int(kw.get("ignore_eos", False))
+            s.frequency_penalty, s.presence_penalty = kw.get("frequency_penalty", 0.0), kw.get("presence_penalty", 0.0)
+            if seeds is not None and seeds[i] is not None and seeds[i] >= 0:
+                s.seed = seeds[i]
+        reqs = (ctypes.c_uint64 * n)()
+        _check(lib().mx_submit_batch(self._h, n, ptrs, lens.ctypes.data, samp, mts.ctypes.data, reqs))
+        return list(reqs)
 
     def wait(self, req: int, cap: Optional[int] = None):
         """Block until the request finishes; (generated ids, finish reason).  The buffer holds the

@@ -16,6 +16,13 @@ together and are micro-batched on the GPU, while concurrent *identical*
 prompts still compute once (the second waits for the first, as with the lock).
 The cache contents and eviction order are unchanged.
 
+The request handler keeps its signature but no longer answers one message at a
+time: the reference's single lock-step ``Rep0`` loop (p2p:84-98) becomes
+``n_contexts`` concurrent REP contexts (nng's ``Rep0`` contexts; SURVEY.md §8f
+item 1), each a worker that receives, runs ``cached_inference`` and replies on
+its own context, so concurrent requests from the wire reach the engine together
+and are micro-batched.  A transport without contexts keeps the lock-step loop.
+
 The gossip (zmq PUB/SUB) and RPC (nng REQ/REP) transports are the reference's
 control plane and are out of scope; they are imported
 lazily, and tests inject in-process transports instead.
@@ -40,7 +47,7 @@ class Timeout(Exception):
 
 class LlamaP2PNode:
     def __init__(self, model_path, port, known_peers=None, cache_size=100, secret_key=None, *, model=None,
-                 transport=None, llama_kwargs=None):
+                 transport=None, llama_kwargs=None, n_contexts=64):
         """``model`` injects an already-built Llama; ``transport`` injects the networking
         (an object with gossip/subscriber/reply sockets and ``dial(peer)``); without
         it, zmq + pynng are used as in the reference (p2p:24-31)."""
@@ -61,6 +68,7 @@ class LlamaP2PNode:
         self.active = True
         self.secret_key = secret_key or secrets.token_hex(16)
         self.peer_performance = defaultdict(lambda: {"success": 0, "failure": 0, "avg_time": 0})
+        self.n_contexts = n_contexts
 
     # ------------------------------------------------------------ lifecycle
     def start(self, cli: bool = True):
@@ -111,24 +119,55 @@ class LlamaP2PNode:
 
     # ------------------------------------------------------- drop-in boundary
     def handle_requests(self):
+        """p2p:84-98.  With a transport that opens REP contexts: n_contexts workers, each receiving
+        on its own context and replying on it, so requests are served concurrently; otherwise the
+        reference's lock-step loop on the one reply socket."""
+        new_context = getattr(self.transport, "new_context", None)
+        if new_context is None or self.n_contexts <= 1:
+            while self.active:
+                try:
+                    msg = self.transport.recv(timeout=100)
+                    self.handle_one(msg)
+                except Timeout:
+                    continue
+                except Exception as e:
+                    log.error(f"Error handling request: {e}")
+            return
+        workers = [threading.Thread(target=self._context_loop, args=(new_context(),), daemon=True)
+                   for _ in range(self.n_contexts)]
+        for w in workers:
+            w.start()
+        for w in workers:
+            w.join()
+
+    def _context_loop(self, ctx):
         while self.active:
             try:
-                msg = self.transport.recv(timeout=100)
-                self.handle_one(msg)
+                msg = ctx.recv(timeout=100)
             except Timeout:
                 continue
             except Exception as e:
                 log.error(f"Error handling request: {e}")
+                continue
+            try:
+                self.handle_one(msg, reply=ctx)
+            except Exception as e:  # as the reference: logged, no reply on this context
+                log.error(f"Error handling request: {e}")
+        close = getattr(ctx, "close", None)
+        if close:
+            close()
 
-    def handle_one(self, msg: bytes):
-        """Body of the handler loop for one message (p2p:88-94); raises like the reference."""
+    def handle_one(self, msg: bytes, reply=None):
+        """Body of the handler loop for one message (p2p:88-94); raises like the reference.
+        ``reply``: the REP context the message came from (default: the transport's socket)."""
+        out = reply if reply is not None else self.transport
         request = json.loads(msg.decode())
         if request["type"] == "inference" and request.get("secret_key") == self.secret_key:
             result = self.cached_inference(request["prompt"])
             response = {"result": result}
-            self.transport.send(json.dumps(response).encode())
+            out.send(json.dumps(response).encode())
         else:
-            self.transport.send(json.dumps({"error": "Unauthorized"}).encode())
+            out.send(json.dumps({"error": "Unauthorized"}).encode())
 
     def cached_inference(self, prompt):
         with self.lock:
@@ -249,6 +288,7 @@ class _NetTransport:
         self.subscriber = self.context.socket(zmq.SUB)
         self.subscriber.setsockopt_string(zmq.SUBSCRIBE, "")
         self.reply_socket = pynng.Rep0()
+        self.reply_socket.recv_timeout = 100  # ms: lets the context workers notice shutdown
         self.reply_socket.listen(f"tcp://0.0.0.0:{port + 1}")
 
     def connect(self, peer):
@@ -272,6 +312,11 @@ class _NetTransport:
     def send(self, data):
         self.reply_socket.send(data)
 
+    def new_context(self):
+        """A REP context of the reply socket (nng: each context has its own receive/reply state,
+        so several requests are in progress at once on one socket)."""
+        return _NetContext(self.reply_socket.new_context(), self._pynng)
+
     def request(self, peer, data):
         with self._pynng.Req0() as s:
             s.dial(f"tcp://{peer}")
@@ -283,3 +328,82 @@ class _NetTransport:
         self.subscriber.close()
         self.reply_socket.close()
         self.context.term()
+
+
+class _NetContext:
+    def __init__(self, ctx, pynng):
+        self._ctx, self._pynng = ctx, pynng
+
+    def recv(self, timeout=100):  # the socket's recv_timeout bounds the wait
+        try:
+            return self._ctx.recv()
+        except self._pynng.Timeout:
+            raise Timeout()
+
+    def send(self, data):
+        self._ctx.send(data)
+
+    def close(self):
+        self._ctx.close()
+
+
+class LocalTransport:
+    """In-process stand-in for the node's nng REP socket with concurrent contexts: clients call
+    ``request(data)`` (blocking, like a Req0 round trip); the node's context workers receive the
+    messages in arrival order and each reply goes back to the client that sent that message.
+    Used to drive ``handle_requests`` without a network (tests, tools/serve_config3.py)."""
+
+    def __init__(self):
+        import queue
+
+        self._q = queue.Queue()
+        self._queue_mod = queue
+
+    # client side
+    def request(self, data: bytes, timeout: float = 600.0) -> bytes:
+        box = {"ev": threading.Event(), "reply": None}
+        self._q.put((data, box))
+        if not box["ev"].wait(timeout):
+            raise TimeoutError("no reply")
+        return box["reply"]
+
+    # node side (the reference's control-plane calls are no-ops here)
+    def connect(self, peer): pass
+    def publish(self, msg): pass
+    def poll_gossip(self): return None
+    def close(self): pass
+
+    def recv(self, timeout=100):  # lock-step mode: the one context
+        return self._ctx.recv(timeout)
+
+    def send(self, data):
+        self._ctx.send(data)
+
+    @property
+    def _ctx(self):
+        if not hasattr(self, "_default"):
+            self._default = self.new_context()
+        return self._default
+
+    def new_context(self):
+        return _LocalContext(self)
+
+
+class _LocalContext:
+    def __init__(self, t: LocalTransport):
+        self._t = t
+        self._box = None
+
+    def recv(self, timeout=100):
+        try:
+            data, self._box = self._t._q.get(timeout=timeout / 1000.0)
+        except self._t._queue_mod.Empty:
+            raise Timeout()
+        return data
+
+    def send(self, data):
+        box, self._box = self._box, None
+        if box is None:
+            raise RuntimeError("send without a received request (REP state machine)")
+        box["reply"] = data
+        box["ev"].set()

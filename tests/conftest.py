@@ -73,3 +73,24 @@ def check_greedy_chain(octx, prompt, tokens, what=""):
             lg = octx.eval([t], pos)[0]
             pos += 1
     return exact
+
+
+def check_chain_batched(octx, prompt, tokens, what=""):
+    """Teacher-force the oracle along the engine's greedy tokens in ONE evaluation (all logits of
+    prompt + tokens[:-1]); every pick must be the oracle argmax or a near tie (2x tolerance).
+    Returns (exact matches, near-tie positions)."""
+    import numpy as np
+
+    seq = np.concatenate([np.asarray(prompt, np.int32), np.asarray(tokens[:-1], np.int32)])
+    lg = octx.eval(seq, 0, all_logits=True)[len(prompt) - 1:]
+    exact, ties = 0, []
+    for k, t in enumerate(tokens):
+        row = lg[k]
+        tol = 2 * (1e-2 * abs(float(row.max())) + 2e-2 * float(np.abs(row).max()))
+        assert float(row.max() - row[int(t)]) <= tol, (f"{what}: step {k} picked {t} ({row[int(t)]:.4f}) but the "
+                                                       f"oracle max is {row.max():.4f} at {int(row.argmax())}")
+        if int(t) == int(row.argmax()):
+            exact += 1
+        else:
+            ties.append(k)
+    return exact, ties

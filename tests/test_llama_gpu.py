@@ -68,7 +68,9 @@ def test_sampling_device_topk_equals_host_chain():
         for kw in ({"temperature": 0.8, "top_k": 40, "top_p": 0.95, "min_p": 0.05},   # llama-cpp defaults
                    {"top_k": 5, "temperature": 1.3}, {"top_k": 64, "top_p": 0.8, "min_p": 0.0, "temperature": 0.5}):
             out.append(list(eng.generate(prompts[0], 24, seed=7, ignore_eos=True, **kw)[0]))
-            reqs = [eng.submit(p, 16, seed=11 + i, ignore_eos=True, **kw) for i, p in enumerate(prompts)]
+            # submitted atomically: one admission round, so the batch composition (and with it the
+            # kernel path of every step) is the same in both engines
+            reqs = eng.submit_many(prompts, 16, seeds=[11 + i for i in range(len(prompts))], ignore_eos=True, **kw)
             out += [list(eng.wait(r)[0]) for r in reqs]
         eng.close()
         return out

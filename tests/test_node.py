@@ -166,3 +166,58 @@ def test_concurrent_prompts_overlap_but_identical_prompts_compute_once(model_fil
     assert dt < 0.5, "different prompts were serialised"
     assert sorted(c["prompt"] for c in m.calls) == ["a", "b", "c"]
     assert [res[i] for i in range(5)] == ["<a>", "<b>", "<c>", "<a>", "<a>"]
+
+
+def _serve(n):
+    t = threading.Thread(target=n.handle_requests, daemon=True)
+    t.start()
+    return t
+
+
+@pytest.mark.parametrize("n_contexts", [1, 32])
+def test_concurrent_handler_contexts(model_file, n_contexts):
+    """handle_requests over REP contexts: 32 clients on the wire at once are served concurrently
+    (n_contexts > 1), each gets its own reply; with one context the handler is the reference's
+    lock-step loop (requests serialised)."""
+    from llama_p2p_amd.node import LocalTransport
+
+    m = FakeModel(delay=0.1)
+    tr = LocalTransport()
+    n = LlamaP2PNode(model_file, 5000, cache_size=100, secret_key="k", model=m, transport=tr, n_contexts=n_contexts)
+    th = _serve(n)
+    out = {}
+
+    def client(i):
+        req = {"type": "inference", "prompt": f"p{i}", "secret_key": "k" if i % 8 else "bad"}
+        out[i] = json.loads(tr.request(json.dumps(req).encode()))
+
+    cs = [threading.Thread(target=client, args=(i,)) for i in range(32)]
+    t0 = time.time()
+    for c in cs:
+        c.start()
+    for c in cs:
+        c.join()
+    dt = time.time() - t0
+    n.active = False
+    th.join(timeout=2)
+    for i in range(32):
+        assert out[i] == ({"result": f"<p{i}>"} if i % 8 else {"error": "Unauthorized"})
+    if n_contexts > 1:
+        assert dt < 1.0, f"32 requests took {dt:.2f}s: not served concurrently"
+    else:
+        assert dt > 2.5, "one context must serialise (28 model calls x 0.1 s)"
+    assert len(m.calls) == 28
+
+
+def test_handler_context_bad_json_gets_no_reply(model_file):
+    from llama_p2p_amd.node import LocalTransport
+
+    tr = LocalTransport()
+    n = LlamaP2PNode(model_file, 5000, secret_key="k", model=FakeModel(), transport=tr, n_contexts=4)
+    th = _serve(n)
+    with pytest.raises(TimeoutError):
+        tr.request(b"{bad", timeout=0.5)  # the reference logs the error and sends nothing
+    assert json.loads(tr.request(json.dumps({"type": "inference", "prompt": "q", "secret_key": "k"}).encode())) == \
+        {"result": "<q>"}
+    n.active = False
+    th.join(timeout=2)

@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
         > $OUT/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
       tail -3 $OUT/pytest_gpu.log ;;
     smoke)
@@ -20,7 +20,7 @@ for s in $STEPS; do
         || { tail -30 $OUT/smoke.log; exit 1; }
       tail -2 $OUT/smoke.log ;;
     bench)
-      timeout -k 10 400 python -u bench.py > $OUT/bench.log 2>&1 || { tail -30 $OUT/bench.log; exit 1; }
+      timeout -k 10 450 python -u bench.py > $OUT/bench.log 2>&1 || { tail -30 $OUT/bench.log; exit 1; }
       tail -1 $OUT/bench.log ;;
     prof)
       MX_NO_GRAPHS=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- \

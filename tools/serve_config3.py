@@ -2,14 +2,16 @@
 """BASELINE.json config 3 through the drop-in node: Llama-3-8B bf16 serving 32
 concurrent synthetic requests with the result cache on.
 
-32 client threads call ``LlamaP2PNode.cached_inference(prompt)`` (p2p:120-133; the model call is
-the reference's ``self.model(prompt, max_tokens=100)`` with llama-cpp-python's default sampling),
-then the same 32 prompts are submitted again (all cache hits).  Reported: generated tokens/s of
+32 clients send inference requests over the node's request socket at once (an in-process REP
+transport with concurrent contexts, node.LocalTransport): ``handle_requests`` (p2p:84-98) ->
+``cached_inference`` (p2p:120-133) -> the reference's ``self.model(prompt, max_tokens=100)``
+(llama-cpp-python's default sampling, or greedy with --greedy), then the same 32 prompts are
+sent again (all cache hits).  Reported: generated tokens/s of
 the first wave (hits excluded), the second wave's hit rate and latency, and, for comparison, the
 reference's serialised behaviour (one request at a time, as its lock around the model call does)
 timed on a bounded sample of the same prompts.  One JSON line on stdout.
 
-    python tools/serve_config3.py [--model synthetic:llama3-8b] [--n 32] [--serial 4]
+    python tools/serve_config3.py [--model synthetic:llama3-8b] [--n 32] [--serial 4] [--greedy]
 """
 import argparse
 import json
@@ -21,21 +23,15 @@ import time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 
-class _NoNet:
-    """No gossip/RPC sockets: requests enter through cached_inference directly."""
-
-    def __getattr__(self, name):
-        return lambda *a, **k: None
-
-
 class _Counting:
     """Wraps the Llama object to count completion tokens (cached_inference returns text only)."""
 
-    def __init__(self, llm):
+    def __init__(self, llm, extra=None):
         self.llm, self.tokens, self.calls, self.lock = llm, 0, 0, threading.Lock()
+        self.extra = extra or {}
 
     def __call__(self, prompt, **kw):
-        out = self.llm(prompt, **kw)
+        out = self.llm(prompt, **kw, **self.extra)
         with self.lock:
             self.tokens += out["usage"]["completion_tokens"]
             self.calls += 1
@@ -65,14 +61,18 @@ def main():
     ap.add_argument("--model", default="synthetic:llama3-8b")
     ap.add_argument("--n", type=int, default=32)
     ap.add_argument("--serial", type=int, default=4, help="requests timed one at a time (reference lock)")
+    ap.add_argument("--greedy", action="store_true", help="temperature 0 (the parity setting) instead of the defaults")
     args = ap.parse_args()
     from llama_p2p_amd.llama import Llama
-    from llama_p2p_amd.node import LlamaP2PNode
+    from llama_p2p_amd.node import LlamaP2PNode, LocalTransport
 
     llm = Llama(model_path=args.model, verbose=False, n_seq_max=max(args.n, 1))
     llm("warm up", max_tokens=4)
-    counting = _Counting(llm)
-    node = LlamaP2PNode(args.model, 5000, cache_size=100, secret_key="k", model=counting, transport=_NoNet())
+    counting = _Counting(llm, {"temperature": 0.0} if args.greedy else None)
+    tr = LocalTransport()
+    node = LlamaP2PNode(args.model, 5000, cache_size=100, secret_key="k", model=counting, transport=tr,
+                        n_contexts=args.n)
+    threading.Thread(target=node.handle_requests, daemon=True).start()
     tok = lambda t: llm.tokenize(t.encode(), add_bos=True, special=True)  # noqa: E731
     prompts = make_text_prompts(args.n, tok)
 
@@ -81,7 +81,8 @@ def main():
 
         def run(i):
             t = time.perf_counter()
-            node.cached_inference(ps[i])
+            reply = json.loads(tr.request(json.dumps({"type": "inference", "prompt": ps[i], "secret_key": "k"}).encode()))
+            assert "result" in reply, reply
             lat[i] = time.perf_counter() - t
 
         th = [threading.Thread(target=run, args=(i,)) for i in range(len(ps))]
@@ -107,10 +108,12 @@ def main():
         sdt = time.perf_counter() - t0
         serial = {"requests": args.serial, "tok_s": round((counting.tokens - tok0) / sdt, 1),
                   "s_per_request": round(sdt / args.serial, 3)}
+    node.active = False
     llm.close()
     print(json.dumps({
-        "workload": f"config 3: {args.model}, {args.n} concurrent cached_inference calls "
-                    f"(max_tokens=100, default sampling), then the same {args.n} again",
+        "workload": f"config 3: {args.model}, {args.n} concurrent requests through handle_requests "
+                    f"(REP contexts) -> cached_inference (max_tokens=100, "
+                    f"{'greedy' if args.greedy else 'default sampling'}), then the same {args.n} again",
         "wave1": {"requests": args.n, "generated_tokens": gen1, "wall_s": round(dt1, 3),
                   "tok_s": round(gen1 / dt1, 1), "p50_latency_s": round(sorted(lat1)[len(lat1) // 2], 3)},
         "wave2": {"requests": args.n, "hit_rate": round(hits / args.n, 3), "wall_s": round(dt2, 4),
