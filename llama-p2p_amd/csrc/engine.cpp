@@ -129,6 +129,9 @@ struct mx_engine {
   int n_embd = 0, n_layer = 0, n_head = 0, n_head_kv = 0, head_dim = 0, n_embd_kv = 0, n_ff = 0, n_vocab = 0;
   int n_ctx_train = 0;
   float eps = 1e-5f, rope_base = 10000.f;
+  // RoPE frequency factors (GGUF rope_freqs.weight, Llama-3.1; empty = none) and linear scaling
+  std::vector<float> rope_ff;
+  float rope_freq_scale = 1.0f;
   int bos = 1, eos = 2;
   int n_ctx = 512, n_seq_max = 64, lb = 0, le = 0, device = 0;
   bool has_embed = true, has_head = true, use_graphs = true;
@@ -280,14 +283,18 @@ int mx_engine::init_common() {
   HIPC(hipMemsetAsync(kcache, 0, layer_kv_stride * nl * sizeof(_Float16), stream));
   HIPC(hipMemsetAsync(vcache, 0, layer_kv_stride * nl * sizeof(_Float16), stream));
 
-  // RoPE table, ggml_rope_cache_init recipe: theta *= powf(base, -2/d) in f32
+  // RoPE table, ggml_rope_cache_init + rope_yarn (ext_factor 0, mscale 1): theta *= powf(base, -2/d)
+  // as an f32 running product, divided by the frequency factor, times the linear freq_scale
+  if (!rope_ff.empty() && (int)rope_ff.size() != head_dim / 2) return fail(MX_ERR_MODEL, "rope_freqs.weight size");
   std::vector<float> cs((size_t)n_ctx * head_dim);
   const float theta_scale = powf(rope_base, -2.0f / (float)head_dim);
   for (int p = 0; p < n_ctx; p++) {
     float theta = (float)p;
     for (int i = 0; i < head_dim / 2; i++) {
-      cs[((size_t)p * (head_dim / 2) + i) * 2] = cosf(theta);
-      cs[((size_t)p * (head_dim / 2) + i) * 2 + 1] = sinf(theta);
+      const float ff = rope_ff.empty() ? 1.0f : rope_ff[i];
+      const float th = rope_freq_scale * (theta / ff);
+      cs[((size_t)p * (head_dim / 2) + i) * 2] = cosf(th);
+      cs[((size_t)p * (head_dim / 2) + i) * 2 + 1] = sinf(th);
       theta *= theta_scale;
     }
   }
@@ -452,6 +459,26 @@ int mx_engine::load_gguf(const std::string& path) {
   if (!n_embd || !n_layer || !n_head || !n_ff) return fail(MX_ERR_MODEL, "missing llama.* hyper-parameters");
   if ((int)f.get_num("llama.rope.dimension_count", n_embd / n_head) != n_embd / n_head)
     return fail(MX_ERR_MODEL, "partial RoPE (rope.dimension_count != head_dim) is not supported");
+  {  // RoPE scaling: llama.cpp's "linear" (freq_scale = 1/factor) and Llama-3.1 frequency factors
+    const GGUFValue* st = f.get("llama.rope.scaling.type");
+    const std::string stype = st ? st->str : "none";
+    const double factor = f.get_num("llama.rope.scaling.factor", 0.0);
+    if (stype == "linear") {
+      if (!(factor > 0)) return fail(MX_ERR_MODEL, "linear RoPE scaling without a positive factor");
+      rope_freq_scale = (float)(1.0 / factor);
+    } else if (stype != "none" && !stype.empty()) {
+      return fail(MX_ERR_MODEL, "RoPE scaling type '" + stype + "' is not supported (none, linear and rope_freqs are)");
+    }
+    if (const GGUFTensor* rf = f.tensor("rope_freqs.weight")) {
+      const int half = n_embd / n_head / 2;
+      if (rf->type != 0 || rf->ne.size() != 1 || (int)rf->ne[0] != half)
+        return fail(MX_ERR_MODEL, "rope_freqs.weight must be f32 [head_dim/2]");
+      rope_ff.resize(half);
+      memcpy(rope_ff.data(), f.data(*rf), half * 4);
+      for (float v : rope_ff)
+        if (!(v > 0)) return fail(MX_ERR_MODEL, "rope_freqs.weight has a non-positive factor");
+    }
+  }
   if (le < 0 || le > n_layer) le = n_layer;
   // Matrix types.  All BF16 -> the bf16 path; all Q8_0 -> the Q8_0 path (int8 MFMA on the blocks);
   // any other mix of F32 / F16 / BF16 / Q4_0 / Q8_0 / Q4_K / Q5_K / Q6_K (Q4_K_M, Q5_K_M, ... files)

@@ -1359,24 +1359,27 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_kernel(AttnArgs a) {
   attn_decode_body<D, G, NW, FIN>(a, blockIdx.x, blockIdx.y);
 }
 
-#ifndef ATTN_WAVES
-#define ATTN_WAVES 8  // 16 waves measured slower (merge of 16 partials; tools/gpu/ab_lib.sh)
-#endif
-template <int D, bool FIN>
-static void launch_attn_df(const AttnArgs& a, hipStream_t s) {
+template <int D, bool FIN, int NW>
+static void launch_attn_dfw(const AttnArgs& a, hipStream_t s) {
   dim3 grid(a.n_head_kv, a.M);
   switch (a.n_head / a.n_head_kv) {
-    case 1: attn_decode_kernel<D, 1, ATTN_WAVES, FIN><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
-    case 2: attn_decode_kernel<D, 2, ATTN_WAVES, FIN><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
-    case 4: attn_decode_kernel<D, 4, ATTN_WAVES, FIN><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
-    case 8: attn_decode_kernel<D, 8, ATTN_WAVES, FIN><<<grid, 64 * ATTN_WAVES, 0, s>>>(a); break;
+    case 1: attn_decode_kernel<D, 1, NW, FIN><<<grid, 64 * NW, 0, s>>>(a); break;
+    case 2: attn_decode_kernel<D, 2, NW, FIN><<<grid, 64 * NW, 0, s>>>(a); break;
+    case 4: attn_decode_kernel<D, 4, NW, FIN><<<grid, 64 * NW, 0, s>>>(a); break;
+    case 8: attn_decode_kernel<D, 8, NW, FIN><<<grid, 64 * NW, 0, s>>>(a); break;
   }
 }
 
+// Waves per work-group: 8 for decode-sized grids (<= 64 rows: n_head_kv x M work-groups do not fill
+// the chip, so each work-group splits its positions over more waves); 4 once the grid alone fills
+// it (>= 128 rows, e.g. a prefill chunk whose rows are not 16-position blocks).  Measured in round 2
+// (profiles/round2_attention.txt): 16 waves was slower at every size, 4 waves 2.3x faster at 4096
+// rows and 7-20% slower at 1-32 rows.
 template <int D>
 static void launch_attn_d(const AttnArgs& a, hipStream_t s) {
-  if (a.slabs) launch_attn_df<D, true>(a, s);
-  else launch_attn_df<D, false>(a, s);
+  if (a.slabs) launch_attn_dfw<D, true, 8>(a, s);
+  else if (a.M >= 128) launch_attn_dfw<D, false, 4>(a, s);
+  else launch_attn_dfw<D, false, 8>(a, s);
 }
 
 void launch_attention(const AttnArgs& a, hipStream_t s) {

@@ -435,12 +435,14 @@ def _mixed_type(wtype: str, name: str) -> int:
 
 
 def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = None, wtype: str = "bf16",
-                         dequant_from: str = None):
+                         dequant_from: str = None, rope_freqs=None, rope_scaling=None):
     """Write a LLaMA GGUF with the synthetic weights of synth.py: every matrix bf16, or (wtype
     "q8_0") the Q8_0 quantisation of those bf16 matrices; norms f32 either way.  wtype "q4_k_m",
     "q5_k_m", "q4_0", "f16": matrices in those per-tensor types (MIXED), with random valid blocks
     (seeded) for the quantised ones and the synthetic values for f16.  dequant_from: a GGUF of the
-    same shape whose matrices are written here dequantised (dequantize(), then bf16 RNE) as BF16."""
+    same shape whose matrices are written here dequantised (dequantize(), then bf16 RNE) as BF16.
+    rope_freqs: a rope_freqs.weight tensor (head_dim/2 f32, Llama-3.1 style); rope_scaling:
+    (type, factor) written as llama.rope.scaling.type / .factor."""
     from . import synth
 
     if wtype not in ("bf16", "q8_0") and wtype not in MIXED:
@@ -461,6 +463,9 @@ def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = Non
     w.add_uint32("llama.attention.head_count_kv", shape.n_head_kv)
     w.add_float32("llama.attention.layer_norm_rms_epsilon", shape.eps)
     w.add_float32("llama.rope.freq_base", shape.rope_base)
+    if rope_scaling is not None:
+        w.add_string("llama.rope.scaling.type", rope_scaling[0])
+        w.add_float32("llama.rope.scaling.factor", rope_scaling[1])
     w.add_uint32("llama.vocab_size", shape.n_vocab)
     toks, scores, types = synthetic_spm_vocab(shape.n_vocab)
     w.add_string("tokenizer.ggml.model", "llama")
@@ -492,5 +497,10 @@ def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = Non
         else:
             w.add_tensor_info(name, arr.shape, GGML_BF16 if kind == "bf16" else GGML_F32)
             arrays.append(arr)
+    if rope_freqs is not None:
+        rf = np.ascontiguousarray(rope_freqs, dtype=np.float32)
+        assert rf.shape == (shape.head_dim // 2,)
+        w.add_tensor_info("rope_freqs.weight", rf.shape, GGML_F32)
+        arrays.append(rf)
     w.write(arrays)
     return path

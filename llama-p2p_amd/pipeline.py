@@ -62,6 +62,32 @@ def partition_layers(n_layer: int, layer_cost: float, head_cost: float, n_stages
     return [tuple(b) for b in best(0, 0)[2]]
 
 
+def stage_plan(shape, n_stages: int, seqs_per_micro_batch: int, n_ctx: int, hbm_bytes: int = 288 * 10 ** 9):
+    """Byte-balanced stages of ``shape`` and each stage's device memory: bf16 weights (+ the token
+    embedding table on stage 0, output norm + lm_head on the last), the f16 KV cache for the
+    S * M slots the pipeline keeps (n_seq_max = S micro-batches x M sequences, each of n_ctx
+    positions rounded up to 64), and the engine's prefill-chunk activations.  Raises if a stage does
+    not fit ``hbm_bytes`` (288 GB per MI355X)."""
+    h, kv, ff, V = shape.n_embd, shape.n_embd_kv, shape.n_ff, shape.n_vocab
+    layer_bytes = 2 * (2 * h * h + 2 * h * kv + 3 * h * ff) + 2 * h * 4
+    head_bytes = 2 * V * h + h * 4
+    parts = partition_layers(shape.n_layer, layer_bytes, head_bytes, n_stages, embed_cost=0)
+    slots = n_stages * seqs_per_micro_batch
+    ctx_stride = (n_ctx + 63) // 64 * 64
+    kv_per_layer = 2 * slots * ctx_stride * kv * 2
+    act = 4096 * (3 * h * 4 + 2 * h * 2 + ff * 2)  # PREFILL_ROWS rows: x, q, ssq-ish f32 + bf16 operands
+    plan = []
+    for s, (lb, le) in enumerate(parts):
+        nl = le - lb
+        w = nl * layer_bytes + (V * h * 2 if s == 0 else 0) + (head_bytes if s == n_stages - 1 else 0)
+        total = w + nl * kv_per_layer + act
+        if total > hbm_bytes:
+            raise ValueError(f"stage {s} ({nl} layers) needs {total / 1e9:.1f} GB > {hbm_bytes / 1e9:.0f} GB")
+        plan.append({"stage": s, "layers": (lb, le), "weight_bytes": w, "kv_bytes": nl * kv_per_layer,
+                     "total_bytes": total})
+    return plan
+
+
 class TorchComm:
     """Point-to-point hand-offs over torch.distributed (nccl = RCCL on ROCm, or gloo).
 

@@ -72,6 +72,8 @@ typedef struct {
     uint8_t *tok_embd_q8, *output_q8; /* Q8_0 blocks or NULL */
     float *out_norm;
     orc_layer *layers;
+    float *rope_ff;         /* rope_freqs.weight [head_dim/2] (Llama-3.1 frequency factors) or NULL */
+    float rope_freq_scale;  /* 1 / llama.rope.scaling.factor for "linear" scaling, else 1 */
 } orc_model;
 
 typedef struct {
@@ -159,6 +161,7 @@ orc_model *orc_create(const orc_hparams *hp, int flags) {
     orc_model *m = (orc_model *)calloc(1, sizeof(orc_model));
     m->hp = *hp;
     m->flags = flags;
+    m->rope_freq_scale = 1.0f;
     m->head_dim = hp->n_embd / hp->n_head;
     m->n_embd_kv = m->head_dim * hp->n_head_kv;
     size_t h = hp->n_embd, kv = m->n_embd_kv, ff = hp->n_ff, V = hp->n_vocab;
@@ -190,6 +193,7 @@ void orc_free(orc_model *m) {
         for (int k = 0; k < 9; k++) free(L->q8[k]);
     }
     free(m->tok_embd_q8); free(m->output_q8);
+    free(m->rope_ff);
     free(m->layers); free(m->tok_embd); free(m->output); free(m->out_norm); free(m);
 }
 
@@ -197,6 +201,18 @@ void orc_free(orc_model *m) {
 enum { K_TOK_EMBD = 1, K_OUT_NORM = 2, K_OUTPUT = 3 };
 enum { L_ATTN_NORM, L_Q, L_K, L_V, L_O, L_FFN_NORM, L_GATE, L_UP, L_DOWN };
 static uint64_t layer_tid(int l, int k) { return 16u + 16u * (uint64_t)l + (uint64_t)k; }
+
+/* RoPE frequency factors (rope_freqs.weight, head_dim/2 floats; NULL clears) and linear
+ * scaling (freq_scale = 1 / llama.rope.scaling.factor); used by contexts created afterwards. */
+void orc_set_rope(orc_model *m, const float *freq_factors, float freq_scale) {
+    free(m->rope_ff);
+    m->rope_ff = NULL;
+    if (freq_factors) {
+        m->rope_ff = (float *)malloc(sizeof(float) * (size_t)(m->head_dim / 2));
+        memcpy(m->rope_ff, freq_factors, sizeof(float) * (size_t)(m->head_dim / 2));
+    }
+    m->rope_freq_scale = freq_scale;
+}
 
 void orc_fill_synthetic(orc_model *m, uint64_t seed) {
     size_t h = m->hp.n_embd, kv = m->n_embd_kv, ff = m->hp.n_ff, V = m->hp.n_vocab;
@@ -397,15 +413,18 @@ orc_ctx *orc_ctx_create(orc_model *m, int n_ctx) {
         c->k[l] = calloc((size_t)n_ctx * m->n_embd_kv, esz);
         c->v[l] = calloc((size_t)n_ctx * m->n_embd_kv, esz);
     }
-    /* rope cache, ggml_rope_cache_init (ext_factor 0, freq_scale 1, mscale 1) */
+    /* rope cache, ggml_rope_cache_init + rope_yarn with ext_factor 0 and mscale 1:
+     * theta_i = freq_scale * ((p * theta_scale^i, an f32 running product) / freq_factor_i) */
     int half = m->head_dim / 2;
     c->rope_cs = (float *)malloc((size_t)n_ctx * half * 2 * sizeof(float));
     float theta_scale = powf(m->hp.rope_base, -2.0f / (float)m->head_dim);
     for (int p = 0; p < n_ctx; p++) {
         float theta = (float)p;
         for (int i = 0; i < half; i++) {
-            c->rope_cs[((size_t)p * half + i) * 2 + 0] = cosf(theta);
-            c->rope_cs[((size_t)p * half + i) * 2 + 1] = sinf(theta);
+            const float ff = m->rope_ff ? m->rope_ff[i] : 1.0f;
+            const float th = m->rope_freq_scale * (theta / ff);
+            c->rope_cs[((size_t)p * half + i) * 2 + 0] = cosf(th);
+            c->rope_cs[((size_t)p * half + i) * 2 + 1] = sinf(th);
             theta *= theta_scale;
         }
     }

@@ -53,6 +53,7 @@ def lib():
         L.orc_quantize_q8.argtypes = [vp]
         L.orc_quantize_q8.restype = i32
         L.orc_set_q8_jitter.argtypes = [ctypes.c_float]
+        L.orc_set_rope.argtypes = [vp, vp, ctypes.c_float]
         L.orc_ctx_create.restype = vp
         L.orc_ctx_create.argtypes = [vp, i32]
         L.orc_ctx_free.argtypes = [vp]
@@ -94,6 +95,11 @@ class OracleModel:
         blocks = np.ascontiguousarray(blocks, dtype=np.uint8)
         if lib().orc_set_tensor_q8(self._m, layer, kind, blocks.ctypes.data):
             raise ValueError(f"orc_set_tensor_q8({layer},{kind}) failed")
+
+    def set_rope(self, freq_factors=None, freq_scale: float = 1.0):
+        """Llama-3.1 RoPE frequency factors (head_dim/2 floats) and linear scaling (1/factor)."""
+        self._ff = None if freq_factors is None else np.ascontiguousarray(freq_factors, dtype=np.float32)
+        lib().orc_set_rope(self._m, self._ff.ctypes.data if self._ff is not None else None, freq_scale)
 
     def quantize_q8(self):
         """Every matrix -> Q8_0 of its bf16 values (ggml quantize_row_q8_0_ref)."""

@@ -52,14 +52,15 @@ def permute_rows(w: np.ndarray, n_head: int) -> np.ndarray:
     return w.reshape(n_head, 2, d // 2, *w.shape[1:]).swapaxes(1, 2).reshape(w.shape)
 
 
-def hf_model(shape, seed):
+def hf_model(shape, seed, rope_parameters=None):
     import torch
     from transformers import LlamaConfig, LlamaForCausalLM
 
+    extra = {"rope_parameters": dict(rope_parameters, rope_theta=shape.rope_base)} if rope_parameters else {}
     cfg = LlamaConfig(vocab_size=shape.n_vocab, hidden_size=shape.n_embd, intermediate_size=shape.n_ff,
                       num_hidden_layers=shape.n_layer, num_attention_heads=shape.n_head,
                       num_key_value_heads=shape.n_head_kv, rms_norm_eps=shape.eps, rope_theta=shape.rope_base,
-                      max_position_embeddings=4096, tie_word_embeddings=False, attn_implementation="eager")
+                      max_position_embeddings=4096, tie_word_embeddings=False, attn_implementation="eager", **extra)
     torch.manual_seed(0)
     model = LlamaForCausalLM(cfg).float().eval()
     t = {name: (kind, arr) for name, kind, arr in synth.synth_tensors(shape, seed)}
@@ -106,6 +107,43 @@ def make(shape_name: str):
     print(f"wrote {path}: ids {ids.shape}, logits {logits.shape}, max|logit| {np.abs(logits).max():.3f}")
 
 
+# RoPE scaling (SURVEY §8a a8 for Llama-3.1 GGUFs): transformers' "llama3" rope type
+# (its inv_freq is the base frequencies divided by llama.cpp's rope_freqs.weight factors -- stored
+# here as ff = base_inv_freq / hf_inv_freq, what convert_hf_to_gguf writes) and "linear" (llama.cpp
+# freq_scale = 1 / factor).  original_max_position_embeddings is small so the scaled band reaches
+# frequencies that matter within the 40-token sequence.
+ROPE_CASES = {
+    "llama3": {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+               "original_max_position_embeddings": 32},
+    "linear": {"rope_type": "linear", "factor": 4.0},
+}
+
+
+def make_rope(shape_name: str, case: str):
+    import torch
+
+    shape = synth.SHAPES[shape_name]
+    params = ROPE_CASES[case]
+    rng = np.random.default_rng(4321)
+    ids = np.concatenate([[1], rng.integers(3, shape.n_vocab, SEQ_LEN - 1)]).astype(np.int32)
+    model = hf_model(shape, SEED, params)
+    d = shape.head_dim
+    base_inv = 1.0 / (shape.rope_base ** (np.arange(0, d, 2, dtype=np.float64) / d))
+    hf_inv = model.model.rotary_emb.inv_freq.double().numpy()
+    if case == "linear":
+        ff, freq_scale = np.ones(d // 2, np.float32), np.float32(1.0 / params["factor"])
+    else:
+        ff, freq_scale = (base_inv / hf_inv).astype(np.float32), np.float32(1.0)
+    with torch.no_grad():
+        out = model(torch.from_numpy(ids.astype(np.int64))[None], use_cache=False)
+    logits = out.logits[0].float().numpy().astype(np.float32)
+    path = os.path.join(HERE, f"hf_{shape_name}_rope_{case}.npz")
+    np.savez_compressed(path, ids=ids, logits=logits, shape=shape_name, seed=SEED, rope_ff=ff, freq_scale=freq_scale)
+    print(f"wrote {path}: factors {ff.min():.3f}..{ff.max():.3f}, freq_scale {freq_scale}")
+
+
 if __name__ == "__main__":
     for s in SHAPES:
         make(s)
+    for case in ROPE_CASES:
+        make_rope("test-tiny", case)

@@ -386,3 +386,75 @@ def test_hbm_probes_plausible(mx):
     assert "work-groups" in rdesc and "work-groups" in cdesc
     with pytest.raises(mx.MxError):
         mx._check(mx.lib().mx_probe_read(0, 0, 1, None, None, 0))  # zero bytes: argument error, no launch
+
+
+@pytest.mark.parametrize("case", ["llama3", "linear"])
+def test_gguf_rope_scaling_vs_oracle(mx, oracle_mod, tmp_path, case):
+    """A Llama-3.1-style GGUF (rope_freqs.weight frequency factors) and a linear-scaled one
+    (llama.rope.scaling.type/factor): the engine builds the same RoPE table as the oracle, which
+    tests/test_oracle.py pins to transformers' "llama3" / "linear" rope types."""
+    from llama_p2p_amd import gguf, synth
+
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", f"hf_test-tiny_rope_{case}.npz"))
+    shape = synth.SHAPES["test-tiny"]
+    path = str(tmp_path / f"rope_{case}.gguf")
+    if case == "llama3":
+        gguf.write_synthetic_gguf(path, shape, seed=0, rope_freqs=g["rope_ff"])
+    else:
+        gguf.write_synthetic_gguf(path, shape, seed=0, rope_scaling=("linear", 4.0))
+    eng = mx.Engine(path, n_ctx=64, n_seq_max=2)
+    got = eng.forward_logits(g["ids"])
+    eng.close()
+    om = oracle_mod.OracleModel(shape, seed=0)
+    om.set_rope(g["rope_ff"] if case == "llama3" else None, float(g["freq_scale"]))
+    ref = om.context(64).eval(g["ids"], 0, all_logits=True)
+    assert_logits_close(got, ref, f"rope {case}")
+    assert_tokens_match(got, ref, f"rope {case}")
+    plain = oracle_mod.OracleModel(shape, seed=0).context(64).eval(g["ids"], 0, all_logits=True)
+    assert np.abs(got - ref).max() < 0.25 * np.abs(plain - ref).max()  # the scaling is really applied
+
+
+def test_gguf_unsupported_rope_scaling_rejected(mx, tmp_path):
+    from llama_p2p_amd import gguf, synth
+
+    path = str(tmp_path / "yarn.gguf")
+    gguf.write_synthetic_gguf(path, synth.SHAPES["test-tiny"], seed=0, rope_scaling=("yarn", 4.0))
+    with pytest.raises(mx.MxError) as ei:
+        mx.Engine(path, n_ctx=64, n_seq_max=2)
+    assert ei.value.code == mx.MX_ERR_MODEL and "yarn" in str(ei.value)
+
+
+def test_llama3_70b_full_size_row_consistency(mx):
+    """Config 5's model at full size on one GPU (141 GB of bf16 weights): a 24-row decode step (wide
+    GEMVs, split-K slabs, attention finishing q/k/v) and the same sequence's 1-row step (norm on
+    load, row-tile-persistent GEMVs) agree.  The two paths sum in different orders, so over 80 layers
+    each drifts from exact arithmetic independently; each is held to the bf16 tolerance against the
+    oracle elsewhere (test_70b_geometry_all_paths: the 70B geometry per path), so their difference
+    is bounded by twice that tolerance, and the greedy pick must agree wherever the gap exceeds it.
+    (The CPU oracle cannot run 70B at test time.)"""
+    from conftest import assert_logits_close, assert_tokens_match
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES["llama3-70b"]
+    eng = mx.Engine("synthetic:llama3-70b:seed=0", n_ctx=64, n_seq_max=24)
+    assert eng.info.n_layer == 80 and eng.info.weight_bytes > 138e9
+    seqs = [_seq(shape, 9, seed=300 + i) for i in range(24)]
+    slots, pos, ids = [], [], []
+    for i, sq in enumerate(seqs):
+        slots += [i] * 8
+        pos += list(range(8))
+        ids += [int(t) for t in sq[:8]]
+    assert eng.forward_rows(slots, pos, ids, want_logits=False) is None  # GEMM prefill, 192 rows
+    wide = eng.forward_rows(list(range(24)), [8] * 24, [int(sq[8]) for sq in seqs])
+    for i in (0, 11, 23):
+        one = eng.forward_rows([i], [8], [int(seqs[i][8])])
+        ref = wide[i]
+        d = np.abs(one[0] - ref)
+        tol2 = 2 * (1e-2 * np.abs(ref) + 2e-2 * np.abs(ref).max())
+        print(f"70b row {i}: max|d| {d.max():.4f} (max|logit| {np.abs(ref).max():.3f}), rms ratio "
+              f"{np.sqrt((d ** 2).mean() / (ref ** 2).mean()):.2e}, argmax {int(one[0].argmax())} vs {int(ref.argmax())}")
+        assert (d <= tol2).all(), f"70b row {i}: {(d > tol2).sum()} logits beyond twice the tolerance"
+        top = np.sort(ref)[::-1]
+        if top[0] - top[1] > 2 * tol2.max():
+            assert int(one[0].argmax()) == int(ref.argmax())
+    eng.close()

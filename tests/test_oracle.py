@@ -104,3 +104,24 @@ def test_context_overflow_rejected(oracle_mod):
     m = oracle_mod.OracleModel(synth.SHAPES["test-tiny"], seed=0)
     with pytest.raises(ValueError):
         m.context(8).eval(list(range(3, 12)), 0)
+
+
+@pytest.mark.parametrize("case", ["llama3", "linear"])
+def test_oracle_rope_scaling_matches_transformers(oracle_mod, case):
+    """RoPE frequency factors (GGUF rope_freqs.weight, Llama-3.1) and linear scaling: the oracle with
+    the fixture's factors / freq_scale matches transformers' "llama3" / "linear" rope types; without
+    them the logits are clearly different (the scaling reaches the positions used)."""
+    from llama_p2p_amd import synth
+
+    g = _golden(f"test-tiny_rope_{case}")
+    sh = synth.SHAPES["test-tiny"]
+    m = oracle_mod.OracleModel(sh, seed=int(g["seed"]), exact=True)
+    plain = m.context(64).eval(g["ids"], 0, all_logits=True)
+    m.set_rope(g["rope_ff"] if case == "llama3" else None, float(g["freq_scale"]))
+    got = m.context(64).eval(g["ids"], 0, all_logits=True)
+    ref = g["logits"]
+    assert np.abs(got - ref).max() < 5e-5 * np.abs(ref).max()
+    assert np.abs(plain - ref).max() > 100 * np.abs(got - ref).max()
+    # unit factors and scale 1 are the identity, bit for bit
+    m.set_rope(np.ones(sh.head_dim // 2, np.float32), 1.0)
+    assert np.array_equal(m.context(64).eval(g["ids"], 0, all_logits=True), plain)

@@ -277,3 +277,22 @@ def test_ungrouped_schedule_deadlocks_under_rendezvous():
     # the transport is strict enough to catch the hazard: the same ops, each posted alone
     errs, _ = _run_rendezvous(2, grouped=False, timeout=2)
     assert errs and all(isinstance(e, TimeoutError) for e in errs)
+
+
+def test_70b_eight_stage_plan_fits():
+    """Config 5: Llama-3-70B bf16 over 8 stages, n_seq_max = S*M = 8 x 32 slots of 512 positions per
+    stage: byte-balanced contiguous layers (every layer on exactly one stage, lm_head on the last)
+    and every stage within one MI355X's 288 GB; the whole model would also fit one GPU."""
+    from llama_p2p_amd import pipeline, synth
+
+    sh = synth.SHAPES["llama3-70b"]
+    plan = pipeline.stage_plan(sh, 8, 32, 512)
+    assert [p["layers"][0] for p in plan][0] == 0 and plan[-1]["layers"][1] == sh.n_layer
+    assert all(plan[i]["layers"][1] == plan[i + 1]["layers"][0] for i in range(7))
+    w = [p["weight_bytes"] for p in plan]
+    assert max(w) < 1.15 * (sum(w) / 8) + 2 * sh.n_vocab * sh.n_embd  # balanced by bytes
+    assert all(p["total_bytes"] < 288e9 for p in plan)
+    single = pipeline.stage_plan(sh, 1, 32, 512)
+    assert single[0]["total_bytes"] < 288e9  # config 5's model also fits one GPU (bench llama3_70b)
+    with pytest.raises(ValueError):
+        pipeline.stage_plan(sh, 1, 32, 512, hbm_bytes=100 * 10 ** 9)
