@@ -17,7 +17,7 @@
 //   * K is split across the waves of a work-group (register ring of U loads
 //     in flight per wave), partial tiles are summed through LDS, and the
 //     epilogue fuses RoPE + KV-cache store, SwiGLU, or the residual add.
-#include "kernels.h"
+#include "device_common.h"
 
 #include <math.h>
 #include <stdio.h>
@@ -27,51 +27,6 @@
 #include <type_traits>
 
 namespace mx {
-
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
-typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
-typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
-typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
-typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
-
-__device__ __forceinline__ float bf2f(uint32_t h) { return __uint_as_float(h << 16); }
-// round-nearest-even f32 -> bf16 bits (ggml_compute_fp32_to_bf16 without the NaN branch)
-__device__ __forceinline__ uint32_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
-}
-__device__ __forceinline__ float round_f16(float f) { return (float)(_Float16)f; }
-
-// ---------------------------------------------------------------------------
-// synthetic weights (llama-p2p_amd/synth.py is the spec; bit-identical)
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ float synth_value(uint64_t seed, uint64_t tid, uint64_t idx, float scale) {
-  uint64_t z = seed * 0x9E3779B97F4A7C15ull + tid * 0xD1B54A32D192ED03ull + idx;
-  z += 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  uint32_t s = (uint32_t)(z & 0xffff) + (uint32_t)((z >> 16) & 0xffff) + (uint32_t)((z >> 32) & 0xffff) +
-               (uint32_t)(z >> 48);
-  return (float)((int32_t)s - 131070) * scale;
-}
-
-// Destination row of logical row `row` in a packed matrix (see kernels.h):
-//   PACK_ROWS:     row + offset           (q|k|v stacked into one QKV matrix, or plain)
-//   PACK_GATE/UP:  16*(row/8) + (0|8) + row%8   -- ffn_gate and ffn_up rows interleaved by
-//                  halves of each 16-row tile, so one tile yields 8 SwiGLU outputs
-__device__ __forceinline__ int packed_row(int row, int mode, int offset) {
-  if (mode == PACK_GATE) return 16 * (row >> 3) + (row & 7);
-  if (mode == PACK_UP) return 16 * (row >> 3) + 8 + (row & 7);
-  return row + offset;
-}
-__device__ __forceinline__ size_t packed_index(int P, int col, int KT) {
-  const size_t tile = (size_t)(P >> 4) * KT + (col >> 5);
-  const int lane = (P & 15) + 16 * ((col & 31) >> 3);
-  return tile * TILE_ELEMS + lane * 8 + (col & 7);
-}
 
 __global__ void synth_packed_kernel(uint16_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale,
                                     int mode, int offset) {
@@ -100,11 +55,6 @@ __global__ void synth_rowmajor_kernel(uint16_t* dst, size_t n, uint64_t seed, ui
 __global__ void synth_norm_kernel(float* dst, size_t n, uint64_t seed, uint64_t tid, float scale) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     dst[i] = 1.0f + synth_value(seed, tid, i, scale);
-}
-
-static int fill_grid(size_t n) {
-  size_t g = (n + 255) / 256;
-  return (int)(g > 8192 ? 8192 : (g == 0 ? 1 : g));
 }
 
 void launch_synth_packed(uint16_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, int mode,
@@ -364,80 +314,6 @@ __device__ __forceinline__ void xs_build(const XsRegs<MM>& r, const MMArgs& a, u
         *reinterpret_cast<u32x2*>(xs + c * pitch + i) = o;
       }
     }
-  }
-}
-
-// KV cache layout.  Each (slot, kv head) owns ctx_stride * D f16 of K and as many of V, stored as
-// 1 KiB tiles in the lane order of the MFMA B operand that reads them, so every wave-instruction
-// of the attention kernels loads one contiguous 1 KiB (llama.cpp keeps K [pos][d] and V transposed
-// [d][pos] for the same reason on the CPU):
-//   K: tile (pos/16, d/32) = 16 positions x 32 dims, lane = pos%16 + 16*((d%32)/8), element d%8
-//      (the B operand of QK^T, v_mfma_f32_16x16x32_f16: k = dims, n = positions)
-//   V: tile (pos/32, d/16) = 32 positions x 16 dims, lane = d%16 + 16*((pos%32)/8), element pos%8
-//      (the B operand of P.V: k = positions, n = dims)
-__device__ __forceinline__ size_t kv_k_off(int pos, int d, int D) {
-  return (((size_t)(pos >> 4) * (D >> 5) + (d >> 5)) * 64 + (pos & 15) + 16 * ((d & 31) >> 3)) * 8 + (d & 7);
-}
-__device__ __forceinline__ size_t kv_v_off(int pos, int d, int D) {
-  return (((size_t)(pos >> 5) * (D >> 4) + (d >> 4)) * 64 + (d & 15) + 16 * ((pos & 31) >> 3)) * 8 + (pos & 7);
-}
-
-// q/k/v rows [row, row+4) of token column `col`: RoPE (mode NORM, adjacent pairs) on q and k,
-// q -> f32 buffer, k / v -> the f16 K / V caches (layout above).
-__device__ __forceinline__ void qkv_store(const MMArgs& a, int row, int col, f32x4 s) {
-  const int d = a.head_dim;
-  const int pos = a.pos[col];
-  if (pos < 0 || pos >= a.n_ctx) return;  // never write outside the slot's KV rows
-  if (row < a.n_q + a.n_kv) {
-    const bool is_q = row < a.n_q;
-    const int rl = is_q ? row : row - a.n_q;
-    const int dd = rl % d;  // multiple of 4
-    const f32x4 csv = *reinterpret_cast<const f32x4*>(a.rope_cs + ((size_t)pos * (d / 2) + dd / 2) * 2);
-    f32x4 o;
-    o[0] = s[0] * csv[0] - s[1] * csv[1];
-    o[1] = s[0] * csv[1] + s[1] * csv[0];
-    o[2] = s[2] * csv[2] - s[3] * csv[3];
-    o[3] = s[2] * csv[3] + s[3] * csv[2];
-    if (is_q) {
-      *reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + row) = o;
-    } else {
-      _Float16* kp = a.kc + (size_t)a.slot[col] * a.slot_stride + (size_t)(rl / d) * a.ctx_stride * d + kv_k_off(pos, dd, d);
-      *reinterpret_cast<f16x4*>(kp) = f16x4{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
-    }
-  } else {
-    const int rl = row - a.n_q - a.n_kv;
-    _Float16* vh = a.vc + (size_t)a.slot[col] * a.slot_stride + (size_t)(rl / d) * a.ctx_stride * d;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) vh[kv_v_off(pos, rl % d + i, d)] = (_Float16)s[i];
-  }
-}
-
-// One C-layout unit of a finished 16-row tile: rows 16*tile + 4*(l>>4) + i (i < 4) of token
-// column `col`.  SWIGLU tiles hold 8 gate rows (lanes 0-31) and the matching up rows (lanes l+32).
-template <int EPI>
-__device__ __forceinline__ void epi_store(const MMArgs& a, int tile, int l, int col, f32x4 s, f32x4 up) {
-  if constexpr (EPI == EPI_F32 || EPI == EPI_SLAB) {
-    const int row = tile * 16 + (l >> 4) * 4;
-    *reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + row) = s;
-  } else if constexpr (EPI == EPI_RESID) {
-    const int row = tile * 16 + (l >> 4) * 4;
-    f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + row);
-    *px = *px + s;
-  } else if constexpr (EPI == EPI_SWIGLU) {
-    const int row = tile * 8 + (l >> 4) * 4;  // ffn row of gate lane l / up lane l+32
-    f32x4 f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) f[i] = (s[i] / (1.0f + expf(-s[i]))) * up[i];
-    if (a.actf) {
-      *reinterpret_cast<f32x4*>(a.actf + (size_t)col * a.lda + row) = f;
-    } else {
-      u32x2 o;
-      o[0] = f2bf(f[0]) | (f2bf(f[1]) << 16);
-      o[1] = f2bf(f[2]) | (f2bf(f[3]) << 16);
-      *reinterpret_cast<u32x2*>(a.act + (size_t)col * a.lda + row) = o;
-    }
-  } else {  // EPI_QKV
-    qkv_store(a, tile * 16 + (l >> 4) * 4, col, s);
   }
 }
 
@@ -1132,7 +1008,7 @@ __device__ __forceinline__ float row16_sum(float v) {
 constexpr float LOG2E = 1.4426950408889634f;
 
 // One (kv head, row) of decode attention, by the NW waves of the calling work-group.  Wave w takes
-// chunks w, w + NW, ... and issues each chunk's K/V loads when it reaches it (issuing two chunks
+// chunks w, w + NW, ... and issues each later chunk's K/V loads when it reaches it (issuing two chunks
 // ahead measured slower: 18.6 vs 11.1 us at 32 rows, profiles/round2_attention.txt).  FIN: q/k/v
 // still as the wide path's split-K slabs (finished here, see below).  Everything that only the
 // chunk holding `pos` (FIN) or the partial last chunk needs sits behind a wave-uniform branch, so
@@ -1174,7 +1050,11 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
     for (int t = 0; t < DT; ++t)
       f.v[t] = *reinterpret_cast<const f16x8*>(Vb + (((size_t)(p0 / 32) * DT + t) * 64 + lane) * 8);
   };
+  // the wave's first chunk is loaded before anything else: its latency overlaps the q load (and the
+  // FIN slab sums) instead of following them.  FIN writes this position's K/V below; the chunk
+  // holding it is patched from LDS in compute(), so a stale read of that position is harmless.
   KV A;
+  if (w * CH < ctx) load(A, w);
 
   // wide path: q/k/v of this (kv head, token) are still split-K partial slabs -- sum them in slab
   // order (bit-identical to qkv_finish_kernel), RoPE q and k, write this position's K and V into
@@ -1309,7 +1189,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
     __builtin_amdgcn_wave_barrier();  // Ps[w] is rewritten next chunk only after every lane read it
   };
   for (int ch = w; ch * CH < ctx; ch += NW) {
-    load(A, ch);
+    if (ch != w) load(A, ch);
     compute(A, ch);
   }
   stamp(3);  // chunk loop done
@@ -1815,8 +1695,6 @@ void launch_attention_prefill(const AttnArgs& a, hipStream_t s) {
 // 64-k groups are permuted so a lane's 16-byte B fragment of both blocks is one
 // load.  Decode reads 1.0625 bytes per weight instead of 2.
 // ---------------------------------------------------------------------------
-typedef __attribute__((ext_vector_type(4))) int i32x4;
-typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 // permuted byte position of logical k in a Q8_0 activation row: within each 64-k group,
 // lane group g reads 16 bytes = k 8g..8g+7 (block 0) then k 32+8g..32+8g+7 (block 1)
@@ -1922,19 +1800,6 @@ void launch_synth_q8_rowmajor(uint8_t* dst, int N, int K, uint64_t seed, uint64_
 // Used when a file's layer matrices are not all BF16 or all Q8_0 (Q4_K_M, Q5_K_M, Q4_0, F16 ...):
 // the model then runs on the bf16 path.  gguf.py dequantize() is the same restatement.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float f16b(const uint8_t* p) {
-  return (float)__builtin_bit_cast(_Float16, (uint16_t)(p[0] | (p[1] << 8)));
-}
-__device__ __forceinline__ void scale_min_k4(int j, const uint8_t* q, int& sc, int& m) {
-  if (j < 4) {
-    sc = q[j] & 63;
-    m = q[j + 4] & 63;
-  } else {
-    sc = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
-    m = (q[j + 4] >> 4) | ((q[j] >> 6) << 4);
-  }
-}
-
 __global__ void dequant_bf16_kernel(uint16_t* dst, const uint8_t* src, int type, size_t nblocks) {
 #pragma clang fp contract(off)  // no fused multiply-subtract: one rounding per operation, as ggml's C
   for (size_t b = blockIdx.x * (size_t)blockDim.x + threadIdx.x; b < nblocks; b += (size_t)gridDim.x * blockDim.x) {
