@@ -185,17 +185,20 @@ def run_single(args):
     return res
 
 
-def q8_bench(args):
-    """The same model quantised to Q8_0 (a llama.cpp Q8_0 GGUF): batch-1 and
-    M-sequence greedy decode, and the Q8 gate/up kernel against the HBM roofline.  Algorithmic
-    bytes = the Q8_0 weights (1.0625 B/weight in packed tiles) + K/V + logits."""
+def quant_bench(args, wtype: str, steps: int):
+    """The same model shape as a llama.cpp quantised GGUF: "q8_0" (the Q8_0
+    quantisation of the synthetic bf16 weights) or "q4_k_m" (llama.cpp's Q4_K_M recipe: Q4_K with
+    Q6_K attn_v / ffn_down on the use_more_bits layers and a Q6_K output, synthetic K-quant blocks).
+    Batch-1 and M-sequence greedy decode and the gate/up kernel against the HBM roofline.
+    Algorithmic bytes = the packed weights (Q8_0 1.0625 B/weight; K-quants their GGUF block bytes,
+    +2.8% for byte-aligned Q4_K scales) + K/V + logits."""
     from llama_p2p_amd import synth
     from llama_p2p_amd.engine import Engine
 
     shape = synth.SHAPES[args.model]
     M = args.seqs
-    eng = Engine(f"synthetic:{args.model}:seed=0:q8_0", n_ctx=args.n_ctx, n_seq_max=max(M, 1))
-    assert eng.info.weight_type == 8
+    eng = Engine(f"synthetic:{args.model}:seed=0:{wtype}", n_ctx=args.n_ctx, n_seq_max=max(M, 1))
+    assert eng.info.weight_type == {"q8_0": 8, "q4_k_m": 12}[wtype]
     prompts = make_prompts(shape.n_vocab, M)
     slots, pos, ids = [], [], []
     for i, p in enumerate(prompts):
@@ -203,9 +206,9 @@ def q8_bench(args):
         pos += list(range(len(p) - 1))
         ids += [int(t) for t in p[:-1]]
     eng.forward_rows(slots, pos, ids, want_logits=False)
-    out = {"model": f"{args.model} Q8_0 (quantisation of the same synthetic bf16 weights)",
-           "weight_bytes": int(eng.info.weight_bytes)}
-    steps = args.q8_steps
+    desc = {"q8_0": "Q8_0 (quantisation of the same synthetic bf16 weights)",
+            "q4_k_m": "Q4_K_M (llama.cpp recipe types, synthetic K-quant blocks; native int8-MFMA K-quant path)"}
+    out = {"model": f"{args.model} {desc[wtype]}", "weight_bytes": int(eng.info.weight_bytes)}
     b = eng.batch(slots=list(range(M)), pos=[len(p) - 1 for p in prompts], ids=[int(p[-1]) for p in prompts],
                   max_steps=4 + steps)
     for _ in range(4):
@@ -236,12 +239,16 @@ def q8_bench(args):
     out["batch1"] = {"tok_s": round(1.0 / d1, 2), "ms_per_token": round(d1 * 1e3, 3),
                      "hbm_frac": round(b1_bytes / d1 / 1e9 / HBM_PEAK_GBS, 4),
                      "roofline_tok_s": round(HBM_PEAK_GBS * 1e9 / b1_bytes, 1)}
+    h = shape.n_embd
     for m in (1, M):
         us, wbytes = eng.profile_kernel(2, m, iters=3)
-        kb = wbytes + m * shape.n_embd + m * shape.n_embd // 8 + m * shape.n_ff * 4
-        out[f"gate_up_M{m}"] = {"kernel": "mq8_kernel<EPI_SWIGLU>", "us_per_launch": round(us, 2),
-                                "bytes_per_launch": int(kb), "achieved_gbs": round(kb / us / 1e3, 1),
-                                "frac": round(kb / us / 1e3 / HBM_PEAK_GBS, 4)}
+        if wtype == "q8_0":
+            kb = wbytes + m * h + m * h // 8 + m * shape.n_ff * 4   # int8 rows + scales in, f32 act out
+        else:
+            kb = wbytes + m * h + m * h // 64 + m * h // 8 + m * shape.n_ff * 4  # Q8_K rows, d, sub-block sums
+        out[f"gate_up_M{m}"] = {"kernel": {"q8_0": "mq8_kernel", "q4_k_m": "mkq_kernel"}[wtype] + "<EPI_SWIGLU>",
+                                "us_per_launch": round(us, 2), "bytes_per_launch": int(kb),
+                                "achieved_gbs": round(kb / us / 1e3, 1), "frac": round(kb / us / 1e3 / HBM_PEAK_GBS, 4)}
     eng.close()
     return out
 
@@ -417,6 +424,7 @@ def main():
     ap.add_argument("--prefill-prompts", type=int, default=32)
     ap.add_argument("--prefill-len", type=int, default=128)
     ap.add_argument("--q8-steps", type=int, default=32, help="Q8_0 decode steps (0: skip the Q8_0 section)")
+    ap.add_argument("--kq-steps", type=int, default=32, help="Q4_K_M decode steps (0: skip the Q4_K_M section)")
     ap.add_argument("--tiny-tokens", type=int, default=128,
                     help="TinyLlama-1.1B batch-1 tokens (config 2; 0: skip the section)")
     ap.add_argument("--big-steps", type=int, default=8, help="Llama-3-70B decode steps (0: skip the section)")
@@ -464,7 +472,9 @@ def main():
         line["tinyllama"] = sec.run("tinyllama", lambda: tiny_bench(args))
     line["hbm_probe"] = sec.run("hbm_probe", hbm_probe)
     if args.q8_steps > 0:
-        line["q8_0"] = sec.run("q8_0", lambda: q8_bench(args))
+        line["q8_0"] = sec.run("q8_0", lambda: quant_bench(args, "q8_0", args.q8_steps))
+    if args.kq_steps > 0:
+        line["q4_k_m"] = sec.run("q4_k_m", lambda: quant_bench(args, "q4_k_m", args.kq_steps))
     if args.big_steps > 0:
         line["llama3_70b"] = sec.run("llama3_70b", lambda: big_bench(args))
     line["section_seconds"] = sec.seconds

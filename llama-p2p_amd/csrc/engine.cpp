@@ -79,9 +79,60 @@ enum { L_ATTN_NORM, L_Q, L_K, L_V, L_O, L_FFN_NORM, L_GATE, L_UP, L_DOWN };
 uint64_t layer_tid(int l, int k) { return 16u + 16u * (uint64_t)l + (uint64_t)k; }
 float std_scale(double std) { return (float)(std / sqrt(4294967295.0 / 3.0)); }
 
+// Row segments of one packed K-quant matrix (MMArgs kq_*): rows appended in order, consecutive rows
+// of one ggml type share a segment (q|k Q4_K + v Q6_K = two segments).
+struct KqMat {
+  int n = 0;
+  int type[3] = {0, 0, 0}, tile_end[3] = {0, 0, 0};
+  size_t off[3] = {0, 0, 0};
+  size_t bytes = 0;
+  int rows = 0;
+  bool add(int t, int r, int K) {
+    if (n && type[n - 1] == t) {
+      tile_end[n - 1] += r / 16;
+    } else {
+      if (n == 3) return false;
+      type[n] = t;
+      off[n] = bytes;
+      tile_end[n] = (n ? tile_end[n - 1] : 0) + r / 16;
+      n++;
+    }
+    bytes += kq_matrix_bytes(t, r, K);
+    rows += r;
+    return true;
+  }
+  // segment holding packed row `row`, and that row's index within the segment
+  int seg(int row, int* row_in_seg) const {
+    int i = 0;
+    while (i < n - 1 && row / 16 >= tile_end[i]) i++;
+    *row_in_seg = row - 16 * (i ? tile_end[i - 1] : 0);
+    return i;
+  }
+  void set(MMArgs& a) const {
+    a.kq_n = n;
+    for (int i = 0; i < 3; i++) {
+      a.kq_type[i] = type[i];
+      a.kq_tile_end[i] = tile_end[i];
+      a.kq_off[i] = off[i];
+    }
+  }
+};
+
+// ggml type of a tensor in llama.cpp's Q4_K_M / Q5_K_M recipes (llama_tensor_get_type, Oct 2024;
+// synth.py kq_tensor_type is the same rule): output Q6_K; attn_v and ffn_down Q6_K on the
+// use_more_bits layers; attn_v of an 80-layer (70B) Q4_K_M model otherwise Q5_K; the rest `base`.
+bool use_more_bits(int i, int n) { return i < n / 8 || i >= 7 * n / 8 || (i - n / 8) % 3 == 2; }
+int kq_recipe_type(int base, int kind, int layer, int n_layer) {  // kind: L_* or -1 output, -2 token_embd
+  if (kind == -1) return 14;
+  if ((kind == 3 || kind == 8) && use_more_bits(layer, n_layer)) return 14;  // L_V, L_DOWN
+  if (kind == 3 && n_layer == 80 && base == 12) return 13;
+  return base;
+}
+
 struct Layer {
   uint16_t *qkv = nullptr, *o = nullptr, *gu = nullptr, *down = nullptr;
   float *attn_norm = nullptr, *ffn_norm = nullptr;
+  KqMat kq_qkv, kq_o, kq_gu, kq_down;  // K-quant model: segments of the four packed matrices
 };
 
 struct Request {
@@ -162,6 +213,14 @@ struct mx_engine {
   bool wq8 = false, embd_q8 = false, out_q8 = false;
   bool q8_ql = getenv("MX_NO_Q8_QL") == nullptr;  // Q8_0 GEMVs of <= 4 rows quantise their operand on load
   uint8_t* tok_embd8 = nullptr;
+  // K-quant model (Q4_K / Q5_K / Q6_K matrices: llama.cpp's Q4_K_M / Q5_K_M; kquant.hip): packed
+  // K-quant tiles, activations as Q8_K rows (q in xq8, d in xqd, sub-block sums in xkb)
+  bool wkq = false;
+  int kq_main_type = 0;          // type of ffn_gate (mx_model_info.weight_type)
+  int embd_kq_type = 0;          // token_embd kept as K-quant GGUF blocks when non-zero
+  uint8_t* tok_embd_kq = nullptr;
+  float* xkb = nullptr;
+  KqMat kq_out;
   int8_t* xq8 = nullptr;    // Q8_0 activation rows [PREFILL_ROWS][max(h, ff)]
   float* xqd = nullptr;     // their block scales
   float *attn_f = nullptr, *act_f = nullptr;  // f32 attention output / SwiGLU product (quantised next)
@@ -207,7 +266,7 @@ struct mx_engine {
     return 0;
   }
   int init_common();
-  int load_synthetic(const Shape& s, uint64_t seed, bool q8 = false);
+  int load_synthetic(const Shape& s, uint64_t seed, bool q8 = false, int kq_base = 0);
   int load_gguf(const std::string& path);
   int enqueue_forward(int M, const int* ids, const int* pos, const int* slot, const void* x_in, void* x_out,
                       bool head, const int* rowmap, int n_out, bool argmax, int* ids_next, int* pos_next, int* hist,
@@ -218,10 +277,13 @@ struct mx_engine {
   int enqueue_forward_q8(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap, int n_out,
                          bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count,
                          int max_hist, hipStream_t s);
+  int enqueue_forward_kq(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap, int n_out,
+                         bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count,
+                         int max_hist, hipStream_t s);
   int enqueue_forward_gemm(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap,
                            int n_out, hipStream_t s);
   bool gemm_ok() const {  // chunks of PREFILL_ROWS rows can run (the Q8_0 path takes any row count)
-    if (wq8) return true;
+    if (wq8 || wkq) return true;
     return gemm_supported(n_embd + 2 * n_embd_kv, n_embd) && gemm_supported(n_embd, n_embd) &&
            gemm_supported(2 * n_ff, n_embd) && gemm_supported(n_embd, n_ff);
   }
@@ -266,6 +328,7 @@ int mx_engine::init_common() {
     return fail(MX_ERR_ARG, "n_embd, n_ff must be multiples of 32 and n_vocab, n_embd_kv of 16");
   if (wq8 && (n_embd % Q8_TILE_K || n_ff % Q8_TILE_K))
     return fail(MX_ERR_ARG, "Q8_0 models need n_embd and n_ff multiples of 64");
+  if (wkq && (n_embd % 256 || n_ff % 256)) return fail(MX_ERR_ARG, "K-quant models need n_embd and n_ff multiples of 256");
   if (le < 0 || le > n_layer) le = n_layer;
   if (lb < 0 || lb >= le) return fail(MX_ERR_ARG, "bad layer range");
   has_embed = lb == 0;
@@ -328,12 +391,14 @@ int mx_engine::init_common() {
   if (int rc = alloc((void**)&d_rowmap, (size_t)R * 4)) return rc;
   if (int rc = alloc((void**)&sched_hist, (size_t)MAX_ROWS * SCHED_KMAX * 4)) return rc;
   if (int rc = alloc((void**)&sched_hist_count, (size_t)MAX_ROWS * 4)) return rc;
-  if (wq8) {
+  if (wq8 || wkq) {
     const size_t kmax = std::max(n_embd, n_ff);
     if (int rc = alloc((void**)&xq8, (size_t)R * kmax)) return rc;
     if (int rc = alloc((void**)&xqd, (size_t)R * (kmax / 32) * 4)) return rc;
     if (int rc = alloc((void**)&attn_f, (size_t)R * n_embd * 4)) return rc;
     if (int rc = alloc((void**)&act_f, (size_t)R * n_ff * 4)) return rc;
+    if (wkq)
+      if (int rc = alloc((void**)&xkb, (size_t)R * (kmax / 32) * 4)) return rc;
   }
   // poison-free start: zero activations so padded MFMA columns never read uninitialised memory
   HIPC(hipMemsetAsync(xn, 0, (size_t)R * n_embd * 2, stream));
@@ -368,14 +433,94 @@ static int alloc_layer(mx_engine* e, Layer& L) {
   return 0;
 }
 
-int mx_engine::load_synthetic(const Shape& s, uint64_t seed, bool q8) {
+// K-quant layer: segments from the seven matrix types (L_Q, L_K, L_V, L_O, L_GATE == L_UP, L_DOWN)
+static int alloc_layer_kq(mx_engine* e, Layer& L, const int t[9]) {
+  const int h = e->n_embd, kv = e->n_embd_kv, ff = e->n_ff;
+  L.kq_qkv = L.kq_o = L.kq_gu = L.kq_down = KqMat();
+  L.kq_qkv.add(t[L_Q], h, h);
+  L.kq_qkv.add(t[L_K], kv, h);
+  L.kq_qkv.add(t[L_V], kv, h);
+  L.kq_o.add(t[L_O], h, h);
+  if (t[L_GATE] != t[L_UP]) return fail(MX_ERR_MODEL, "ffn_gate and ffn_up of different K-quant types");
+  L.kq_gu.add(t[L_GATE], 2 * ff, h);
+  L.kq_down.add(t[L_DOWN], h, ff);
+  if (int rc = e->alloc((void**)&L.qkv, L.kq_qkv.bytes)) return rc;
+  if (int rc = e->alloc((void**)&L.o, L.kq_o.bytes)) return rc;
+  if (int rc = e->alloc((void**)&L.gu, L.kq_gu.bytes)) return rc;
+  if (int rc = e->alloc((void**)&L.down, L.kq_down.bytes)) return rc;
+  if (int rc = e->alloc((void**)&L.attn_norm, (size_t)h * 4)) return rc;
+  if (int rc = e->alloc((void**)&L.ffn_norm, (size_t)h * 4)) return rc;
+  e->weight_bytes += L.kq_qkv.bytes + L.kq_o.bytes + L.kq_gu.bytes + L.kq_down.bytes + 2 * (size_t)h * 4;
+  return 0;
+}
+
+// pack GGUF blocks of `rows` logical rows into a K-quant matrix at packed row `row0` (mode as launch_pack)
+static int pack_kq_rows(const KqMat& km, uint16_t* base, const uint8_t* blocks, int type, int rows, int K, int mode,
+                        int row0, hipStream_t s) {
+  int in_seg = 0;
+  const int sg = km.seg(row0, &in_seg);
+  if (km.type[sg] != type) return -1;
+  return launch_pack_kq((uint8_t*)base + km.off[sg], blocks, type, rows, K, mode, in_seg, s);
+}
+
+int mx_engine::load_synthetic(const Shape& s, uint64_t seed, bool q8, int kq_base) {
   n_embd = s.n_embd; n_layer = s.n_layer; n_head = s.n_head; n_head_kv = s.n_head_kv; n_ff = s.n_ff;
   n_vocab = s.n_vocab; rope_base = s.rope_base; eps = s.eps; n_ctx_train = s.n_ctx_train;
   if (le < 0 || le > n_layer) le = n_layer;
   wq8 = embd_q8 = out_q8 = q8;
+  wkq = kq_base != 0;
   if (int rc = init_common()) return rc;
   const float ws = std_scale(0.02), ns = std_scale(0.1);
   const int h = n_embd, kv = n_embd_kv, ff = n_ff, V = n_vocab;
+  if (wkq) {  // synth.py kq_tensor: the recipe's types, synthetic GGUF blocks packed like a file's
+    kq_main_type = kq_base;
+    const int bb_max = kq_block_bytes(14) > kq_block_bytes(kq_base) ? kq_block_bytes(14) : kq_block_bytes(kq_base);
+    const size_t stage_bytes = std::max({(size_t)V * h, (size_t)ff * h, (size_t)h * h}) / 256 * bb_max;
+    uint8_t* stage = nullptr;
+    HIPC(hipMalloc((void**)&stage, stage_bytes));
+    int rc = 0;
+    auto mat = [&](const KqMat& km, uint16_t* base, int type, uint64_t tid, int rows, int K, int mode, int row0) -> int {
+      if (launch_synth_kq_blocks(stage, type, (size_t)rows * K / 256, seed, tid, stream)) return fail(MX_ERR_ARG, "synth kq");
+      if (pack_kq_rows(km, base, stage, type, rows, K, mode, row0, stream)) return fail(MX_ERR_ARG, "pack kq");
+      return 0;
+    };
+    if (has_embed) {
+      embd_kq_type = kq_base;
+      if ((rc = alloc((void**)&tok_embd_kq, (size_t)V * (h / 256) * kq_block_bytes(kq_base)))) goto kq_out_label;
+      launch_synth_kq_blocks(tok_embd_kq, kq_base, (size_t)V * h / 256, seed, TID_TOK_EMBD, stream);
+      weight_bytes += (size_t)(h / 256) * kq_block_bytes(kq_base);
+    }
+    if (has_head) {
+      kq_out = KqMat();
+      kq_out.add(kq_recipe_type(kq_base, -1, 0, n_layer), V, h);
+      if ((rc = alloc((void**)&output, kq_out.bytes)) || (rc = alloc((void**)&out_norm, (size_t)h * 4))) goto kq_out_label;
+      if ((rc = mat(kq_out, output, kq_out.type[0], TID_OUTPUT, V, h, PACK_ROWS, 0))) goto kq_out_label;
+      launch_synth_norm(out_norm, h, seed, TID_OUT_NORM, ns, stream);
+      weight_bytes += kq_out.bytes + h * 4;
+    }
+    for (int l = lb; l < le && !rc; l++) {
+      Layer& L = layers[l - lb];
+      int t[9] = {0};
+      for (int k : {L_Q, L_K, L_V, L_O, L_GATE, L_UP, L_DOWN}) t[k] = kq_recipe_type(kq_base, k, l, n_layer);
+      if ((rc = alloc_layer_kq(this, L, t))) break;
+      launch_synth_norm(L.attn_norm, h, seed, layer_tid(l, L_ATTN_NORM), ns, stream);
+      launch_synth_norm(L.ffn_norm, h, seed, layer_tid(l, L_FFN_NORM), ns, stream);
+      if ((rc = mat(L.kq_qkv, L.qkv, t[L_Q], layer_tid(l, L_Q), h, h, PACK_ROWS, 0)) ||
+          (rc = mat(L.kq_qkv, L.qkv, t[L_K], layer_tid(l, L_K), kv, h, PACK_ROWS, h)) ||
+          (rc = mat(L.kq_qkv, L.qkv, t[L_V], layer_tid(l, L_V), kv, h, PACK_ROWS, h + kv)) ||
+          (rc = mat(L.kq_o, L.o, t[L_O], layer_tid(l, L_O), h, h, PACK_ROWS, 0)) ||
+          (rc = mat(L.kq_gu, L.gu, t[L_GATE], layer_tid(l, L_GATE), ff, h, PACK_GATE, 0)) ||
+          (rc = mat(L.kq_gu, L.gu, t[L_UP], layer_tid(l, L_UP), ff, h, PACK_UP, 0)) ||
+          (rc = mat(L.kq_down, L.down, t[L_DOWN], layer_tid(l, L_DOWN), h, ff, PACK_ROWS, 0)))
+        break;
+    }
+  kq_out_label:
+    hipStreamSynchronize(stream);
+    hipFree(stage);
+    if (rc) return rc;
+    HIPC(hipGetLastError());
+    return 0;
+  }
   if (q8) {  // the Q8_0 quantisation of the bf16 synthetic model (what llama-quantize makes of it)
     if (has_embed) {
       if (int rc = alloc((void**)&tok_embd8, (size_t)V * (h / 32) * 34)) return rc;
@@ -481,8 +626,10 @@ int mx_engine::load_gguf(const std::string& path) {
   }
   if (le < 0 || le > n_layer) le = n_layer;
   // Matrix types.  All BF16 -> the bf16 path; all Q8_0 -> the Q8_0 path (int8 MFMA on the blocks);
-  // any other mix of F32 / F16 / BF16 / Q4_0 / Q8_0 / Q4_K / Q5_K / Q6_K (Q4_K_M, Q5_K_M, ... files)
-  // -> every matrix is dequantised to bf16 at load (ggml's dequantize_row_*) and runs on the bf16 path.
+  // all Q4_K / Q5_K / Q6_K with ffn_gate and ffn_up of one type (llama.cpp's Q4_K_M, Q5_K_M files) ->
+  // the K-quant path (kquant.hip: int8 MFMA on the blocks with Q8_K activations); any other mix of
+  // F32 / F16 / BF16 / Q4_0 / Q8_0 / K-quants -> every matrix is dequantised to bf16 at load
+  // (ggml's dequantize_row_*) and runs on the bf16 path.
   bool deq = false;
   size_t raw_max = 0;
   {
@@ -492,7 +639,7 @@ int mx_engine::load_gguf(const std::string& path) {
     for (int l = b0; l < e0; l++)
       for (const char* k : kinds) mats.push_back("blk." + std::to_string(l) + "." + k + ".weight");
     if (e0 == n_layer) mats.push_back(f.tensor("output.weight") ? "output.weight" : "token_embd.weight");
-    int n8 = 0, n30 = 0;
+    int n8 = 0, n30 = 0, nkq = 0;
     for (const std::string& nm : mats) {
       const GGUFTensor* t = f.tensor(nm);
       if (!t) return fail(MX_ERR_MODEL, "missing tensor " + nm);
@@ -501,11 +648,19 @@ int mx_engine::load_gguf(const std::string& path) {
                                       " is not supported (F32, F16, BF16, Q4_0, Q8_0, Q4_K, Q5_K, Q6_K are)");
       n8 += t->type == 8;
       n30 += t->type == 30;
+      nkq += t->type == 12 || t->type == 13 || t->type == 14;
       raw_max = std::max(raw_max, (size_t)t->nbytes);
     }
     wq8 = out_q8 = n8 == (int)mats.size();
-    deq = !wq8 && n30 != (int)mats.size();
+    wkq = nkq == (int)mats.size() && n_embd % 256 == 0 && n_ff % 256 == 0;
+    for (int l = b0; l < e0 && wkq; l++) {
+      const std::string p = "blk." + std::to_string(l) + ".";
+      if (f.tensor(p + "ffn_gate.weight")->type != f.tensor(p + "ffn_up.weight")->type) wkq = false;
+    }
+    if (wkq) kq_main_type = f.tensor("blk." + std::to_string(b0) + ".ffn_gate.weight")->type;
+    deq = !wq8 && !wkq && n30 != (int)mats.size();
     embd_q8 = te->type == 8;
+    if (wkq && (te->type == 12 || te->type == 13 || te->type == 14)) embd_kq_type = te->type;
     if (te->type != 30 && te->type != 8) {
       if (!ggml_block_elems(te->type))
         return fail(MX_ERR_MODEL, "token_embd.weight: ggml type " + std::to_string(te->type) + " is not supported");
@@ -521,7 +676,7 @@ int mx_engine::load_gguf(const std::string& path) {
   uint16_t* stage = nullptr;
   uint8_t* stage_raw = nullptr;
   HIPC(hipMalloc((void**)&stage, stage_bytes));
-  if (raw_max && (deq || (te->type != 30 && te->type != 8))) {
+  if (raw_max && (deq || wkq || (te->type != 30 && te->type != 8))) {
     if (hipMalloc((void**)&stage_raw, raw_max) != hipSuccess) {
       hipFree(stage);
       return fail(MX_ERR_HIP, "staging buffer");
@@ -569,7 +724,79 @@ int mx_engine::load_gguf(const std::string& path) {
     HIPC(hipMemcpy(dst, f.data(*t), (size_t)h * 4, hipMemcpyHostToDevice));
     return 0;
   };
+  // K-quant matrix: raw blocks to the device, packed into the segment holding packed row row0
+  auto upload_kq = [&](const std::string& name, int rows, int cols, const KqMat& km, uint16_t* dst, int mode,
+                       int row0) -> int {
+    const GGUFTensor* t = f.tensor(name);
+    if (!t) return fail(MX_ERR_MODEL, "missing tensor " + name);
+    if (t->ne.size() != 2 || (int)t->ne[0] != cols || (int)t->ne[1] != rows)
+      return fail(MX_ERR_MODEL, "tensor " + name + " has unexpected shape");
+    HIPC(hipMemcpy(stage_raw, f.data(*t), t->nbytes, hipMemcpyHostToDevice));
+    if (pack_kq_rows(km, dst, stage_raw, t->type, rows, cols, mode, row0, stream))
+      return fail(MX_ERR_MODEL, "tensor " + name + ": K-quant type does not match its matrix segment");
+    HIPC(hipStreamSynchronize(stream));
+    return 0;
+  };
+  auto kq_layer_types = [&](int l, int t[9]) {
+    const std::string p = "blk." + std::to_string(l) + ".";
+    static const char* nm[9] = {nullptr, "attn_q", "attn_k", "attn_v", "attn_output", nullptr, "ffn_gate", "ffn_up", "ffn_down"};
+    for (int k = 0; k < 9; k++) t[k] = nm[k] ? f.tensor(p + nm[k] + ".weight")->type : 0;
+  };
   int rc = 0;
+  if (wkq) {
+    if (has_embed) {
+      const GGUFTensor* t = f.tensor("token_embd.weight");
+      if (t->ne.size() != 2 || (int)t->ne[0] != h || (int)t->ne[1] != V) {
+        rc = fail(MX_ERR_MODEL, "tensor token_embd.weight has unexpected shape");
+        goto out;
+      }
+      if (embd_kq_type) {  // GET_ROWS dequantises the blocks per lookup (dequantize_row_q*_K)
+        if ((rc = alloc((void**)&tok_embd_kq, t->nbytes))) goto out;
+        if (hipMemcpy(tok_embd_kq, f.data(*t), t->nbytes, hipMemcpyHostToDevice) != hipSuccess) {
+          rc = fail(MX_ERR_HIP, "upload token_embd");
+          goto out;
+        }
+        weight_bytes += t->nbytes / V;
+      } else if (t->type == 30) {
+        if ((rc = alloc((void**)&tok_embd, t->nbytes))) goto out;
+        if (hipMemcpy(tok_embd, f.data(*t), t->nbytes, hipMemcpyHostToDevice) != hipSuccess) {
+          rc = fail(MX_ERR_HIP, "upload token_embd");
+          goto out;
+        }
+        weight_bytes += (size_t)h * 2;
+      } else {
+        rc = fail(MX_ERR_MODEL, "token_embd.weight: K-quant models take a Q4_K/Q5_K/Q6_K or BF16 token_embd");
+        goto out;
+      }
+    }
+    if (has_head) {
+      const char* oname = f.tensor("output.weight") ? "output.weight" : "token_embd.weight";  // tied embeddings
+      kq_out = KqMat();
+      kq_out.add(f.tensor(oname)->type, V, h);
+      if ((rc = alloc((void**)&output, kq_out.bytes))) goto out;
+      if ((rc = alloc((void**)&out_norm, (size_t)h * 4))) goto out;
+      if ((rc = upload_kq(oname, V, h, kq_out, output, PACK_ROWS, 0))) goto out;
+      if ((rc = upload_norm("output_norm.weight", out_norm))) goto out;
+      weight_bytes += kq_out.bytes + h * 4;
+    }
+    for (int l = lb; l < le; l++) {
+      Layer& L = layers[l - lb];
+      const std::string p = "blk." + std::to_string(l) + ".";
+      int t[9];
+      kq_layer_types(l, t);
+      if ((rc = alloc_layer_kq(this, L, t))) goto out;
+      if ((rc = upload_norm(p + "attn_norm.weight", L.attn_norm))) goto out;
+      if ((rc = upload_norm(p + "ffn_norm.weight", L.ffn_norm))) goto out;
+      if ((rc = upload_kq(p + "attn_q.weight", h, h, L.kq_qkv, L.qkv, PACK_ROWS, 0))) goto out;
+      if ((rc = upload_kq(p + "attn_k.weight", kv, h, L.kq_qkv, L.qkv, PACK_ROWS, h))) goto out;
+      if ((rc = upload_kq(p + "attn_v.weight", kv, h, L.kq_qkv, L.qkv, PACK_ROWS, h + kv))) goto out;
+      if ((rc = upload_kq(p + "attn_output.weight", h, h, L.kq_o, L.o, PACK_ROWS, 0))) goto out;
+      if ((rc = upload_kq(p + "ffn_gate.weight", ff, h, L.kq_gu, L.gu, PACK_GATE, 0))) goto out;
+      if ((rc = upload_kq(p + "ffn_up.weight", ff, h, L.kq_gu, L.gu, PACK_UP, 0))) goto out;
+      if ((rc = upload_kq(p + "ffn_down.weight", h, ff, L.kq_down, L.down, PACK_ROWS, 0))) goto out;
+    }
+    goto out;
+  }
   if (has_embed) {
     const GGUFTensor* t = f.tensor("token_embd.weight");
     if (t->ne.size() != 2 || (int)t->ne[0] != h || (int)t->ne[1] != V) {
@@ -632,16 +859,23 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
   const bool wide = use_wide && M > 16;
   // RMS_NORM applied on load by the consuming GEMV (M <= 16); the residual-stream writers
   // (embedding, attn_output, ffn_down, or ssq_kernel for a stage's x_in) leave per-tile partials
-  const bool nol = !wide && !wq8 && norm_on_load && mm_can_norm_on_load(M, h);
+  const bool nol = !wide && !wq8 && !wkq && norm_on_load && mm_can_norm_on_load(M, h);
   const bool qql = q8_on_load(M);
   if (x_in) {
     HIPC(hipMemcpyAsync(x, x_in, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
     if (nol || qql) launch_ssq(x, M, h, ssq, s);
   } else {
     if (!has_embed) return fail(MX_ERR_STATE, "this stage has no token embedding: x_in required");
-    if (embd_q8) launch_embed_q8(x, tok_embd8, ids, M, h, (nol || qql) ? ssq : nullptr, s);
-    else launch_embed(x, tok_embd, ids, M, h, (nol || qql) ? ssq : nullptr, s);
+    if (embd_kq_type) {
+      if (launch_embed_kq(x, tok_embd_kq, embd_kq_type, ids, M, h, s)) return fail(MX_ERR_ARG, "K-quant embedding");
+    } else if (embd_q8) {
+      launch_embed_q8(x, tok_embd8, ids, M, h, (nol || qql) ? ssq : nullptr, s);
+    } else {
+      launch_embed(x, tok_embd, ids, M, h, (nol || qql) ? ssq : nullptr, s);
+    }
   }
+  if (wkq) return enqueue_forward_kq(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next, pos_next, hist,
+                                     hist_stride, hist_count, max_hist, s);
   if (wq8) return enqueue_forward_q8(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next, pos_next, hist,
                                      hist_stride, hist_count, max_hist, s);
   if (M > MAX_ROWS) {
@@ -864,6 +1098,69 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     site = 16;
     operand(g, x, h, out_norm, n_out, (rowmap || n_out != M) ? rowmap : nullptr);
     if (launch_mq8(EPI_F32, g, s)) return fail(MX_ERR_ARG, "q8 lm_head launch shape");
+    if (argmax)
+      launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, ids_next, pos_next, hist, hist_stride,
+                    hist_count, max_hist, s);
+  }
+  HIPC(hipGetLastError());
+  return 0;
+}
+
+// K-quant model, any M <= PREFILL_ROWS: every MUL_MAT takes Q8_K activation rows made by the norm
+// (RMS_NORM + MUL + quantise) or by launch_quantize_q8k from the f32 attention output / SwiGLU
+// product -- ggml's conversion of src1 to the K-quants' vec_dot_type.
+int mx_engine::enqueue_forward_kq(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap,
+                                  int n_out, bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride,
+                                  int* hist_count, int max_hist, hipStream_t s) {
+  const int h = n_embd, kv = n_embd_kv, ff = n_ff;
+  if (head && n_out > MAX_ROWS) return fail(MX_ERR_ARG, "logits for at most 64 rows per forward");
+  auto operand = [&](MMArgs& m, const KqMat& km, const float* src, int K, const float* norm_w, int rows,
+                     const int* rmap) -> int {
+    const int rc = norm_w ? launch_rmsnorm_q8k(xq8, xqd, xkb, src, norm_w, rmap, rows, K, eps, s)
+                          : launch_quantize_q8k(xq8, xqd, xkb, src, K, rows, K, s);
+    m.xq = xq8; m.xd = xqd; m.xb = xkb;
+    km.set(m);
+    return rc;
+  };
+  for (int li = 0; li < (int)layers.size(); li++) {
+    const Layer& L = layers[li];
+    _Float16* kc = kcache + layer_kv_stride * li;
+    _Float16* vc = vcache + layer_kv_stride * li;
+    MMArgs a{};
+    a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M;
+    if (operand(a, L.kq_qkv, x, h, L.attn_norm, M, nullptr)) return fail(MX_ERR_ARG, "kq norm shape");
+    a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
+    a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
+    a.slot_stride = slot_stride;
+    if (launch_mkq(EPI_QKV, a, s)) return fail(MX_ERR_ARG, "kq qkv launch shape");
+    AttnArgs at{};
+    at.q = q; at.kc = kc; at.vc = vc; at.pos = pos; at.slot = slot;
+    at.outf = attn_f; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
+    at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;
+    at.scale = 1.0f / sqrtf((float)head_dim);
+    if (M > MAX_ROWS && rows_blocked) launch_attention_prefill(at, s);
+    else launch_attention(at, s);
+    MMArgs b{};
+    b.W = L.o; b.N = h; b.K = h; b.M = M; b.out = x; b.ldo = h;
+    if (operand(b, L.kq_o, attn_f, h, nullptr, M, nullptr) || launch_mkq(EPI_RESID, b, s))
+      return fail(MX_ERR_ARG, "kq attn_output launch shape");
+    MMArgs c{};
+    c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.actf = act_f; c.lda = ff;
+    if (operand(c, L.kq_gu, x, h, L.ffn_norm, M, nullptr) || launch_mkq(EPI_SWIGLU, c, s))
+      return fail(MX_ERR_ARG, "kq gate/up launch shape");
+    MMArgs d{};
+    d.W = L.down; d.N = h; d.K = ff; d.M = M; d.out = x; d.ldo = h;
+    if (operand(d, L.kq_down, act_f, ff, nullptr, M, nullptr) || launch_mkq(EPI_RESID, d, s))
+      return fail(MX_ERR_ARG, "kq ffn_down launch shape");
+  }
+  if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
+  if (head) {
+    if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
+    MMArgs g{};
+    g.W = output; g.N = n_vocab; g.K = h; g.M = n_out; g.out = logits; g.ldo = n_vocab;
+    if (operand(g, kq_out, x, h, out_norm, n_out, (rowmap || n_out != M) ? rowmap : nullptr) ||
+        launch_mkq(EPI_F32, g, s))
+      return fail(MX_ERR_ARG, "kq lm_head launch shape");
     if (argmax)
       launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, ids_next, pos_next, hist, hist_stride,
                     hist_count, max_hist, s);
@@ -1369,6 +1666,7 @@ int mx_engine_create(const char* model_path, const mx_opts* opts, mx_engine** ou
     std::string rest = path.substr(10), name = rest;
     uint64_t seed = o.seed;
     bool q8 = false;
+    int kq = 0;
     size_t c = rest.find(':');
     if (c != std::string::npos) {
       name = rest.substr(0, c);
@@ -1378,6 +1676,8 @@ int mx_engine_create(const char* model_path, const mx_opts* opts, mx_engine** ou
         const std::string part = tail.substr(0, e2);
         if (part.rfind("seed=", 0) == 0) seed = strtoull(part.c_str() + 5, nullptr, 10);
         else if (part == "q8_0") q8 = true;
+        else if (part == "q4_k_m") kq = 12;
+        else if (part == "q5_k_m") kq = 13;
         else if (part != "bf16") return fail(MX_ERR_MODEL, "unknown synthetic option '" + part + "'");
         tail = e2 == std::string::npos ? "" : tail.substr(e2 + 1);
       }
@@ -1386,7 +1686,7 @@ int mx_engine_create(const char* model_path, const mx_opts* opts, mx_engine** ou
     for (const Shape& k : kShapes)
       if (name == k.name) s = &k;
     if (!s) return fail(MX_ERR_MODEL, "unknown synthetic shape '" + name + "'");
-    rc = e->load_synthetic(*s, seed, q8);
+    rc = e->load_synthetic(*s, seed, q8, kq);
   } else {
     rc = e->load_gguf(path);
   }
@@ -1411,7 +1711,7 @@ int mx_engine_info(const mx_engine* e, mx_model_info* o) {
   o->eps = e->eps; o->rope_base = e->rope_base; o->bos_id = e->bos; o->eos_id = e->eos;
   o->n_ctx = e->n_ctx; o->n_seq_max = e->n_seq_max; o->layer_begin = e->lb; o->layer_end = e->le;
   o->has_embed = e->has_embed; o->has_head = e->has_head; o->weight_bytes = e->weight_bytes;
-  o->weight_type = e->wq8 ? 8 : 30;
+  o->weight_type = e->wq8 ? 8 : e->wkq ? e->kq_main_type : 30;
   return 0;
 }
 
@@ -1826,7 +2126,36 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
           return launch_mq8(EPI_F32, a, s);
       }
     }
-    if (e->wq8 && (kind == 5 || kind == 6)) return -1;
+    if (e->wkq && kind <= 4) {  // K-quant weights: the activations are Q8_K rows in xq8/xqd/xkb
+      a.xq = e->xq8; a.xd = e->xqd; a.xb = e->xkb;
+      switch (kind) {
+        case 0:
+          a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.out = e->q; a.ldo = h; a.n_q = h; a.n_kv = kv;
+          a.head_dim = e->head_dim; a.pos = e->d_pos; a.slot = e->d_slot; a.rope_cs = e->rope_cs;
+          a.kc = e->kcache + e->layer_kv_stride * li; a.vc = e->vcache + e->layer_kv_stride * li;
+          a.n_ctx = e->n_ctx; a.ctx_stride = e->ctx_stride; a.n_head_kv = e->n_head_kv; a.slot_stride = e->slot_stride;
+          L.kq_qkv.set(a);
+          per = L.kq_qkv.bytes;
+          return launch_mkq(EPI_QKV, a, s);
+        case 1: case 3:
+          a.W = kind == 1 ? L.o : L.down; a.N = h; a.K = kind == 1 ? h : ff; a.out = e->x; a.ldo = h;
+          (kind == 1 ? L.kq_o : L.kq_down).set(a);
+          per = (kind == 1 ? L.kq_o : L.kq_down).bytes;
+          return launch_mkq(EPI_RESID, a, s);
+        case 2:
+          a.W = L.gu; a.N = 2 * ff; a.K = h; a.actf = e->act_f; a.lda = ff;
+          L.kq_gu.set(a);
+          per = L.kq_gu.bytes;
+          return launch_mkq(EPI_SWIGLU, a, s);
+        case 4:
+          if (!e->has_head) return -1;
+          a.W = e->output; a.N = e->n_vocab; a.K = h; a.out = e->logits; a.ldo = e->n_vocab;
+          e->kq_out.set(a);
+          per = e->kq_out.bytes;
+          return launch_mkq(EPI_F32, a, s);
+      }
+    }
+    if ((e->wq8 || e->wkq) && (kind >= 5 && kind <= 6)) return -1;
     switch (kind) {
       case 0:
         a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.X = e->xn; a.ldx = h; a.out = e->q; a.ldo = h; a.n_q = h;

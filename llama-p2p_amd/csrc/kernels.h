@@ -65,6 +65,15 @@ struct MMArgs {
   int n_ctx, ctx_stride, n_head_kv;
   size_t slot_stride;          // elements per slot in kc/vc = n_head_kv*ctx_stride*head_dim
   size_t slab_stride;          // EPI_SLAB: floats between consecutive K-split partial slabs
+  // K-quant weights (mkq_kernel): activations as Q8_K rows -- xq int8 [M][K] (permuted within each
+  // super-block, kquant.hip), xd f32 [M][K/256], xb f32 [M][K/32] (sub-block sums of q) -- and W
+  // as up to 3 row segments of one ggml type each (e.g. q|k Q4_K, v Q6_K): segment i holds packed
+  // tiles [kq_tile_end[i-1], kq_tile_end[i]) at byte offset kq_off[i] from W
+  const float* xb;
+  int kq_n;
+  int kq_type[3];
+  int kq_tile_end[3];
+  size_t kq_off[3];
 };
 
 struct AttnArgs {
@@ -157,6 +166,26 @@ void launch_quantize_q8(int8_t* xq, float* xd, const float* src, int ld, int M, 
 // partials when a.ssq.
 int launch_mq8(int epi, const MMArgs& a, hipStream_t s);
 bool mq8_can_quantize_on_load(int M, int K, bool norm);
+
+// ---- K-quant weights (GGUF Q4_K 12, Q5_K 13, Q6_K 14), kquant.hip.  Packed tile =
+// 16 rows x 256 k (one super-block per row) in MFMA operand lane order: kq_tile_bytes(type) bytes
+// (2368 / 2880 / 3360), tiles nt-major like the bf16 tiles.
+int kq_tile_bytes(int type);  // 0 for a type without a K-quant tile
+int kq_block_bytes(int type);  // GGUF block bytes per 256 weights (144 / 176 / 210)
+inline size_t kq_matrix_bytes(int type, int N, int K) { return (size_t)N / 16 * (K / 256) * kq_tile_bytes(type); }
+// GGUF blocks [N][K/256] -> packed tiles (packed_row modes as launch_pack); -1 for a bad type/shape
+int launch_pack_kq(uint8_t* dst, const uint8_t* src_blocks, int type, int N, int K, int mode, int row_offset,
+                   hipStream_t s);
+// the synthetic model's GGUF blocks (synth.py kq_blocks), row-major
+int launch_synth_kq_blocks(uint8_t* dst, int type, size_t nblocks, uint64_t seed, uint64_t tid, hipStream_t s);
+// GET_ROWS of a K-quant token_embd (dequantize_row_q{4,5,6}_K, f32)
+int launch_embed_kq(float* x, const uint8_t* tok_blocks, int type, const int* ids, int M, int n, hipStream_t s);
+// RMS_NORM + MUL then Q8_K (xq [M][n], xd [M][n/256], xb [M][n/32]); plain Q8_K of f32 rows
+int launch_rmsnorm_q8k(int8_t* xq, float* xd, float* xb, const float* x, const float* w, const int* row_map, int M,
+                       int n, float eps, hipStream_t s);
+int launch_quantize_q8k(int8_t* xq, float* xd, float* xb, const float* src, int ld, int M, int n, hipStream_t s);
+// K-quant x Q8_K products for any M (grid.y: groups of 64 tokens), the usual epilogues (SWIGLU: actf)
+int launch_mkq(int epi, const MMArgs& a, hipStream_t s);
 
 // top-k (k <= TOPK_MAX) candidates per logits row, value descending, ties by lower id; ws: M*64*k
 constexpr int TOPK_MAX = 64;

@@ -53,6 +53,8 @@ __global__ void synth_rowmajor_kernel(uint16_t* dst, size_t n, uint64_t seed, ui
 }
 
 __global__ void synth_norm_kernel(float* dst, size_t n, uint64_t seed, uint64_t tid, float scale) {
+  // 1 + v rounded twice, as synth.py and the oracle (hipcc would otherwise contract it into an fma)
+#pragma clang fp contract(off)
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     dst[i] = 1.0f + synth_value(seed, tid, i, scale);
 }

@@ -1,0 +1,584 @@
+// kquant.hip -- K-quant weights (GGUF Q4_K, Q5_K, Q6_K) on the int8 MFMA path  (SURVEY §8a a16).
+//
+// llama.cpp runs a K-quant MUL_MAT as ggml_vec_dot_q{4,5,6}_K_q8_K: the f32 activation row is
+// quantised to Q8_K (per 256 values: iscale = -127/max, q = nearest_int(iscale*x), d = 1/iscale,
+// bsums per 16), and every super-block of 256 weights contributes an exact int32
+//   Q4_K / Q5_K:  S = sum_j sc_j * (q_w . q_x over 32-value sub-block j),  Mn = sum_j m_j * bsum32_j
+//   Q6_K:         S = sum_g sc_g * (q_w . q_x over 16-value group g)        (q_w = 6-bit value - 32)
+// scaled in f32:  acc += (f16(d) * d_x) * S  -  (f16(dmin) * d_x) * Mn.
+// Here the q_w . q_x products run on v_mfma_i32_16x16x32_i8 (16 rows x 16 tokens x one 32-k
+// sub-block; Q6_K two per sub-block, each with the lanes of the other 16-k group zeroed), the
+// mins term on v_mfma_f32_16x16x4_f32 (exact: every operand and sum is an integer < 2^24) and the
+// scale multiply-adds in int32 on the VALU -- so each super-block integer equals ggml's and only
+// the f32 accumulation order differs (ggml's own SIMD paths differ from its scalar one the same way).
+//
+// Weights are repacked at load into tiles of 16 rows x 256 k (kernels.h kq_tile_bytes) whose byte
+// order is the lane order of the MFMA operands: a wave reads each tile region as contiguous 16 B
+// per lane, and the 4-bit fields unpack with two mask/shift operations per 8 values.  Bytes per
+// weight equal the GGUF's (Q6_K exactly; Q4_K / Q5_K +2.8% / +2.3% for byte-aligned scales).
+// Activation rows are Q8_K images made once per GEMV by the producer side (RMS_NORM + quantise, or
+// quantise of the attention output / SwiGLU product), k permuted within each super-block so a
+// lane's 8-byte B fragments of all 8 sub-blocks are one 64-byte run.
+#include "device_common.h"
+
+namespace mx {
+
+// ---------------------------------------------------------------------------
+// Packed tile layout, per 16 rows x 256 k (one super-block of 16 weight rows):
+//   [0, 2048)   QS: lane l (row r = l&15, k-slice g = l>>4) owns 8 dwords D[0..7], D[j] holding
+//               the low 4 bits of value (j, e) -- k = 32j + 8g + e -- in byte e&3, nibble e>>2;
+//               D[0..3] at 16*l, D[4..7] at 1024 + 16*l
+//   Q5_K  [2048, 2560): lane l's 2 dwords at 2048 + 8l: bit 4 of value (j, e) at bit
+//               8*(e&3) + (u&7) of dword u>>3, u = 2j + (e>>2)
+//   Q6_K  [2048, 3072): lane l's 4 dwords at 2048 + 16l: bits 4-5 of value (j, e) at bits
+//               8*(e&3) + 2*(u&3) of dword u>>2
+//   Q4_K / Q5_K scales at SC = 2048 / 2560:  SC + 8r + j: 6-bit scale of row r, sub-block j;
+//               SC + 128 + 2l: mins (row l&15, sub-blocks l>>4 and 4 + (l>>4));
+//               SC + 256 + 4r: f16 d, f16 dmin of row r
+//   Q6_K scales at SC = 3072:  SC + 16r + g: int8 scale of row r, 16-value group g;
+//               SC + 256 + 2r: f16 d of row r
+// ---------------------------------------------------------------------------
+template <int T>
+struct KqTile;
+template <>
+struct KqTile<12> {
+  static constexpr int BYTES = 2368, SC = 2048, BLOCK = 144;
+};
+template <>
+struct KqTile<13> {
+  static constexpr int BYTES = 2880, SC = 2560, BLOCK = 176;
+};
+template <>
+struct KqTile<14> {
+  static constexpr int BYTES = 3360, SC = 3072, BLOCK = 210;
+};
+
+int kq_tile_bytes(int type) {
+  return type == 12 ? KqTile<12>::BYTES : type == 13 ? KqTile<13>::BYTES : type == 14 ? KqTile<14>::BYTES : 0;
+}
+int kq_block_bytes(int type) {
+  return type == 12 ? KqTile<12>::BLOCK : type == 13 ? KqTile<13>::BLOCK : type == 14 ? KqTile<14>::BLOCK : 0;
+}
+
+// The 256 values of one GGUF super-block in k order (Q4_K 0..15, Q5_K 0..31, Q6_K 0..63 before
+// the -32) -- ggml-common.h block_q4_K {d, dmin, scales[12], qs[128]}, block_q5_K {d, dmin,
+// scales[12], qh[32], qs[128]}, block_q6_K {ql[128], qh[64], scales[16], d}.
+__device__ __forceinline__ int kq_value(int type, const uint8_t* b, int k) {
+  if (type == 14) {
+    const int h = k >> 7, i = (k >> 5) & 3, l = k & 31;
+    const int L = b[64 * h + 32 * (i & 1) + l];
+    const int H = b[128 + 32 * h + l];
+    return ((i < 2 ? L & 15 : L >> 4) | (((H >> (2 * i)) & 3) << 4));
+  }
+  const int g = k >> 6, hi = (k >> 5) & 1, l = k & 31;
+  const uint8_t* qs = b + (type == 13 ? 48 : 16);
+  int v = hi ? qs[32 * g + l] >> 4 : qs[32 * g + l] & 15;
+  if (type == 13) v |= ((b[16 + l] >> (2 * g + hi)) & 1) << 4;
+  return v;
+}
+
+// One thread per (row, super-block): decode the GGUF block, write the row's bytes of its tile.
+template <int T>
+__global__ void pack_kq_kernel(uint8_t* dst, const uint8_t* src, int N, int K, int mode, int offset) {
+  const int SB = K / 256;
+  const size_t total = (size_t)N * SB;
+  for (size_t it = blockIdx.x * (size_t)blockDim.x + threadIdx.x; it < total; it += (size_t)gridDim.x * blockDim.x) {
+    const int row = (int)(it / SB), sb = (int)(it % SB);
+    const uint8_t* b = src + it * KqTile<T>::BLOCK;
+    const int P = packed_row(row, mode, offset);
+    uint8_t* tile = dst + ((size_t)(P >> 4) * SB + sb) * KqTile<T>::BYTES;
+    const int r = P & 15;
+    for (int g = 0; g < 4; ++g) {
+      const int lane = r + 16 * g;
+      uint32_t D[8] = {0, 0, 0, 0, 0, 0, 0, 0}, H[4] = {0, 0, 0, 0};
+      for (int j = 0; j < 8; ++j)
+        for (int e = 0; e < 8; ++e) {
+          const int v = kq_value(T, b, 32 * j + 8 * g + e);
+          D[j] |= (uint32_t)(v & 15) << (8 * (e & 3) + 4 * (e >> 2));
+          const int u = 2 * j + (e >> 2);
+          if (T == 13) H[u >> 3] |= (uint32_t)((v >> 4) & 1) << (8 * (e & 3) + (u & 7));
+          if (T == 14) H[u >> 2] |= (uint32_t)((v >> 4) & 3) << (8 * (e & 3) + 2 * (u & 3));
+        }
+      for (int j = 0; j < 8; ++j) *reinterpret_cast<uint32_t*>(tile + (j >> 2) * 1024 + 16 * lane + 4 * (j & 3)) = D[j];
+      if (T == 13)
+        for (int c = 0; c < 2; ++c) *reinterpret_cast<uint32_t*>(tile + 2048 + 8 * lane + 4 * c) = H[c];
+      if (T == 14)
+        for (int c = 0; c < 4; ++c) *reinterpret_cast<uint32_t*>(tile + 2048 + 16 * lane + 4 * c) = H[c];
+    }
+    constexpr int SC = KqTile<T>::SC;
+    if (T == 14) {
+      for (int g = 0; g < 16; ++g) tile[SC + 16 * r + g] = b[192 + g];
+      tile[SC + 256 + 2 * r] = b[208];
+      tile[SC + 256 + 2 * r + 1] = b[209];
+    } else {
+      const uint8_t* q = b + 4;  // get_scale_min_k4
+      uint8_t sc[8], mn[8];
+      for (int j = 0; j < 8; ++j) {
+        if (j < 4) {
+          sc[j] = q[j] & 63;
+          mn[j] = q[j + 4] & 63;
+        } else {
+          sc[j] = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
+          mn[j] = (q[j + 4] >> 4) | ((q[j] >> 6) << 4);
+        }
+        tile[SC + 8 * r + j] = sc[j];
+      }
+      for (int g = 0; g < 4; ++g) {
+        tile[SC + 128 + 2 * (r + 16 * g)] = mn[g];
+        tile[SC + 128 + 2 * (r + 16 * g) + 1] = mn[g + 4];
+      }
+      for (int c = 0; c < 4; ++c) tile[SC + 256 + 4 * r + c] = b[c];
+    }
+  }
+}
+
+int launch_pack_kq(uint8_t* dst, const uint8_t* src, int type, int N, int K, int mode, int offset, hipStream_t s) {
+  if (K % 256 || N % 8) return -1;
+  const int g = fill_grid((size_t)N * (K / 256));
+  switch (type) {
+    case 12: pack_kq_kernel<12><<<g, 256, 0, s>>>(dst, src, N, K, mode, offset); return 0;
+    case 13: pack_kq_kernel<13><<<g, 256, 0, s>>>(dst, src, N, K, mode, offset); return 0;
+    case 14: pack_kq_kernel<14><<<g, 256, 0, s>>>(dst, src, N, K, mode, offset); return 0;
+  }
+  return -1;
+}
+
+// Synthetic K-quant blocks (synth.py kq_blocks is the spec): byte i of the tensor's block stream
+// is byte i%8 of the synthetic hash of i/8; the f16 scale fields are then fixed-exponent bit
+// patterns with a random mantissa byte, Q6_K's int8 scales folded into [-24, 23].
+__device__ __forceinline__ uint64_t synth_hash(uint64_t seed, uint64_t tid, uint64_t idx) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + tid * 0xD1B54A32D192ED03ull + idx;
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void synth_kq_kernel(uint8_t* dst, int type, int bb, size_t nblocks, uint64_t seed, uint64_t tid) {
+  for (size_t b = blockIdx.x * (size_t)blockDim.x + threadIdx.x; b < nblocks; b += (size_t)gridDim.x * blockDim.x) {
+    uint8_t* p = dst + b * bb;
+    for (int i = 0; i < bb; ++i) {
+      const uint64_t gi = (uint64_t)b * bb + i;
+      p[i] = (uint8_t)(synth_hash(seed, tid, gi >> 3) >> (8 * (gi & 7)));
+    }
+    if (type == 14) {
+      for (int j = 0; j < 16; ++j) p[192 + j] = (uint8_t)(int8_t)((int)(p[192 + j] % 48) - 24);
+      const uint32_t d = 0x0500u + p[208];
+      p[208] = (uint8_t)d;
+      p[209] = (uint8_t)(d >> 8);
+    } else {
+      const uint32_t d = 0x0500u + p[0], mn = (type == 13 ? 0x1500u : 0x1100u) + p[1];
+      p[0] = (uint8_t)d;
+      p[1] = (uint8_t)(d >> 8);
+      p[2] = (uint8_t)mn;
+      p[3] = (uint8_t)(mn >> 8);
+    }
+  }
+}
+
+int launch_synth_kq_blocks(uint8_t* dst, int type, size_t nblocks, uint64_t seed, uint64_t tid, hipStream_t s) {
+  const int bb = kq_block_bytes(type);
+  if (!bb) return -1;
+  synth_kq_kernel<<<fill_grid(nblocks), 256, 0, s>>>(dst, type, bb, nblocks, seed, tid);
+  return 0;
+}
+
+// GET_ROWS of a K-quant token_embd: dequantize_row_q{4,5,6}_K (f32, one rounding per operation)
+__global__ __launch_bounds__(256) void embed_kq_kernel(float* x, const uint8_t* tok, int type, int bb, const int* ids,
+                                                       int n) {
+#pragma clang fp contract(off)
+  const int c = blockIdx.x;
+  const uint8_t* row = tok + (size_t)ids[c] * (n / 256) * bb;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const uint8_t* b = row + (size_t)(k / 256) * bb;
+    const int kk = k % 256;
+    const int v = kq_value(type, b, kk);
+    float y;
+    if (type == 14) {
+      const float d = (float)__builtin_bit_cast(_Float16, (uint16_t)(b[208] | (b[209] << 8)));
+      y = (d * (float)(int8_t)b[192 + kk / 16]) * (float)(v - 32);
+    } else {
+      const int j = kk / 32;
+      const uint8_t* q = b + 4;
+      const int sc = j < 4 ? q[j] & 63 : (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
+      const int mn = j < 4 ? q[j + 4] & 63 : (q[j + 4] >> 4) | ((q[j] >> 6) << 4);
+      const float d = (float)__builtin_bit_cast(_Float16, (uint16_t)(b[0] | (b[1] << 8)));
+      const float dmin = (float)__builtin_bit_cast(_Float16, (uint16_t)(b[2] | (b[3] << 8)));
+      y = (d * (float)sc) * (float)v - dmin * (float)mn;
+    }
+    x[(size_t)c * n + k] = y;
+  }
+}
+
+int launch_embed_kq(float* x, const uint8_t* tok, int type, const int* ids, int M, int n, hipStream_t s) {
+  const int bb = kq_block_bytes(type);
+  if (!bb || n % 256) return -1;
+  embed_kq_kernel<<<M, 256, 0, s>>>(x, tok, type, bb, ids, n);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Q8_K activation rows.  xq int8 [M][K]: within super-block s, logical k = 256s + 32j + 8g + e
+// sits at 256s + 64g + 8j + e (lane group g's 8 sub-block fragments contiguous); xd f32 [M][K/256]
+// (d = 1/iscale); xb f32 [M][K/32]: the sum of the 32 q of sub-block j at 8s + 2(j&3) + (j>>2)
+// (the B operand order of the mins MFMA).
+// One wave per super-block: lane t holds x[256s + 4t .. 4t+3].
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void q8k_store(f32x4 v, int t, int8_t* qsb, float* dsb, float* xbsb) {
+  float a = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+  float amax = a;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+  // ggml takes max = the signed value of the FIRST element with |x| == amax
+  int first = 1 << 20;
+  float cand = 0.f;
+#pragma unroll
+  for (int i = 3; i >= 0; --i)
+    if (fabsf(v[i]) == amax) {
+      first = 4 * t + i;
+      cand = v[i];
+    }
+  int key = first;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) key = min(key, __shfl_xor(key, o));
+  const float mx = __shfl(cand, (key >> 2) & 63);
+  uint32_t w = 0;
+  int qs[4] = {0, 0, 0, 0};
+  float d = 0.f;
+  if (amax != 0.f) {
+    const float iscale = -127.f / mx;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = (int)__builtin_rintf(iscale * v[i]);
+      qs[i] = q < 127 ? q : 127;
+      w |= (uint32_t)(uint8_t)(int8_t)qs[i] << (8 * i);
+    }
+    d = 1.f / iscale;
+  }
+  const int j = t >> 3, g = (t >> 1) & 3;
+  *reinterpret_cast<uint32_t*>(qsb + 64 * g + 8 * j + 4 * (t & 1)) = w;
+  int bs = qs[0] + qs[1] + qs[2] + qs[3];
+  bs += __shfl_xor(bs, 1);
+  bs += __shfl_xor(bs, 2);
+  bs += __shfl_xor(bs, 4);
+  if ((t & 7) == 0) xbsb[2 * (j & 3) + (j >> 2)] = (float)bs;
+  if (t == 0) *dsb = d;
+}
+
+// RMS_NORM + MUL (norm_q8_kernel's arithmetic), then Q8_K; one work-group (4 waves) per row
+__global__ __launch_bounds__(256) void norm_q8k_kernel(int8_t* xq, float* xd, float* xb, const float* x, const float* w,
+                                                       const int* row_map, int n, float eps) {
+  const int c = blockIdx.x;
+  const int r = row_map ? row_map[c] : c;
+  const float* xr = x + (size_t)r * n;
+  double acc = 0.0;
+  for (int i = threadIdx.x * 4; i < n; i += 1024) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc += (double)(v[j] * v[j]);
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  __shared__ double part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  const double sum = part[0] + part[1] + part[2] + part[3];
+  const float scale = 1.0f / sqrtf((float)(sum / n) + eps);
+  const int t = threadIdx.x & 63;
+  for (int s = threadIdx.x >> 6; s < n / 256; s += 4) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(xr + 256 * s + 4 * t);
+    const f32x4 g = *reinterpret_cast<const f32x4*>(w + 256 * s + 4 * t);
+    f32x4 y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = (v[j] * scale) * g[j];
+    q8k_store(y, t, xq + (size_t)c * n + 256 * s, xd + (size_t)c * (n / 256) + s, xb + (size_t)c * (n / 32) + 8 * s);
+  }
+}
+
+__global__ __launch_bounds__(256) void quantize_q8k_kernel(int8_t* xq, float* xd, float* xb, const float* src, int ld,
+                                                           int n) {
+  const int c = blockIdx.x;
+  const int t = threadIdx.x & 63;
+  for (int s = threadIdx.x >> 6; s < n / 256; s += 4)
+    q8k_store(*reinterpret_cast<const f32x4*>(src + (size_t)c * ld + 256 * s + 4 * t), t, xq + (size_t)c * n + 256 * s,
+              xd + (size_t)c * (n / 256) + s, xb + (size_t)c * (n / 32) + 8 * s);
+}
+
+int launch_rmsnorm_q8k(int8_t* xq, float* xd, float* xb, const float* x, const float* w, const int* row_map, int M, int n,
+                       float eps, hipStream_t s) {
+  if (n % 256 || M < 1) return -1;
+  norm_q8k_kernel<<<M, 256, 0, s>>>(xq, xd, xb, x, w, row_map, n, eps);
+  return 0;
+}
+int launch_quantize_q8k(int8_t* xq, float* xd, float* xb, const float* src, int ld, int M, int n, hipStream_t s) {
+  if (n % 256 || M < 1) return -1;
+  quantize_q8k_kernel<<<M, 256, 0, s>>>(xq, xd, xb, src, ld, n);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// K-quant x Q8_K MUL_MAT.  Work-group = RT row tiles of one segment (one ggml type) x NB column
+// tiles of 16 tokens (grid.y: groups of 16*NB tokens); its KS waves split the K/256 super-blocks,
+// each keeping a ring of U super-blocks' loads in flight; partial tiles are summed through LDS and
+// finished by the same epilogues as the bf16 / Q8_0 GEMVs (kernels.hip epi_store).
+// ---------------------------------------------------------------------------
+template <int RT, int NB>
+struct KqFrag {
+  u32x4 qs[RT][2];
+  u32x4 h[RT];      // Q5_K: dwords 0-1; Q6_K: 0-3
+  u32x4 sc[RT][4];  // Q4_K / Q5_K: [0..1]; Q6_K: [0..3]
+  u32x4 dm[RT];     // Q4_K / Q5_K: f16 (d, dmin) x 4 rows; Q6_K: dwords 0-1 = f16 d x 4 rows
+  uint32_t mn[RT];
+  u32x4 x[NB][4];
+  float dx[NB];
+  f32x2 xb[NB];
+};
+
+template <int T, int KS, int RT, int NB, int EPI, int U>
+__device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int tile_in_seg, int tile0,
+                                         f32x4 (*red)[RT][NB][64]) {
+  constexpr int TB = KqTile<T>::BYTES, SC = KqTile<T>::SC;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int g = lane >> 4;
+  const int SB = a.K / 256;
+  const int kb = (SB * w) / KS, ke = (SB * (w + 1)) / KS;
+  const int cb = blockIdx.y * 16 * NB;
+
+  const uint8_t* Wr[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) Wr[r] = W + (size_t)(tile_in_seg + r) * SB * TB;
+  const int8_t* Xq[NB];
+  const float* Xd[NB];
+  const float* Xb[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    int col = cb + n * 16 + (lane & 15);
+    col = col < a.M ? col : a.M - 1;  // padded columns re-read a valid row (outputs dropped)
+    Xq[n] = a.xq + (size_t)col * a.K + 64 * g;
+    Xd[n] = a.xd + (size_t)col * SB;
+    Xb[n] = a.xb + (size_t)col * (a.K / 32) + 2 * g;
+  }
+
+  f32x4 acc[RT][NB];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  using Frag = KqFrag<RT, NB>;
+  auto load = [&](Frag& f, int sb) {
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const uint8_t* t = Wr[r] + (size_t)sb * TB;
+      f.qs[r][0] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t) + lane);
+      f.qs[r][1] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t + 1024) + lane);
+      if constexpr (T == 13) {
+        const u32x2 hv = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(t + 2048) + lane);
+        f.h[r] = u32x4{hv[0], hv[1], 0u, 0u};
+      }
+      if constexpr (T == 14) f.h[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t + 2048) + lane);
+      if constexpr (T == 14) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) f.sc[r][c] = *reinterpret_cast<const u32x4*>(t + SC + 64 * g + 16 * c);
+        const u32x2 dv = *reinterpret_cast<const u32x2*>(t + SC + 256 + 8 * g);
+        f.dm[r] = u32x4{dv[0], dv[1], 0u, 0u};
+      } else {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) f.sc[r][c] = *reinterpret_cast<const u32x4*>(t + SC + 32 * g + 16 * c);
+        f.mn[r] = *reinterpret_cast<const uint16_t*>(t + SC + 128 + 2 * lane);
+        f.dm[r] = *reinterpret_cast<const u32x4*>(t + SC + 256 + 16 * g);
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) f.x[n][c] = *reinterpret_cast<const u32x4*>(Xq[n] + (size_t)sb * 256 + 16 * c);
+      f.dx[n] = Xd[n][sb];
+      if constexpr (T != 14) f.xb[n] = *reinterpret_cast<const f32x2*>(Xb[n] + 8 * sb);
+    }
+  };
+  auto compute = [&](const Frag& f) {
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      uint32_t D[8];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        D[c] = f.qs[r][0][c];
+        D[4 + c] = f.qs[r][1][c];
+      }
+      uint32_t scw[16];
+#pragma unroll
+      for (int c = 0; c < (T == 14 ? 4 : 2); ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) scw[4 * c + e] = f.sc[r][c][e];
+      // sub-block by sub-block: unpack its A operand and scales once, then one MFMA (Q6_K: two)
+      // per column tile into that tile's int32 super-block sums
+      i32x4 S[NB];
+#pragma unroll
+      for (int n = 0; n < NB; ++n) S[n] = i32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uint32_t lo = D[j] & 0x0F0F0F0Fu, hi = (D[j] >> 4) & 0x0F0F0F0Fu;
+        if constexpr (T == 13) {
+          const uint32_t H = f.h[r][j >> 2];
+          lo |= ((H >> ((2 * j) & 7)) & 0x01010101u) << 4;
+          hi |= ((H >> ((2 * j + 1) & 7)) & 0x01010101u) << 4;
+        }
+        if constexpr (T == 14) {
+          const uint32_t H = f.h[r][j >> 1];
+          lo |= ((H >> (4 * (j & 1))) & 0x03030303u) << 4;
+          hi |= ((H >> (4 * (j & 1) + 2)) & 0x03030303u) << 4;
+          lo = ((lo | 0x80808080u) - 0x20202020u) ^ 0x80808080u;  // bytewise q - 32
+          hi = ((hi | 0x80808080u) - 0x20202020u) ^ 0x80808080u;
+        }
+        const long A = (long)(((unsigned long)hi << 32) | lo);
+        if constexpr (T == 14) {
+          // int8 scales of row 4g+i, groups 2j and 2j+1: bytes 16i + 2j, +1 of the row group's 64
+          int s0[4], s1[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t sw = scw[4 * i + (j >> 1)];
+            s0[i] = (int)(int8_t)(sw >> (16 * (j & 1)));
+            s1[i] = (int)(int8_t)(sw >> (16 * (j & 1) + 8));
+          }
+          const long A0 = g < 2 ? A : 0l, A1 = g < 2 ? 0l : A;
+#pragma unroll
+          for (int n = 0; n < NB; ++n) {
+            const u32x4& xc = f.x[n][j >> 1];
+            const long B = (long)(((unsigned long)xc[2 * (j & 1) + 1] << 32) | xc[2 * (j & 1)]);
+            const i32x4 P0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(A0, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+            const i32x4 P1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(A1, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) S[n][i] += __mul24(s0[i], P0[i]) + __mul24(s1[i], P1[i]);  // |P| < 2^17
+          }
+        } else {
+          int sc[4];  // 6-bit scales of row 4g+i, sub-block j: byte 8i + j of the row group's 32
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sc[i] = (int)((scw[2 * i + (j >> 2)] >> (8 * (j & 3))) & 0xFFu);
+#pragma unroll
+          for (int n = 0; n < NB; ++n) {
+            const u32x4& xc = f.x[n][j >> 1];
+            const long B = (long)(((unsigned long)xc[2 * (j & 1) + 1] << 32) | xc[2 * (j & 1)]);
+            const i32x4 P = __builtin_amdgcn_mfma_i32_16x16x32_i8(A, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) S[n][i] += __mul24(sc[i], P[i]);
+          }
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        const float dx = f.dx[n];
+        if constexpr (T == 14) {
+          const f16x4 d4 = __builtin_bit_cast(f16x4, u32x2{f.dm[r][0], f.dm[r][1]});
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[r][n][i] += ((float)d4[i] * dx) * (float)S[n][i];
+        } else {
+          // mins: sum_j m[row][j] * bsum32[j][col] on the f32 MFMA (k = sub-block g, then g + 4)
+          const float m0 = (float)(f.mn[r] & 0xFFu), m1 = (float)((f.mn[r] >> 8) & 0xFFu);
+          f32x4 Mn = __builtin_amdgcn_mfma_f32_16x16x4f32(m0, f.xb[n][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          Mn = __builtin_amdgcn_mfma_f32_16x16x4f32(m1, f.xb[n][1], Mn, 0, 0, 0);
+          const f16x8 dm = __builtin_bit_cast(f16x8, f.dm[r]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            acc[r][n][i] += ((float)dm[2 * i] * dx) * (float)S[n][i];
+            acc[r][n][i] -= ((float)dm[2 * i + 1] * dx) * Mn[i];
+          }
+        }
+      }
+    }
+  };
+
+  Frag ring[U];
+  int sb = kb;
+  const int nfull = (ke - kb) / U;
+  if (nfull > 0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) load(ring[u], sb + u);
+    for (int ch = 1; ch < nfull; ++ch) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        compute(ring[u]);
+        load(ring[u], sb + U + u);
+      }
+      sb += U;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) compute(ring[u]);
+    sb += U;
+  }
+  for (; sb < ke; ++sb) {
+    Frag f;
+    load(f, sb);
+    compute(f);
+  }
+
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) red[w][r][n][lane] = acc[r][n];
+  __syncthreads();
+
+  constexpr int LU = (EPI == EPI_SWIGLU) ? 32 : 64;
+  constexpr int UNITS = RT * NB * LU;
+  for (int u = threadIdx.x; u < UNITS; u += 64 * KS) {
+    const int l = u % LU;
+    const int n = (u / LU) % NB;
+    const int r = (u / LU) / NB;
+    const int col = cb + n * 16 + (l & 15);
+    if (col >= a.M) continue;
+    f32x4 s = red[0][r][n][l];
+#pragma unroll
+    for (int ww = 1; ww < KS; ++ww) s += red[ww][r][n][l];
+    f32x4 up = s;
+    if constexpr (EPI == EPI_SWIGLU) {
+      up = red[0][r][n][l + 32];
+#pragma unroll
+      for (int ww = 1; ww < KS; ++ww) up += red[ww][r][n][l + 32];
+    }
+    epi_store<EPI>(a, tile0 + r, l, col, s, up);
+  }
+}
+
+template <int KS, int RT, int NB, int EPI, int U>
+__global__ __launch_bounds__(64 * KS) void mkq_kernel(MMArgs a) {
+  __shared__ f32x4 red[KS][RT][NB][64];
+  const int tile0 = blockIdx.x * RT;
+  int seg = 0;
+  while (seg < a.kq_n - 1 && tile0 >= a.kq_tile_end[seg]) ++seg;
+  const int t_begin = seg ? a.kq_tile_end[seg - 1] : 0;
+  const uint8_t* W = reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[seg];
+  switch (a.kq_type[seg]) {
+    case 12: mkq_body<12, KS, RT, NB, EPI, U>(a, W, tile0 - t_begin, tile0, red); break;
+    case 13: mkq_body<13, KS, RT, NB, EPI, U>(a, W, tile0 - t_begin, tile0, red); break;
+    case 14: mkq_body<14, KS, RT, NB, EPI, U>(a, W, tile0 - t_begin, tile0, red); break;
+  }
+}
+
+template <int EPI>
+static void launch_mkq_epi(const MMArgs& a, int ntiles, hipStream_t s) {
+  if (a.M <= 16) {
+    mkq_kernel<8, 1, 1, EPI, 2><<<dim3(ntiles, 1), 512, 0, s>>>(a);
+  } else if (a.M <= 32) {
+    mkq_kernel<8, 1, 2, EPI, 2><<<dim3(ntiles, 1), 512, 0, s>>>(a);
+  } else {
+    mkq_kernel<8, 1, 2, EPI, 1><<<dim3(ntiles, (a.M + 31) / 32), 512, 0, s>>>(a);
+  }
+}
+
+int launch_mkq(int epi, const MMArgs& a, hipStream_t s) {
+  if (a.M < 1 || a.K % 256 || a.N % TILE_N || !a.xq || !a.xd || !a.xb) return -1;
+  if (a.kq_n < 1 || a.kq_n > 3 || a.kq_tile_end[a.kq_n - 1] * TILE_N != a.N) return -1;
+  for (int i = 0; i < a.kq_n; ++i)
+    if (!kq_tile_bytes(a.kq_type[i]) || (i && a.kq_tile_end[i] <= a.kq_tile_end[i - 1])) return -1;
+  if (epi == EPI_SWIGLU && !a.actf) return -1;
+  const int ntiles = a.N / TILE_N;
+  switch (epi) {
+    case EPI_F32: launch_mkq_epi<EPI_F32>(a, ntiles, s); return 0;
+    case EPI_RESID: launch_mkq_epi<EPI_RESID>(a, ntiles, s); return 0;
+    case EPI_QKV: launch_mkq_epi<EPI_QKV>(a, ntiles, s); return 0;
+    case EPI_SWIGLU: launch_mkq_epi<EPI_SWIGLU>(a, ntiles, s); return 0;
+  }
+  return -1;
+}
+
+}  // namespace mx

@@ -413,9 +413,9 @@ def synth_q8_0_tensor(arr_bf16: np.ndarray) -> np.ndarray:
     return quantize_q8_0(synth.bf16_bits_to_f32(arr_bf16))
 
 
-# per-tensor types of the mixed test files, after llama.cpp's ftype recipes (Q4_K_M: Q6_K for attn_v,
-# ffn_down and output; Q4_0: Q6_K output) -- the weights of these are random valid blocks, not
-# quantisations of the synthetic model
+# per-tensor types of the mixed test files (Q4_0: Q6_K output) -- the weights of these are random
+# valid blocks, not quantisations of the synthetic model.  "q4_k_m" / "q5_k_m" files follow
+# synth.kq_tensor_type (llama.cpp's per-layer recipe) instead of these entries.
 MIXED = {
     "q4_k_m": {"token_embd": GGML_Q4_K, "output": GGML_Q6_K, "attn_v": GGML_Q6_K, "ffn_down": GGML_Q6_K,
                "*": GGML_Q4_K},
@@ -439,7 +439,8 @@ def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = Non
     """Write a LLaMA GGUF with the synthetic weights of synth.py: every matrix bf16, or (wtype
     "q8_0") the Q8_0 quantisation of those bf16 matrices; norms f32 either way.  wtype "q4_k_m",
     "q5_k_m", "q4_0", "f16": matrices in those per-tensor types (MIXED), with random valid blocks
-    (seeded) for the quantised ones and the synthetic values for f16.  dequant_from: a GGUF of the
+    (seeded) for the quantised ones and the synthetic values for f16 -- except "q4_k_m" / "q5_k_m", whose
+    tensors take llama.cpp's per-layer recipe types with synth.kq_tensor's blocks.  dequant_from: a GGUF of the
     same shape whose matrices are written here dequantised (dequantize(), then bf16 RNE) as BF16.
     rope_freqs: a rope_freqs.weight tensor (head_dim/2 f32, Llama-3.1 style); rope_scaling:
     (type, factor) written as llama.rope.scaling.type / .factor."""
@@ -487,6 +488,16 @@ def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = Non
         elif kind == "bf16" and wtype == "q8_0":
             w.add_tensor_info(name, arr.shape, GGML_Q8_0)
             arrays.append(synth_q8_0_tensor(arr))
+        elif kind == "bf16" and wtype in synth.KQ_FTYPES:
+            # llama.cpp's recipe types per tensor, the synthetic K-quant blocks of synth.kq_tensor
+            # (the same bytes the engine's "synthetic:<shape>:<wtype>" model packs)
+            if name in ("token_embd.weight", "output.weight"):
+                k, layer = name.split(".")[0], 0
+            else:
+                _, layer, k, _ = name.split(".")
+            t, blocks = synth.kq_tensor(wtype, k, int(layer), shape, seed)
+            w.add_tensor_info(name, arr.shape, t)
+            arrays.append(blocks)
         elif kind == "bf16" and wtype in MIXED:
             t = _mixed_type(wtype, name)
             w.add_tensor_info(name, arr.shape, t)

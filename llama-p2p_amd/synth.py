@@ -163,6 +163,95 @@ def synth_tensors(shape: LlamaShape, seed: int):
     yield "output.weight", "bf16", synth_weight_bf16(seed, TID_OUTPUT, V, h)
 
 
+# ---------------------------------------------------------------------------------------------
+# K-quant synthetic models ("synthetic:<shape>:q4_k_m" / ":q5_k_m"): the per-tensor ggml types of
+# llama.cpp's Q4_K_M / Q5_K_M recipes (llama_tensor_get_type, Oct 2024) with synthetic blocks.
+# ---------------------------------------------------------------------------------------------
+GGML_Q4_K, GGML_Q5_K, GGML_Q6_K = 12, 13, 14
+KQ_BLOCK_BYTES = {GGML_Q4_K: 144, GGML_Q5_K: 176, GGML_Q6_K: 210}
+KQ_FTYPES = {"q4_k_m": GGML_Q4_K, "q5_k_m": GGML_Q5_K}
+
+
+def use_more_bits(i_layer: int, n_layers: int) -> bool:
+    """llama.cpp use_more_bits: the first and last eighth of the layers and every third in between."""
+    return i_layer < n_layers // 8 or i_layer >= 7 * n_layers // 8 or (i_layer - n_layers // 8) % 3 == 2
+
+
+def kq_tensor_type(ftype: str, kind: str, layer: int, n_layer: int) -> int:
+    """ggml type of one tensor of a Q4_K_M / Q5_K_M model.  kind: 'token_embd', 'output' or a layer
+    kind ('attn_q', 'attn_k', 'attn_v', 'attn_output', 'ffn_gate', 'ffn_up', 'ffn_down').
+    output -> Q6_K; attn_v and ffn_down -> Q6_K on use_more_bits layers; attn_v of an 80-layer
+    (70B) Q4_K_M model otherwise Q5_K; everything else the ftype's base type."""
+    base = KQ_FTYPES[ftype]
+    if kind == "output":
+        return GGML_Q6_K
+    if kind in ("attn_v", "ffn_down") and use_more_bits(layer, n_layer):
+        return GGML_Q6_K
+    if kind == "attn_v" and n_layer == 80 and base == GGML_Q4_K:
+        return GGML_Q5_K
+    return base
+
+
+def _hash64(seed: int, tid: int, idx: np.ndarray) -> np.ndarray:
+    base = (seed * 0x9E3779B97F4A7C15 + tid * 0xD1B54A32D192ED03) & _M64
+    with np.errstate(over="ignore"):
+        z = idx.astype(np.uint64) + np.uint64(base)
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def kq_blocks(ggml_type: int, nblocks: int, seed: int, tid: int) -> np.ndarray:
+    """Synthetic GGUF blocks of a K-quant tensor, uint8 [nblocks][block bytes].  Byte i of the tensor's
+    block stream is byte i%8 of hash(seed, tid, i//8); then the f16 scales are set without any float
+    conversion: d = 0x0500 + (its first random byte) (7.6e-5 .. 9.5e-5), dmin = 0x1100 (Q4_K) /
+    0x1500 (Q5_K) + the next byte, and Q6_K's int8 scales are folded into [-24, 23] (byte % 48 - 24),
+    so weights come out roughly zero-mean with std ~0.02-0.05.  The engine (csrc/kquant.hip
+    synth_kq_kernel) and the oracle (orc_kq_synth_blocks) compute the same bytes."""
+    bb = KQ_BLOCK_BYTES[ggml_type]
+    n = nblocks * bb
+    z = _hash64(seed, tid, np.arange((n + 7) // 8, dtype=np.uint64))
+    b = z.view(np.uint8)[:n].reshape(nblocks, bb).copy()  # little-endian: byte k of word = bits 8k..
+    if ggml_type == GGML_Q6_K:
+        b[:, 192:208] = ((b[:, 192:208].astype(np.int32) % 48) - 24).astype(np.int8).view(np.uint8)
+        d = 0x0500 + b[:, 208].astype(np.uint16)
+        b[:, 208], b[:, 209] = (d & 0xFF).astype(np.uint8), (d >> 8).astype(np.uint8)
+    else:
+        d = 0x0500 + b[:, 0].astype(np.uint16)
+        m = (0x1500 if ggml_type == GGML_Q5_K else 0x1100) + b[:, 1].astype(np.uint16)
+        b[:, 0], b[:, 1] = (d & 0xFF).astype(np.uint8), (d >> 8).astype(np.uint8)
+        b[:, 2], b[:, 3] = (m & 0xFF).astype(np.uint8), (m >> 8).astype(np.uint8)
+    return b
+
+
+def kq_tensor(ftype: str, kind: str, layer: int, shape: "LlamaShape", seed: int):
+    """(ggml type, uint8 blocks [rows][row bytes]) of one K-quant synthetic matrix (GGUF order)."""
+    h, kv, ff, V = shape.n_embd, shape.n_embd_kv, shape.n_ff, shape.n_vocab
+    rows, cols = {"token_embd": (V, h), "output": (V, h), "attn_q": (h, h), "attn_k": (kv, h),
+                  "attn_v": (kv, h), "attn_output": (h, h), "ffn_gate": (ff, h), "ffn_up": (ff, h),
+                  "ffn_down": (h, ff)}[kind]
+    kidx = {"attn_q": L_Q, "attn_k": L_K, "attn_v": L_V, "attn_output": L_O, "ffn_gate": L_GATE,
+            "ffn_up": L_UP, "ffn_down": L_DOWN}
+    tid = TID_TOK_EMBD if kind == "token_embd" else TID_OUTPUT if kind == "output" else layer_tid(layer, kidx[kind])
+    t = kq_tensor_type(ftype, kind, layer, shape.n_layer)
+    blocks = kq_blocks(t, rows * cols // 256, seed, tid)
+    return t, blocks.reshape(rows, cols // 256 * KQ_BLOCK_BYTES[t])
+
+
+def kq_weight_bytes_per_token(shape: "LlamaShape", ftype: str) -> int:
+    """Bytes a batch-1 decode step streams for a K-quant model: every layer matrix and the output
+    head at their GGUF block sizes, the f32 norms and one token_embd row."""
+    h, kv, ff, V, L = shape.n_embd, shape.n_embd_kv, shape.n_ff, shape.n_vocab, shape.n_layer
+    tot = V * h // 256 * KQ_BLOCK_BYTES[kq_tensor_type(ftype, "output", 0, L)]
+    tot += h // 256 * KQ_BLOCK_BYTES[kq_tensor_type(ftype, "token_embd", 0, L)]
+    for l in range(L):
+        for kind, n in (("attn_q", h * h), ("attn_k", kv * h), ("attn_v", kv * h), ("attn_output", h * h),
+                        ("ffn_gate", ff * h), ("ffn_up", ff * h), ("ffn_down", h * ff)):
+            tot += n // 256 * KQ_BLOCK_BYTES[kq_tensor_type(ftype, kind, l, L)]
+    return tot + (2 * L + 1) * h * 4
+
+
 def parse_synthetic_path(path: str):
     """``synthetic:<shape>[:seed=N]`` -> (LlamaShape, seed) or None."""
     if not isinstance(path, str) or not path.startswith("synthetic:"):

@@ -34,6 +34,14 @@
  *     GET_ROWS of a Q8_0 token_embd dequantises: x = q * f32(d).  Weight blocks come
  *     from the caller (the bytes of the GGUF) or from orc_quantize_q8 (ggml
  *     quantize_row_q8_0_ref: ties away from zero), never from the engine.
+ *   - K-quant weights (Q4_K 12, Q5_K 13, Q6_K 14: llama.cpp's Q4_K_M / Q5_K_M files, SURVEY §8a
+ *     a16): MUL_MAT quantises the activation rows to Q8_K (vec_dot_type of the K-quants,
+ *     ggml quantize_row_q8_K_ref: per 256, iscale = -127/max with max the signed value of
+ *     largest magnitude, q = nearest_int(iscale*x), d = 1/iscale, bsums per 16), then
+ *     ggml_vec_dot_q{4,5,6}_K_q8_K in their generic (scalar) form: exact int32 super-block
+ *     sums, f32 scales.  GET_ROWS of a K-quant token_embd is dequantize_row_q{4,5,6}_K.
+ *     Source: ggml-quants.c / ggml-common.h of llama.cpp (the version llama-cpp-python 0.3.1
+ *     vendors, Oct 2024) -- restated from the published algorithm, not copied.
  * ORC_EXACT mode drops every bf16/f16 activation rounding (fp32 math over the
  * same bf16 weights): that is what tests cross-check against
  * transformers.LlamaForCausalLM (an independent implementation) to pin the
@@ -62,6 +70,8 @@ typedef struct {
     uint16_t *wq, *wk, *wv, *wo, *wg, *wu, *wd; /* bf16 */
     float *attn_norm, *ffn_norm;
     uint8_t *q8[9]; /* Q8_0 blocks by L_* kind (NULL: the bf16 matrix is used) */
+    uint8_t *kq[9]; /* K-quant blocks by L_* kind (NULL: not a K-quant matrix) */
+    int kq_type[9];
 } orc_layer;
 
 typedef struct {
@@ -70,6 +80,8 @@ typedef struct {
     int head_dim, n_embd_kv;
     uint16_t *tok_embd, *output; /* bf16 [V][h] */
     uint8_t *tok_embd_q8, *output_q8; /* Q8_0 blocks or NULL */
+    uint8_t *tok_embd_kq, *output_kq; /* K-quant blocks or NULL */
+    int tok_embd_kq_type, output_kq_type;
     float *out_norm;
     orc_layer *layers;
     float *rope_ff;         /* rope_freqs.weight [head_dim/2] (Llama-3.1 frequency factors) or NULL */
@@ -190,9 +202,9 @@ void orc_free(orc_model *m) {
         orc_layer *L = &m->layers[l];
         free(L->wq); free(L->wk); free(L->wv); free(L->wo); free(L->wg); free(L->wu); free(L->wd);
         free(L->attn_norm); free(L->ffn_norm);
-        for (int k = 0; k < 9; k++) free(L->q8[k]);
+        for (int k = 0; k < 9; k++) { free(L->q8[k]); free(L->kq[k]); }
     }
-    free(m->tok_embd_q8); free(m->output_q8);
+    free(m->tok_embd_q8); free(m->output_q8); free(m->tok_embd_kq); free(m->output_kq);
     free(m->rope_ff);
     free(m->layers); free(m->tok_embd); free(m->output); free(m->out_norm); free(m);
 }
@@ -368,11 +380,17 @@ static float dot_q8_0(const uint8_t *w, const int8_t *q, const float *d, int n) 
 }
 
 /* Sensitivity probe for tests: a relative perturbation of up to q8_jitter (deterministic hash
- * noise) on every activation before it is quantised.  0 = off (the restatement proper).  The
+ * noise) on every activation before it is quantised (Q8_0 and Q8_K).  0 = off (the restatement proper).  The
  * Q8_0 forward is discontinuous in its inputs (x*id crossing a rounding boundary moves q by one
  * step), so the tests bound the engine's deviation by the oracle's own under 1e-6 noise. */
 static float q8_jitter = 0.0f;
 void orc_set_q8_jitter(float eps) { q8_jitter = eps; }
+static void jitter_row(const float *xr, float *xj, int n_in, int t, int n_out) {
+    for (int i = 0; i < n_in; i++) {
+        unsigned hsh = (unsigned)i * 2654435761u + (unsigned)t * 97u + (unsigned)n_out;
+        xj[i] = q8_jitter != 0.0f ? xr[i] * (1.0f + q8_jitter * (float)((int)(hsh % 2001u) - 1000) / 1000.0f) : xr[i];
+    }
+}
 
 static void matmul_q8(float *y, const uint8_t *W, const float *x, int T, int n_in, int n_out) {
     int8_t *xq = (int8_t *)malloc((size_t)T * n_in);
@@ -381,10 +399,7 @@ static void matmul_q8(float *y, const uint8_t *W, const float *x, int T, int n_i
     for (int t = 0; t < T; t++) {
         const float *xr = x + (size_t)t * n_in;
         if (xj) {
-            for (int i = 0; i < n_in; i++) {
-                unsigned hsh = (unsigned)i * 2654435761u + (unsigned)t * 97u + (unsigned)n_out;
-                xj[i] = xr[i] * (1.0f + q8_jitter * (float)((int)(hsh % 2001u) - 1000) / 1000.0f);
-            }
+            jitter_row(xr, xj, n_in, t, n_out);
             xr = xj;
         }
         quantize_act_q8_0(xr, n_in, xq + (size_t)t * n_in, xd + (size_t)t * (n_in / QK8_0));
@@ -398,6 +413,280 @@ static void matmul_q8(float *y, const uint8_t *W, const float *x, int T, int n_i
                                                 xd + (size_t)t * (n_in / QK8_0), n_in);
     free(xq);
     free(xd);
+}
+
+
+/* ------------------------------------------------------------------ K-quants */
+#define QK_K 256
+
+int orc_kq_block_bytes(int type) { return type == 12 ? 144 : type == 13 ? 176 : type == 14 ? 210 : 0; }
+
+/* ggml get_scale_min_k4: the 6-bit (scale, min) pair j of the 12 packed bytes */
+static void scale_min_k4(int j, const uint8_t *q, int *sc, int *mn) {
+    if (j < 4) {
+        *sc = q[j] & 63;
+        *mn = q[j + 4] & 63;
+    } else {
+        *sc = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
+        *mn = (q[j + 4] >> 4) | ((q[j] >> 6) << 4);
+    }
+}
+
+/* The 256 integer values of one super-block, in k order (Q4_K 0..15, Q5_K 0..31, Q6_K -32..31),
+ * and its 16-element scales (Q6_K) or 32-element (scale, min) pairs (Q4_K / Q5_K).
+ * Layouts: ggml-common.h block_q4_K {d, dmin, scales[12], qs[128]}, block_q5_K {d, dmin,
+ * scales[12], qh[32], qs[128]}, block_q6_K {ql[128], qh[64], scales[16], d}. */
+static void kq_values(int type, const uint8_t *b, int *v) {
+    if (type == 12 || type == 13) {
+        const uint8_t *qh = b + 16, *qs = b + (type == 13 ? 48 : 16);
+        for (int g = 0; g < 4; g++)
+            for (int l = 0; l < 32; l++) {
+                int lo = qs[32 * g + l] & 15, hi = qs[32 * g + l] >> 4;
+                if (type == 13) {
+                    lo += (qh[l] >> (2 * g)) & 1 ? 16 : 0;
+                    hi += (qh[l] >> (2 * g + 1)) & 1 ? 16 : 0;
+                }
+                v[64 * g + l] = lo;
+                v[64 * g + 32 + l] = hi;
+            }
+    } else {
+        const uint8_t *ql = b, *qh = b + 128;
+        for (int h = 0; h < 2; h++)
+            for (int l = 0; l < 32; l++) {
+                const int L0 = ql[64 * h + l], L1 = ql[64 * h + 32 + l], H = qh[32 * h + l];
+                v[128 * h + l] = ((L0 & 15) | (((H >> 0) & 3) << 4)) - 32;
+                v[128 * h + 32 + l] = ((L1 & 15) | (((H >> 2) & 3) << 4)) - 32;
+                v[128 * h + 64 + l] = ((L0 >> 4) | (((H >> 4) & 3) << 4)) - 32;
+                v[128 * h + 96 + l] = ((L1 >> 4) | (((H >> 6) & 3) << 4)) - 32;
+            }
+    }
+}
+
+/* ggml dequantize_row_q4_K / q5_K / q6_K: f32, one rounding per operation (C11, no contraction) */
+int orc_kq_dequant(int type, const uint8_t *x, float *y, int64_t k) {
+    const int bb = orc_kq_block_bytes(type);
+    if (!bb || k % QK_K) return -1;
+    int v[QK_K];
+    for (int64_t i = 0; i < k / QK_K; i++) {
+        const uint8_t *b = x + i * bb;
+        float *yb = y + i * QK_K;
+        kq_values(type, b, v);
+        if (type == 14) {
+            uint16_t dh;
+            memcpy(&dh, b + 208, 2);
+            const float d = f16_to_f32(dh);
+            const int8_t *sc = (const int8_t *)(b + 192);
+            for (int j = 0; j < QK_K; j++) yb[j] = d * (float)sc[j / 16] * (float)v[j];
+        } else {
+            uint16_t dh, mh;
+            memcpy(&dh, b, 2);
+            memcpy(&mh, b + 2, 2);
+            const float d = f16_to_f32(dh), dmin = f16_to_f32(mh);
+            for (int j = 0; j < 8; j++) {
+                int sc, mn;
+                scale_min_k4(j, b + 4, &sc, &mn);
+                const float d1 = d * (float)sc, m1 = dmin * (float)mn;
+                for (int l = 0; l < 32; l++) yb[32 * j + l] = d1 * (float)v[32 * j + l] - m1;
+            }
+        }
+    }
+    return 0;
+}
+
+/* ggml block_q8_K */
+typedef struct {
+    float d;
+    int8_t qs[QK_K];
+    int16_t bsums[QK_K / 16];
+} q8k_block;
+
+/* ggml nearest_int: round half to even through the 1.5*2^23 trick */
+static inline int nearest_int(float fval) {
+    float val = fval + 12582912.f;
+    int i;
+    memcpy(&i, &val, sizeof(int));
+    return (i & 0x007fffff) - 0x00400000;
+}
+
+/* ggml quantize_row_q8_K_ref (what x86 quantize_row_q8_K runs) */
+static void quantize_row_q8_K(const float *x, q8k_block *y, int64_t k) {
+    for (int64_t i = 0; i < k / QK_K; i++, x += QK_K) {
+        float max = 0, amax = 0;
+        for (int j = 0; j < QK_K; j++) {
+            const float ax = fabsf(x[j]);
+            if (ax > amax) { amax = ax; max = x[j]; }
+        }
+        if (!amax) {
+            y[i].d = 0;
+            memset(y[i].qs, 0, QK_K);
+            memset(y[i].bsums, 0, sizeof(y[i].bsums));
+            continue;
+        }
+        const float iscale = -127.f / max;
+        for (int j = 0; j < QK_K; j++) {
+            const int v = nearest_int(iscale * x[j]);
+            y[i].qs[j] = (int8_t)(v < 127 ? v : 127);
+        }
+        for (int j = 0; j < QK_K / 16; j++) {
+            int sum = 0;
+            for (int ii = 0; ii < 16; ii++) sum += y[i].qs[j * 16 + ii];
+            y[i].bsums[j] = (int16_t)sum;
+        }
+        y[i].d = 1 / iscale;
+    }
+}
+
+/* ggml_vec_dot_q4_K_q8_K / q5_K / q6_K, generic form: per super-block 8 int32 lane sums of
+ * scale * (w . x) (and, for Q4_K / Q5_K, sum(bsums * mins)), scaled in f32. */
+static float vec_dot_kq(int type, const uint8_t *vx, const q8k_block *y, int n) {
+    const int bb = orc_kq_block_bytes(type);
+    float sums[8] = {0};
+    float sumf = 0;
+    int v[QK_K];
+    for (int i = 0; i < n / QK_K; i++) {
+        const uint8_t *b = vx + (size_t)i * bb;
+        kq_values(type, b, v);
+        int32_t aux32[8] = {0};
+        const int8_t *q8 = y[i].qs;
+        if (type == 14) {
+            const int8_t *sc = (const int8_t *)(b + 192);
+            for (int j = 0; j < QK_K / 16; j++) {
+                const int scale = sc[j];
+                for (int half = 0; half < 2; half++)
+                    for (int l = 0; l < 8; l++) aux32[l] += scale * (int16_t)(q8[16 * j + 8 * half + l] * v[16 * j + 8 * half + l]);
+            }
+            uint16_t dh;
+            memcpy(&dh, b + 208, 2);
+            const float d = f16_to_f32(dh) * y[i].d;
+            for (int l = 0; l < 8; l++) sums[l] += d * aux32[l];
+        } else {
+            int scales[8], mins[8];
+            for (int j = 0; j < 8; j++) scale_min_k4(j, b + 4, &scales[j], &mins[j]);
+            int sumi = 0;
+            for (int j = 0; j < QK_K / 16; j++) sumi += y[i].bsums[j] * mins[j / 2];
+            for (int j = 0; j < QK_K / 32; j++)
+                for (int quarter = 0; quarter < 4; quarter++)
+                    for (int l = 0; l < 8; l++)
+                        aux32[l] += scales[j] * (int16_t)(q8[32 * j + 8 * quarter + l] * v[32 * j + 8 * quarter + l]);
+            uint16_t dh, mh;
+            memcpy(&dh, b, 2);
+            memcpy(&mh, b + 2, 2);
+            const float d = f16_to_f32(dh) * y[i].d;
+            for (int l = 0; l < 8; l++) sums[l] += d * aux32[l];
+            const float dmin = f16_to_f32(mh) * y[i].d;
+            sumf -= dmin * sumi;
+        }
+    }
+    for (int l = 0; l < 8; l++) sumf += sums[l];
+    return sumf;
+}
+
+static void jitter_row(const float *xr, float *xj, int n_in, int t, int n_out);
+
+static void matmul_kq(float *y, int type, const uint8_t *W, const float *x, int T, int n_in, int n_out) {
+    const int nb = n_in / QK_K;
+    q8k_block *xq = (q8k_block *)malloc(sizeof(q8k_block) * (size_t)T * nb);
+    float *xj = (float *)malloc(sizeof(float) * n_in);
+    for (int t = 0; t < T; t++) {
+        jitter_row(x + (size_t)t * n_in, xj, n_in, t, n_out);  /* the Q8_0 path's sensitivity probe */
+        quantize_row_q8_K(xj, xq + (size_t)t * nb, n_in);
+    }
+    free(xj);
+    const size_t rb = (size_t)nb * orc_kq_block_bytes(type);
+#pragma omp parallel for schedule(static)
+    for (int o = 0; o < n_out; o++)
+        for (int t = 0; t < T; t++) y[(size_t)t * n_out + o] = vec_dot_kq(type, W + (size_t)o * rb, xq + (size_t)t * nb, n_in);
+    free(xq);
+}
+
+/* test hooks: the Q8_K image of one row (qs [k], d [k/256], bsums [k/16]) and one dot product */
+int orc_kq_quantize_q8k(const float *x, int64_t k, int8_t *qs, float *d, int16_t *bsums) {
+    if (k % QK_K) return -1;
+    q8k_block *y = (q8k_block *)malloc(sizeof(q8k_block) * (size_t)(k / QK_K));
+    quantize_row_q8_K(x, y, k);
+    for (int64_t i = 0; i < k / QK_K; i++) {
+        memcpy(qs + i * QK_K, y[i].qs, QK_K);
+        d[i] = y[i].d;
+        memcpy(bsums + i * 16, y[i].bsums, 32);
+    }
+    free(y);
+    return 0;
+}
+float orc_kq_vec_dot(int type, const uint8_t *w, const float *x, int n) {
+    q8k_block *y = (q8k_block *)malloc(sizeof(q8k_block) * (size_t)(n / QK_K));
+    quantize_row_q8_K(x, y, n);
+    const float r = vec_dot_kq(type, w, y, n);
+    free(y);
+    return r;
+}
+
+/* Synthetic K-quant blocks (llama-p2p_amd/synth.py kq_blocks is the spec; the engine's
+ * synth_kq_kernel is bit-identical): every byte from the synthetic hash, then the f16 scale
+ * fields set to fixed-exponent bit patterns with a random mantissa byte (no float conversion),
+ * and Q6_K's int8 scales folded into [-24, 23]. */
+static uint64_t synth_hash(uint64_t seed, uint64_t tid, uint64_t idx) {
+    uint64_t z = seed * 0x9E3779B97F4A7C15ull + tid * 0xD1B54A32D192ED03ull + idx;
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+int orc_kq_synth_blocks(int type, int64_t nblocks, uint64_t seed, uint64_t tid, uint8_t *out) {
+    const int bb = orc_kq_block_bytes(type);
+    if (!bb) return -1;
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < nblocks; b++) {
+        uint8_t *p = out + b * bb;
+        for (int i = 0; i < bb; i++) {
+            const uint64_t gi = (uint64_t)b * bb + i;
+            p[i] = (uint8_t)(synth_hash(seed, tid, gi >> 3) >> (8 * (gi & 7)));
+        }
+        if (type == 14) {
+            for (int j = 0; j < 16; j++) p[192 + j] = (uint8_t)(int8_t)((int)(p[192 + j] % 48) - 24);
+            const uint16_t d = (uint16_t)(0x0500 + p[208]);
+            p[208] = (uint8_t)d; p[209] = (uint8_t)(d >> 8);
+        } else {
+            const uint16_t d = (uint16_t)(0x0500 + p[0]), mn = (uint16_t)((type == 13 ? 0x1500 : 0x1100) + p[1]);
+            p[0] = (uint8_t)d; p[1] = (uint8_t)(d >> 8);
+            p[2] = (uint8_t)mn; p[3] = (uint8_t)(mn >> 8);
+        }
+    }
+    return 0;
+}
+
+/* Make one matrix a K-quant from caller bytes (GGUF blocks, rows x cols/256 blocks). */
+int orc_set_tensor_kq(orc_model *m, int layer, int kind, int type, const void *blocks) {
+    size_t h = m->hp.n_embd, kv = m->n_embd_kv, ff = m->hp.n_ff, V = m->hp.n_vocab;
+    size_t rows = 0, cols = 0;
+    uint8_t **slot = NULL;
+    int *tslot = NULL;
+    const int bb = orc_kq_block_bytes(type);
+    if (!bb) return -1;
+    if (layer < 0) {
+        if (kind == K_TOK_EMBD) { rows = V; cols = h; slot = &m->tok_embd_kq; tslot = &m->tok_embd_kq_type; }
+        else if (kind == K_OUTPUT) { rows = V; cols = h; slot = &m->output_kq; tslot = &m->output_kq_type; }
+        else return -1;
+    } else {
+        if (layer >= m->hp.n_layer) return -1;
+        orc_layer *L = &m->layers[layer];
+        switch (kind) {
+        case L_Q: rows = h; cols = h; break;
+        case L_K: case L_V: rows = kv; cols = h; break;
+        case L_O: rows = h; cols = h; break;
+        case L_GATE: case L_UP: rows = ff; cols = h; break;
+        case L_DOWN: rows = h; cols = ff; break;
+        default: return -1;
+        }
+        slot = &L->kq[kind];
+        tslot = &L->kq_type[kind];
+    }
+    if (cols % QK_K) return -1;
+    const size_t nbytes = rows * (cols / QK_K) * bb;
+    free(*slot);
+    *slot = (uint8_t *)malloc(nbytes);
+    memcpy(*slot, blocks, nbytes);
+    *tslot = type;
+    return 0;
 }
 
 /* ------------------------------------------------------------------ context */
@@ -484,9 +773,10 @@ static void matmul_bf16(float *y, const uint16_t *W, const float *x, int T, int 
     }
 }
 
-static void matmul(float *y, const uint16_t *W, const uint8_t *Wq8, const float *x, int T, int n_in, int n_out,
-                   int exact, uint16_t *scratch) {
-    if (Wq8) matmul_q8(y, Wq8, x, T, n_in, n_out);
+static void matmul(float *y, const uint16_t *W, const uint8_t *Wq8, const uint8_t *Wkq, int kq_type, const float *x,
+                   int T, int n_in, int n_out, int exact, uint16_t *scratch) {
+    if (Wkq) matmul_kq(y, kq_type, Wkq, x, T, n_in, n_out);
+    else if (Wq8) matmul_q8(y, Wq8, x, T, n_in, n_out);
     else matmul_bf16(y, W, x, T, n_in, n_out, exact, scratch);
 }
 
@@ -531,7 +821,10 @@ int orc_eval(orc_ctx *c, const int32_t *ids, int n, int pos0, float *logits, int
     const float kq_scale = 1.0f / sqrtf((float)d);
 
     for (int t = 0; t < T; t++) {
-        if (m->tok_embd_q8) { /* GET_ROWS of Q8_0: dequantize_row_q8_0 */
+        if (m->tok_embd_kq) { /* GET_ROWS of a K-quant: dequantize_row_q{4,5,6}_K */
+            const size_t rb = (size_t)(h / QK_K) * orc_kq_block_bytes(m->tok_embd_kq_type);
+            orc_kq_dequant(m->tok_embd_kq_type, m->tok_embd_kq + (size_t)ids[t] * rb, x + (size_t)t * h, h);
+        } else if (m->tok_embd_q8) { /* GET_ROWS of Q8_0: dequantize_row_q8_0 */
             const uint8_t *rw = m->tok_embd_q8 + (size_t)ids[t] * (h / QK8_0) * Q8_0_BLOCK;
             for (int i = 0; i < h; i++) {
                 uint16_t dh;
@@ -546,9 +839,9 @@ int orc_eval(orc_ctx *c, const int32_t *ids, int n, int pos0, float *logits, int
     for (int l = 0; l < hp->n_layer; l++) {
         orc_layer *L = &m->layers[l];
         for (int t = 0; t < T; t++) rmsnorm(cur + (size_t)t * h, x + (size_t)t * h, L->attn_norm, h, hp->eps);
-        matmul(q, L->wq, L->q8[L_Q], cur, T, h, h, exact, scratch);
-        matmul(k, L->wk, L->q8[L_K], cur, T, h, kvd, exact, scratch);
-        matmul(v, L->wv, L->q8[L_V], cur, T, h, kvd, exact, scratch);
+        matmul(q, L->wq, L->q8[L_Q], L->kq[L_Q], L->kq_type[L_Q], cur, T, h, h, exact, scratch);
+        matmul(k, L->wk, L->q8[L_K], L->kq[L_K], L->kq_type[L_K], cur, T, h, kvd, exact, scratch);
+        matmul(v, L->wv, L->q8[L_V], L->kq[L_V], L->kq_type[L_V], cur, T, h, kvd, exact, scratch);
         for (int t = 0; t < T; t++) {
             const float *cs = c->rope_cs + (size_t)(pos0 + t) * (d / 2) * 2;
             rope_rows(q + (size_t)t * h, nh, d, cs);
@@ -618,23 +911,23 @@ int orc_eval(orc_ctx *c, const int32_t *ids, int n, int pos0, float *logits, int
                 free(s);
             }
         }
-        matmul(tmp, L->wo, L->q8[L_O], att, T, h, h, exact, scratch);
+        matmul(tmp, L->wo, L->q8[L_O], L->kq[L_O], L->kq_type[L_O], att, T, h, h, exact, scratch);
         for (size_t i = 0; i < (size_t)T * h; i++) x[i] += tmp[i];
         /* ffn */
         for (int t = 0; t < T; t++) rmsnorm(cur + (size_t)t * h, x + (size_t)t * h, L->ffn_norm, h, hp->eps);
-        matmul(u, L->wu, L->q8[L_UP], cur, T, h, ff, exact, scratch);
-        matmul(g, L->wg, L->q8[L_GATE], cur, T, h, ff, exact, scratch);
+        matmul(u, L->wu, L->q8[L_UP], L->kq[L_UP], L->kq_type[L_UP], cur, T, h, ff, exact, scratch);
+        matmul(g, L->wg, L->q8[L_GATE], L->kq[L_GATE], L->kq_type[L_GATE], cur, T, h, ff, exact, scratch);
         for (size_t i = 0; i < (size_t)T * ff; i++) {
             float gg = g[i];
             g[i] = (gg / (1.0f + expf(-gg))) * u[i];
         }
-        matmul(tmp, L->wd, L->q8[L_DOWN], g, T, ff, h, exact, scratch);
+        matmul(tmp, L->wd, L->q8[L_DOWN], L->kq[L_DOWN], L->kq_type[L_DOWN], g, T, ff, h, exact, scratch);
         for (size_t i = 0; i < (size_t)T * h; i++) x[i] += tmp[i];
     }
     int t0 = all_logits ? 0 : T - 1;
     int nt = T - t0;
     for (int t = 0; t < nt; t++) rmsnorm(cur + (size_t)t * h, x + (size_t)(t0 + t) * h, m->out_norm, h, hp->eps);
-    matmul(logits, m->output, m->output_q8, cur, nt, h, V, exact, scratch);
+    matmul(logits, m->output, m->output_q8, m->output_kq, m->output_kq_type, cur, nt, h, V, exact, scratch);
 
     free(x); free(cur); free(q); free(k); free(v); free(att); free(g); free(u); free(tmp); free(scratch);
     return 0;

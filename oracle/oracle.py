@@ -53,6 +53,18 @@ def lib():
         L.orc_quantize_q8.argtypes = [vp]
         L.orc_quantize_q8.restype = i32
         L.orc_set_q8_jitter.argtypes = [ctypes.c_float]
+        L.orc_set_tensor_kq.argtypes = [vp, i32, i32, i32, vp]
+        L.orc_set_tensor_kq.restype = i32
+        L.orc_kq_synth_blocks.argtypes = [i32, ctypes.c_int64, u64, u64, vp]
+        L.orc_kq_synth_blocks.restype = i32
+        L.orc_kq_dequant.argtypes = [i32, vp, vp, ctypes.c_int64]
+        L.orc_kq_dequant.restype = i32
+        L.orc_kq_quantize_q8k.argtypes = [vp, ctypes.c_int64, vp, vp, vp]
+        L.orc_kq_quantize_q8k.restype = i32
+        L.orc_kq_vec_dot.argtypes = [i32, vp, vp, i32]
+        L.orc_kq_vec_dot.restype = ctypes.c_float
+        L.orc_kq_block_bytes.argtypes = [i32]
+        L.orc_kq_block_bytes.restype = i32
         L.orc_set_rope.argtypes = [vp, vp, ctypes.c_float]
         L.orc_ctx_create.restype = vp
         L.orc_ctx_create.argtypes = [vp, i32]
@@ -95,6 +107,31 @@ class OracleModel:
         blocks = np.ascontiguousarray(blocks, dtype=np.uint8)
         if lib().orc_set_tensor_q8(self._m, layer, kind, blocks.ctypes.data):
             raise ValueError(f"orc_set_tensor_q8({layer},{kind}) failed")
+
+    def set_tensor_kq(self, layer: int, kind: int, ggml_type: int, blocks: np.ndarray):
+        """Make one matrix a K-quant (Q4_K 12, Q5_K 13, Q6_K 14) from GGUF block bytes."""
+        blocks = np.ascontiguousarray(blocks, dtype=np.uint8)
+        if lib().orc_set_tensor_kq(self._m, layer, kind, ggml_type, blocks.ctypes.data):
+            raise ValueError(f"orc_set_tensor_kq({layer},{kind},{ggml_type}) failed")
+
+    def kq_synthetic(self, ftype: str, seed: int):
+        """Every matrix -> the K-quant synthetic blocks of ``synthetic:<shape>:<ftype>`` (synth.kq_tensor
+        types; blocks from the oracle's own generator, orc_kq_synth_blocks)."""
+        import sys
+        sys.path.insert(0, os.path.dirname(HERE))
+        from llama_p2p_amd import synth
+
+        sh = self.shape
+        h, kv, ff, V = sh.n_embd, sh.n_embd_kv, sh.n_ff, sh.n_vocab
+        mats = [(-1, 1, "token_embd", V * h, synth.TID_TOK_EMBD), (-1, 3, "output", V * h, synth.TID_OUTPUT)]
+        for l in range(sh.n_layer):
+            for kind, k, n in (("attn_q", synth.L_Q, h * h), ("attn_k", synth.L_K, kv * h), ("attn_v", synth.L_V, kv * h),
+                               ("attn_output", synth.L_O, h * h), ("ffn_gate", synth.L_GATE, ff * h),
+                               ("ffn_up", synth.L_UP, ff * h), ("ffn_down", synth.L_DOWN, h * ff)):
+                mats.append((l, k, kind, n, synth.layer_tid(l, k)))
+        for layer, k, kind, n, tid in mats:
+            t = synth.kq_tensor_type(ftype, kind, layer, sh.n_layer)
+            self.set_tensor_kq(layer, k, t, kq_synth_blocks(t, n // 256, seed, tid))
 
     def set_rope(self, freq_factors=None, freq_scale: float = 1.0):
         """Llama-3.1 RoPE frequency factors (head_dim/2 floats) and linear scaling (1/factor)."""
@@ -160,6 +197,40 @@ class OracleContext:
 def q8_jitter(eps: float):
     """Relative activation noise before every Q8_0 quantisation (sensitivity probe; 0 = off)."""
     lib().orc_set_q8_jitter(eps)
+
+
+def kq_synth_blocks(ggml_type: int, nblocks: int, seed: int, tid: int) -> np.ndarray:
+    """The oracle's synthetic K-quant blocks (uint8 [nblocks][block bytes])."""
+    bb = lib().orc_kq_block_bytes(ggml_type)
+    out = np.empty((nblocks, bb), np.uint8)
+    if lib().orc_kq_synth_blocks(ggml_type, nblocks, seed, tid, out.ctypes.data):
+        raise ValueError("orc_kq_synth_blocks failed")
+    return out
+
+
+def kq_dequant(ggml_type: int, blocks: np.ndarray, n: int) -> np.ndarray:
+    blocks = np.ascontiguousarray(blocks, dtype=np.uint8)
+    out = np.empty(n, np.float32)
+    if lib().orc_kq_dequant(ggml_type, blocks.ctypes.data, out.ctypes.data, n):
+        raise ValueError("orc_kq_dequant failed")
+    return out
+
+
+def kq_quantize_q8k(x: np.ndarray):
+    """Q8_K image of one activation row: (qs int8 [n], d f32 [n/256], bsums int16 [n/16])."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    n = x.size
+    qs, d, bs = np.empty(n, np.int8), np.empty(n // 256, np.float32), np.empty(n // 16, np.int16)
+    if lib().orc_kq_quantize_q8k(x.ctypes.data, n, qs.ctypes.data, d.ctypes.data, bs.ctypes.data):
+        raise ValueError("orc_kq_quantize_q8k failed")
+    return qs, d, bs
+
+
+def kq_vec_dot(ggml_type: int, blocks: np.ndarray, x: np.ndarray) -> float:
+    """ggml_vec_dot_q{4,5,6}_K_q8_K of one weight row with the Q8_K image of x."""
+    blocks = np.ascontiguousarray(blocks, dtype=np.uint8)
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    return float(lib().orc_kq_vec_dot(ggml_type, blocks.ctypes.data, x.ctypes.data, x.size))
 
 
 def argmax_lowest(logits: np.ndarray) -> int:

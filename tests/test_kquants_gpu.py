@@ -1,8 +1,15 @@
-"""K-quant / Q4_0 / F16 GGUF files on the GPU: the engine dequantises every
-matrix at load (dequant_bf16_kernel) and runs the bf16 path.  Checks: (1) a Q4_K_M / Q5_K_M / Q4_0 /
-F16 file gives bit-identical logits to a BF16 file holding numpy's dequantisation of the same blocks
-(gguf.dequantize, pinned to ggml's loops by tests/test_kquants.py) -- so the device decoder equals
-the host one bit for bit; (2) those logits follow the CPU oracle built from the same bf16 weights."""
+"""Quantised GGUF files on the GPU.
+
+Native K-quants (Q4_K_M / Q5_K_M: Q4_K, Q5_K, Q6_K matrices; csrc/kquant.hip): int8 MFMA over packed
+K-quant tiles with Q8_K activations, against the CPU oracle's restatement of ggml's
+quantize_row_q8_K + ggml_vec_dot_q{4,5,6}_K_q8_K (pinned to scalar transcriptions of ggml's loops in
+tests/test_kquants.py) for every row regime, the device greedy loop, the GGUF loader against on-device
+synthesis, and Llama-3-8B Q4_K_M at full size.  Tolerance as tests/test_q8_gpu.py: the bf16 one, and
+2x the oracle's own deviation under 1e-6 relative input noise (Q8_K rounding is discontinuous).
+
+Other block types (Q4_0, F16 files): the engine dequantises every matrix at load
+(dequant_bf16_kernel) and runs the bf16 path -- bit-identical to a BF16 file holding numpy's
+dequantisation of the same blocks, and close to the CPU oracle built from those bf16 weights."""
 import numpy as np
 import pytest
 
@@ -33,7 +40,7 @@ def _oracle_from_gguf(oracle_mod, path, shape):
     return om
 
 
-@pytest.mark.parametrize("wtype", ["q4_k_m", "q5_k_m", "q4_0", "f16"])
+@pytest.mark.parametrize("wtype", ["q4_0", "f16"])
 def test_dequantised_file_equals_bf16_file_and_oracle(oracle_mod, tmp_path, wtype):
     from llama_p2p_amd import engine, gguf, synth
 
@@ -54,3 +61,148 @@ def test_dequantised_file_equals_bf16_file_and_oracle(oracle_mod, tmp_path, wtyp
     assert_tokens_match(la, ref, wtype)
     a.close()
     b.close()
+
+
+# ------------------------------------------------------------------------------------ native K-quants
+@pytest.fixture(scope="module")
+def mx():
+    from llama_p2p_amd import engine
+
+    engine.lib()
+    return engine
+
+
+def _seq(shape, n, seed=7):
+    rng = np.random.default_rng(seed)
+    return np.concatenate([[1], rng.integers(3, shape.n_vocab, n - 1)]).astype(np.int32)
+
+
+def _oracle_kq(oracle_mod, shape, seed, ftype):
+    om = oracle_mod.OracleModel(shape, seed=seed)
+    om.kq_synthetic(ftype, seed)
+    return om
+
+
+@pytest.mark.parametrize("ftype", ["q4_k_m", "q5_k_m"])
+def test_kq_gguf_equals_synthetic(mx, tmp_path, ftype):
+    """A Q4_K_M / Q5_K_M GGUF (synth.kq_tensor blocks, C++ parser, pack_kq_kernel) and the on-device
+    synthesis of the same model give bit-identical logits; the info reports the K-quant type."""
+    from llama_p2p_amd import gguf, synth
+
+    shape = synth.SHAPES["test-tiny"]
+    path = str(tmp_path / f"tiny_{ftype}.gguf")
+    gguf.write_synthetic_gguf(path, shape, seed=3, wtype=ftype)
+    ids = _seq(shape, 24)
+    a = mx.Engine(path, n_ctx=64, n_seq_max=2)
+    b = mx.Engine(f"synthetic:test-tiny:seed=3:{ftype}", n_ctx=64, n_seq_max=2)
+    t = synth.KQ_FTYPES[ftype]
+    assert a.info.weight_type == t and b.info.weight_type == t
+    la, lb = a.forward_logits(ids), b.forward_logits(ids)
+    assert np.array_equal(la, lb)
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("name,ftype", [("test-tiny", "q4_k_m"), ("test-d128", "q4_k_m"), ("test-d128", "q5_k_m"),
+                                        ("test-h4096", "q4_k_m")])
+def test_kq_prefill_and_decode_vs_oracle(mx, oracle_mod, name, ftype):
+    """100-row prefill (64-row logits chunks: the 33-64-row and 17-32-row kernels), then 12 single-row
+    decode steps, teacher-forced, against the oracle's K-quant forward."""
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES[name]
+    ids = _seq(shape, 112, seed=5)
+    eng = mx.Engine(f"synthetic:{name}:seed=0:{ftype}", n_ctx=256, n_seq_max=2)
+    octx = _oracle_kq(oracle_mod, shape, 0, ftype).context(256)
+    got = eng.forward_logits(ids[:100], 0, slot=1)
+    ref = octx.eval(ids[:100], 0, all_logits=True)
+    assert_logits_close(got, ref, f"{name} {ftype} prefill")
+    assert_tokens_match(got, ref, f"{name} {ftype} prefill")
+    err = np.abs(got - ref).max()
+    oracle_mod.q8_jitter(1e-6)
+    try:
+        jit = _oracle_kq(oracle_mod, shape, 0, ftype).context(256).eval(ids[:100], 0, all_logits=True)
+    finally:
+        oracle_mod.q8_jitter(0.0)
+    self_dev = np.abs(jit - ref).max()
+    print(f"{name} {ftype}: prefill max|d| {err:.4g}, oracle self-deviation {self_dev:.4g}, max|ref| "
+          f"{np.abs(ref).max():.4g}")
+    assert err <= 2 * self_dev + 1e-4 * np.abs(ref).max(), (err, self_dev)
+    gs, rs = [], []
+    for p in range(100, 112):
+        gs.append(eng.forward_logits(ids[p:p + 1], p, slot=1))
+        rs.append(octx.eval(ids[p:p + 1], p))
+    g, r = np.concatenate(gs), np.concatenate(rs)
+    assert_logits_close(g, r, f"{name} {ftype} decode")
+    assert_tokens_match(g, r, f"{name} {ftype} decode")
+    eng.close()
+
+
+def test_kq_wide_rows_and_greedy_loop_vs_oracle(mx, oracle_mod):
+    """24 sequences decoded together (the 17-32-row kernel) through the device greedy loop, every
+    picked token checked along the oracle's teacher-forced chain."""
+    from llama_p2p_amd import synth
+
+    from conftest import check_chain_batched
+
+    shape = synth.SHAPES["test-d128"]
+    M, G = 24, 6
+    rng = np.random.default_rng(12)
+    prompts = [np.concatenate([[1], rng.integers(3, shape.n_vocab, int(rng.integers(3, 12)))]).astype(np.int32)
+               for _ in range(M)]
+    eng = mx.Engine("synthetic:test-d128:seed=0:q4_k_m", n_ctx=64, n_seq_max=M)
+    slots, pos, ids = [], [], []
+    for i, p in enumerate(prompts):
+        slots += [i] * (len(p) - 1)
+        pos += list(range(len(p) - 1))
+        ids += [int(t) for t in p[:-1]]
+    eng.forward_rows(slots, pos, ids, want_logits=False)
+    b = eng.batch(slots=list(range(M)), pos=[len(p) - 1 for p in prompts], ids=[int(p[-1]) for p in prompts],
+                  max_steps=G)
+    for _ in range(G):
+        b.step()
+    toks = b.tokens()
+    b.close()
+    om = _oracle_kq(oracle_mod, shape, 0, "q4_k_m")
+    exact = 0
+    for i, p in enumerate(prompts):
+        e, _ = check_chain_batched(om.context(64), p, toks[i].tolist(), f"seq {i}")
+        exact += e
+    assert exact >= 0.9 * M * G
+    eng.close()
+
+
+def test_kq_llama3_8b_q4_k_m_full_size(mx):
+    """Llama-3-8B Q4_K_M at full size: the bytes a decode step streams match the recipe's GGUF
+    bytes (synth.kq_weight_bytes_per_token, +<3% for byte-aligned K-quant scales), 1-row logits
+    equal the same sequence's row inside a 32-row step (within twice the bf16 tolerance: the two
+    column-tile kernels differ only in f32 summation order), and the greedy loop runs."""
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES["llama3-8b"]
+    eng = mx.Engine("synthetic:llama3-8b:seed=0:q4_k_m", n_ctx=64, n_seq_max=32)
+    want = synth.kq_weight_bytes_per_token(shape, "q4_k_m")
+    assert want <= eng.info.weight_bytes <= 1.03 * want, (eng.info.weight_bytes, want)
+    rng = np.random.default_rng(2)
+    seqs = [np.concatenate([[128000], rng.integers(3, shape.n_vocab, 8)]).astype(np.int32) for _ in range(32)]
+    slots, pos, ids = [], [], []
+    for i, sq in enumerate(seqs):
+        slots += [i] * 8
+        pos += list(range(8))
+        ids += [int(t) for t in sq[:8]]
+    eng.forward_rows(slots, pos, ids, want_logits=False)
+    wide = eng.forward_rows(list(range(32)), [8] * 32, [int(sq[8]) for sq in seqs])
+    for i in (0, 17, 31):
+        one = eng.forward_rows([i], [8], [int(seqs[i][8])])
+        ref = wide[i]
+        d = np.abs(one[0] - ref)
+        tol2 = 2 * (1e-2 * np.abs(ref) + 2e-2 * np.abs(ref).max())
+        print(f"8b q4_k_m row {i}: max|d| {d.max():.4f} (max|logit| {np.abs(ref).max():.3f})")
+        assert (d <= tol2).all()
+    b = eng.batch(slots=list(range(32)), pos=[9] * 32, ids=[int(np.argmax(w)) for w in wide], max_steps=4)
+    for _ in range(4):
+        b.step()
+    toks = b.tokens()
+    assert toks.shape == (32, 4) and (toks >= 0).all() and (toks < shape.n_vocab).all()
+    b.close()
+    eng.close()

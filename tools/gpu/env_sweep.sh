@@ -7,7 +7,7 @@ TAG=$1; MATCH=$2; shift 2
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-ARGS="--steps 32 --warmup 4 --no-cpu-baseline --prefill-prompts 0 --q8-steps 0 --tiny-tokens 64 --big-steps 0"
+ARGS="--steps 32 --warmup 4 --no-cpu-baseline --prefill-prompts 0 --q8-steps 0 --kq-steps 0 --tiny-tokens 64 --big-steps 0"
 i=0
 for E in "$@"; do
   i=$((i+1))
