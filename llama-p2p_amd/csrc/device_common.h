@@ -148,4 +148,26 @@ __device__ __forceinline__ void scale_min_k4(int j, const uint8_t* q, int& sc, i
   }
 }
 
+// Reductions over the 16 lanes of a DPP row (the 16 positions of one C-layout row): rotations
+// within the row, so every lane ends with the result.  One VOP2-DPP instruction per step (the
+// builtin route adds a move and an fmax canonicalisation per step, and __shfl_xor is a chain of
+// ds_bpermute round trips); "s_nop 1" covers the VALU-write -> DPP-read hazard of the previous step.
+#define MX_ROW_STEP(op, v, n)                                                                        \
+  asm volatile("s_nop 1\n\t" op "_dpp %0, %1, %1 row_ror:" #n " row_mask:0xf bank_mask:0xf" : "=v"(v) \
+               : "v"(v))
+__device__ __forceinline__ float row16_max(float v) {
+  MX_ROW_STEP("v_max_f32", v, 8);
+  MX_ROW_STEP("v_max_f32", v, 4);
+  MX_ROW_STEP("v_max_f32", v, 2);
+  MX_ROW_STEP("v_max_f32", v, 1);
+  return v;
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  MX_ROW_STEP("v_add_f32", v, 8);
+  MX_ROW_STEP("v_add_f32", v, 4);
+  MX_ROW_STEP("v_add_f32", v, 2);
+  MX_ROW_STEP("v_add_f32", v, 1);
+  return v;
+}
+#undef MX_ROW_STEP
 }  // namespace mx

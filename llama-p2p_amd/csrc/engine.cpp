@@ -1076,7 +1076,6 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     b.W = L.o; b.N = h; b.K = h; b.M = M; b.out = x; b.ldo = h;
     site = 2;
     operand(b, attn_f, h, nullptr, M, nullptr);
-    b.ssq = ql ? ssq : nullptr; b.np = h / 16;  // partials of the new residual for gate/up's norm
     if (launch_mq8(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "q8 attn_output launch shape");
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.actf = act_f; c.lda = ff;
@@ -1087,7 +1086,6 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     d.W = L.down; d.N = h; d.K = ff; d.M = M; d.out = x; d.ldo = h;
     site = 8;
     operand(d, act_f, ff, nullptr, M, nullptr);
-    d.ssq = ql ? ssq : nullptr; d.np = h / 16;  // for the next layer's qkv (or lm_head) norm
     if (launch_mq8(EPI_RESID, d, s)) return fail(MX_ERR_ARG, "q8 ffn_down launch shape");
   }
   if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
@@ -1114,12 +1112,13 @@ int mx_engine::enqueue_forward_kq(int M, const int* pos, const int* slot, void* 
                                   int* hist_count, int max_hist, hipStream_t s) {
   const int h = n_embd, kv = n_embd_kv, ff = n_ff;
   if (head && n_out > MAX_ROWS) return fail(MX_ERR_ARG, "logits for at most 64 rows per forward");
+  // (a v_dot4 kernel quantising on load for <= 4 rows measured slower: 3.09 vs 2.80 ms per 8B token)
   auto operand = [&](MMArgs& m, const KqMat& km, const float* src, int K, const float* norm_w, int rows,
                      const int* rmap) -> int {
+    km.set(m);
     const int rc = norm_w ? launch_rmsnorm_q8k(xq8, xqd, xkb, src, norm_w, rmap, rows, K, eps, s)
                           : launch_quantize_q8k(xq8, xqd, xkb, src, K, rows, K, s);
     m.xq = xq8; m.xd = xqd; m.xb = xkb;
-    km.set(m);
     return rc;
   };
   for (int li = 0; li < (int)layers.size(); li++) {
@@ -1142,16 +1141,16 @@ int mx_engine::enqueue_forward_kq(int M, const int* pos, const int* slot, void* 
     else launch_attention(at, s);
     MMArgs b{};
     b.W = L.o; b.N = h; b.K = h; b.M = M; b.out = x; b.ldo = h;
-    if (operand(b, L.kq_o, attn_f, h, nullptr, M, nullptr) || launch_mkq(EPI_RESID, b, s))
-      return fail(MX_ERR_ARG, "kq attn_output launch shape");
+    if (operand(b, L.kq_o, attn_f, h, nullptr, M, nullptr)) return fail(MX_ERR_ARG, "kq quantise shape");
+    if (launch_mkq(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "kq attn_output launch shape");
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.actf = act_f; c.lda = ff;
     if (operand(c, L.kq_gu, x, h, L.ffn_norm, M, nullptr) || launch_mkq(EPI_SWIGLU, c, s))
       return fail(MX_ERR_ARG, "kq gate/up launch shape");
     MMArgs d{};
     d.W = L.down; d.N = h; d.K = ff; d.M = M; d.out = x; d.ldo = h;
-    if (operand(d, L.kq_down, act_f, ff, nullptr, M, nullptr) || launch_mkq(EPI_RESID, d, s))
-      return fail(MX_ERR_ARG, "kq ffn_down launch shape");
+    if (operand(d, L.kq_down, act_f, ff, nullptr, M, nullptr)) return fail(MX_ERR_ARG, "kq quantise shape");
+    if (launch_mkq(EPI_RESID, d, s)) return fail(MX_ERR_ARG, "kq ffn_down launch shape");
   }
   if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
   if (head) {

@@ -184,7 +184,7 @@ int launch_embed_kq(float* x, const uint8_t* tok_blocks, int type, const int* id
 int launch_rmsnorm_q8k(int8_t* xq, float* xd, float* xb, const float* x, const float* w, const int* row_map, int M,
                        int n, float eps, hipStream_t s);
 int launch_quantize_q8k(int8_t* xq, float* xd, float* xb, const float* src, int ld, int M, int n, hipStream_t s);
-// K-quant x Q8_K products for any M (grid.y: groups of 64 tokens), the usual epilogues (SWIGLU: actf)
+// K-quant x Q8_K products for any M (grid.y: groups of 32 tokens), the usual epilogues (SWIGLU: actf)
 int launch_mkq(int epi, const MMArgs& a, hipStream_t s);
 
 // top-k (k <= TOPK_MAX) candidates per logits row, value descending, ties by lower id; ws: M*64*k

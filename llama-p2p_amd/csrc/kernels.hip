@@ -985,28 +985,6 @@ bool mm_can_norm_on_load(int M, int K) {
 // [pos][d] (B operand of QK^T = contiguous 16 B per lane) and V transposed
 // [d][pos] (B operand of P.V = contiguous 16 B per lane).
 // ---------------------------------------------------------------------------
-// Reductions over the 16 lanes of a DPP row (the 16 positions of one C-layout row): rotations
-// within the row, so every lane ends with the result.  One VOP2-DPP instruction per step (the
-// builtin route adds a move and an fmax canonicalisation per step, and __shfl_xor is a chain of
-// ds_bpermute round trips); "s_nop 1" covers the VALU-write -> DPP-read hazard of the previous step.
-#define MX_ROW_STEP(op, v, n)                                                                        \
-  asm volatile("s_nop 1\n\t" op "_dpp %0, %1, %1 row_ror:" #n " row_mask:0xf bank_mask:0xf" : "=v"(v) \
-               : "v"(v))
-__device__ __forceinline__ float row16_max(float v) {
-  MX_ROW_STEP("v_max_f32", v, 8);
-  MX_ROW_STEP("v_max_f32", v, 4);
-  MX_ROW_STEP("v_max_f32", v, 2);
-  MX_ROW_STEP("v_max_f32", v, 1);
-  return v;
-}
-__device__ __forceinline__ float row16_sum(float v) {
-  MX_ROW_STEP("v_add_f32", v, 8);
-  MX_ROW_STEP("v_add_f32", v, 4);
-  MX_ROW_STEP("v_add_f32", v, 2);
-  MX_ROW_STEP("v_add_f32", v, 1);
-  return v;
-}
-#undef MX_ROW_STEP
 constexpr float LOG2E = 1.4426950408889634f;
 
 // One (kv head, row) of decode attention, by the NW waves of the calling work-group.  Wave w takes

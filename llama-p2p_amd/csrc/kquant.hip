@@ -33,8 +33,7 @@ namespace mx {
 //   Q6_K  [2048, 3072): lane l's 4 dwords at 2048 + 16l: bits 4-5 of value (j, e) at bits
 //               8*(e&3) + 2*(u&3) of dword u>>2
 //   Q4_K / Q5_K scales at SC = 2048 / 2560:  SC + 8r + j: 6-bit scale of row r, sub-block j;
-//               SC + 128 + 2l: mins (row l&15, sub-blocks l>>4 and 4 + (l>>4));
-//               SC + 256 + 4r: f16 d, f16 dmin of row r
+//               SC + 128 + 8r + j: 6-bit min of row r, sub-block j;  SC + 256 + 4r: f16 d, f16 dmin
 //   Q6_K scales at SC = 3072:  SC + 16r + g: int8 scale of row r, 16-value group g;
 //               SC + 256 + 2r: f16 d of row r
 // ---------------------------------------------------------------------------
@@ -123,10 +122,7 @@ __global__ void pack_kq_kernel(uint8_t* dst, const uint8_t* src, int N, int K, i
         }
         tile[SC + 8 * r + j] = sc[j];
       }
-      for (int g = 0; g < 4; ++g) {
-        tile[SC + 128 + 2 * (r + 16 * g)] = mn[g];
-        tile[SC + 128 + 2 * (r + 16 * g) + 1] = mn[g + 4];
-      }
+      for (int j = 0; j < 8; ++j) tile[SC + 128 + 8 * r + j] = mn[j];
       for (int c = 0; c < 4; ++c) tile[SC + 256 + 4 * r + c] = b[c];
     }
   }
@@ -183,30 +179,33 @@ int launch_synth_kq_blocks(uint8_t* dst, int type, size_t nblocks, uint64_t seed
   return 0;
 }
 
-// GET_ROWS of a K-quant token_embd: dequantize_row_q{4,5,6}_K (f32, one rounding per operation)
+// GET_ROWS of a K-quant token_embd: dequantize_row_q{4,5,6}_K (f32, one rounding per operation);
+// thread = 16 consecutive values
 __global__ __launch_bounds__(256) void embed_kq_kernel(float* x, const uint8_t* tok, int type, int bb, const int* ids,
                                                        int n) {
 #pragma clang fp contract(off)
   const int c = blockIdx.x;
   const uint8_t* row = tok + (size_t)ids[c] * (n / 256) * bb;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    const uint8_t* b = row + (size_t)(k / 256) * bb;
-    const int kk = k % 256;
-    const int v = kq_value(type, b, kk);
-    float y;
-    if (type == 14) {
-      const float d = (float)__builtin_bit_cast(_Float16, (uint16_t)(b[208] | (b[209] << 8)));
-      y = (d * (float)(int8_t)b[192 + kk / 16]) * (float)(v - 32);
-    } else {
-      const int j = kk / 32;
-      const uint8_t* q = b + 4;
-      const int sc = j < 4 ? q[j] & 63 : (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
-      const int mn = j < 4 ? q[j + 4] & 63 : (q[j + 4] >> 4) | ((q[j] >> 6) << 4);
-      const float d = (float)__builtin_bit_cast(_Float16, (uint16_t)(b[0] | (b[1] << 8)));
-      const float dmin = (float)__builtin_bit_cast(_Float16, (uint16_t)(b[2] | (b[3] << 8)));
-      y = (d * (float)sc) * (float)v - dmin * (float)mn;
+  for (int t = threadIdx.x; t < n / 16; t += blockDim.x) {
+    for (int k = 16 * t; k < 16 * t + 16; ++k) {
+      const uint8_t* b = row + (size_t)(k / 256) * bb;
+      const int kk = k % 256;
+      const int v = kq_value(type, b, kk);
+      float y;
+      if (type == 14) {
+        const float d = (float)__builtin_bit_cast(_Float16, (uint16_t)(b[208] | (b[209] << 8)));
+        y = (d * (float)(int8_t)b[192 + kk / 16]) * (float)(v - 32);
+      } else {
+        const int j = kk / 32;
+        const uint8_t* q = b + 4;
+        const int sc = j < 4 ? q[j] & 63 : (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
+        const int mn = j < 4 ? q[j + 4] & 63 : (q[j + 4] >> 4) | ((q[j] >> 6) << 4);
+        const float d = (float)__builtin_bit_cast(_Float16, (uint16_t)(b[0] | (b[1] << 8)));
+        const float dmin = (float)__builtin_bit_cast(_Float16, (uint16_t)(b[2] | (b[3] << 8)));
+        y = (d * (float)sc) * (float)v - dmin * (float)mn;
+      }
+      x[(size_t)c * n + k] = y;
     }
-    x[(size_t)c * n + k] = y;
   }
 }
 
@@ -222,96 +221,110 @@ int launch_embed_kq(float* x, const uint8_t* tok, int type, const int* ids, int 
 // sits at 256s + 64g + 8j + e (lane group g's 8 sub-block fragments contiguous); xd f32 [M][K/256]
 // (d = 1/iscale); xb f32 [M][K/32]: the sum of the 32 q of sub-block j at 8s + 2(j&3) + (j>>2)
 // (the B operand order of the mins MFMA).
-// One wave per super-block: lane t holds x[256s + 4t .. 4t+3].
+// One DPP row (16 lanes) per super-block, lane t holding k = 16t .. 16t+15: the max and the
+// first-max search are row16 DPP reductions (no LDS round trips), 4 super-blocks per wave.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void q8k_store(f32x4 v, int t, int8_t* qsb, float* dsb, float* xbsb) {
-  float a = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-  float amax = a;
+__device__ __forceinline__ void q8k_row(const float (&v)[16], int t, int8_t* qsb, float* dsb, float* xbsb) {
+  float a = 0.f;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+  for (int i = 0; i < 16; ++i) a = fmaxf(a, fabsf(v[i]));
+  const float amax = row16_max(a);
   // ggml takes max = the signed value of the FIRST element with |x| == amax
   int first = 1 << 20;
-  float cand = 0.f;
 #pragma unroll
-  for (int i = 3; i >= 0; --i)
-    if (fabsf(v[i]) == amax) {
-      first = 4 * t + i;
-      cand = v[i];
-    }
-  int key = first;
+  for (int i = 15; i >= 0; --i)
+    if (fabsf(v[i]) == amax) first = 16 * t + i;
+  const int key = (int)-row16_max(-(float)first);  // exact: keys < 2^24
+  float mine = 0.f;
+  if (first == key) {
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) key = min(key, __shfl_xor(key, o));
-  const float mx = __shfl(cand, (key >> 2) & 63);
-  uint32_t w = 0;
-  int qs[4] = {0, 0, 0, 0};
+    for (int i = 0; i < 16; ++i)
+      if (16 * t + i == key) mine = v[i];
+  }
+  const float mx = row16_sum(mine);  // only the owner lane contributes
+  int q[16];
   float d = 0.f;
   if (amax != 0.f) {
     const float iscale = -127.f / mx;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = (int)__builtin_rintf(iscale * v[i]);
-      qs[i] = q < 127 ? q : 127;
-      w |= (uint32_t)(uint8_t)(int8_t)qs[i] << (8 * i);
+    for (int i = 0; i < 16; ++i) {
+      const int r = (int)__builtin_rintf(iscale * v[i]);
+      q[i] = r < 127 ? r : 127;
     }
     d = 1.f / iscale;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) q[i] = 0;
   }
-  const int j = t >> 3, g = (t >> 1) & 3;
-  *reinterpret_cast<uint32_t*>(qsb + 64 * g + 8 * j + 4 * (t & 1)) = w;
-  int bs = qs[0] + qs[1] + qs[2] + qs[3];
+  // k = 16t + i: sub-block j = t >> 1, lane group g = 2(t&1) + (i >> 3), e = i & 7
+  const int j = t >> 1;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    u32x2 w = u32x2{0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) w[e >> 2] |= (uint32_t)(uint8_t)(int8_t)q[8 * h + e] << (8 * (e & 3));
+    *reinterpret_cast<u32x2*>(qsb + 64 * (2 * (t & 1) + h) + 8 * j) = w;
+  }
+  int bs = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) bs += q[i];
   bs += __shfl_xor(bs, 1);
-  bs += __shfl_xor(bs, 2);
-  bs += __shfl_xor(bs, 4);
-  if ((t & 7) == 0) xbsb[2 * (j & 3) + (j >> 2)] = (float)bs;
+  if ((t & 1) == 0) xbsb[2 * (j & 3) + (j >> 2)] = (float)bs;
   if (t == 0) *dsb = d;
 }
 
-// RMS_NORM + MUL (norm_q8_kernel's arithmetic), then Q8_K; one work-group (4 waves) per row
-__global__ __launch_bounds__(256) void norm_q8k_kernel(int8_t* xq, float* xd, float* xb, const float* x, const float* w,
-                                                       const int* row_map, int n, float eps) {
-  const int c = blockIdx.x;
+// grid (ceil(K/256/16), M), 256 threads: super-block s = 16*blockIdx.x + threadIdx.x/16 of row
+// blockIdx.y; with norm_w, RMS_NORM + MUL first (sum of squares of the whole row in double, every
+// work-group of the row computing it the same way: norm_q8_kernel's arithmetic)
+template <bool NORM>
+__global__ __launch_bounds__(256) void q8k_kernel(int8_t* xq, float* xd, float* xb, const float* src, int ld,
+                                                  const float* w, const int* row_map, int n, float eps) {
+  const int c = blockIdx.y;
   const int r = row_map ? row_map[c] : c;
-  const float* xr = x + (size_t)r * n;
-  double acc = 0.0;
-  for (int i = threadIdx.x * 4; i < n; i += 1024) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
+  const float* xr = src + (size_t)r * ld;
+  float scale = 1.0f;
+  if constexpr (NORM) {
+    double acc = 0.0;
+    for (int i = threadIdx.x * 4; i < n; i += 1024) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc += (double)(v[j] * v[j]);
+      for (int j = 0; j < 4; ++j) acc += (double)(v[j] * v[j]);
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    __shared__ double part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    const double sum = part[0] + part[1] + part[2] + part[3];
+    scale = 1.0f / sqrtf((float)(sum / n) + eps);
   }
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-  __shared__ double part[4];
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  const double sum = part[0] + part[1] + part[2] + part[3];
-  const float scale = 1.0f / sqrtf((float)(sum / n) + eps);
-  const int t = threadIdx.x & 63;
-  for (int s = threadIdx.x >> 6; s < n / 256; s += 4) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(xr + 256 * s + 4 * t);
-    const f32x4 g = *reinterpret_cast<const f32x4*>(w + 256 * s + 4 * t);
-    f32x4 y;
+  const int s = 16 * blockIdx.x + (threadIdx.x >> 4);
+  if (s >= n / 256) return;
+  const int t = threadIdx.x & 15;
+  float v[16];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) y[j] = (v[j] * scale) * g[j];
-    q8k_store(y, t, xq + (size_t)c * n + 256 * s, xd + (size_t)c * (n / 256) + s, xb + (size_t)c * (n / 32) + 8 * s);
+  for (int i = 0; i < 16; i += 4) {
+    const f32x4 x4 = *reinterpret_cast<const f32x4*>(xr + 256 * s + 16 * t + i);
+    if constexpr (NORM) {
+      const f32x4 g4 = *reinterpret_cast<const f32x4*>(w + 256 * s + 16 * t + i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[i + e] = (x4[e] * scale) * g4[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[i + e] = x4[e];
+    }
   }
-}
-
-__global__ __launch_bounds__(256) void quantize_q8k_kernel(int8_t* xq, float* xd, float* xb, const float* src, int ld,
-                                                           int n) {
-  const int c = blockIdx.x;
-  const int t = threadIdx.x & 63;
-  for (int s = threadIdx.x >> 6; s < n / 256; s += 4)
-    q8k_store(*reinterpret_cast<const f32x4*>(src + (size_t)c * ld + 256 * s + 4 * t), t, xq + (size_t)c * n + 256 * s,
-              xd + (size_t)c * (n / 256) + s, xb + (size_t)c * (n / 32) + 8 * s);
+  q8k_row(v, t, xq + (size_t)c * n + 256 * s, xd + (size_t)c * (n / 256) + s, xb + (size_t)c * (n / 32) + 8 * s);
 }
 
 int launch_rmsnorm_q8k(int8_t* xq, float* xd, float* xb, const float* x, const float* w, const int* row_map, int M, int n,
                        float eps, hipStream_t s) {
   if (n % 256 || M < 1) return -1;
-  norm_q8k_kernel<<<M, 256, 0, s>>>(xq, xd, xb, x, w, row_map, n, eps);
+  q8k_kernel<true><<<dim3((n / 256 + 15) / 16, M), 256, 0, s>>>(xq, xd, xb, x, n, w, row_map, n, eps);
   return 0;
 }
 int launch_quantize_q8k(int8_t* xq, float* xd, float* xb, const float* src, int ld, int M, int n, hipStream_t s) {
   if (n % 256 || M < 1) return -1;
-  quantize_q8k_kernel<<<M, 256, 0, s>>>(xq, xd, xb, src, ld, n);
+  q8k_kernel<false><<<dim3((n / 256 + 15) / 16, M), 256, 0, s>>>(xq, xd, xb, src, ld, nullptr, nullptr, n, 0.f);
   return 0;
 }
 
@@ -385,7 +398,8 @@ __device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int 
       } else {
 #pragma unroll
         for (int c = 0; c < 2; ++c) f.sc[r][c] = *reinterpret_cast<const u32x4*>(t + SC + 32 * g + 16 * c);
-        f.mn[r] = *reinterpret_cast<const uint16_t*>(t + SC + 128 + 2 * lane);
+        const u32x2 mw = *reinterpret_cast<const u32x2*>(t + SC + 128 + 8 * (lane & 15));
+        f.mn[r] = ((mw[0] >> (8 * g)) & 0xFFu) | (((mw[1] >> (8 * g)) & 0xFFu) << 8);  // mins g, g + 4
         f.dm[r] = *reinterpret_cast<const u32x4*>(t + SC + 256 + 16 * g);
       }
     }
