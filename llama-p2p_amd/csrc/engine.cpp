@@ -906,12 +906,12 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
     a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
     a.slot_stride = slot_stride;
-    if (launch_mm(EPI_QKV, a, s)) return fail(MX_ERR_ARG, "qkv launch shape");
     AttnArgs at{};
     at.q = q; at.kc = kc; at.vc = vc; at.pos = pos; at.slot = slot;
     at.out = attn_out; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
     at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;
     at.scale = 1.0f / sqrtf((float)head_dim);
+    if (launch_mm(EPI_QKV, a, s)) return fail(MX_ERR_ARG, "qkv launch shape");
     MMArgs b{};
     b.W = L.o; b.N = h; b.K = h; b.X = attn_out; b.ldx = h; b.M = M; b.out = x; b.ldo = h;
     if (use_pers && nol && mm_pers_supported(EPI_SWIGLU, M, 2 * ff, h)) {  // partials for gate/up's norm on load
@@ -1076,6 +1076,7 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     b.W = L.o; b.N = h; b.K = h; b.M = M; b.out = x; b.ldo = h;
     site = 2;
     operand(b, attn_f, h, nullptr, M, nullptr);
+    b.ssq = ql ? ssq : nullptr; b.np = h / 16;  // partials of the new residual for gate/up's norm
     if (launch_mq8(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "q8 attn_output launch shape");
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.actf = act_f; c.lda = ff;
@@ -1086,6 +1087,7 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     d.W = L.down; d.N = h; d.K = ff; d.M = M; d.out = x; d.ldo = h;
     site = 8;
     operand(d, act_f, ff, nullptr, M, nullptr);
+    d.ssq = ql ? ssq : nullptr; d.np = h / 16;  // for the next layer's qkv (or lm_head) norm
     if (launch_mq8(EPI_RESID, d, s)) return fail(MX_ERR_ARG, "q8 ffn_down launch shape");
   }
   if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));

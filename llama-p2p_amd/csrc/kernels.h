@@ -31,6 +31,30 @@ enum Epilogue : int {
   EPI_SLAB = 4,    // split-K partial: out = slab[ksplit][col][row] (reduced by resid_norm / qkv_finish)
 };
 
+struct AttnArgs {
+  const float* q;        // [M][n_head*head_dim] f32 (post-RoPE)
+  const _Float16* kc;    // [slots][n_head_kv][ctx_stride * head_dim], 1 KiB B-operand tiles (kernels.hip)
+  const _Float16* vc;    // [slots][n_head_kv][ctx_stride * head_dim], 1 KiB B-operand tiles
+  const int* pos;        // [M]  query position; attends to [0, pos]
+  const int* slot;       // [M]
+  uint16_t* out;         // bf16 [M][ldo] (src1 of attn_output)
+  int ldo;
+  float* outf;           // f32 [M][ldo] instead of out (Q8_0 models quantise it next)
+  int M, n_head, n_head_kv, head_dim, n_ctx, ctx_stride;
+  size_t slot_stride;
+  float scale;
+  // qkv still as split-K partial slabs (wide path): the kernel sums them in slab order, applies
+  // RoPE, stores this position's K/V into the caches and keeps q and the new K/V in LDS
+  const float* slabs;    // [nslab][M][n_q + 2*n_kv] or nullptr (q / caches already final)
+  int nslab;
+  size_t slab_stride;
+  const float* rope_cs;  // [n_ctx][head_dim/2][2]
+  _Float16 *kc_w, *vc_w; // writable views of kc / vc
+  // diagnosis only (mx_profile_kernel with MX_ATTN_TRACE): per (row, kv head, wave) 8 wall-clock
+  // stamps (100 MHz) at the kernel's phases; nullptr normally
+  unsigned long long* trace;
+};
+
 struct MMArgs {
   const uint16_t* W;   // packed tiles
   int N, K;            // logical W[N][K]; for SWIGLU N = 2*n_ff (interleaved tiles)
@@ -76,29 +100,6 @@ struct MMArgs {
   size_t kq_off[3];
 };
 
-struct AttnArgs {
-  const float* q;        // [M][n_head*head_dim] f32 (post-RoPE)
-  const _Float16* kc;    // [slots][n_head_kv][ctx_stride * head_dim], 1 KiB B-operand tiles (kernels.hip)
-  const _Float16* vc;    // [slots][n_head_kv][ctx_stride * head_dim], 1 KiB B-operand tiles
-  const int* pos;        // [M]  query position; attends to [0, pos]
-  const int* slot;       // [M]
-  uint16_t* out;         // bf16 [M][ldo] (src1 of attn_output)
-  int ldo;
-  float* outf;           // f32 [M][ldo] instead of out (Q8_0 models quantise it next)
-  int M, n_head, n_head_kv, head_dim, n_ctx, ctx_stride;
-  size_t slot_stride;
-  float scale;
-  // qkv still as split-K partial slabs (wide path): the kernel sums them in slab order, applies
-  // RoPE, stores this position's K/V into the caches and keeps q and the new K/V in LDS
-  const float* slabs;    // [nslab][M][n_q + 2*n_kv] or nullptr (q / caches already final)
-  int nslab;
-  size_t slab_stride;
-  const float* rope_cs;  // [n_ctx][head_dim/2][2]
-  _Float16 *kc_w, *vc_w; // writable views of kc / vc
-  // diagnosis only (mx_profile_kernel with MX_ATTN_TRACE): per (row, kv head, wave) 8 wall-clock
-  // stamps (100 MHz) at the kernel's phases; nullptr normally
-  unsigned long long* trace;
-};
 
 
 // packing / synthetic weights.  mode: PACK_ROWS (logical row r -> packed row r + offset),

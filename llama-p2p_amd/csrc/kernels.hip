@@ -320,11 +320,10 @@ __device__ __forceinline__ void xs_build(const XsRegs<MM>& r, const MMArgs& a, u
 }
 
 template <int KS, int RT, int NB, int EPI, int U, bool XS>
-__global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
+__device__ __forceinline__ void mm_body(const MMArgs& a, int tile0) {
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int KT = a.K / TILE_K;
-  const int tile0 = blockIdx.x * RT;
   const int kb = (KT * w) / KS, ke = (KT * (w + 1)) / KS;
 
   __shared__ f32x4 red[KS][RT][NB][64];
@@ -458,6 +457,11 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
     }
     epi_store<EPI>(a, tile0 + r, l, col, s, up);
   }
+}
+
+template <int KS, int RT, int NB, int EPI, int U, bool XS>
+__global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
+  mm_body<KS, RT, NB, EPI, U, XS>(a, blockIdx.x * RT);
 }
 
 template <int KS, int RT, int EPI, int U>

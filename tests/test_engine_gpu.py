@@ -458,3 +458,4 @@ def test_llama3_70b_full_size_row_consistency(mx):
         if top[0] - top[1] > 2 * tol2.max():
             assert int(one[0].argmax()) == int(ref.argmax())
     eng.close()
+
