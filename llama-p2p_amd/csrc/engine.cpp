@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <map>
@@ -1361,6 +1362,17 @@ int32_t mx_engine::sample_chain(Request* r, std::vector<std::pair<float, int>>& 
 // reads it), lm_head only on each request's last prompt row, and the first token by the device
 // argmax (ties -> lowest id) or, for sampling requests, the host sampler chain.
 int mx_engine::prefill_batch(std::vector<Request*>& reqs) {
+  static const bool trace = getenv("MX_SCHED_TRACE") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  struct Log {
+    const std::chrono::steady_clock::time_point t0;
+    size_t n;
+    ~Log() {
+      if (trace)
+        fprintf(stderr, "sched: prefill %zu requests %.3f ms\n", n,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+  } log{t0, reqs.size()};
   std::vector<int32_t> slots, pos, ids;
   std::vector<int> end_row(reqs.size());
   for (size_t q = 0; q < reqs.size(); q++) {
@@ -1469,8 +1481,12 @@ int mx_engine::sched_step(std::vector<Request*>& rows) {
     return enqueue_forward(M, d_ids, d_pos, d_slot, nullptr, nullptr, true, nullptr, M, true, d_ids, d_pos,
                            sched_hist, SCHED_KMAX, sched_hist_count, SCHED_KMAX, s);
   };
+  static const bool trace = getenv("MX_SCHED_TRACE") != nullptr;  // per-round timing on stderr
+  const auto t0 = std::chrono::steady_clock::now();
+  bool captured = false;
   auto it = sched_graphs.find(M);
   if (use_graphs && it == sched_graphs.end()) {
+    captured = true;
     hipGraph_t g;
     HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     int rc = step();
@@ -1512,6 +1528,10 @@ int mx_engine::sched_step(std::vector<Request*>& rows) {
     HIPC(hipMemcpyAsync(lg.data(), logits, (size_t)M * n_vocab * 4, hipMemcpyDeviceToHost, s));
   }
   HIPC(hipStreamSynchronize(s));
+  if (trace) {
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    fprintf(stderr, "sched: decode M=%d K=%d %s%.3f ms\n", M, K, captured ? "(graph captured) " : "", ms);
+  }
   std::lock_guard<std::mutex> lk(mu);
   for (int i = 0; i < M; i++) {
     Request* r = rows[i];

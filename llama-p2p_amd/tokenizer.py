@@ -18,9 +18,11 @@ Host-side only: tokenization is negligible next to the forward pass.
 from __future__ import annotations
 
 import heapq
+import re
 from typing import Dict, List, Optional, Sequence
 
 SPACE = "▁"
+_SPM_SEGMENT = re.compile(SPACE + "+[^" + SPACE + "]*|[^" + SPACE + "]+")  # split before SPACE after non-SPACE
 TOKEN_NORMAL, TOKEN_UNKNOWN, TOKEN_CONTROL, TOKEN_USER, TOKEN_UNUSED, TOKEN_BYTE = 1, 2, 3, 4, 5, 6
 
 LLAMA3_PRETOKENIZE = (r"(?:'[sS]|'[tT]|'[rR][eE]|'[vV][eE]|'[mM]|'[lL][lL]|'[dD])|[^\r\n\p{L}\p{N}]?\p{L}+|"
@@ -69,6 +71,12 @@ class Tokenizer:
         self._b2u = _bytes_to_unicode()
         self._u2b = {v: k for k, v in self._b2u.items()}
         self._re = None
+        # SPM text splits exactly at every SPACE that follows a non-SPACE character when no vocabulary
+        # piece holds such a pair (merges never cross those boundaries), and BPE works per regex word:
+        # both tokenise repeated segments once (per-segment cache; llama.cpp tokenises in C++)
+        self._spm_split = not any(SPACE in t[1:] and any(t[i] == SPACE and t[i - 1] != SPACE for i in range(1, len(t)))
+                                  for t in self.tokens)
+        self._seg_cache: Dict[str, List[int]] = {}
 
     # ------------------------------------------------------------------ load
     @classmethod
@@ -121,10 +129,26 @@ class Tokenizer:
             parts = nxt
         return parts
 
+    def _cached(self, seg: str, fn) -> List[int]:
+        ids = self._seg_cache.get(seg)
+        if ids is None:
+            if len(self._seg_cache) > 200000:
+                self._seg_cache.clear()
+            ids = self._seg_cache[seg] = fn(seg)
+        return ids
+
     def _spm(self, text: str) -> List[int]:
         text = text.replace(" ", SPACE)
         if not text:
             return []
+        if not self._spm_split:
+            return self._spm_seg(text)
+        out: List[int] = []
+        for m in _SPM_SEGMENT.finditer(text):
+            out.extend(self._cached(m.group(0), self._spm_seg))
+        return out
+
+    def _spm_seg(self, text: str) -> List[int]:
         sym = list(text)  # UTF-8 characters
         n = len(sym)
         prev = list(range(-1, n - 1))
@@ -174,22 +198,27 @@ class Tokenizer:
             self._re = regex.compile(LLAMA3_PRETOKENIZE)
         out = []
         for word in self._re.findall(text):
-            w = [self._b2u[b] for b in word.encode("utf-8")]
-            while len(w) > 1:
-                best, bi = None, -1
-                for i in range(len(w) - 1):
-                    r = self.bpe_ranks.get((w[i], w[i + 1]))
-                    if r is not None and (best is None or r < best):
-                        best, bi = r, i
-                if best is None:
-                    break
-                w = w[:bi] + [w[bi] + w[bi + 1]] + w[bi + 2:]
-            for piece in w:
-                pid = self.piece_to_id.get(piece)
-                if pid is None:
-                    out.extend(self.piece_to_id.get(c, self.unk_id) for c in piece)
-                else:
-                    out.append(pid)
+            out.extend(self._cached(word, self._bpe_word))
+        return out
+
+    def _bpe_word(self, word: str) -> List[int]:
+        out = []
+        w = [self._b2u[b] for b in word.encode("utf-8")]
+        while len(w) > 1:
+            best, bi = None, -1
+            for i in range(len(w) - 1):
+                r = self.bpe_ranks.get((w[i], w[i + 1]))
+                if r is not None and (best is None or r < best):
+                    best, bi = r, i
+            if best is None:
+                break
+            w = w[:bi] + [w[bi] + w[bi + 1]] + w[bi + 2:]
+        for piece in w:
+            pid = self.piece_to_id.get(piece)
+            if pid is None:
+                out.extend(self.piece_to_id.get(c, self.unk_id) for c in piece)
+            else:
+                out.append(pid)
         return out
 
     # ------------------------------------------------------------ detokenize

@@ -71,3 +71,23 @@ def test_bpe_matches_tokenizers(tmp_path):
         ours = tok.tokenize(s.encode(), add_bos=False)
         assert ours == t.encode(s).ids, s
         assert tok.detokenize(ours).decode("utf-8") == s, s
+
+
+def test_spm_segment_cache_is_exact():
+    """Segmenting SPM text before every SPACE that follows a non-SPACE (the per-segment cache) gives
+    the same ids as merging the whole text, for a vocabulary with no piece holding such a pair; a
+    vocabulary that holds one falls back to whole-text merging."""
+    from llama_p2p_amd import gguf
+    from llama_p2p_amd.tokenizer import SPACE, Tokenizer
+
+    toks, scores, types = gguf.synthetic_spm_vocab(4096)
+    tok = Tokenizer(toks, scores, types, "llama", bos_id=1, eos_id=2)
+    assert tok._spm_split
+    rng = random.Random(5)
+    words = ["node", "peer", "the", "llama", "a", "12", "x.y", "é", "  ", "   "]
+    for _ in range(50):
+        s = " ".join(rng.choice(words) for _ in range(rng.randint(1, 40)))
+        whole = tok._spm_seg((" " + s).replace(" ", SPACE))
+        assert tok.tokenize(s.encode(), add_bos=False) == whole
+    bad = Tokenizer(list(toks) + ["e" + SPACE], list(scores) + [0.0], list(types) + [TOKEN_NORMAL], "llama")
+    assert not bad._spm_split
