@@ -202,6 +202,10 @@ struct mx_engine {
   bool use_wide = getenv("MX_NO_WIDE") == nullptr;  // 17..64-row forward through mm_wide (LDS-shared activations)
   float* slabs = nullptr;                           // split-K partials [8][MAX_ROWS][n_embd + 2 n_embd_kv]
   size_t slab_stride = 0;
+  float* gslabs = nullptr;  // split-K partials of small-M prefill GEMMs, [S][M][N] (launch_gemm_split)
+  static constexpr size_t GSLAB_FLOATS = (size_t)32 << 20;
+  // work-groups a split prefill GEMM aims at (MX_GEMM_SPLIT_TARGET; 0 = one K range per tile)
+  int gemm_split_target = getenv("MX_GEMM_SPLIT_TARGET") ? atoi(getenv("MX_GEMM_SPLIT_TARGET")) : 256;
   int ctx_stride = 0;  // KV positions allocated per slot (n_ctx rounded up to KV_POS_ALIGN)
   uint64_t weight_bytes = 0;
 
@@ -376,6 +380,8 @@ int mx_engine::init_common() {
   }
   slab_stride = (size_t)MAX_ROWS * (n_embd + 2 * n_embd_kv);
   if (int rc = alloc((void**)&slabs, slab_stride * 8 * 4)) return rc;
+  if (!wq8 && !wkq)
+    if (int rc = alloc((void**)&gslabs, GSLAB_FLOATS * 4)) return rc;
   if (int rc = alloc((void**)&ssq, (size_t)R * (n_embd / 16) * 4)) return rc;
   if (int rc = alloc((void**)&am_val, (size_t)R * 64 * 4)) return rc;
   if (has_head) {
@@ -1176,17 +1182,19 @@ int mx_engine::enqueue_forward_kq(int M, const int* pos, const int* slot, void* 
 int mx_engine::enqueue_forward_gemm(int M, const int* pos, const int* slot, void* x_out, bool head,
                                     const int* rowmap, int n_out, hipStream_t s) {
   const int h = n_embd, kv = n_embd_kv, ff = n_ff;
+  const size_t gstride = (size_t)M * h;  // RESID partial slabs [S][M][h]
+  int nslab = 0;                         // ... not yet folded into x
   for (int li = 0; li < (int)layers.size(); li++) {
     const Layer& L = layers[li];
     _Float16* kc = kcache + layer_kv_stride * li;
     _Float16* vc = vcache + layer_kv_stride * li;
-    launch_rmsnorm(xn, h, x, L.attn_norm, nullptr, M, h, eps, s);
+    launch_resid_norm(xn, h, x, gslabs, nslab, gstride, L.attn_norm, M, h, eps, s);
     MMArgs a{};
     a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M; a.X = xn; a.ldx = h;
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
     a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
     a.slot_stride = slot_stride;
-    if (launch_gemm(EPI_QKV, a, s)) return fail(MX_ERR_ARG, "prefill qkv GEMM shape");
+    if (launch_gemm_split(EPI_QKV, a, gslabs, GSLAB_FLOATS, gemm_split_target, s) < 0) return fail(MX_ERR_ARG, "prefill qkv GEMM shape");
     AttnArgs at{};
     at.q = q; at.kc = kc; at.vc = vc; at.pos = pos; at.slot = slot;
     at.out = attn_out; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
@@ -1196,15 +1204,19 @@ int mx_engine::enqueue_forward_gemm(int M, const int* pos, const int* slot, void
     else launch_attention(at, s);
     MMArgs b{};
     b.W = L.o; b.N = h; b.K = h; b.X = attn_out; b.ldx = h; b.M = M; b.out = x; b.ldo = h;
-    if (launch_gemm(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "prefill attn_output GEMM shape");
-    launch_rmsnorm(xn, h, x, L.ffn_norm, nullptr, M, h, eps, s);
+    if ((nslab = launch_gemm_split(EPI_RESID, b, gslabs, GSLAB_FLOATS, gemm_split_target, s)) < 0)
+      return fail(MX_ERR_ARG, "prefill attn_output GEMM shape");
+    launch_resid_norm(xn, h, x, gslabs, nslab, gstride, L.ffn_norm, M, h, eps, s);
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.X = xn; c.ldx = h; c.act = act; c.lda = ff;
-    if (launch_gemm(EPI_SWIGLU, c, s)) return fail(MX_ERR_ARG, "prefill gate/up GEMM shape");
+    if (launch_gemm_split(EPI_SWIGLU, c, gslabs, GSLAB_FLOATS, gemm_split_target, s) < 0)
+      return fail(MX_ERR_ARG, "prefill gate/up GEMM shape");
     MMArgs d{};
     d.W = L.down; d.N = h; d.K = ff; d.X = act; d.ldx = ff; d.M = M; d.out = x; d.ldo = h;
-    if (launch_gemm(EPI_RESID, d, s)) return fail(MX_ERR_ARG, "prefill ffn_down GEMM shape");
+    if ((nslab = launch_gemm_split(EPI_RESID, d, gslabs, GSLAB_FLOATS, gemm_split_target, s)) < 0)
+      return fail(MX_ERR_ARG, "prefill ffn_down GEMM shape");
   }
+  if (nslab) launch_resid_norm(nullptr, 0, x, gslabs, nslab, gstride, nullptr, M, h, eps, s);
   if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
   if (head) {
     if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");

@@ -140,6 +140,11 @@ void launch_attention_prefill(const AttnArgs& a, hipStream_t s);
 // prefill (> MAX_ROWS rows): MFMA GEMM over packed weights with the same epilogues (N % 256, K % 64)
 bool gemm_supported(int N, int K);
 int launch_gemm(int epi, const MMArgs& a, hipStream_t s);
+// the same GEMM split over K when it has too few work-groups to fill the CUs (small prefills;
+// ~target work-groups, 0 = never split): partials go to `slabs` ([S][M][N] floats, at most slab_floats); QKV / SWIGLU are finished
+// inside; returns S for EPI_RESID (the caller folds the partials with launch_resid_norm, slab
+// stride M*N), 0 when the epilogue ran in place, -1 on a bad shape
+int launch_gemm_split(int epi, const MMArgs& a, float* slabs, size_t slab_floats, int target, hipStream_t s);
 // ---- Q8_0 weights.  Packed tile = 16 rows x 64 k, Q8_TILE_BYTES:
 // [0,1024): int8 A operands of two v_mfma_i32_16x16x32_i8, lane l = row l&15 holds 8 bytes of
 // block 0 (k 8(l>>4)..+8) then 8 bytes of block 1 (k 32+8(l>>4)..+8); [1024,1088): f16 block

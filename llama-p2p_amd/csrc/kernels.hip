@@ -1432,6 +1432,8 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(MMArgs a) {
   const int nmb = (a.M + GB_M - 1) / GB_M;
   const int mb = wgid % nmb, nb = wgid / nmb;
   const int KT = a.K / TILE_K, NS = a.K / GKC;
+  // split-K (grid.y > 1, EPI_SLAB): this block's K-steps [s0, s1)
+  const int ks = blockIdx.y, s0 = NS * ks / gridDim.y, s1 = NS * (ks + 1) / gridDim.y;
   const int m0 = mb * GB_M;
   const int r16 = lane & 15;
 
@@ -1461,10 +1463,10 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(MMArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  issue(0, 0);
-  for (int st = 0; st < NS; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < NS) {
+  issue(s0, 0);
+  for (int st = s0; st < s1; ++st) {
+    const int buf = (st - s0) & 1;
+    if (st + 1 < s1) {
       issue(st + 1, buf ^ 1);
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this thread's copies of step st landed
     } else {
@@ -1513,11 +1515,69 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(MMArgs a) {
       }
       const int col = m0 + wm * 128 + j * 16 + r16;
       if (col >= a.M || (EPI == EPI_SWIGLU && lane >= 32)) continue;
-      epi_store<EPI>(a, tile0 + r, lane, col, sv, up);
+      if constexpr (EPI == EPI_SLAB) {
+        const int row = (tile0 + r) * 16 + (lane >> 4) * 4;
+        *reinterpret_cast<f32x4*>(a.out + (size_t)ks * a.slab_stride + (size_t)col * a.ldo + row) = sv;
+      } else {
+        epi_store<EPI>(a, tile0 + r, lane, col, sv, up);
+      }
     }
 }
 
+// gate/up split-K partials -> sum in slab order -> SwiGLU -> bf16 act (the EPI_SWIGLU epilogue's
+// values: slab tile t holds gate rows 8t..8t+7 in rows 16t..16t+7 and the up rows after them)
+__global__ __launch_bounds__(256) void swiglu_finish_kernel(MMArgs a, const float* slabs, int nslab, size_t stride) {
+  const int quads = a.N / 8;  // 4-row groups of ffn rows
+  const int total = a.M * quads;
+  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < total; u += gridDim.x * blockDim.x) {
+    const int col = u / quads, fr = (u % quads) * 4;
+    const int srow = (fr >> 3) * 16 + (fr & 7);
+    const float* p = slabs + (size_t)col * a.N + srow;
+    f32x4 g = *reinterpret_cast<const f32x4*>(p), up = *reinterpret_cast<const f32x4*>(p + 8);
+    for (int k = 1; k < nslab; ++k) {
+      g += *reinterpret_cast<const f32x4*>(p + k * stride);
+      up += *reinterpret_cast<const f32x4*>(p + k * stride + 8);
+    }
+    f32x4 f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = (g[i] / (1.0f + expf(-g[i]))) * up[i];
+    u32x2 o;
+    o[0] = f2bf(f[0]) | (f2bf(f[1]) << 16);
+    o[1] = f2bf(f[2]) | (f2bf(f[3]) << 16);
+    *reinterpret_cast<u32x2*>(a.act + (size_t)col * a.lda + fr) = o;
+  }
+}
+
 bool gemm_supported(int N, int K) { return N % GB_N == 0 && K % GKC == 0; }
+
+// K split that brings a small-M GEMM to ~target work-groups (at M <= 256 a Llama-3-8B
+// GEMM has 16..112 of them, one per 256 weight rows: most CUs idle), bounded by the slab space
+// and by >= 4 K-steps per split; 1 = no split
+static int gemm_split(const MMArgs& a, size_t slab_floats, int target) {
+  const int base = (a.N / GB_N) * ((a.M + GB_M - 1) / GB_M);
+  const int NS = a.K / GKC;
+  int S = (target + base / 2) / base;
+  S = std::min(S, std::min(16, NS / 4));
+  while (S > 1 && (size_t)S * a.M * a.N > slab_floats) S--;
+  return std::max(S, 1);
+}
+
+int launch_gemm_split(int epi, const MMArgs& a, float* slabs, size_t slab_floats, int target, hipStream_t s) {
+  if (a.M < 1 || !a.X || !gemm_supported(a.N, a.K)) return -1;
+  const int S = (slabs && epi != EPI_F32 && target > 0) ? gemm_split(a, slab_floats, target) : 1;
+  if (S == 1) return launch_gemm(epi, a, s) ? -1 : 0;
+  MMArgs p = a;
+  p.out = slabs;
+  p.ldo = a.N;
+  p.slab_stride = (size_t)a.M * a.N;
+  dim3 grid((a.N / GB_N) * ((a.M + GB_M - 1) / GB_M), S);
+  gemm2_kernel<EPI_SLAB><<<grid, 512, 0, s>>>(p);
+  const int total = epi == EPI_SWIGLU ? a.M * a.N / 8 : a.M * a.N / 4;
+  const int blocks = std::min((total + 255) / 256, 2048);
+  if (epi == EPI_QKV) qkv_finish_kernel<<<blocks, 256, 0, s>>>(a, slabs, S, p.slab_stride);
+  else if (epi == EPI_SWIGLU) swiglu_finish_kernel<<<blocks, 256, 0, s>>>(a, slabs, S, p.slab_stride);
+  return epi == EPI_RESID ? S : 0;
+}
 
 int launch_gemm(int epi, const MMArgs& a, hipStream_t s) {
   if (a.M < 1 || !a.X || !gemm_supported(a.N, a.K)) return -1;

@@ -188,13 +188,16 @@ def test_wide_decode_batch_vs_oracle(mx, oracle_mod):
     eng.close()
 
 
-@pytest.mark.parametrize("name,n_prompt", [("test-tiny", 700), ("test-d128", 300), ("test-h4096", 300)])
-def test_gemm_prefill_vs_oracle(mx, oracle_mod, name, n_prompt):
-    """Prompts of > 64 tokens without logits run as 512-row chunks of MFMA GEMMs (prefill path);
-    the next decode step attends to the K/V they stored: its logits must match the oracle, and the
-    prompt's last-row logits from a 64-row-chunk run must match the oracle too."""
+@pytest.mark.parametrize("split", ["256", "0"])
+@pytest.mark.parametrize("name,n_prompt", [("test-tiny", 700), ("test-d128", 300), ("test-h4096", 300),
+                                           ("test-h4096", 100)])
+def test_gemm_prefill_vs_oracle(mx, oracle_mod, monkeypatch, name, n_prompt, split):
+    """Prompts of > 64 tokens without logits run as MFMA GEMMs (prefill path), split over K into
+    partial slabs when the GEMM has too few work-groups (MX_GEMM_SPLIT_TARGET, 0 = never); the next
+    decode step attends to the K/V they stored: its logits must match the oracle."""
     from llama_p2p_amd import synth
 
+    monkeypatch.setenv("MX_GEMM_SPLIT_TARGET", split)
     shape = synth.SHAPES[name]
     ids = _seq(shape, n_prompt + 1, seed=31)
     eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=1024, n_seq_max=2)
