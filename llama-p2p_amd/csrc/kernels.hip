@@ -187,7 +187,7 @@ static void launch_norm_ns(uint16_t* y, int ldy, float* x, const float* slabs, s
                            const int* row_map, int M, int n, float eps, hipStream_t s) {
   if (n == 4096)
     norm_kernel<NS, 1><<<M, 1024, 0, s>>>(y, ldy, x, slabs, stride, w, row_map, n, eps);
-  else
+  else if constexpr (NS <= 8)  // 16 slabs: n 4096 only (register budget)
     norm_kernel<NS, 2><<<M, 1024, 0, s>>>(y, ldy, x, slabs, stride, w, row_map, n, eps);
 }
 
@@ -226,8 +226,10 @@ __global__ __launch_bounds__(256) void norm_generic_kernel(uint16_t* y, int ldy,
 
 static void launch_norm_impl(uint16_t* y, int ldy, float* x, const float* slabs, int nslab, size_t stride,
                              const float* w, const int* row_map, int M, int n, float eps, hipStream_t s) {
-  if ((n == 4096 || n == 8192) && (nslab == 0 || nslab == 1 || nslab == 2 || nslab == 4 || nslab == 8)) {
+  if ((n == 4096 || n == 8192) && (nslab == 0 || nslab == 1 || nslab == 2 || nslab == 4 || nslab == 8 ||
+                                   (nslab == 16 && n == 4096))) {
     switch (nslab) {
+      case 16: launch_norm_ns<16>(y, ldy, x, slabs, stride, w, row_map, M, n, eps, s); return;
       case 8: launch_norm_ns<8>(y, ldy, x, slabs, stride, w, row_map, M, n, eps, s); return;
       case 0: launch_norm_ns<0>(y, ldy, x, slabs, stride, w, row_map, M, n, eps, s); return;
       case 1: launch_norm_ns<1>(y, ldy, x, slabs, stride, w, row_map, M, n, eps, s); return;
@@ -1407,122 +1409,22 @@ namespace mx {
 // Prefill GEMM (> 64 rows): out = X[M][K] . W[N][K]^T with the decode epilogues, bf16 MFMA
 // 16x16x32, f32 accumulation (SURVEY §8a a7, a11, a12 at prefill; §8d prefill FLOPs).  Block = 8
 // waves, tile 256 weight rows x 256 tokens; wave (wn, wm) = 64 rows (4 packed row tiles) x 128
-// tokens (8 column tiles).  Both operands staged global -> LDS by LDS-DMA (global_load_lds, 16 B per lane)
-// into two 64 KiB buffers, one 64-deep K-step ahead, raw barriers with counted vmcnt so the DMA
-// of step s+1 stays in flight while step s is multiplied (cdna_hip_programming.md §5).
+// tokens (8 column tiles).  Both operands staged global -> LDS by LDS-DMA (global_load_lds, 16 B
+// per lane) in units of one 32-deep k-tile (16 KiB of A + 16 KiB of B) through a ring of NBUF
+// buffers: NBUF-1 k-tiles in flight, one raw barrier per k-tile with a counted vmcnt (never 0
+// before the tail), and the fragments of the next k-tile read into a second register set while
+// this k-tile's MFMAs run (cdna_hip_programming.md §5 "Pipelining across barriers").  Against the
+// round-1 form (two 64 KiB buffers, one 64-deep step in flight): +2-4 % at 512-4096 rows.
 // The packed weight tiles are lane-linear 1 KiB A fragments, so a wave-instruction copies one
 // tile verbatim; token rows are gathered per lane into the same lane-linear B-fragment images
 // (lane l = token l&15, k 8(l>>4)..+8 of a 32-deep k-tile), so every ds_read_b128 is
 // conflict-free without a swizzle.  Blocks are remapped so the token blocks of one weight block
-// run on one XCD (shared L2).
+// run on one XCD (shared L2); small GEMMs split K over grid.y into partial slabs (EPI_SLAB).
 // ---------------------------------------------------------------------------
 constexpr int GB_N = 256, GB_M = 256, GKC = 64;
+constexpr int GEMM_NBUF = 4;  // k-tile buffers (5: 160 KiB, no faster; tools/gpu/r2x.sh)
 typedef __attribute__((address_space(1))) const void gvoid;
 typedef __attribute__((address_space(3))) void lvoid;
-
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm2_kernel(MMArgs a) {
-  __shared__ __attribute__((aligned(1024))) uint8_t lds[2 * 65536];
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wn = w & 3, wm = w >> 2;
-  // XCD-aware block order (bijective): blocks dispatched to one XCD get consecutive ids
-  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
-  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
-  const int nmb = (a.M + GB_M - 1) / GB_M;
-  const int mb = wgid % nmb, nb = wgid / nmb;
-  const int KT = a.K / TILE_K, NS = a.K / GKC;
-  // split-K (grid.y > 1, EPI_SLAB): this block's K-steps [s0, s1)
-  const int ks = blockIdx.y, s0 = NS * ks / gridDim.y, s1 = NS * (ks + 1) / gridDim.y;
-  const int m0 = mb * GB_M;
-  const int r16 = lane & 15;
-
-  // this thread's DMA sources: wave w copies A tiles and B tiles w*4 .. w*4+3 of each K-step
-  const uint8_t* asrc[4];
-  const uint16_t* bsrc[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int t = w * 4 + i, rt = t >> 1, kt = t & 1;
-    asrc[i] = reinterpret_cast<const uint8_t*>(a.W) + ((size_t)(nb * 16 + rt) * KT + kt) * 1024 + lane * 16;
-    const int tok = min(m0 + rt * 16 + r16, a.M - 1);  // rows past M re-read the last row (outputs dropped)
-    bsrc[i] = a.X + (size_t)tok * a.ldx + kt * 32 + 8 * (lane >> 4);
-  }
-  auto issue = [&](int st, int buf) {
-    uint8_t* base = lds + buf * 65536;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int t = w * 4 + i;
-      __builtin_amdgcn_global_load_lds((gvoid*)(asrc[i] + (size_t)st * 2048), (lvoid*)(base + t * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gvoid*)(bsrc[i] + (size_t)st * GKC), (lvoid*)(base + 32768 + t * 1024), 16, 0, 0);
-    }
-  };
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  issue(s0, 0);
-  for (int st = s0; st < s1; ++st) {
-    const int buf = (st - s0) & 1;
-    if (st + 1 < s1) {
-      issue(st + 1, buf ^ 1);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this thread's copies of step st landed
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();  // ... and every other wave's
-    asm volatile("" ::: "memory");
-    const uint8_t* Ab = lds + buf * 65536;
-    const uint8_t* Bb = Ab + 32768;
-    // all 24 fragments of the step are read up front, and iglp_opt(0) interleaves the ds_reads with
-    // the MFMAs (+3.6 % prefill over the default schedule; s_setprio(1) around the MFMAs: -12 %;
-    // tools/gpu/gemm_ab2.sh)
-    __builtin_amdgcn_iglp_opt(0);
-    u32x4 af[2][4], bf[2][8];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) af[kt][r] = *reinterpret_cast<const u32x4*>(Ab + ((wn * 4 + r) * 2 + kt) * 1024 + lane * 16);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) bf[kt][j] = *reinterpret_cast<const u32x4*>(Bb + ((wm * 8 + j) * 2 + kt) * 1024 + lane * 16);
-    }
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[kt][r]),
-                                                              __builtin_bit_cast(bf16x8, bf[kt][j]), acc[r][j], 0, 0, 0);
-
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave is done reading buf before step st+2 is copied into it
-    asm volatile("" ::: "memory");
-  }
-
-  const int tile0 = nb * (GB_N / 16) + wn * 4;
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const f32x4 sv = acc[r][j];
-      f32x4 up = sv;
-      if constexpr (EPI == EPI_SWIGLU) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(sv[i], 32);
-      }
-      const int col = m0 + wm * 128 + j * 16 + r16;
-      if (col >= a.M || (EPI == EPI_SWIGLU && lane >= 32)) continue;
-      if constexpr (EPI == EPI_SLAB) {
-        const int row = (tile0 + r) * 16 + (lane >> 4) * 4;
-        *reinterpret_cast<f32x4*>(a.out + (size_t)ks * a.slab_stride + (size_t)col * a.ldo + row) = sv;
-      } else {
-        epi_store<EPI>(a, tile0 + r, lane, col, sv, up);
-      }
-    }
-}
 
 // gate/up split-K partials -> sum in slab order -> SwiGLU -> bf16 act (the EPI_SWIGLU epilogue's
 // values: slab tile t holds gate rows 8t..8t+7 in rows 16t..16t+7 and the up rows after them)
@@ -1548,7 +1450,140 @@ __global__ __launch_bounds__(256) void swiglu_finish_kernel(MMArgs a, const floa
   }
 }
 
+template <int EPI, int NBUF>
+__global__ __launch_bounds__(512, 1) void gemm_kernel(MMArgs a) {
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[NBUF * 32768];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wn = w & 3, wm = w >> 2;
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int nmb = (a.M + GB_M - 1) / GB_M;
+  const int mb = wgid % nmb, nb = wgid / nmb;
+  const int KT = a.K / TILE_K;
+  const int ks = blockIdx.y, t0 = KT * ks / gridDim.y, t1 = KT * (ks + 1) / gridDim.y;
+  const int m0 = mb * GB_M;
+  const int r16 = lane & 15;
+
+  // wave w copies A tiles 2w, 2w+1 and B (token) tiles 2w, 2w+1 of every k-tile.  Sources as a
+  // wave-uniform base + a 32-bit per-lane offset (3 VGPRs instead of 8: the loop runs at the cap)
+  const uint8_t* abase = reinterpret_cast<const uint8_t*>(a.W) + (size_t)(nb * 16 + w * 2) * KT * 1024;
+  const size_t astep = (size_t)KT * 1024;  // next row tile
+  const uint32_t aoff = lane * 16;
+  uint32_t boff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int tok = min(m0 + (w * 2 + i) * 16 + r16, a.M - 1);
+    boff[i] = (uint32_t)tok * (uint32_t)a.ldx + 8 * (lane >> 4);
+  }
+  auto issue = [&](int kt) {
+    uint8_t* base = lds + (kt % NBUF) * 32768;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int t = w * 2 + i;
+      __builtin_amdgcn_global_load_lds((gvoid*)(abase + i * astep + (size_t)kt * 1024 + aoff), (lvoid*)(base + t * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gvoid*)(a.X + boff[i] + (size_t)kt * TILE_K), (lvoid*)(base + 16384 + t * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  struct Frags {
+    u32x4 a[4], b[8];
+  };
+  auto read = [&](Frags& f, int kt) {
+    const uint8_t* Ab = lds + (kt % NBUF) * 32768;
+    const uint8_t* Bb = Ab + 16384;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) f.a[r] = *reinterpret_cast<const u32x4*>(Ab + (wn * 4 + r) * 1024 + lane * 16);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f.b[j] = *reinterpret_cast<const u32x4*>(Bb + (wm * 8 + j) * 1024 + lane * 16);
+  };
+  auto mfma = [&](const Frags& f) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.a[r]),
+                                                            __builtin_bit_cast(bf16x8, f.b[j]), acc[r][j], 0, 0, 0);
+  };
+  // wait until this thread's copies of k-tile `kt` landed, given that k-tiles up to `issued` were issued
+  auto wait_tile = [&](int kt, int issued) {
+    const int later = min(issued, t1 - 1) - kt;
+    if (later >= 4) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (later == 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (later == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  // the fragments of k-tile kt+1 are read from LDS while k-tile kt's MFMAs run; every buffer holds
+  // one k-tile: kt+1 (being read) and kt+2 .. kt+NBUF (in flight)
+#pragma unroll
+  for (int i = 0; i < NBUF; ++i)
+    if (t0 + i < t1) issue(t0 + i);
+  Frags F0, F1;
+  wait_tile(t0, t0 + NBUF - 1);
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  read(F0, t0);
+  auto step = [&](Frags& cur, Frags& nxt, int kt) {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of kt landed (the compiler sees it)
+    if (kt + 1 < t1) {
+      wait_tile(kt + 1, kt + NBUF - 1);
+      __builtin_amdgcn_s_barrier();  // kt+1 landed for every wave; nobody reads buffer kt any more
+      asm volatile("" ::: "memory");
+      if (kt + NBUF < t1) issue(kt + NBUF);  // into buffer kt
+    }
+    // unconditional (the last k-tile re-reads its own buffer, unused): a branch here would join
+    // the paths between these reads and the MFMAs, and the join waits for the reads
+    read(nxt, min(kt + 1, t1 - 1));
+    mfma(cur);
+    // the 12 reads first, then the 32 MFMAs (the default schedule issued the reads behind 24 MFMAs)
+    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);
+  };
+  int kt = t0;
+  for (; kt + 1 < t1; kt += 2) {
+    step(F0, F1, kt);
+    step(F1, F0, kt + 1);
+  }
+  if (kt < t1) step(F0, F1, kt);
+
+  const int tile0 = nb * (GB_N / 16) + wn * 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 sv = acc[r][j];
+      f32x4 up = sv;
+      if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(sv[i], 32);
+      }
+      const int col = m0 + wm * 128 + j * 16 + r16;
+      if (col >= a.M || (EPI == EPI_SWIGLU && lane >= 32)) continue;
+      if constexpr (EPI == EPI_SLAB) {
+        const int row = (tile0 + r) * 16 + (lane >> 4) * 4;
+        *reinterpret_cast<f32x4*>(a.out + (size_t)ks * a.slab_stride + (size_t)col * a.ldo + row) = sv;
+      } else {
+        epi_store<EPI>(a, tile0 + r, lane, col, sv, up);
+      }
+    }
+}
+
 bool gemm_supported(int N, int K) { return N % GB_N == 0 && K % GKC == 0; }
+
+template <int EPI>
+static void launch_gemm_v(const MMArgs& a, dim3 grid, hipStream_t s) {
+  gemm_kernel<EPI, GEMM_NBUF><<<grid, 512, 0, s>>>(a);
+}
 
 // K split that brings a small-M GEMM to ~target work-groups (at M <= 256 a Llama-3-8B
 // GEMM has 16..112 of them, one per 256 weight rows: most CUs idle), bounded by the slab space
@@ -1556,10 +1591,11 @@ bool gemm_supported(int N, int K) { return N % GB_N == 0 && K % GKC == 0; }
 static int gemm_split(const MMArgs& a, size_t slab_floats, int target) {
   const int base = (a.N / GB_N) * ((a.M + GB_M - 1) / GB_M);
   const int NS = a.K / GKC;
-  int S = (target + base / 2) / base;
-  S = std::min(S, std::min(16, NS / 4));
-  while (S > 1 && (size_t)S * a.M * a.N > slab_floats) S--;
-  return std::max(S, 1);
+  // a power of two (the resid_norm that folds RESID partials has 1024-thread forms for 2..16)
+  int S = 1;
+  while (S < 16 && 2 * S * base <= target + base / 2 && 2 * S * 4 <= NS && (size_t)2 * S * a.M * a.N <= slab_floats)
+    S *= 2;
+  return S;
 }
 
 int launch_gemm_split(int epi, const MMArgs& a, float* slabs, size_t slab_floats, int target, hipStream_t s) {
@@ -1571,7 +1607,7 @@ int launch_gemm_split(int epi, const MMArgs& a, float* slabs, size_t slab_floats
   p.ldo = a.N;
   p.slab_stride = (size_t)a.M * a.N;
   dim3 grid((a.N / GB_N) * ((a.M + GB_M - 1) / GB_M), S);
-  gemm2_kernel<EPI_SLAB><<<grid, 512, 0, s>>>(p);
+  launch_gemm_v<EPI_SLAB>(p, grid, s);
   const int total = epi == EPI_SWIGLU ? a.M * a.N / 8 : a.M * a.N / 4;
   const int blocks = std::min((total + 255) / 256, 2048);
   if (epi == EPI_QKV) qkv_finish_kernel<<<blocks, 256, 0, s>>>(a, slabs, S, p.slab_stride);
@@ -1583,10 +1619,10 @@ int launch_gemm(int epi, const MMArgs& a, hipStream_t s) {
   if (a.M < 1 || !a.X || !gemm_supported(a.N, a.K)) return -1;
   const int grid = (a.N / GB_N) * ((a.M + GB_M - 1) / GB_M);
   switch (epi) {
-    case EPI_F32: gemm2_kernel<EPI_F32><<<grid, 512, 0, s>>>(a); return 0;
-    case EPI_RESID: gemm2_kernel<EPI_RESID><<<grid, 512, 0, s>>>(a); return 0;
-    case EPI_QKV: gemm2_kernel<EPI_QKV><<<grid, 512, 0, s>>>(a); return 0;
-    case EPI_SWIGLU: gemm2_kernel<EPI_SWIGLU><<<grid, 512, 0, s>>>(a); return 0;
+    case EPI_F32: launch_gemm_v<EPI_F32>(a, grid, s); return 0;
+    case EPI_RESID: launch_gemm_v<EPI_RESID>(a, grid, s); return 0;
+    case EPI_QKV: launch_gemm_v<EPI_QKV>(a, grid, s); return 0;
+    case EPI_SWIGLU: launch_gemm_v<EPI_SWIGLU>(a, grid, s); return 0;
   }
   return -1;
 }
