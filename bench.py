@@ -246,9 +246,12 @@ def quant_bench(args, wtype: str, steps: int):
             kb = wbytes + m * h + m * h // 8 + m * shape.n_ff * 4   # int8 rows + scales in, f32 act out
         else:
             kb = wbytes + m * h + m * h // 64 + m * h // 8 + m * shape.n_ff * 4  # Q8_K rows, d, sub-block sums
-        out[f"gate_up_M{m}"] = {"kernel": {"q8_0": "mq8_kernel", "q4_k_m": "mkq_kernel"}[wtype] + "<EPI_SWIGLU>",
+        kname = {"q8_0": "mq8_kernel", "q4_k_m": "mkq_pers_kernel" if m <= 16 else "mkq_kernel"}[wtype]
+        out[f"gate_up_M{m}"] = {"kernel": kname + "<EPI_SWIGLU>",
                                 "us_per_launch": round(us, 2), "bytes_per_launch": int(kb),
                                 "achieved_gbs": round(kb / us / 1e3, 1), "frac": round(kb / us / 1e3 / HBM_PEAK_GBS, 4)}
+    if wtype == "q4_k_m" and args.prefill_prompts > 0:  # > 64-row chunks: dequantised bf16 GEMMs
+        out["prefill"] = prefill_bench(eng, shape, args.prefill_prompts, args.prefill_len)
     eng.close()
     return out
 
@@ -367,7 +370,7 @@ def prefill_bench(eng, shape, n_prompts: int, plen: int):
         slots += [i] * plen
         pos += list(range(plen))
         ids += [1] + [int(t) for t in rng.integers(3, shape.n_vocab, plen - 1)]
-    eng.forward_rows(slots[:64], pos[:64], ids[:64], want_logits=False)  # warm
+    eng.forward_rows(slots[:2 * plen], pos[:2 * plen], ids[:2 * plen], want_logits=False)  # warm (GEMM path)
     eng.sync()
     t0 = time.perf_counter()
     eng.forward_rows(slots, pos, ids, want_logits=False)

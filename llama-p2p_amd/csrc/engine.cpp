@@ -203,6 +203,8 @@ struct mx_engine {
   float* slabs = nullptr;                           // split-K partials [8][MAX_ROWS][n_embd + 2 n_embd_kv]
   size_t slab_stride = 0;
   float* gslabs = nullptr;  // split-K partials of small-M prefill GEMMs, [S][M][N] (launch_gemm_split)
+  // K-quant model prefill: one layer's four matrices dequantised to packed bf16 for the GEMM path
+  uint16_t *kqd_qkv = nullptr, *kqd_o = nullptr, *kqd_gu = nullptr, *kqd_down = nullptr;
   static constexpr size_t GSLAB_FLOATS = (size_t)32 << 20;
   // work-groups a split prefill GEMM aims at (MX_GEMM_SPLIT_TARGET; 0 = one K range per tile)
   int gemm_split_target = getenv("MX_GEMM_SPLIT_TARGET") ? atoi(getenv("MX_GEMM_SPLIT_TARGET")) : 256;
@@ -287,10 +289,12 @@ struct mx_engine {
                          int max_hist, hipStream_t s);
   int enqueue_forward_gemm(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap,
                            int n_out, hipStream_t s);
-  bool gemm_ok() const {  // chunks of PREFILL_ROWS rows can run (the Q8_0 path takes any row count)
-    if (wq8 || wkq) return true;
+  bool gemm_shapes() const {  // the bf16 prefill GEMM takes every matrix of a layer
     return gemm_supported(n_embd + 2 * n_embd_kv, n_embd) && gemm_supported(n_embd, n_embd) &&
            gemm_supported(2 * n_ff, n_embd) && gemm_supported(n_embd, n_ff);
+  }
+  bool gemm_ok() const {  // chunks of PREFILL_ROWS rows can run (the Q8_0 / K-quant paths take any row count)
+    return wq8 || wkq || gemm_shapes();
   }
   int enqueue_forward_wide(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap,
                            int n_out, bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride,
@@ -380,8 +384,15 @@ int mx_engine::init_common() {
   }
   slab_stride = (size_t)MAX_ROWS * (n_embd + 2 * n_embd_kv);
   if (int rc = alloc((void**)&slabs, slab_stride * 8 * 4)) return rc;
-  if (!wq8 && !wkq)
+  if (!wq8 && gemm_shapes())
     if (int rc = alloc((void**)&gslabs, GSLAB_FLOATS * 4)) return rc;
+  if (wkq && gemm_shapes()) {
+    const size_t h = n_embd, kv = n_embd_kv, ff = n_ff;
+    if (int rc = alloc((void**)&kqd_qkv, (h + 2 * kv) * h * 2)) return rc;
+    if (int rc = alloc((void**)&kqd_o, h * h * 2)) return rc;
+    if (int rc = alloc((void**)&kqd_gu, 2 * ff * h * 2)) return rc;
+    if (int rc = alloc((void**)&kqd_down, h * ff * 2)) return rc;
+  }
   if (int rc = alloc((void**)&ssq, (size_t)R * (n_embd / 16) * 4)) return rc;
   if (int rc = alloc((void**)&am_val, (size_t)R * 64 * 4)) return rc;
   if (has_head) {
@@ -881,6 +892,8 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
       launch_embed(x, tok_embd, ids, M, h, (nol || qql) ? ssq : nullptr, s);
     }
   }
+  if (wkq && M > MAX_ROWS && kqd_qkv && !argmax && !(head && n_out > MAX_ROWS))
+    return enqueue_forward_gemm(M, pos, slot, x_out, head, rowmap, n_out, s);  // dequantised bf16 GEMMs
   if (wkq) return enqueue_forward_kq(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next, pos_next, hist,
                                      hist_stride, hist_count, max_hist, s);
   if (wq8) return enqueue_forward_q8(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next, pos_next, hist,
@@ -1178,19 +1191,32 @@ int mx_engine::enqueue_forward_kq(int M, const int* pos, const int* slot, void* 
 }
 
 // Prefill chunk of MAX_ROWS < M <= PREFILL_ROWS rows: MFMA GEMMs read each weight once per 256
-// rows (not once per 64 as the wide decode kernels would); RMS_NORM as its own launch.
+// rows (not once per 64 as the wide decode kernels would); RMS_NORM as its own launch.  A K-quant
+// model's layer is first dequantised to bf16 tiles (launch_dequant_kq: ~0.6 GB of HBM traffic per
+// Llama-3-8B layer, a few % of a 4096-row chunk's GEMM time) -- the route llama.cpp's GPU backends
+// take for large batches; decode keeps the int8-MFMA K-quant GEMVs with Q8_K activations.
 int mx_engine::enqueue_forward_gemm(int M, const int* pos, const int* slot, void* x_out, bool head,
                                     const int* rowmap, int n_out, hipStream_t s) {
   const int h = n_embd, kv = n_embd_kv, ff = n_ff;
   const size_t gstride = (size_t)M * h;  // RESID partial slabs [S][M][h]
   int nslab = 0;                         // ... not yet folded into x
+  auto dequant = [&](uint16_t* dst, const KqMat& km, const uint16_t* w, int K) -> int {
+    return launch_dequant_kq(dst, w, K, km.n, km.type, km.tile_end, km.off, s);
+  };
   for (int li = 0; li < (int)layers.size(); li++) {
     const Layer& L = layers[li];
     _Float16* kc = kcache + layer_kv_stride * li;
     _Float16* vc = vcache + layer_kv_stride * li;
+    const uint16_t *Wqkv = L.qkv, *Wo = L.o, *Wgu = L.gu, *Wdown = L.down;
+    if (wkq) {
+      if (dequant(kqd_qkv, L.kq_qkv, L.qkv, h) || dequant(kqd_o, L.kq_o, L.o, h) || dequant(kqd_gu, L.kq_gu, L.gu, h) ||
+          dequant(kqd_down, L.kq_down, L.down, ff))
+        return fail(MX_ERR_ARG, "K-quant dequantisation shape");
+      Wqkv = kqd_qkv, Wo = kqd_o, Wgu = kqd_gu, Wdown = kqd_down;
+    }
     launch_resid_norm(xn, h, x, gslabs, nslab, gstride, L.attn_norm, M, h, eps, s);
     MMArgs a{};
-    a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M; a.X = xn; a.ldx = h;
+    a.W = Wqkv; a.N = h + 2 * kv; a.K = h; a.M = M; a.X = xn; a.ldx = h;
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
     a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
     a.slot_stride = slot_stride;
@@ -1203,16 +1229,16 @@ int mx_engine::enqueue_forward_gemm(int M, const int* pos, const int* slot, void
     if (rows_blocked) launch_attention_prefill(at, s);
     else launch_attention(at, s);
     MMArgs b{};
-    b.W = L.o; b.N = h; b.K = h; b.X = attn_out; b.ldx = h; b.M = M; b.out = x; b.ldo = h;
+    b.W = Wo; b.N = h; b.K = h; b.X = attn_out; b.ldx = h; b.M = M; b.out = x; b.ldo = h;
     if ((nslab = launch_gemm_split(EPI_RESID, b, gslabs, GSLAB_FLOATS, gemm_split_target, s)) < 0)
       return fail(MX_ERR_ARG, "prefill attn_output GEMM shape");
     launch_resid_norm(xn, h, x, gslabs, nslab, gstride, L.ffn_norm, M, h, eps, s);
     MMArgs c{};
-    c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.X = xn; c.ldx = h; c.act = act; c.lda = ff;
+    c.W = Wgu; c.N = 2 * ff; c.K = h; c.M = M; c.X = xn; c.ldx = h; c.act = act; c.lda = ff;
     if (launch_gemm_split(EPI_SWIGLU, c, gslabs, GSLAB_FLOATS, gemm_split_target, s) < 0)
       return fail(MX_ERR_ARG, "prefill gate/up GEMM shape");
     MMArgs d{};
-    d.W = L.down; d.N = h; d.K = ff; d.X = act; d.ldx = ff; d.M = M; d.out = x; d.ldo = h;
+    d.W = Wdown; d.N = h; d.K = ff; d.X = act; d.ldx = ff; d.M = M; d.out = x; d.ldo = h;
     if ((nslab = launch_gemm_split(EPI_RESID, d, gslabs, GSLAB_FLOATS, gemm_split_target, s)) < 0)
       return fail(MX_ERR_ARG, "prefill ffn_down GEMM shape");
   }
@@ -1221,10 +1247,18 @@ int mx_engine::enqueue_forward_gemm(int M, const int* pos, const int* slot, void
   if (head) {
     if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
     if (!rowmap) return fail(MX_ERR_ARG, "prefill head needs a row map");
-    launch_rmsnorm(xn, h, x, out_norm, rowmap, n_out, h, eps, s);
     MMArgs g{};
-    g.W = output; g.N = n_vocab; g.K = h; g.M = n_out; g.X = xn; g.ldx = h; g.out = logits; g.ldo = n_vocab;
-    if (launch_mm(EPI_F32, g, s)) return fail(MX_ERR_ARG, "lm_head launch shape");
+    g.W = output; g.N = n_vocab; g.K = h; g.M = n_out; g.out = logits; g.ldo = n_vocab;
+    if (wkq) {  // the K-quant head as at decode: Q8_K rows of the normed last rows
+      kq_out.set(g);
+      if (launch_rmsnorm_q8k(xq8, xqd, xkb, x, out_norm, rowmap, n_out, h, eps, s)) return fail(MX_ERR_ARG, "kq norm");
+      g.xq = xq8; g.xd = xqd; g.xb = xkb;
+      if (launch_mkq(EPI_F32, g, s)) return fail(MX_ERR_ARG, "kq lm_head launch shape");
+    } else {
+      launch_rmsnorm(xn, h, x, out_norm, rowmap, n_out, h, eps, s);
+      g.X = xn; g.ldx = h;
+      if (launch_mm(EPI_F32, g, s)) return fail(MX_ERR_ARG, "lm_head launch shape");
+    }
   }
   HIPC(hipGetLastError());
   return 0;

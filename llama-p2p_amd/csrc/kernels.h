@@ -192,6 +192,9 @@ int launch_rmsnorm_q8k(int8_t* xq, float* xd, float* xb, const float* x, const f
 int launch_quantize_q8k(int8_t* xq, float* xd, float* xb, const float* src, int ld, int M, int n, hipStream_t s);
 // K-quant x Q8_K products for any M (grid.y: groups of 32 tokens), the usual epilogues (SWIGLU: actf)
 int launch_mkq(int epi, const MMArgs& a, hipStream_t s);
+// packed K-quant matrix (segments as in MMArgs) -> packed bf16 tiles [N/16][K/32] x 1 KiB (prefill GEMM)
+int launch_dequant_kq(uint16_t* dst, const void* W, int K, int kq_n, const int* type, const int* tile_end,
+                      const size_t* off, hipStream_t s);
 
 // top-k (k <= TOPK_MAX) candidates per logits row, value descending, ties by lower id; ws: M*64*k
 constexpr int TOPK_MAX = 64;

@@ -329,6 +329,85 @@ int launch_quantize_q8k(int8_t* xq, float* xd, float* xb, const float* src, int 
 }
 
 // ---------------------------------------------------------------------------
+// Dequantisation of packed K-quant tiles into packed bf16 tiles (kernels.h layout: 16 rows x 32 k
+// per 1 KiB lane-linear A fragment) for the prefill GEMM.  ggml's dequantize_row_q{4,5,6}_K values
+// in f32 (Q4_K/Q5_K: (d*sc)*q - dmin*m; Q6_K: (d*sc)*(q-32)), rounded to bf16 like the bf16 path's
+// weights.  One wave per (16-row tile, super-block): lane l holds row l&15, k 8(l>>4)..+8 of each
+// 32-k sub-block j -- the i8 MFMA A-operand bytes of kq_compute, which are also the bf16 A layout.
+// ---------------------------------------------------------------------------
+template <int T>
+__global__ __launch_bounds__(256) void dequant_kq_kernel(uint16_t* dst, const uint8_t* src, int tile_begin, int ntiles,
+                                                         int SB) {
+  constexpr int TB = KqTile<T>::BYTES, SC = KqTile<T>::SC;
+  const int lane = threadIdx.x & 63;
+  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);  // (tile in segment, super-block)
+  if (unit >= ntiles * SB) return;
+  const int tile = unit / SB, sb = unit % SB;
+  const uint8_t* t = src + (size_t)unit * TB;  // tiles are [tile][super-block] in the segment
+  const int r = lane & 15, g = lane >> 4;
+  const u32x4 q0 = *reinterpret_cast<const u32x4*>(t + 16 * lane);
+  const u32x4 q1 = *reinterpret_cast<const u32x4*>(t + 1024 + 16 * lane);
+  const uint32_t D[8] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3]};
+  u32x4 H = u32x4{0u, 0u, 0u, 0u};
+  if constexpr (T == 13) {
+    const u32x2 hv = *reinterpret_cast<const u32x2*>(t + 2048 + 8 * lane);
+    H = u32x4{hv[0], hv[1], 0u, 0u};
+  }
+  if constexpr (T == 14) H = *reinterpret_cast<const u32x4*>(t + 2048 + 16 * lane);
+  const int KT = SB * 8;
+  uint16_t* out = dst + ((size_t)(tile_begin + tile) * KT + 8 * sb) * 512 + 8 * lane;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t lo = D[j] & 0x0F0F0F0Fu, hi = (D[j] >> 4) & 0x0F0F0F0Fu;
+    if constexpr (T == 13) {
+      lo |= ((H[j >> 2] >> ((2 * j) & 7)) & 0x01010101u) << 4;
+      hi |= ((H[j >> 2] >> ((2 * j + 1) & 7)) & 0x01010101u) << 4;
+    }
+    if constexpr (T == 14) {
+      lo |= ((H[j >> 1] >> (4 * (j & 1))) & 0x03030303u) << 4;
+      hi |= ((H[j >> 1] >> (4 * (j & 1) + 2)) & 0x03030303u) << 4;
+    }
+    float y[8];
+    if constexpr (T == 14) {
+      const float d = f16b(t + SC + 256 + 2 * r);
+      const int sc = (int)(int8_t)t[SC + 16 * r + 2 * j + (g >> 1)];
+      const float ds = d * (float)sc;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) y[e] = ds * (float)((int)(((e < 4 ? lo : hi) >> (8 * (e & 3))) & 0xFFu) - 32);
+    } else {
+      const float d = f16b(t + SC + 256 + 4 * r);
+      const float dmin = f16b(t + SC + 256 + 4 * r + 2);
+      const float d1 = d * (float)t[SC + 32 * (r >> 2) + 8 * (r & 3) + j];
+      const float m1 = dmin * (float)t[SC + 128 + 8 * r + j];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) y[e] = d1 * (float)((((e < 4 ? lo : hi) >> (8 * (e & 3))) & 0xFFu)) - m1;
+    }
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = f2bf(y[2 * e]) | (f2bf(y[2 * e + 1]) << 16);
+    *reinterpret_cast<u32x4*>(out + (size_t)j * 512) = o;
+  }
+}
+
+int launch_dequant_kq(uint16_t* dst, const void* W, int K, int kq_n, const int* type, const int* tile_end,
+                      const size_t* off, hipStream_t s) {
+  if (K % 256 || kq_n < 1 || kq_n > 3) return -1;
+  const int SB = K / 256;
+  for (int i = 0; i < kq_n; ++i) {
+    const int t0 = i ? tile_end[i - 1] : 0, nt = tile_end[i] - t0;
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(W) + off[i];
+    const int blocks = (nt * SB + 3) / 4;
+    switch (type[i]) {
+      case 12: dequant_kq_kernel<12><<<blocks, 256, 0, s>>>(dst, src, t0, nt, SB); break;
+      case 13: dequant_kq_kernel<13><<<blocks, 256, 0, s>>>(dst, src, t0, nt, SB); break;
+      case 14: dequant_kq_kernel<14><<<blocks, 256, 0, s>>>(dst, src, t0, nt, SB); break;
+      default: return -1;
+    }
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
 // K-quant x Q8_K MUL_MAT.  Work-group = RT row tiles of one segment (one ggml type) x NB column
 // tiles of 16 tokens (grid.y: groups of 16*NB tokens); its KS waves split the K/256 super-blocks,
 // each keeping a ring of U super-blocks' loads in flight; partial tiles are summed through LDS and
@@ -346,10 +425,142 @@ struct KqFrag {
   f32x2 xb[NB];
 };
 
+// One super-block of RT weight tiles (Wt[r] = tile r's bytes at this super-block) and NB column
+// tiles of Q8_K activations (Xq/Xd/Xb at this lane's column, Xq/Xb offset by its k group)
+template <int T, int RT, int NB>
+__device__ __forceinline__ void kq_load(KqFrag<RT, NB>& f, const uint8_t* const (&Wt)[RT], const int8_t* const (&Xq)[NB],
+                                        const float* const (&Xd)[NB], const float* const (&Xb)[NB], int sb, int lane,
+                                        int g) {
+  constexpr int SC = KqTile<T>::SC;
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    const uint8_t* t = Wt[r];
+    f.qs[r][0] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t) + lane);
+    f.qs[r][1] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t + 1024) + lane);
+    if constexpr (T == 13) {
+      const u32x2 hv = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(t + 2048) + lane);
+      f.h[r] = u32x4{hv[0], hv[1], 0u, 0u};
+    }
+    if constexpr (T == 14) f.h[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t + 2048) + lane);
+    if constexpr (T == 14) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) f.sc[r][c] = *reinterpret_cast<const u32x4*>(t + SC + 64 * g + 16 * c);
+      const u32x2 dv = *reinterpret_cast<const u32x2*>(t + SC + 256 + 8 * g);
+      f.dm[r] = u32x4{dv[0], dv[1], 0u, 0u};
+    } else {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) f.sc[r][c] = *reinterpret_cast<const u32x4*>(t + SC + 32 * g + 16 * c);
+      const u32x2 mw = *reinterpret_cast<const u32x2*>(t + SC + 128 + 8 * (lane & 15));
+      f.mn[r] = ((mw[0] >> (8 * g)) & 0xFFu) | (((mw[1] >> (8 * g)) & 0xFFu) << 8);  // mins g, g + 4
+      f.dm[r] = *reinterpret_cast<const u32x4*>(t + SC + 256 + 16 * g);
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) f.x[n][c] = *reinterpret_cast<const u32x4*>(Xq[n] + (size_t)sb * 256 + 16 * c);
+    f.dx[n] = Xd[n][sb];
+    if constexpr (T != 14) f.xb[n] = *reinterpret_cast<const f32x2*>(Xb[n] + 8 * sb);
+  }
+}
+
+// the super-block's contribution to acc (int8 MFMA per 32-k sub-block, f32 scales as ggml)
+template <int T, int RT, int NB>
+__device__ __forceinline__ void kq_compute(f32x4 (&acc)[RT][NB], const KqFrag<RT, NB>& f, int g) {
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    uint32_t D[8];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      D[c] = f.qs[r][0][c];
+      D[4 + c] = f.qs[r][1][c];
+    }
+    uint32_t scw[16];
+#pragma unroll
+    for (int c = 0; c < (T == 14 ? 4 : 2); ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) scw[4 * c + e] = f.sc[r][c][e];
+    // sub-block by sub-block: unpack its A operand and scales once, then one MFMA (Q6_K: two)
+    // per column tile into that tile's int32 super-block sums
+    i32x4 S[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) S[n] = i32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint32_t lo = D[j] & 0x0F0F0F0Fu, hi = (D[j] >> 4) & 0x0F0F0F0Fu;
+      if constexpr (T == 13) {
+        const uint32_t H = f.h[r][j >> 2];
+        lo |= ((H >> ((2 * j) & 7)) & 0x01010101u) << 4;
+        hi |= ((H >> ((2 * j + 1) & 7)) & 0x01010101u) << 4;
+      }
+      if constexpr (T == 14) {
+        const uint32_t H = f.h[r][j >> 1];
+        lo |= ((H >> (4 * (j & 1))) & 0x03030303u) << 4;
+        hi |= ((H >> (4 * (j & 1) + 2)) & 0x03030303u) << 4;
+        lo = ((lo | 0x80808080u) - 0x20202020u) ^ 0x80808080u;  // bytewise q - 32
+        hi = ((hi | 0x80808080u) - 0x20202020u) ^ 0x80808080u;
+      }
+      const long A = (long)(((unsigned long)hi << 32) | lo);
+      if constexpr (T == 14) {
+        // int8 scales of row 4g+i, groups 2j and 2j+1: bytes 16i + 2j, +1 of the row group's 64
+        int s0[4], s1[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t sw = scw[4 * i + (j >> 1)];
+          s0[i] = (int)(int8_t)(sw >> (16 * (j & 1)));
+          s1[i] = (int)(int8_t)(sw >> (16 * (j & 1) + 8));
+        }
+        const long A0 = g < 2 ? A : 0l, A1 = g < 2 ? 0l : A;
+#pragma unroll
+        for (int n = 0; n < NB; ++n) {
+          const u32x4& xc = f.x[n][j >> 1];
+          const long B = (long)(((unsigned long)xc[2 * (j & 1) + 1] << 32) | xc[2 * (j & 1)]);
+          const i32x4 P0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(A0, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+          const i32x4 P1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(A1, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) S[n][i] += __mul24(s0[i], P0[i]) + __mul24(s1[i], P1[i]);  // |P| < 2^17
+        }
+      } else {
+        int sc[4];  // 6-bit scales of row 4g+i, sub-block j: byte 8i + j of the row group's 32
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sc[i] = (int)((scw[2 * i + (j >> 2)] >> (8 * (j & 3))) & 0xFFu);
+#pragma unroll
+        for (int n = 0; n < NB; ++n) {
+          const u32x4& xc = f.x[n][j >> 1];
+          const long B = (long)(((unsigned long)xc[2 * (j & 1) + 1] << 32) | xc[2 * (j & 1)]);
+          const i32x4 P = __builtin_amdgcn_mfma_i32_16x16x32_i8(A, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) S[n][i] += __mul24(sc[i], P[i]);
+        }
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const float dx = f.dx[n];
+      if constexpr (T == 14) {
+        const f16x4 d4 = __builtin_bit_cast(f16x4, u32x2{f.dm[r][0], f.dm[r][1]});
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[r][n][i] += ((float)d4[i] * dx) * (float)S[n][i];
+      } else {
+        // mins: sum_j m[row][j] * bsum32[j][col] on the f32 MFMA (k = sub-block g, then g + 4)
+        const float m0 = (float)(f.mn[r] & 0xFFu), m1 = (float)((f.mn[r] >> 8) & 0xFFu);
+        f32x4 Mn = __builtin_amdgcn_mfma_f32_16x16x4f32(m0, f.xb[n][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        Mn = __builtin_amdgcn_mfma_f32_16x16x4f32(m1, f.xb[n][1], Mn, 0, 0, 0);
+        const f16x8 dm = __builtin_bit_cast(f16x8, f.dm[r]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[r][n][i] += ((float)dm[2 * i] * dx) * (float)S[n][i];
+          acc[r][n][i] -= ((float)dm[2 * i + 1] * dx) * Mn[i];
+        }
+      }
+    }
+  }
+}
+
 template <int T, int KS, int RT, int NB, int EPI, int U>
 __device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int tile_in_seg, int tile0,
                                          f32x4 (*red)[RT][NB][64]) {
-  constexpr int TB = KqTile<T>::BYTES, SC = KqTile<T>::SC;
+  constexpr int TB = KqTile<T>::BYTES;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int g = lane >> 4;
@@ -380,127 +591,12 @@ __device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int 
 
   using Frag = KqFrag<RT, NB>;
   auto load = [&](Frag& f, int sb) {
+    const uint8_t* Wt[RT];
 #pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      const uint8_t* t = Wr[r] + (size_t)sb * TB;
-      f.qs[r][0] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t) + lane);
-      f.qs[r][1] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t + 1024) + lane);
-      if constexpr (T == 13) {
-        const u32x2 hv = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(t + 2048) + lane);
-        f.h[r] = u32x4{hv[0], hv[1], 0u, 0u};
-      }
-      if constexpr (T == 14) f.h[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t + 2048) + lane);
-      if constexpr (T == 14) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) f.sc[r][c] = *reinterpret_cast<const u32x4*>(t + SC + 64 * g + 16 * c);
-        const u32x2 dv = *reinterpret_cast<const u32x2*>(t + SC + 256 + 8 * g);
-        f.dm[r] = u32x4{dv[0], dv[1], 0u, 0u};
-      } else {
-#pragma unroll
-        for (int c = 0; c < 2; ++c) f.sc[r][c] = *reinterpret_cast<const u32x4*>(t + SC + 32 * g + 16 * c);
-        const u32x2 mw = *reinterpret_cast<const u32x2*>(t + SC + 128 + 8 * (lane & 15));
-        f.mn[r] = ((mw[0] >> (8 * g)) & 0xFFu) | (((mw[1] >> (8 * g)) & 0xFFu) << 8);  // mins g, g + 4
-        f.dm[r] = *reinterpret_cast<const u32x4*>(t + SC + 256 + 16 * g);
-      }
-    }
-#pragma unroll
-    for (int n = 0; n < NB; ++n) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) f.x[n][c] = *reinterpret_cast<const u32x4*>(Xq[n] + (size_t)sb * 256 + 16 * c);
-      f.dx[n] = Xd[n][sb];
-      if constexpr (T != 14) f.xb[n] = *reinterpret_cast<const f32x2*>(Xb[n] + 8 * sb);
-    }
+    for (int r = 0; r < RT; ++r) Wt[r] = Wr[r] + (size_t)sb * TB;
+    kq_load<T, RT, NB>(f, Wt, Xq, Xd, Xb, sb, lane, g);
   };
-  auto compute = [&](const Frag& f) {
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      uint32_t D[8];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        D[c] = f.qs[r][0][c];
-        D[4 + c] = f.qs[r][1][c];
-      }
-      uint32_t scw[16];
-#pragma unroll
-      for (int c = 0; c < (T == 14 ? 4 : 2); ++c)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) scw[4 * c + e] = f.sc[r][c][e];
-      // sub-block by sub-block: unpack its A operand and scales once, then one MFMA (Q6_K: two)
-      // per column tile into that tile's int32 super-block sums
-      i32x4 S[NB];
-#pragma unroll
-      for (int n = 0; n < NB; ++n) S[n] = i32x4{0, 0, 0, 0};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        uint32_t lo = D[j] & 0x0F0F0F0Fu, hi = (D[j] >> 4) & 0x0F0F0F0Fu;
-        if constexpr (T == 13) {
-          const uint32_t H = f.h[r][j >> 2];
-          lo |= ((H >> ((2 * j) & 7)) & 0x01010101u) << 4;
-          hi |= ((H >> ((2 * j + 1) & 7)) & 0x01010101u) << 4;
-        }
-        if constexpr (T == 14) {
-          const uint32_t H = f.h[r][j >> 1];
-          lo |= ((H >> (4 * (j & 1))) & 0x03030303u) << 4;
-          hi |= ((H >> (4 * (j & 1) + 2)) & 0x03030303u) << 4;
-          lo = ((lo | 0x80808080u) - 0x20202020u) ^ 0x80808080u;  // bytewise q - 32
-          hi = ((hi | 0x80808080u) - 0x20202020u) ^ 0x80808080u;
-        }
-        const long A = (long)(((unsigned long)hi << 32) | lo);
-        if constexpr (T == 14) {
-          // int8 scales of row 4g+i, groups 2j and 2j+1: bytes 16i + 2j, +1 of the row group's 64
-          int s0[4], s1[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t sw = scw[4 * i + (j >> 1)];
-            s0[i] = (int)(int8_t)(sw >> (16 * (j & 1)));
-            s1[i] = (int)(int8_t)(sw >> (16 * (j & 1) + 8));
-          }
-          const long A0 = g < 2 ? A : 0l, A1 = g < 2 ? 0l : A;
-#pragma unroll
-          for (int n = 0; n < NB; ++n) {
-            const u32x4& xc = f.x[n][j >> 1];
-            const long B = (long)(((unsigned long)xc[2 * (j & 1) + 1] << 32) | xc[2 * (j & 1)]);
-            const i32x4 P0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(A0, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
-            const i32x4 P1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(A1, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) S[n][i] += __mul24(s0[i], P0[i]) + __mul24(s1[i], P1[i]);  // |P| < 2^17
-          }
-        } else {
-          int sc[4];  // 6-bit scales of row 4g+i, sub-block j: byte 8i + j of the row group's 32
-#pragma unroll
-          for (int i = 0; i < 4; ++i) sc[i] = (int)((scw[2 * i + (j >> 2)] >> (8 * (j & 3))) & 0xFFu);
-#pragma unroll
-          for (int n = 0; n < NB; ++n) {
-            const u32x4& xc = f.x[n][j >> 1];
-            const long B = (long)(((unsigned long)xc[2 * (j & 1) + 1] << 32) | xc[2 * (j & 1)]);
-            const i32x4 P = __builtin_amdgcn_mfma_i32_16x16x32_i8(A, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) S[n][i] += __mul24(sc[i], P[i]);
-          }
-        }
-      }
-#pragma unroll
-      for (int n = 0; n < NB; ++n) {
-        const float dx = f.dx[n];
-        if constexpr (T == 14) {
-          const f16x4 d4 = __builtin_bit_cast(f16x4, u32x2{f.dm[r][0], f.dm[r][1]});
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[r][n][i] += ((float)d4[i] * dx) * (float)S[n][i];
-        } else {
-          // mins: sum_j m[row][j] * bsum32[j][col] on the f32 MFMA (k = sub-block g, then g + 4)
-          const float m0 = (float)(f.mn[r] & 0xFFu), m1 = (float)((f.mn[r] >> 8) & 0xFFu);
-          f32x4 Mn = __builtin_amdgcn_mfma_f32_16x16x4f32(m0, f.xb[n][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          Mn = __builtin_amdgcn_mfma_f32_16x16x4f32(m1, f.xb[n][1], Mn, 0, 0, 0);
-          const f16x8 dm = __builtin_bit_cast(f16x8, f.dm[r]);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            acc[r][n][i] += ((float)dm[2 * i] * dx) * (float)S[n][i];
-            acc[r][n][i] -= ((float)dm[2 * i + 1] * dx) * Mn[i];
-          }
-        }
-      }
-    }
-  };
+  auto compute = [&](const Frag& f) { kq_compute<T, RT, NB>(acc, f, g); };
 
   Frag ring[U];
   int sb = kb;
@@ -568,6 +664,135 @@ __global__ __launch_bounds__(64 * KS) void mkq_kernel(MMArgs a) {
   }
 }
 
+// Tile-persistent form for <= 16 tokens and a single-type matrix (gate/up, attn_output, ffn_down,
+// lm_head of a K-quant file): mkq_kernel gives each work-group one 16-row tile, so gate/up (1792
+// tiles) runs 7 rounds of short work-groups, each paying the first-load latency; here G work-groups
+// walk tiles blockIdx.x, +G, ... with every wave's super-block ring running across the tile seams
+// (kernels.hip mm_pers_kernel's scheme: partials meet in a double-buffered LDS array behind a raw
+// barrier that waits for the LDS writes only; wave 0 finishes tile i while the others stream tile
+// i+1).  Same K split (KS waves) and summation order per tile as mkq_kernel (hipcc's fma contraction
+// of the scale arithmetic may still differ by an ulp).
+template <int T, int KS, int NKW, int TPW, int NB, int EPI, int U>
+__global__ __launch_bounds__(64 * KS) void mkq_pers_kernel(MMArgs a) {
+  constexpr int TB = KqTile<T>::BYTES;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int g = lane >> 4;
+  const int SB = KS * NKW;
+  const int kb = w * NKW;
+  const int G = gridDim.x;
+  const int ntiles = a.N / TILE_N;
+  __shared__ f32x4 red[2][KS][NB][64];
+
+  const uint8_t* W = reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[0];
+  const int8_t* Xq[NB];
+  const float* Xd[NB];
+  const float* Xb[NB];
+  int colr[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    colr[n] = n * 16 + (lane & 15);
+    const int col = colr[n] < a.M ? colr[n] : a.M - 1;
+    Xq[n] = a.xq + (size_t)col * a.K + 64 * g;
+    Xd[n] = a.xd + (size_t)col * SB;
+    Xb[n] = a.xb + (size_t)col * (a.K / 32) + 2 * g;
+  }
+  using Frag = KqFrag<1, NB>;
+  // flat ring position f = tile i of this work-group, super-block kb + k (phantom tiles past the
+  // end re-read the last tile; their outputs are dropped)
+  auto load = [&](Frag& fr, int f) {
+    const int i = f / NKW, k = f % NKW;
+    const int tile = min((int)blockIdx.x + i * G, ntiles - 1);
+    const uint8_t* Wt[1] = {W + ((size_t)tile * SB + kb + k) * TB};
+    kq_load<T, 1, NB>(fr, Wt, Xq, Xd, Xb, kb + k, lane, g);
+  };
+  constexpr int LU = (EPI == EPI_SWIGLU) ? 32 : 64;
+  auto finish = [&](int i) {
+    const int tile = blockIdx.x + i * G;
+    if (w != 0 || tile >= ntiles) return;
+    f32x4 (*rb)[NB][64] = red[i & 1];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      if (lane >= LU || colr[n] >= a.M) continue;
+      f32x4 s = rb[0][n][lane];
+      f32x4 up = (EPI == EPI_SWIGLU) ? rb[0][n][lane + 32] : s;
+#pragma unroll 3
+      for (int ww = 1; ww < KS; ++ww) {
+        s += rb[ww][n][lane];
+        if constexpr (EPI == EPI_SWIGLU) up += rb[ww][n][lane + 32];
+      }
+      epi_store<EPI>(a, tile, lane, colr[n], s, up);
+    }
+  };
+
+  Frag ring[U];
+#pragma unroll
+  for (int f = 0; f < U; ++f) load(ring[f], f);
+  // fully unrolled over the TPW tiles (a loop back-edge renames the ring with moves that wait for
+  // the loads, draining it)
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    f32x4 acc[1][NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) acc[0][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < NKW; ++k) {
+      const int f = i * NKW + k;
+      kq_compute<T, 1, NB>(acc, ring[f % U], g);
+      if (f + U < TPW * NKW) load(ring[f % U], f + U);
+    }
+#pragma unroll
+    for (int n = 0; n < NB; ++n) red[i & 1][w][n][lane] = acc[0][n];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only: the ring stays in flight
+    __builtin_amdgcn_s_barrier();
+    finish(i);
+    __builtin_amdgcn_sched_barrier(0);  // no hoisting across tiles (it spilled the ring)
+  }
+}
+
+template <int T, int NKW, int TPW, int NB, int EPI, int U>
+static void launch_kq_pers_t(const MMArgs& a, int ntiles, hipStream_t s) {
+  const int grid = (ntiles + TPW - 1) / TPW;
+  mkq_pers_kernel<T, 8, NKW, TPW, NB, EPI, U><<<grid, 512, 0, s>>>(a);
+}
+
+// single-type matrices of the Llama shapes: gate/up (K 4096, 1792 tiles / TinyLlama K 2048, 704),
+// attn_output / ffn_down (h 4096: 256 tiles, one per work-group: the KS split is mkq_kernel's), the
+// lm_head (128256 / 32000 rows); -1 = no instantiation (mkq_kernel runs)
+template <int T, int NB, int EPI>
+static int launch_kq_pers_ty(const MMArgs& a, int ntiles, hipStream_t s) {
+  const int SB = a.K / 256;
+  if constexpr (EPI == EPI_SWIGLU) {
+    if (SB == 16 && ntiles == 1792) return launch_kq_pers_t<T, 2, 7, NB, EPI, 2>(a, ntiles, s), 0;
+    if (SB == 8 && ntiles == 704) return launch_kq_pers_t<T, 1, 3, NB, EPI, 2>(a, ntiles, s), 0;
+  } else {
+    if (SB == 16 && ntiles > 256 * 8) return launch_kq_pers_t<T, 2, 8, NB, EPI, 2>(a, ntiles, s), 0;  // 16: spills
+    if (SB == 8 && ntiles > 256 * 4) return launch_kq_pers_t<T, 1, 8, NB, EPI, 2>(a, ntiles, s), 0;
+  }
+  return -1;
+}
+
+static int launch_kq_pers(int epi, const MMArgs& a, int ntiles, hipStream_t s) {
+  // MX_NO_KQ_PERS: the one-tile-per-work-group kernel (read per launch: tests compare the two)
+  if (getenv("MX_NO_KQ_PERS") || a.kq_n != 1 || a.M > 16) return -1;  // 17-32 rows (two column tiles): spills
+  const int t = a.kq_type[0];
+  auto by_nb = [&](auto nb) -> int {
+    constexpr int NB = decltype(nb)::value;
+    switch (epi) {
+      case EPI_SWIGLU:
+        return t == 12 ? launch_kq_pers_ty<12, NB, EPI_SWIGLU>(a, ntiles, s)
+             : t == 13 ? launch_kq_pers_ty<13, NB, EPI_SWIGLU>(a, ntiles, s)
+                       : launch_kq_pers_ty<14, NB, EPI_SWIGLU>(a, ntiles, s);
+      case EPI_F32:
+        return t == 12 ? launch_kq_pers_ty<12, NB, EPI_F32>(a, ntiles, s)
+             : t == 13 ? launch_kq_pers_ty<13, NB, EPI_F32>(a, ntiles, s)
+                       : launch_kq_pers_ty<14, NB, EPI_F32>(a, ntiles, s);
+    }
+    return -1;
+  };
+  return by_nb(std::integral_constant<int, 1>{});
+}
+
 template <int EPI>
 static void launch_mkq_epi(const MMArgs& a, int ntiles, hipStream_t s) {
   if (a.M <= 16) {
@@ -586,6 +811,7 @@ int launch_mkq(int epi, const MMArgs& a, hipStream_t s) {
     if (!kq_tile_bytes(a.kq_type[i]) || (i && a.kq_tile_end[i] <= a.kq_tile_end[i - 1])) return -1;
   if (epi == EPI_SWIGLU && !a.actf) return -1;
   const int ntiles = a.N / TILE_N;
+  if (launch_kq_pers(epi, a, ntiles, s) == 0) return 0;
   switch (epi) {
     case EPI_F32: launch_mkq_epi<EPI_F32>(a, ntiles, s); return 0;
     case EPI_RESID: launch_mkq_epi<EPI_RESID>(a, ntiles, s); return 0;

@@ -206,3 +206,63 @@ def test_kq_llama3_8b_q4_k_m_full_size(mx):
     assert toks.shape == (32, 4) and (toks >= 0).all() and (toks < shape.n_vocab).all()
     b.close()
     eng.close()
+
+
+@pytest.mark.parametrize("name,ftype", [("test-8b-ffn", "q4_k_m"), ("test-tiny-ffn", "q4_k_m"), ("test-tiny-ffn", "q5_k_m"),
+                                        ("test-8b-v128k", "q4_k_m")])
+def test_kq_persistent_gemv_vs_grouped_and_oracle(mx, oracle_mod, monkeypatch, name, ftype):
+    """<= 16 rows of a single-type K-quant matrix with the Llama gate/up or lm_head geometry run the
+    tile-persistent kernel (mkq_pers_kernel).  Against the one-tile-per-work-group kernel
+    (MX_NO_KQ_PERS=1): same K split and per-tile summation order, but hipcc may contract the f32
+    scale arithmetic differently (1-ulp differences that a Q8_K rounding step can amplify), so the
+    two agree within twice the bf16 tolerance; 4 single-row decode steps and a 5-row prefill match
+    the oracle's K-quant forward within the bf16 tolerance, greedy tokens equal (the 1e-6-noise
+    self-deviation bound of the tests above is not used: at this shape the oracle's noise does not
+    flip any Q8_K rounding, so that bound degenerates to ~1e-5)."""
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES[name]
+    ids = _seq(shape, 12, seed=9)
+
+    def run():
+        eng = mx.Engine(f"synthetic:{name}:seed=0:{ftype}", n_ctx=64, n_seq_max=2)
+        eng.forward_logits(ids[:8], 0, slot=0)
+        steps = np.concatenate([eng.forward_logits(ids[p:p + 1], p, slot=0) for p in range(8, 12)])
+        five = eng.forward_logits(ids[:5], 0, slot=1)
+        eng.close()
+        return steps, five
+
+    got, five_p = run()
+    monkeypatch.setenv("MX_NO_KQ_PERS", "1")
+    ref, five_r = run()
+    for g, r in ((got, ref), (five_p, five_r)):
+        tol2 = 2 * (1e-2 * np.abs(r) + 2e-2 * np.abs(r).max(axis=-1, keepdims=True))
+        assert (np.abs(g - r) <= tol2).all()
+
+    octx = _oracle_kq(oracle_mod, shape, 0, ftype).context(64)
+    o_five = octx.eval(ids[:5], 0, all_logits=True)
+    octx2 = _oracle_kq(oracle_mod, shape, 0, ftype).context(64)
+    octx2.eval(ids[:8], 0)
+    o_steps = np.concatenate([octx2.eval(ids[p:p + 1], p) for p in range(8, 12)])
+    for g, o, what in ((got, o_steps, "decode"), (five_p, o_five, "prefill")):
+        assert_logits_close(g, o, f"{name} {ftype} persistent {what}")
+        assert_tokens_match(g, o, f"{name} {ftype} persistent {what}")
+
+
+@pytest.mark.parametrize("name,ftype,n_prompt", [("test-d128", "q4_k_m", 300), ("test-h4096", "q5_k_m", 200),
+                                                 ("test-8b-ffn", "q4_k_m", 150)])
+def test_kq_prefill_gemm_vs_oracle(mx, oracle_mod, name, ftype, n_prompt):
+    """A K-quant prompt of > 64 rows without logits runs as dequantised bf16 GEMMs (launch_dequant_kq
+    + the prefill GEMM; the oracle keeps ggml's Q8_K activations there): the next decode step, which
+    attends to the K/V the GEMM path stored, matches the oracle within the bf16 tolerance."""
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES[name]
+    ids = _seq(shape, n_prompt + 1, seed=31)
+    eng = mx.Engine(f"synthetic:{name}:seed=0:{ftype}", n_ctx=512, n_seq_max=2)
+    assert eng.forward_rows([0] * n_prompt, list(range(n_prompt)), ids[:n_prompt], want_logits=False) is None
+    got = eng.forward_logits(ids[n_prompt:], n_prompt, slot=0)
+    ref = _oracle_kq(oracle_mod, shape, 0, ftype).context(512).eval(ids, 0)
+    assert_logits_close(got, ref, f"{name} {ftype} after K-quant GEMM prefill")
+    assert_tokens_match(got, ref, f"{name} {ftype} after K-quant GEMM prefill")
+    eng.close()
