@@ -931,7 +931,9 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     at.out = attn_out; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
     at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;
     at.scale = 1.0f / sqrtf((float)head_dim);
-    if (launch_mm(EPI_QKV, a, s)) return fail(MX_ERR_ARG, "qkv launch shape");
+    const bool pers_qkv = use_pers && a.X == nullptr && mm_pers_supported(EPI_QKV, M, a.N, h);
+    if ((pers_qkv ? launch_mm_pers(EPI_QKV, a, s) : -1) != 0 && launch_mm(EPI_QKV, a, s))
+      return fail(MX_ERR_ARG, "qkv launch shape");
     MMArgs b{};
     b.W = L.o; b.N = h; b.K = h; b.X = attn_out; b.ldx = h; b.M = M; b.out = x; b.ldo = h;
     if (use_pers && nol && mm_pers_supported(EPI_SWIGLU, M, 2 * ff, h)) {  // partials for gate/up's norm on load

@@ -640,6 +640,12 @@ static const bool pers_resid = getenv("MX_NO_PERS_RESID") == nullptr;  // attn_o
 // lm_head with the output norm on load: correct but neutral at batch 1 (8B 2.804 vs 2.809 ms,
 // TinyLlama 0.750 vs 0.751; tools/gpu/pers_ab4.sh), so opt-in (MX_PERS_HEAD=1)
 static const bool pers_head = getenv("MX_PERS_HEAD") != nullptr;
+// q|k|v of Llama-3-8B (384 tiles: 1.5 rounds of mm_kernel work-groups) as 192 groups x 2 tiles
+// (MX_PERS_QKV=2, default), 128 x 3 (=3) or mm_kernel (=0); read per call (A/B across runs)
+static int qkv_pers_tpw() {
+  const char* v = getenv("MX_PERS_QKV");
+  return v ? atoi(v) : 2;
+}
 
 bool mm_pers_supported(int epi, int M, int N, int K) {
   if (M < 1 || M > 16) return false;
@@ -648,6 +654,7 @@ bool mm_pers_supported(int epi, int M, int N, int K) {
   if (epi == EPI_RESID && pers_resid)
     return N == 4096 && (K == 4096 || K == 14336);
   if (epi == EPI_F32 && pers_head) return (K == 4096 && nt <= 256 * 32) || (K == 2048 && nt <= 256 * 8);
+  if (epi == EPI_QKV) return K == 4096 && nt == 384 && qkv_pers_tpw() > 0;  // Llama-3-8B q|k|v
   return false;
 }
 
@@ -661,6 +668,9 @@ int launch_mm_pers(int epi, const MMArgs& a, hipStream_t s) {
   } else if (epi == EPI_RESID) {
     if (a.K == 4096) return launch_pers_cfg<16, 8, 1, EPI_RESID, 8>(a, s);
     if (a.K == 14336) return launch_pers_cfg<16, 28, 1, EPI_RESID, 14>(a, s);
+  } else if (epi == EPI_QKV) {
+    if (qkv_pers_tpw() == 3) return launch_pers_cfg<16, 8, 3, EPI_QKV, 8>(a, s);
+    return launch_pers_cfg<16, 8, 2, EPI_QKV, 8>(a, s);
   } else if (epi == EPI_F32) {
     if (a.K == 4096) return launch_pers_cfg<16, 8, 32, EPI_F32, 8>(a, s);  // 8B: 251 groups
     if (a.K == 2048) return launch_pers_cfg<16, 4, 8, EPI_F32, 4>(a, s);   // TinyLlama: 250 groups

@@ -797,8 +797,8 @@ template <int EPI>
 static void launch_mkq_epi(const MMArgs& a, int ntiles, hipStream_t s) {
   if (a.M <= 16) {
     mkq_kernel<8, 1, 1, EPI, 2><<<dim3(ntiles, 1), 512, 0, s>>>(a);
-  } else if (a.M <= 32) {
-    mkq_kernel<8, 1, 2, EPI, 2><<<dim3(ntiles, 1), 512, 0, s>>>(a);
+  } else if (a.M <= 32) {  // (a 2-deep ring spills ~460 B/lane at two column tiles: U = 1)
+    mkq_kernel<8, 1, 2, EPI, 1><<<dim3(ntiles, 1), 512, 0, s>>>(a);
   } else {
     mkq_kernel<8, 1, 2, EPI, 1><<<dim3(ntiles, (a.M + 31) / 32), 512, 0, s>>>(a);
   }
