@@ -281,6 +281,12 @@ struct mx_engine {
   bool q8_on_load(int M) const {
     return wq8 && q8_ql && mq8_can_quantize_on_load(M, n_embd, true) && mq8_can_quantize_on_load(M, n_ff, false);
   }
+  // one-token K-quant GEMVs quantise their Q8_K operand on load (no norm / quantise launches);
+  // MX_KQ_NO_QL=1: separate launches (A/B)
+  bool kq_on_load(int M) const {
+    return wkq && getenv("MX_KQ_NO_QL") == nullptr && mkq_can_quantize_on_load(M, n_embd, true) &&
+           mkq_can_quantize_on_load(M, n_ff, false);
+  }
   int enqueue_forward_q8(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap, int n_out,
                          bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count,
                          int max_hist, hipStream_t s);
@@ -878,14 +884,15 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
   // RMS_NORM applied on load by the consuming GEMV (M <= 16); the residual-stream writers
   // (embedding, attn_output, ffn_down, or ssq_kernel for a stage's x_in) leave per-tile partials
   const bool nol = !wide && !wq8 && !wkq && norm_on_load && mm_can_norm_on_load(M, h);
-  const bool qql = q8_on_load(M);
+  const bool qql = q8_on_load(M) || kq_on_load(M);  // residual-stream Σx² partials wanted
   if (x_in) {
     HIPC(hipMemcpyAsync(x, x_in, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
     if (nol || qql) launch_ssq(x, M, h, ssq, s);
   } else {
     if (!has_embed) return fail(MX_ERR_STATE, "this stage has no token embedding: x_in required");
     if (embd_kq_type) {
-      if (launch_embed_kq(x, tok_embd_kq, embd_kq_type, ids, M, h, s)) return fail(MX_ERR_ARG, "K-quant embedding");
+      if (launch_embed_kq(x, tok_embd_kq, embd_kq_type, ids, M, h, qql ? ssq : nullptr, s))
+        return fail(MX_ERR_ARG, "K-quant embedding");
     } else if (embd_q8) {
       launch_embed_q8(x, tok_embd8, ids, M, h, (nol || qql) ? ssq : nullptr, s);
     } else {
@@ -1136,10 +1143,17 @@ int mx_engine::enqueue_forward_kq(int M, const int* pos, const int* slot, void* 
                                   int* hist_count, int max_hist, hipStream_t s) {
   const int h = n_embd, kv = n_embd_kv, ff = n_ff;
   if (head && n_out > MAX_ROWS) return fail(MX_ERR_ARG, "logits for at most 64 rows per forward");
-  // (a v_dot4 kernel quantising on load for <= 4 rows measured slower: 3.09 vs 2.80 ms per 8B token)
+  // One token: every GEMV quantises its Q8_K operand on load (RMS_NORM from the Σx² partials the
+  // residual writers leave); otherwise one norm / quantise launch per GEMV.  (A v_dot4 kernel
+  // quantising on load measured slower: 3.09 vs 2.80 ms per 8B token.)
+  const bool ql = kq_on_load(M);
   auto operand = [&](MMArgs& m, const KqMat& km, const float* src, int K, const float* norm_w, int rows,
                      const int* rmap) -> int {
     km.set(m);
+    if (ql && !rmap) {
+      m.xq = nullptr; m.xf = src; m.norm_w = norm_w; m.eps = eps; m.ssq = norm_w ? ssq : nullptr; m.np = K / 16;
+      return 0;
+    }
     const int rc = norm_w ? launch_rmsnorm_q8k(xq8, xqd, xkb, src, norm_w, rmap, rows, K, eps, s)
                           : launch_quantize_q8k(xq8, xqd, xkb, src, K, rows, K, s);
     m.xq = xq8; m.xd = xqd; m.xb = xkb;
@@ -1166,6 +1180,7 @@ int mx_engine::enqueue_forward_kq(int M, const int* pos, const int* slot, void* 
     MMArgs b{};
     b.W = L.o; b.N = h; b.K = h; b.M = M; b.out = x; b.ldo = h;
     if (operand(b, L.kq_o, attn_f, h, nullptr, M, nullptr)) return fail(MX_ERR_ARG, "kq quantise shape");
+    b.ssq = ql ? ssq : nullptr; b.np = h / 16;  // Σx² partials of the new residual for gate/up
     if (launch_mkq(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "kq attn_output launch shape");
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.actf = act_f; c.lda = ff;
@@ -1174,6 +1189,7 @@ int mx_engine::enqueue_forward_kq(int M, const int* pos, const int* slot, void* 
     MMArgs d{};
     d.W = L.down; d.N = h; d.K = ff; d.M = M; d.out = x; d.ldo = h;
     if (operand(d, L.kq_down, act_f, ff, nullptr, M, nullptr)) return fail(MX_ERR_ARG, "kq quantise shape");
+    d.ssq = ql ? ssq : nullptr; d.np = h / 16;  // ... for the next layer's qkv (and the head)
     if (launch_mkq(EPI_RESID, d, s)) return fail(MX_ERR_ARG, "kq ffn_down launch shape");
   }
   if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));

@@ -185,7 +185,11 @@ int launch_pack_kq(uint8_t* dst, const uint8_t* src_blocks, int type, int N, int
 // the synthetic model's GGUF blocks (synth.py kq_blocks), row-major
 int launch_synth_kq_blocks(uint8_t* dst, int type, size_t nblocks, uint64_t seed, uint64_t tid, hipStream_t s);
 // GET_ROWS of a K-quant token_embd (dequantize_row_q{4,5,6}_K, f32)
-int launch_embed_kq(float* x, const uint8_t* tok_blocks, int type, const int* ids, int M, int n, hipStream_t s);
+// ssq (optional): per-16-element-tile sums of squares of each embedded row (quantise-on-load consumers)
+int launch_embed_kq(float* x, const uint8_t* tok_blocks, int type, const int* ids, int M, int n, float* ssq,
+                    hipStream_t s);
+// one token whose K-quant GEMVs quantise their Q8_K operand on load (xq == nullptr: xf, norm_w, ssq, np)
+bool mkq_can_quantize_on_load(int M, int K, bool norm);
 // RMS_NORM + MUL then Q8_K (xq [M][n], xd [M][n/256], xb [M][n/32]); plain Q8_K of f32 rows
 int launch_rmsnorm_q8k(int8_t* xq, float* xd, float* xb, const float* x, const float* w, const int* row_map, int M,
                        int n, float eps, hipStream_t s);

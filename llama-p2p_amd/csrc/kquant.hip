@@ -182,11 +182,12 @@ int launch_synth_kq_blocks(uint8_t* dst, int type, size_t nblocks, uint64_t seed
 // GET_ROWS of a K-quant token_embd: dequantize_row_q{4,5,6}_K (f32, one rounding per operation);
 // thread = 16 consecutive values
 __global__ __launch_bounds__(256) void embed_kq_kernel(float* x, const uint8_t* tok, int type, int bb, const int* ids,
-                                                       int n) {
+                                                       int n, float* ssq) {
 #pragma clang fp contract(off)
   const int c = blockIdx.x;
   const uint8_t* row = tok + (size_t)ids[c] * (n / 256) * bb;
   for (int t = threadIdx.x; t < n / 16; t += blockDim.x) {
+    double q = 0.0;  // this 16-element tile's sum of squares (the RMS_NORM-on-load partial)
     for (int k = 16 * t; k < 16 * t + 16; ++k) {
       const uint8_t* b = row + (size_t)(k / 256) * bb;
       const int kk = k % 256;
@@ -205,14 +206,16 @@ __global__ __launch_bounds__(256) void embed_kq_kernel(float* x, const uint8_t* 
         y = (d * (float)sc) * (float)v - dmin * (float)mn;
       }
       x[(size_t)c * n + k] = y;
+      q += (double)(y * y);
     }
+    if (ssq) ssq[(size_t)c * (n / 16) + t] = (float)q;
   }
 }
 
-int launch_embed_kq(float* x, const uint8_t* tok, int type, const int* ids, int M, int n, hipStream_t s) {
+int launch_embed_kq(float* x, const uint8_t* tok, int type, const int* ids, int M, int n, float* ssq, hipStream_t s) {
   const int bb = kq_block_bytes(type);
   if (!bb || n % 256) return -1;
-  embed_kq_kernel<<<M, 256, 0, s>>>(x, tok, type, bb, ids, n);
+  embed_kq_kernel<<<M, 256, 0, s>>>(x, tok, type, bb, ids, n, ssq);
   return 0;
 }
 
@@ -338,6 +341,7 @@ int launch_quantize_q8k(int8_t* xq, float* xd, float* xb, const float* src, int 
 template <int T>
 __global__ __launch_bounds__(256) void dequant_kq_kernel(uint16_t* dst, const uint8_t* src, int tile_begin, int ntiles,
                                                          int SB) {
+#pragma clang fp contract(off)  // ggml's dequantize_row_q*_K values: one rounding per operation
   constexpr int TB = KqTile<T>::BYTES, SC = KqTile<T>::SC;
   const int lane = threadIdx.x & 63;
   const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);  // (tile in segment, super-block)
@@ -425,12 +429,9 @@ struct KqFrag {
   f32x2 xb[NB];
 };
 
-// One super-block of RT weight tiles (Wt[r] = tile r's bytes at this super-block) and NB column
-// tiles of Q8_K activations (Xq/Xd/Xb at this lane's column, Xq/Xb offset by its k group)
+// One super-block of RT weight tiles (Wt[r] = tile r's bytes at this super-block) ...
 template <int T, int RT, int NB>
-__device__ __forceinline__ void kq_load(KqFrag<RT, NB>& f, const uint8_t* const (&Wt)[RT], const int8_t* const (&Xq)[NB],
-                                        const float* const (&Xd)[NB], const float* const (&Xb)[NB], int sb, int lane,
-                                        int g) {
+__device__ __forceinline__ void kq_load_w(KqFrag<RT, NB>& f, const uint8_t* const (&Wt)[RT], int lane, int g) {
   constexpr int SC = KqTile<T>::SC;
 #pragma unroll
   for (int r = 0; r < RT; ++r) {
@@ -455,6 +456,13 @@ __device__ __forceinline__ void kq_load(KqFrag<RT, NB>& f, const uint8_t* const 
       f.dm[r] = *reinterpret_cast<const u32x4*>(t + SC + 256 + 16 * g);
     }
   }
+}
+
+// ... and NB column tiles of Q8_K activations (Xq/Xd/Xb at this lane's column, Xq/Xb offset by
+// its k group; global memory, or a quantise-on-load LDS image through the same pointers)
+template <int T, int RT, int NB>
+__device__ __forceinline__ void kq_load_x(KqFrag<RT, NB>& f, const int8_t* const (&Xq)[NB],
+                                          const float* const (&Xd)[NB], const float* const (&Xb)[NB], int sb) {
 #pragma unroll
   for (int n = 0; n < NB; ++n) {
 #pragma unroll
@@ -463,6 +471,73 @@ __device__ __forceinline__ void kq_load(KqFrag<RT, NB>& f, const uint8_t* const 
     if constexpr (T != 14) f.xb[n] = *reinterpret_cast<const f32x2*>(Xb[n] + 8 * sb);
   }
 }
+
+template <int T, int RT, int NB>
+__device__ __forceinline__ void kq_load(KqFrag<RT, NB>& f, const uint8_t* const (&Wt)[RT], const int8_t* const (&Xq)[NB],
+                                        const float* const (&Xd)[NB], const float* const (&Xb)[NB], int sb, int lane,
+                                        int g) {
+  kq_load_w<T, RT, NB>(f, Wt, lane, g);
+  kq_load_x<T, RT, NB>(f, Xq, Xd, Xb, sb);
+}
+
+// Quantise-on-load (one token): this wave's K-slice of super-blocks [kb, kb + nsb), nsb <= 8, of
+// the f32 row xf -- after RMS_NORM+MUL when norm_w (scale from the ssq partials of the residual
+// writers: fixed-order double sum, as xs_build) -- as Q8_K into a wave-private LDS image laid out
+// like the global Q8_K buffers: q [nsb*256] (permuted), d [nsb], b [nsb*8].  Row group rr = lane/16
+// quantises super-blocks rr and rr + 4 with q8k_row (ggml quantize_row_q8_K).  The source values
+// are loaded by ql_load BEFORE the weight ring is issued (a load behind the ring waits for it).
+struct QlRegs {
+  f32x4 x[2][4], w[2][4], sq[2];
+};
+__device__ __forceinline__ void ql_load(QlRegs& r, const MMArgs& a, int kb, int nsb, int lane) {
+  const int t = lane & 15, rr = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int it = rr + 4 * q;
+    if (it < nsb) {
+      const size_t k0 = (size_t)(kb + it) * 256 + 16 * t;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        r.x[q][i] = *reinterpret_cast<const f32x4*>(a.xf + k0 + 4 * i);
+        if (a.norm_w) r.w[q][i] = *reinterpret_cast<const f32x4*>(a.norm_w + k0 + 4 * i);
+      }
+    }
+  }
+  if (a.norm_w)
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      if (lane * 4 + 256 * p < a.np) r.sq[p] = *reinterpret_cast<const f32x4*>(a.ssq + lane * 4 + 256 * p);
+}
+__device__ __forceinline__ void ql_build(const QlRegs& r, const MMArgs& a, int nsb, int lane, int8_t* iq, float* id,
+                                         float* ib) {
+  const int t = lane & 15, rr = lane >> 4;
+  float scale = 1.0f;
+  if (a.norm_w) {
+    double acc = 0.0;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      if (lane * 4 + 256 * p < a.np)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc += (double)r.sq[p][j];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) acc += __shfl_xor(acc, o);
+    scale = 1.0f / sqrtf((float)(acc / a.K) + a.eps);
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int it = rr + 4 * q;
+    if (it < nsb) {  // a whole 16-lane row takes the branch together (q8k_row's DPP rows)
+      float v[16];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * i + e] = a.norm_w ? (r.x[q][i][e] * scale) * r.w[q][i][e] : r.x[q][i][e];
+      q8k_row(v, t, iq + 256 * it, id + it, ib + 8 * it);
+    }
+  }
+}
+constexpr int QL_SB_MAX = 8;                        // super-blocks per wave slice
+constexpr int QL_WAVE_BYTES = QL_SB_MAX * (256 + 4 + 32);  // q, d, b of one slice
 
 // the super-block's contribution to acc (int8 MFMA per 32-k sub-block, f32 scales as ggml)
 template <int T, int RT, int NB>
@@ -557,7 +632,7 @@ __device__ __forceinline__ void kq_compute(f32x4 (&acc)[RT][NB], const KqFrag<RT
   }
 }
 
-template <int T, int KS, int RT, int NB, int EPI, int U>
+template <int T, int KS, int RT, int NB, int EPI, int U, bool QL>
 __device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int tile_in_seg, int tile0,
                                          f32x4 (*red)[RT][NB][64]) {
   constexpr int TB = KqTile<T>::BYTES;
@@ -574,13 +649,23 @@ __device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int 
   const int8_t* Xq[NB];
   const float* Xd[NB];
   const float* Xb[NB];
+  extern __shared__ __attribute__((aligned(16))) uint8_t kq_ql_dyn[];  // QL: per-wave Q8_K images
+  int8_t* iq = reinterpret_cast<int8_t*>(kq_ql_dyn + w * QL_WAVE_BYTES);
+  float* id = reinterpret_cast<float*>(iq + QL_SB_MAX * 256);
+  float* ib = id + QL_SB_MAX;
 #pragma unroll
   for (int n = 0; n < NB; ++n) {
     int col = cb + n * 16 + (lane & 15);
     col = col < a.M ? col : a.M - 1;  // padded columns re-read a valid row (outputs dropped)
-    Xq[n] = a.xq + (size_t)col * a.K + 64 * g;
-    Xd[n] = a.xd + (size_t)col * SB;
-    Xb[n] = a.xb + (size_t)col * (a.K / 32) + 2 * g;
+    if constexpr (QL) {  // one token: the image holds super-blocks kb .. ke-1
+      Xq[n] = iq + 64 * g - kb * 256;
+      Xd[n] = id - kb;
+      Xb[n] = ib + 2 * g - kb * 8;
+    } else {
+      Xq[n] = a.xq + (size_t)col * a.K + 64 * g;
+      Xd[n] = a.xd + (size_t)col * SB;
+      Xb[n] = a.xb + (size_t)col * (a.K / 32) + 2 * g;
+    }
   }
 
   f32x4 acc[RT][NB];
@@ -601,9 +686,30 @@ __device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int 
   Frag ring[U];
   int sb = kb;
   const int nfull = (ke - kb) / U;
+  QlRegs qr;
+  if constexpr (QL) ql_load(qr, a, kb, ke - kb, lane);
   if (nfull > 0) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) load(ring[u], sb + u);
+    for (int u = 0; u < U; ++u) {
+      if constexpr (QL) {
+        const uint8_t* Wt[RT];
+#pragma unroll
+        for (int r = 0; r < RT; ++r) Wt[r] = Wr[r] + (size_t)(sb + u) * TB;
+        kq_load_w<T, RT, NB>(ring[u], Wt, lane, g);
+      } else {
+        load(ring[u], sb + u);
+      }
+    }
+  }
+  if constexpr (QL) {
+    ql_build(qr, a, ke - kb, lane, iq, id, ib);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
+    __builtin_amdgcn_wave_barrier();
+    if (nfull > 0)
+#pragma unroll
+      for (int u = 0; u < U; ++u) kq_load_x<T, RT, NB>(ring[u], Xq, Xd, Xb, sb + u);
+  }
+  if (nfull > 0) {
     for (int ch = 1; ch < nfull; ++ch) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -639,6 +745,22 @@ __device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int 
     f32x4 s = red[0][r][n][l];
 #pragma unroll
     for (int ww = 1; ww < KS; ++ww) s += red[ww][r][n][l];
+    if constexpr (EPI == EPI_RESID) {
+      // residual add, and this tile's share of the next RMS_NORM's sum of squares (quantise-on-load
+      // consumers): lanes l, l^16, l^32, l^48 hold the tile's 16 rows of col (kernels.hip mm_body)
+      f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + (tile0 + r) * 16 + (l >> 4) * 4);
+      const f32x4 xv = *px + s;
+      *px = xv;
+      if (a.ssq) {
+        double q = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q += (double)(xv[i] * xv[i]);
+        q += __shfl_xor(q, 16);
+        q += __shfl_xor(q, 32);
+        if (l < 16) a.ssq[(size_t)col * a.np + tile0 + r] = (float)q;
+      }
+      continue;
+    }
     f32x4 up = s;
     if constexpr (EPI == EPI_SWIGLU) {
       up = red[0][r][n][l + 32];
@@ -649,7 +771,7 @@ __device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int 
   }
 }
 
-template <int KS, int RT, int NB, int EPI, int U>
+template <int KS, int RT, int NB, int EPI, int U, bool QL>
 __global__ __launch_bounds__(64 * KS) void mkq_kernel(MMArgs a) {
   __shared__ f32x4 red[KS][RT][NB][64];
   const int tile0 = blockIdx.x * RT;
@@ -658,9 +780,9 @@ __global__ __launch_bounds__(64 * KS) void mkq_kernel(MMArgs a) {
   const int t_begin = seg ? a.kq_tile_end[seg - 1] : 0;
   const uint8_t* W = reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[seg];
   switch (a.kq_type[seg]) {
-    case 12: mkq_body<12, KS, RT, NB, EPI, U>(a, W, tile0 - t_begin, tile0, red); break;
-    case 13: mkq_body<13, KS, RT, NB, EPI, U>(a, W, tile0 - t_begin, tile0, red); break;
-    case 14: mkq_body<14, KS, RT, NB, EPI, U>(a, W, tile0 - t_begin, tile0, red); break;
+    case 12: mkq_body<12, KS, RT, NB, EPI, U, QL>(a, W, tile0 - t_begin, tile0, red); break;
+    case 13: mkq_body<13, KS, RT, NB, EPI, U, QL>(a, W, tile0 - t_begin, tile0, red); break;
+    case 14: mkq_body<14, KS, RT, NB, EPI, U, QL>(a, W, tile0 - t_begin, tile0, red); break;
   }
 }
 
@@ -672,7 +794,7 @@ __global__ __launch_bounds__(64 * KS) void mkq_kernel(MMArgs a) {
 // barrier that waits for the LDS writes only; wave 0 finishes tile i while the others stream tile
 // i+1).  Same K split (KS waves) and summation order per tile as mkq_kernel (hipcc's fma contraction
 // of the scale arithmetic may still differ by an ulp).
-template <int T, int KS, int NKW, int TPW, int NB, int EPI, int U>
+template <int T, int KS, int NKW, int TPW, int NB, int EPI, int U, bool QL>
 __global__ __launch_bounds__(64 * KS) void mkq_pers_kernel(MMArgs a) {
   constexpr int TB = KqTile<T>::BYTES;
   const int lane = threadIdx.x & 63;
@@ -689,22 +811,36 @@ __global__ __launch_bounds__(64 * KS) void mkq_pers_kernel(MMArgs a) {
   const float* Xd[NB];
   const float* Xb[NB];
   int colr[NB];
+  extern __shared__ __attribute__((aligned(16))) uint8_t kq_ql_dyn[];  // QL: per-wave Q8_K images
+  int8_t* iq = reinterpret_cast<int8_t*>(kq_ql_dyn + w * QL_WAVE_BYTES);
+  float* id = reinterpret_cast<float*>(iq + QL_SB_MAX * 256);
+  float* ib = id + QL_SB_MAX;
 #pragma unroll
   for (int n = 0; n < NB; ++n) {
     colr[n] = n * 16 + (lane & 15);
     const int col = colr[n] < a.M ? colr[n] : a.M - 1;
-    Xq[n] = a.xq + (size_t)col * a.K + 64 * g;
-    Xd[n] = a.xd + (size_t)col * SB;
-    Xb[n] = a.xb + (size_t)col * (a.K / 32) + 2 * g;
+    if constexpr (QL) {
+      Xq[n] = iq + 64 * g - kb * 256;
+      Xd[n] = id - kb;
+      Xb[n] = ib + 2 * g - kb * 8;
+    } else {
+      Xq[n] = a.xq + (size_t)col * a.K + 64 * g;
+      Xd[n] = a.xd + (size_t)col * SB;
+      Xb[n] = a.xb + (size_t)col * (a.K / 32) + 2 * g;
+    }
   }
   using Frag = KqFrag<1, NB>;
   // flat ring position f = tile i of this work-group, super-block kb + k (phantom tiles past the
   // end re-read the last tile; their outputs are dropped)
-  auto load = [&](Frag& fr, int f) {
+  auto load_w = [&](Frag& fr, int f) {
     const int i = f / NKW, k = f % NKW;
     const int tile = min((int)blockIdx.x + i * G, ntiles - 1);
     const uint8_t* Wt[1] = {W + ((size_t)tile * SB + kb + k) * TB};
-    kq_load<T, 1, NB>(fr, Wt, Xq, Xd, Xb, kb + k, lane, g);
+    kq_load_w<T, 1, NB>(fr, Wt, lane, g);
+  };
+  auto load = [&](Frag& fr, int f) {
+    load_w(fr, f);
+    kq_load_x<T, 1, NB>(fr, Xq, Xd, Xb, kb + f % NKW);
   };
   constexpr int LU = (EPI == EPI_SWIGLU) ? 32 : 64;
   auto finish = [&](int i) {
@@ -726,8 +862,20 @@ __global__ __launch_bounds__(64 * KS) void mkq_pers_kernel(MMArgs a) {
   };
 
   Frag ring[U];
+  QlRegs qr;
+  if constexpr (QL) ql_load(qr, a, kb, NKW, lane);  // once per work-group: the slice is the same for every tile
 #pragma unroll
-  for (int f = 0; f < U; ++f) load(ring[f], f);
+  for (int f = 0; f < U; ++f) {
+    if constexpr (QL) load_w(ring[f], f);
+    else load(ring[f], f);
+  }
+  if constexpr (QL) {
+    ql_build(qr, a, NKW, lane, iq, id, ib);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int f = 0; f < U; ++f) kq_load_x<T, 1, NB>(ring[f], Xq, Xd, Xb, kb + f % NKW);
+  }
   // fully unrolled over the TPW tiles (a loop back-edge renames the ring with moves that wait for
   // the loads, draining it)
 #pragma unroll
@@ -753,7 +901,10 @@ __global__ __launch_bounds__(64 * KS) void mkq_pers_kernel(MMArgs a) {
 template <int T, int NKW, int TPW, int NB, int EPI, int U>
 static void launch_kq_pers_t(const MMArgs& a, int ntiles, hipStream_t s) {
   const int grid = (ntiles + TPW - 1) / TPW;
-  mkq_pers_kernel<T, 8, NKW, TPW, NB, EPI, U><<<grid, 512, 0, s>>>(a);
+  if (a.xq == nullptr)
+    mkq_pers_kernel<T, 8, NKW, TPW, NB, EPI, U, true><<<grid, 512, 8 * QL_WAVE_BYTES, s>>>(a);
+  else
+    mkq_pers_kernel<T, 8, NKW, TPW, NB, EPI, U, false><<<grid, 512, 0, s>>>(a);
 }
 
 // single-type matrices of the Llama shapes: gate/up (K 4096, 1792 tiles / TinyLlama K 2048, 704),
@@ -795,17 +946,30 @@ static int launch_kq_pers(int epi, const MMArgs& a, int ntiles, hipStream_t s) {
 
 template <int EPI>
 static void launch_mkq_epi(const MMArgs& a, int ntiles, hipStream_t s) {
-  if (a.M <= 16) {
-    mkq_kernel<8, 1, 1, EPI, 2><<<dim3(ntiles, 1), 512, 0, s>>>(a);
+  if (a.xq == nullptr) {  // one token, quantised on load (launch_mkq checked the slice fits)
+    mkq_kernel<8, 1, 1, EPI, 2, true><<<dim3(ntiles, 1), 512, 8 * QL_WAVE_BYTES, s>>>(a);
+  } else if (a.M <= 16) {
+    mkq_kernel<8, 1, 1, EPI, 2, false><<<dim3(ntiles, 1), 512, 0, s>>>(a);
   } else if (a.M <= 32) {  // (a 2-deep ring spills ~460 B/lane at two column tiles: U = 1)
-    mkq_kernel<8, 1, 2, EPI, 1><<<dim3(ntiles, 1), 512, 0, s>>>(a);
+    mkq_kernel<8, 1, 2, EPI, 1, false><<<dim3(ntiles, 1), 512, 0, s>>>(a);
   } else {
-    mkq_kernel<8, 1, 2, EPI, 1><<<dim3(ntiles, (a.M + 31) / 32), 512, 0, s>>>(a);
+    mkq_kernel<8, 1, 2, EPI, 1, false><<<dim3(ntiles, (a.M + 31) / 32), 512, 0, s>>>(a);
   }
 }
 
+bool mkq_can_quantize_on_load(int M, int K, bool norm) {
+  return M == 1 && K % 256 == 0 && (K / 256 + 7) / 8 <= QL_SB_MAX && (!norm || K / 16 <= 512);
+}
+
 int launch_mkq(int epi, const MMArgs& a, hipStream_t s) {
-  if (a.M < 1 || a.K % 256 || a.N % TILE_N || !a.xq || !a.xd || !a.xb) return -1;
+  if (a.M < 1 || a.K % 256 || a.N % TILE_N) return -1;
+  if (a.xq == nullptr) {  // quantise on load
+    if (!a.xf || !mkq_can_quantize_on_load(a.M, a.K, a.norm_w != nullptr) ||
+        (a.norm_w && (!a.ssq || a.np * 16 != a.K)))
+      return -1;
+  } else if (!a.xd || !a.xb) {
+    return -1;
+  }
   if (a.kq_n < 1 || a.kq_n > 3 || a.kq_tile_end[a.kq_n - 1] * TILE_N != a.N) return -1;
   for (int i = 0; i < a.kq_n; ++i)
     if (!kq_tile_bytes(a.kq_type[i]) || (i && a.kq_tile_end[i] <= a.kq_tile_end[i - 1])) return -1;
