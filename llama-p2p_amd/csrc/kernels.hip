@@ -664,12 +664,7 @@ int launch_mm_pers(int epi, const MMArgs& a, hipStream_t s) {
   if (epi == EPI_SWIGLU) {
     if (a.K == 4096 && ntiles == 1792) return launch_pers_cfg<16, 8, 7, EPI_SWIGLU, 8>(a, s);
     if (a.K == 8192 && ntiles == 3584) return launch_pers_cfg<16, 16, 14, EPI_SWIGLU, 4>(a, s);
-    if (a.K == 2048 && ntiles == 704) {
-      static const int gu_u = getenv("MX_GU2048_U") ? atoi(getenv("MX_GU2048_U")) : 4;  // A/B
-      if (gu_u == 8) return launch_pers_cfg<16, 4, 3, EPI_SWIGLU, 8>(a, s);
-      if (gu_u == 12) return launch_pers_cfg<16, 4, 3, EPI_SWIGLU, 12>(a, s);
-      return launch_pers_cfg<16, 4, 3, EPI_SWIGLU, 4>(a, s);
-    }
+    if (a.K == 2048 && ntiles == 704) return launch_pers_cfg<16, 4, 3, EPI_SWIGLU, 4>(a, s);
   } else if (epi == EPI_RESID) {
     if (a.K == 4096) return launch_pers_cfg<16, 8, 1, EPI_RESID, 8>(a, s);
     if (a.K == 14336) return launch_pers_cfg<16, 28, 1, EPI_RESID, 14>(a, s);
@@ -708,15 +703,12 @@ int launch_mm(int epi, const MMArgs& a, hipStream_t s) {
         if (xs_cfg == 4) return launch_mm_cfg<16, 1, EPI_QKV, 8>(a, s);
       }
     }
-    static const int resid_u = getenv("MX_RESID_U") ? atoi(getenv("MX_RESID_U")) : 4;  // A/B (TinyLlama shapes)
-    static const int qkvxs_u = getenv("MX_QKVXS_U") ? atoi(getenv("MX_QKVXS_U")) : 4;
+    // (TinyLlama: deeper rings -- U = 11 for ffn_down, 8 for q|k|v and gate/up -- measured within
+    // +-3 % of these, tools/gpu/r2ah.sh: the one-token launches there are latency-, not ring-bound)
     switch (epi) {
       case EPI_F32: return launch_mm_cfg<16, 1, EPI_F32, 4>(a, s);
-      case EPI_RESID:
-        if (resid_u == 11 && a.K / TILE_K == 16 * 11) return launch_mm_cfg<16, 1, EPI_RESID, 11>(a, s);
-        return launch_mm_cfg<16, 1, EPI_RESID, 4>(a, s);
+      case EPI_RESID: return launch_mm_cfg<16, 1, EPI_RESID, 4>(a, s);
       case EPI_QKV:  // norm on load: 8-wave groups, 3 per CU, all 384 in one round (profiles/round1_xs_probe.txt)
-        if (qkvxs_u == 8 && a.X == nullptr && a.K == 2048) return launch_mm_cfg<8, 1, EPI_QKV, 8>(a, s);
         return (a.X == nullptr && a.K / 8 <= 512) ? launch_mm_cfg<8, 1, EPI_QKV, 4>(a, s)
                                                   : launch_mm_cfg<16, 1, EPI_QKV, 4>(a, s);
       case EPI_SWIGLU: return launch_mm_cfg<16, 1, EPI_SWIGLU, 4>(a, s);
