@@ -423,7 +423,7 @@ struct KqFrag {
   u32x4 h[RT];      // Q5_K: dwords 0-1; Q6_K: 0-3
   u32x4 sc[RT][4];  // Q4_K / Q5_K: [0..1]; Q6_K: [0..3]
   u32x4 dm[RT];     // Q4_K / Q5_K: f16 (d, dmin) x 4 rows; Q6_K: dwords 0-1 = f16 d x 4 rows
-  uint32_t mn[RT];
+  u32x2 mw[RT];     // Q4_K / Q5_K: the row's 6-bit mins (bytes 0-7 = sub-blocks), raw as loaded
   u32x4 x[NB][4];
   float dx[NB];
   f32x2 xb[NB];
@@ -451,8 +451,8 @@ __device__ __forceinline__ void kq_load_w(KqFrag<RT, NB>& f, const uint8_t* cons
     } else {
 #pragma unroll
       for (int c = 0; c < 2; ++c) f.sc[r][c] = *reinterpret_cast<const u32x4*>(t + SC + 32 * g + 16 * c);
-      const u32x2 mw = *reinterpret_cast<const u32x2*>(t + SC + 128 + 8 * (lane & 15));
-      f.mn[r] = ((mw[0] >> (8 * g)) & 0xFFu) | (((mw[1] >> (8 * g)) & 0xFFu) << 8);  // mins g, g + 4
+      // kept raw: extracting the mins here would wait for this load at once (draining the ring)
+      f.mw[r] = *reinterpret_cast<const u32x2*>(t + SC + 128 + 8 * (lane & 15));
       f.dm[r] = *reinterpret_cast<const u32x4*>(t + SC + 256 + 16 * g);
     }
   }
@@ -618,7 +618,8 @@ __device__ __forceinline__ void kq_compute(f32x4 (&acc)[RT][NB], const KqFrag<RT
         for (int i = 0; i < 4; ++i) acc[r][n][i] += ((float)d4[i] * dx) * (float)S[n][i];
       } else {
         // mins: sum_j m[row][j] * bsum32[j][col] on the f32 MFMA (k = sub-block g, then g + 4)
-        const float m0 = (float)(f.mn[r] & 0xFFu), m1 = (float)((f.mn[r] >> 8) & 0xFFu);
+        const float m0 = (float)((f.mw[r][0] >> (8 * g)) & 0xFFu);  // mins of sub-blocks g, g + 4
+        const float m1 = (float)((f.mw[r][1] >> (8 * g)) & 0xFFu);
         f32x4 Mn = __builtin_amdgcn_mfma_f32_16x16x4f32(m0, f.xb[n][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         Mn = __builtin_amdgcn_mfma_f32_16x16x4f32(m1, f.xb[n][1], Mn, 0, 0, 0);
         const f16x8 dm = __builtin_bit_cast(f16x8, f.dm[r]);
@@ -957,6 +958,181 @@ static void launch_mkq_epi(const MMArgs& a, int ntiles, hipStream_t s) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// K-quant GEMV for 17..64 tokens (32-sequence decode) with the Q8_K activations shared through LDS.
+//
+// mkq_kernel at two column tiles gives every wave its own copy of the activation fragments: per
+// super-block 8 KB of Q8_K per wave against 2.4 KB of Q4_K weights, so it streams ~3x more bytes
+// from L2 than weights from HBM, and with a one-deep ring it waits on both.  Here (as mm_wide_kernel
+// does for bf16) the W waves of a work-group each own one 16-row tile over the whole K and share
+// one staged super-block of activations [16*NB tokens][256 q + 8 sub-block sums + d] in LDS
+// (double-buffered, one barrier per super-block; the next-but-one super-block's pieces are loaded
+// into registers while this one computes), and each wave keeps a U-deep ring of its weight tiles in
+// flight.  Per super-block and tile the arithmetic is kq_compute's (ggml's integer super-block sums,
+// f32 scaling), and the whole K stays in one wave, so the epilogue runs from registers.
+// Single-type matrices (one segment): gate/up and the lm_head of a K-quant file.
+// ---------------------------------------------------------------------------
+template <int T, int W, int NB, int EPI, int U>
+__global__ __launch_bounds__(64 * W) void mkq_wide_kernel(MMArgs a) {
+  constexpr int TB = KqTile<T>::BYTES;
+  constexpr int ROWS = 16 * NB;
+  constexpr int QP = 256 + 16;  // int8 per LDS row: +16 B keeps the 16 token rows' fragment reads conflict-free
+  constexpr int NQ = ROWS * 16;  // 16-B pieces of q per super-block
+  constexpr int NBS = ROWS * 2;  // 16-B pieces of the sub-block sums (8 floats per token)
+  constexpr int PIECES = NQ + NBS;
+  constexpr int NT = 64 * W;
+  constexpr int PPT = (PIECES + NT - 1) / NT;
+  static_assert((U == 2 || U == 4) && ROWS <= NT, "ring depth in activation-set pairs; one d per thread");
+  __shared__ __attribute__((aligned(16))) int8_t sq[2][ROWS][QP];
+  __shared__ __attribute__((aligned(16))) float ssb[2][ROWS][8];
+  __shared__ float sdx[2][ROWS];
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, tid = threadIdx.x;
+  const int SB = a.K / 256;
+  const int tile = blockIdx.x * W + w;
+  const uint8_t* Wr = reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[0] + (size_t)tile * SB * TB;
+
+  // staging: piece p < NQ = 16 B of q (token row p/16, segment p%16), else 16 B of the sums; tokens
+  // >= M re-read token M-1 (outputs dropped); the ragged tail re-stages the last piece
+  const u32x4* xsrc[PPT];
+  int xstep[PPT], xdst[PPT];
+  bool xq_piece[PPT];
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int p = min(tid + i * NT, PIECES - 1);
+    if (p < NQ) {
+      const int row = p / 16, rr = row < a.M ? row : a.M - 1;
+      xsrc[i] = reinterpret_cast<const u32x4*>(a.xq + (size_t)rr * a.K + (p % 16) * 16);
+      xstep[i] = 16;  // u32x4 per super-block
+      xdst[i] = row * QP + (p % 16) * 16;
+      xq_piece[i] = true;
+    } else {
+      const int q = p - NQ, row = q / 2, rr = row < a.M ? row : a.M - 1;
+      xsrc[i] = reinterpret_cast<const u32x4*>(a.xb + (size_t)rr * (a.K / 32) + (q % 2) * 4);
+      xstep[i] = 2;
+      xdst[i] = row * 32 + (q % 2) * 16;
+      xq_piece[i] = false;
+    }
+  }
+  const int drow = tid < ROWS ? (tid < a.M ? tid : a.M - 1) : 0;
+  const float* dsrc = a.xd + (size_t)drow * SB;
+  u32x4 xr[2][PPT];
+  float xdr[2];
+  auto load_x = [&](int set, int sb) {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) xr[set][i] = xsrc[i][sb * xstep[i]];
+    if (tid < ROWS) xdr[set] = dsrc[sb];
+  };
+  auto store_x = [&](int set, int buf) {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      uint8_t* base = xq_piece[i] ? reinterpret_cast<uint8_t*>(&sq[buf][0][0])
+                                  : reinterpret_cast<uint8_t*>(&ssb[buf][0][0]);
+      *reinterpret_cast<u32x4*>(base + xdst[i]) = xr[set][i];
+    }
+    if (tid < ROWS) sdx[buf][tid] = xdr[set];
+  };
+
+  using Frag = KqFrag<1, NB>;
+  Frag ring[U];
+  auto load_w = [&](Frag& f, int sb) {
+    const uint8_t* Wt[1] = {Wr + (size_t)sb * TB};
+    kq_load_w<T, 1, NB>(f, Wt, lane, g);
+  };
+  f32x4 acc[1][NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) acc[0][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_x(0, 0);
+  load_x(1, SB > 1 ? 1 : 0);
+#pragma unroll
+  for (int u = 0; u < U; ++u) load_w(ring[u], u < SB ? u : SB - 1);
+  store_x(0, 0);
+  __syncthreads();
+
+  // super-block sb: activation set H = sb & 1 receives sb + 2; set 1 - H (sb + 1) goes to LDS at the end
+  auto step = [&](auto Hc, auto Rc, int sb) {
+    constexpr int H = decltype(Hc)::value;
+    constexpr int R = decltype(Rc)::value;
+    const int buf = sb & 1;
+    load_x(H, sb + 2 < SB ? sb + 2 : SB - 1);
+    Frag& f = ring[R];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const int row = n * 16 + (lane & 15);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) f.x[n][c] = *reinterpret_cast<const u32x4*>(&sq[buf][row][64 * g + 16 * c]);
+      f.dx[n] = sdx[buf][row];
+      if constexpr (T != 14) f.xb[n] = *reinterpret_cast<const f32x2*>(&ssb[buf][row][2 * g]);
+    }
+    kq_compute<T, 1, NB>(acc, f, g);
+    load_w(f, min(sb + U, SB - 1));  // past the end: re-read the last super-block (no branch)
+    store_x(1 - H, buf ^ 1);
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);  // nothing moves across super-blocks (interleaving them spills)
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  // SB % U == 0 (launch_kq_wide): no data-dependent branch in the loop -- at a branch join hipcc
+  // merges wait counts conservatively, which drains the weight ring
+  for (int sb = 0; sb < SB; sb += U) {
+    step(I0{}, I0{}, sb);
+    if (sb + 1 < SB) step(I1{}, I1{}, sb + 1);
+    if constexpr (U == 4) {
+      if (sb + 2 < SB) step(I0{}, I2{}, sb + 2);
+      if (sb + 3 < SB) step(I1{}, I3{}, sb + 3);
+    }
+  }
+
+  // epilogue from registers: this wave owns its tile over the whole K
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    const f32x4 s = acc[0][n];
+    f32x4 up = s;
+    if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(s[i], 32);
+    }
+    const int col = n * 16 + (lane & 15);
+    if (col >= a.M || (EPI == EPI_SWIGLU && lane >= 32)) continue;
+    epi_store<EPI>(a, tile, lane, col, s, up);
+  }
+}
+
+// two column tiles (17..32 tokens); ring 4 deep for Q4_K / Q5_K, 2 for Q6_K (its 4-deep ring spills)
+template <int T, int W, int EPI>
+static void launch_kq_wide_t(const MMArgs& a, int ntiles, hipStream_t s) {
+  mkq_wide_kernel<T, W, 2, EPI, T == 14 ? 2 : 4><<<ntiles / W, 64 * W, 0, s>>>(a);
+}
+
+template <int EPI>
+static int launch_kq_wide_epi(const MMArgs& a, int ntiles, hipStream_t s) {
+  const int t = a.kq_type[0];
+  auto by_w = [&](auto wc) {
+    constexpr int W = decltype(wc)::value;
+    if (t == 12) launch_kq_wide_t<12, W, EPI>(a, ntiles, s);
+    else if (t == 13) launch_kq_wide_t<13, W, EPI>(a, ntiles, s);
+    else launch_kq_wide_t<14, W, EPI>(a, ntiles, s);
+    return 0;
+  };
+  // waves per work-group sized so the grid covers the 256 CUs (Llama-3-8B gate/up: 1792 = 7 x 256)
+  if (ntiles % 7 == 0 && ntiles / 7 >= 200) return by_w(std::integral_constant<int, 7>{});
+  if (ntiles % 8 == 0 && ntiles / 8 >= 200) return by_w(std::integral_constant<int, 8>{});
+  if (ntiles % 4 == 0) return by_w(std::integral_constant<int, 4>{});
+  return -1;
+}
+
+// 17..32 tokens, one-type matrix, gate/up or lm_head: the LDS-shared form (MX_NO_KQ_WIDE=1: mkq_kernel)
+static int launch_kq_wide(int epi, const MMArgs& a, int ntiles, hipStream_t s) {
+  static const bool off = getenv("MX_NO_KQ_WIDE") != nullptr;
+  if (off || a.M <= 16 || a.M > 32 || a.kq_n != 1 || !a.xq || !a.xd || !a.xb || (a.K / 256) % 4) return -1;
+  if (epi == EPI_SWIGLU) return launch_kq_wide_epi<EPI_SWIGLU>(a, ntiles, s);
+  if (epi == EPI_F32) return launch_kq_wide_epi<EPI_F32>(a, ntiles, s);
+  return -1;
+}
+
 bool mkq_can_quantize_on_load(int M, int K, bool norm) {
   return M == 1 && K % 256 == 0 && (K / 256 + 7) / 8 <= QL_SB_MAX && (!norm || K / 16 <= 512);
 }
@@ -976,6 +1152,7 @@ int launch_mkq(int epi, const MMArgs& a, hipStream_t s) {
   if (epi == EPI_SWIGLU && !a.actf) return -1;
   const int ntiles = a.N / TILE_N;
   if (launch_kq_pers(epi, a, ntiles, s) == 0) return 0;
+  if (launch_kq_wide(epi, a, ntiles, s) == 0) return 0;
   switch (epi) {
     case EPI_F32: launch_mkq_epi<EPI_F32>(a, ntiles, s); return 0;
     case EPI_RESID: launch_mkq_epi<EPI_RESID>(a, ntiles, s); return 0;

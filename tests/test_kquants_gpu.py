@@ -249,6 +249,41 @@ def test_kq_persistent_gemv_vs_grouped_and_oracle(mx, oracle_mod, monkeypatch, n
         assert_tokens_match(g, o, f"{name} {ftype} persistent {what}")
 
 
+@pytest.mark.parametrize("name,ftype,M", [("test-8b-ffn", "q4_k_m", 32), ("test-8b-ffn", "q5_k_m", 20),
+                                          ("test-8b-v128k", "q4_k_m", 32), ("test-tiny-ffn", "q4_k_m", 17)])
+def test_kq_wide_lds_gemv_vs_grouped_and_oracle(mx, oracle_mod, monkeypatch, name, ftype, M):
+    """17-32 rows of a single-type K-quant gate/up or lm_head (Llama-3-8B: 1792 gate/up tiles on 7-wave
+    groups, 8016 Q6_K lm_head tiles on 8-wave groups) run mkq_wide_kernel, the Q8_K activations of a
+    super-block shared by the group's waves through LDS.  Against mkq_kernel (MX_NO_KQ_WIDE=1): the
+    same integer super-block sums, the f32 sum over K in one wave instead of 8 K-slices, so within
+    twice the bf16 tolerance; against the oracle's K-quant forward within the bf16 tolerance."""
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES[name]
+    rng = np.random.default_rng(M)
+    prompts = [np.concatenate([[1], rng.integers(3, shape.n_vocab, int(rng.integers(3, 8)))]).astype(np.int32)
+               for _ in range(M)]
+
+    def run():
+        eng = mx.Engine(f"synthetic:{name}:seed=0:{ftype}", n_ctx=64, n_seq_max=M)
+        for i, p in enumerate(prompts):
+            eng.forward_logits(p[:-1], 0, slot=i)
+        out = eng.forward_rows(list(range(M)), [len(p) - 1 for p in prompts], [int(p[-1]) for p in prompts])
+        eng.close()
+        return out
+
+    got = run()
+    monkeypatch.setenv("MX_NO_KQ_WIDE", "1")
+    ref = run()
+    monkeypatch.delenv("MX_NO_KQ_WIDE")
+    tol2 = 2 * (1e-2 * np.abs(ref) + 2e-2 * np.abs(ref).max(axis=-1, keepdims=True))
+    assert (np.abs(got - ref) <= tol2).all()
+    om = _oracle_kq(oracle_mod, shape, 0, ftype)
+    o = np.stack([om.context(64).eval(p, 0)[0] for p in prompts])
+    assert_logits_close(got, o, f"{name} {ftype} wide M={M}")
+    assert_tokens_match(got, o, f"{name} {ftype} wide M={M}")
+
+
 @pytest.mark.parametrize("name,ftype,n_prompt", [("test-d128", "q4_k_m", 300), ("test-h4096", "q5_k_m", 200),
                                                  ("test-8b-ffn", "q4_k_m", 150)])
 def test_kq_prefill_gemm_vs_oracle(mx, oracle_mod, name, ftype, n_prompt):
