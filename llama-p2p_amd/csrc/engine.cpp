@@ -1147,6 +1147,9 @@ int mx_engine::enqueue_forward_kq(int M, const int* pos, const int* slot, void* 
   // residual writers leave); otherwise one norm / quantise launch per GEMV.  (A v_dot4 kernel
   // quantising on load measured slower: 3.09 vs 2.80 ms per 8B token.)
   const bool ql = kq_on_load(M);
+  // 17..32 rows: attn_output / ffn_down run split-K into slabs (launch_mkq_slab) and the next
+  // RMS_NORM + Q8_K launch folds them into x; nslab = partials not yet folded
+  int nslab = 0;
   auto operand = [&](MMArgs& m, const KqMat& km, const float* src, int K, const float* norm_w, int rows,
                      const int* rmap) -> int {
     km.set(m);
@@ -1154,10 +1157,23 @@ int mx_engine::enqueue_forward_kq(int M, const int* pos, const int* slot, void* 
       m.xq = nullptr; m.xf = src; m.norm_w = norm_w; m.eps = eps; m.ssq = norm_w ? ssq : nullptr; m.np = K / 16;
       return 0;
     }
-    const int rc = norm_w ? launch_rmsnorm_q8k(xq8, xqd, xkb, src, norm_w, rmap, rows, K, eps, s)
-                          : launch_quantize_q8k(xq8, xqd, xkb, src, K, rows, K, s);
+    int rc;
+    if (norm_w && src == x && nslab) {
+      rc = launch_rmsnorm_q8k(xq8, xqd, xkb, src, norm_w, rmap, rows, K, eps, s, slabs, nslab, slab_stride);
+      nslab = 0;
+    } else {
+      rc = norm_w ? launch_rmsnorm_q8k(xq8, xqd, xkb, src, norm_w, rmap, rows, K, eps, s)
+                  : launch_quantize_q8k(xq8, xqd, xkb, src, K, rows, K, s);
+    }
     m.xq = xq8; m.xd = xqd; m.xb = xkb;
     return rc;
+  };
+  auto resid = [&](MMArgs& m) -> int {  // x += W . operand, in place or as slabs for the next operand()
+    if (!ql && M > 16 && M <= 32) {
+      const int ks = launch_mkq_slab(m, slabs, slab_stride, s);
+      if (ks > 0) return nslab = ks, 0;
+    }
+    return launch_mkq(EPI_RESID, m, s);
   };
   for (int li = 0; li < (int)layers.size(); li++) {
     const Layer& L = layers[li];
@@ -1181,7 +1197,7 @@ int mx_engine::enqueue_forward_kq(int M, const int* pos, const int* slot, void* 
     b.W = L.o; b.N = h; b.K = h; b.M = M; b.out = x; b.ldo = h;
     if (operand(b, L.kq_o, attn_f, h, nullptr, M, nullptr)) return fail(MX_ERR_ARG, "kq quantise shape");
     b.ssq = ql ? ssq : nullptr; b.np = h / 16;  // Σx² partials of the new residual for gate/up
-    if (launch_mkq(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "kq attn_output launch shape");
+    if (resid(b)) return fail(MX_ERR_ARG, "kq attn_output launch shape");
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.actf = act_f; c.lda = ff;
     if (operand(c, L.kq_gu, x, h, L.ffn_norm, M, nullptr) || launch_mkq(EPI_SWIGLU, c, s))
@@ -1190,7 +1206,11 @@ int mx_engine::enqueue_forward_kq(int M, const int* pos, const int* slot, void* 
     d.W = L.down; d.N = h; d.K = ff; d.M = M; d.out = x; d.ldo = h;
     if (operand(d, L.kq_down, act_f, ff, nullptr, M, nullptr)) return fail(MX_ERR_ARG, "kq quantise shape");
     d.ssq = ql ? ssq : nullptr; d.np = h / 16;  // ... for the next layer's qkv (and the head)
-    if (launch_mkq(EPI_RESID, d, s)) return fail(MX_ERR_ARG, "kq ffn_down launch shape");
+    if (resid(d)) return fail(MX_ERR_ARG, "kq ffn_down launch shape");
+  }
+  if (nslab && (x_out || !(head && !rowmap && n_out == M))) {  // x itself is read next: fold the partials
+    launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);
+    nslab = 0;
   }
   if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
   if (head) {

@@ -191,11 +191,16 @@ int launch_embed_kq(float* x, const uint8_t* tok_blocks, int type, const int* id
 // one token whose K-quant GEMVs quantise their Q8_K operand on load (xq == nullptr: xf, norm_w, ssq, np)
 bool mkq_can_quantize_on_load(int M, int K, bool norm);
 // RMS_NORM + MUL then Q8_K (xq [M][n], xd [M][n/256], xb [M][n/32]); plain Q8_K of f32 rows
+// (nslab > 0: first fold the split-K slabs of the GEMV that wrote x into x, see launch_mkq_slab)
 int launch_rmsnorm_q8k(int8_t* xq, float* xd, float* xb, const float* x, const float* w, const int* row_map, int M,
-                       int n, float eps, hipStream_t s);
+                       int n, float eps, hipStream_t s, const float* slabs = nullptr, int nslab = 0,
+                       size_t slab_stride = 0);
 int launch_quantize_q8k(int8_t* xq, float* xd, float* xb, const float* src, int ld, int M, int n, hipStream_t s);
 // K-quant x Q8_K products for any M (grid.y: groups of 32 tokens), the usual epilogues (SWIGLU: actf)
 int launch_mkq(int epi, const MMArgs& a, hipStream_t s);
+// 17..32 tokens, attn_output / ffn_down: split-K partials into slabs ([ks][token][N], slab_stride apart)
+// for launch_rmsnorm_q8k to fold; returns ks, or -1 when the shape has no such form (use launch_mkq)
+int launch_mkq_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s);
 // packed K-quant matrix (segments as in MMArgs) -> packed bf16 tiles [N/16][K/32] x 1 KiB (prefill GEMM)
 int launch_dequant_kq(uint16_t* dst, const void* W, int K, int kq_n, const int* type, const int* tile_end,
                       const size_t* off, hipStream_t s);

@@ -279,19 +279,47 @@ __device__ __forceinline__ void q8k_row(const float (&v)[16], int t, int8_t* qsb
 // grid (ceil(K/256/16), M), 256 threads: super-block s = 16*blockIdx.x + threadIdx.x/16 of row
 // blockIdx.y; with norm_w, RMS_NORM + MUL first (sum of squares of the whole row in double, every
 // work-group of the row computing it the same way: norm_q8_kernel's arithmetic)
-template <bool NORM>
+// With nslab > 0 (NORM, one work-group per row, no row_map): src is the residual stream x and the
+// split-K partial slabs of the GEMV that produced it are folded first -- x += slab 0 + slab 1 + ...
+// (resid_norm's order), the sum of squares taken over the folded row and the folded values written
+// back to x by the thread that quantises them.
+template <bool NORM, bool FOLD>
 __global__ __launch_bounds__(256) void q8k_kernel(int8_t* xq, float* xd, float* xb, const float* src, int ld,
-                                                  const float* w, const int* row_map, int n, float eps) {
+                                                  const float* w, const int* row_map, int n, float eps,
+                                                  const float* slabs, int nslab, size_t sstride) {
   const int c = blockIdx.y;
   const int r = row_map ? row_map[c] : c;
   const float* xr = src + (size_t)r * ld;
+  auto fold = [&](f32x4 v, int i) -> f32x4 {  // all slab loads issued before the adds (one round trip)
+    if constexpr (!FOLD) return v;
+    f32x4 sl[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k < nslab) sl[k] = *reinterpret_cast<const f32x4*>(slabs + k * sstride + (size_t)c * n + i);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k < nslab) v += sl[k];
+    return v;
+  };
   float scale = 1.0f;
   if constexpr (NORM) {
     double acc = 0.0;
-    for (int i = threadIdx.x * 4; i < n; i += 1024) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
+    if constexpr (FOLD) {  // n <= 4096: 4 pieces per thread, every load in flight at once
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc += (double)(v[j] * v[j]);
+      for (int it = 0; it < 4; ++it) {
+        const int i = threadIdx.x * 4 + 1024 * it;
+        if (i < n) {
+          const f32x4 v = fold(*reinterpret_cast<const f32x4*>(xr + i), i);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc += (double)(v[j] * v[j]);
+        }
+      }
+    } else {
+      for (int i = threadIdx.x * 4; i < n; i += 1024) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc += (double)(v[j] * v[j]);
+      }
     }
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     __shared__ double part[4];
@@ -306,7 +334,9 @@ __global__ __launch_bounds__(256) void q8k_kernel(int8_t* xq, float* xd, float* 
   float v[16];
 #pragma unroll
   for (int i = 0; i < 16; i += 4) {
-    const f32x4 x4 = *reinterpret_cast<const f32x4*>(xr + 256 * s + 16 * t + i);
+    const int k = 256 * s + 16 * t + i;
+    const f32x4 x4 = fold(*reinterpret_cast<const f32x4*>(xr + k), k);
+    if constexpr (FOLD) *reinterpret_cast<f32x4*>(const_cast<float*>(xr) + k) = x4;  // every read of x is behind the barrier
     if constexpr (NORM) {
       const f32x4 g4 = *reinterpret_cast<const f32x4*>(w + 256 * s + 16 * t + i);
 #pragma unroll
@@ -320,14 +350,20 @@ __global__ __launch_bounds__(256) void q8k_kernel(int8_t* xq, float* xd, float* 
 }
 
 int launch_rmsnorm_q8k(int8_t* xq, float* xd, float* xb, const float* x, const float* w, const int* row_map, int M, int n,
-                       float eps, hipStream_t s) {
+                       float eps, hipStream_t s, const float* slabs, int nslab, size_t slab_stride) {
   if (n % 256 || M < 1) return -1;
-  q8k_kernel<true><<<dim3((n / 256 + 15) / 16, M), 256, 0, s>>>(xq, xd, xb, x, n, w, row_map, n, eps);
+  if (nslab && (row_map || n > 16 * 256 || !slabs)) return -1;  // the fold needs one work-group per row
+  if (nslab)
+    q8k_kernel<true, true><<<dim3(1, M), 256, 0, s>>>(xq, xd, xb, x, n, w, row_map, n, eps, slabs, nslab, slab_stride);
+  else
+    q8k_kernel<true, false><<<dim3((n / 256 + 15) / 16, M), 256, 0, s>>>(xq, xd, xb, x, n, w, row_map, n, eps,
+                                                                        nullptr, 0, 0);
   return 0;
 }
 int launch_quantize_q8k(int8_t* xq, float* xd, float* xb, const float* src, int ld, int M, int n, hipStream_t s) {
   if (n % 256 || M < 1) return -1;
-  q8k_kernel<false><<<dim3((n / 256 + 15) / 16, M), 256, 0, s>>>(xq, xd, xb, src, ld, nullptr, nullptr, n, 0.f);
+  q8k_kernel<false, false><<<dim3((n / 256 + 15) / 16, M), 256, 0, s>>>(xq, xd, xb, src, ld, nullptr, nullptr, n,
+                                                                         0.f, nullptr, 0, 0);
   return 0;
 }
 
@@ -555,57 +591,81 @@ __device__ __forceinline__ void kq_compute(f32x4 (&acc)[RT][NB], const KqFrag<RT
     for (int c = 0; c < (T == 14 ? 4 : 2); ++c)
 #pragma unroll
       for (int e = 0; e < 4; ++e) scw[4 * c + e] = f.sc[r][c][e];
-    // sub-block by sub-block: unpack its A operand and scales once, then one MFMA (Q6_K: two)
-    // per column tile into that tile's int32 super-block sums
+    // sub-block by sub-block: unpack its A operand and scales once, then one MFMA (Q6_K: two) per
+    // column tile; each sub-block's products are scaled into the int32 super-block sums only after
+    // the next sub-block's MFMAs are issued, so the VALU does not wait on an MFMA it just issued
+    // (integer sums: the order changes nothing)
     i32x4 S[NB];
 #pragma unroll
     for (int n = 0; n < NB; ++n) S[n] = i32x4{0, 0, 0, 0};
+    i32x4 Pp[NB], Pp1[NB];  // previous sub-block's products (Q6_K: both 16-value groups)
+    int sp[4], sp1[4];      // ... and its scales
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      uint32_t lo = D[j] & 0x0F0F0F0Fu, hi = (D[j] >> 4) & 0x0F0F0F0Fu;
-      if constexpr (T == 13) {
-        const uint32_t H = f.h[r][j >> 2];
-        lo |= ((H >> ((2 * j) & 7)) & 0x01010101u) << 4;
-        hi |= ((H >> ((2 * j + 1) & 7)) & 0x01010101u) << 4;
+    for (int j = 0; j < 9; ++j) {
+      i32x4 Pc[NB], Pc1[NB];
+      int sc[4], sc1[4];
+      if (j < 8) {
+        uint32_t lo = D[j] & 0x0F0F0F0Fu, hi = (D[j] >> 4) & 0x0F0F0F0Fu;
+        if constexpr (T == 13) {
+          const uint32_t H = f.h[r][j >> 2];
+          lo |= ((H >> ((2 * j) & 7)) & 0x01010101u) << 4;
+          hi |= ((H >> ((2 * j + 1) & 7)) & 0x01010101u) << 4;
+        }
+        if constexpr (T == 14) {
+          const uint32_t H = f.h[r][j >> 1];
+          lo |= ((H >> (4 * (j & 1))) & 0x03030303u) << 4;
+          hi |= ((H >> (4 * (j & 1) + 2)) & 0x03030303u) << 4;
+          lo = ((lo | 0x80808080u) - 0x20202020u) ^ 0x80808080u;  // bytewise q - 32
+          hi = ((hi | 0x80808080u) - 0x20202020u) ^ 0x80808080u;
+        }
+        const long A = (long)(((unsigned long)hi << 32) | lo);
+        if constexpr (T == 14) {
+          // int8 scales of row 4g+i, groups 2j and 2j+1: bytes 16i + 2j, +1 of the row group's 64
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t sw = scw[4 * i + (j >> 1)];
+            sc[i] = (int)(int8_t)(sw >> (16 * (j & 1)));
+            sc1[i] = (int)(int8_t)(sw >> (16 * (j & 1) + 8));
+          }
+          const long A0 = g < 2 ? A : 0l, A1 = g < 2 ? 0l : A;
+#pragma unroll
+          for (int n = 0; n < NB; ++n) {
+            const u32x4& xc = f.x[n][j >> 1];
+            const long B = (long)(((unsigned long)xc[2 * (j & 1) + 1] << 32) | xc[2 * (j & 1)]);
+            Pc[n] = __builtin_amdgcn_mfma_i32_16x16x32_i8(A0, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+            Pc1[n] = __builtin_amdgcn_mfma_i32_16x16x32_i8(A1, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+          }
+        } else {
+          // 6-bit scales of row 4g+i, sub-block j: byte 8i + j of the row group's 32
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sc[i] = (int)((scw[2 * i + (j >> 2)] >> (8 * (j & 3))) & 0xFFu);
+#pragma unroll
+          for (int n = 0; n < NB; ++n) {
+            const u32x4& xc = f.x[n][j >> 1];
+            const long B = (long)(((unsigned long)xc[2 * (j & 1) + 1] << 32) | xc[2 * (j & 1)]);
+            Pc[n] = __builtin_amdgcn_mfma_i32_16x16x32_i8(A, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
+          }
+        }
       }
-      if constexpr (T == 14) {
-        const uint32_t H = f.h[r][j >> 1];
-        lo |= ((H >> (4 * (j & 1))) & 0x03030303u) << 4;
-        hi |= ((H >> (4 * (j & 1) + 2)) & 0x03030303u) << 4;
-        lo = ((lo | 0x80808080u) - 0x20202020u) ^ 0x80808080u;  // bytewise q - 32
-        hi = ((hi | 0x80808080u) - 0x20202020u) ^ 0x80808080u;
+      if (j > 0) {
+#pragma unroll
+        for (int n = 0; n < NB; ++n)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if constexpr (T == 14) S[n][i] += __mul24(sp[i], Pp[n][i]) + __mul24(sp1[i], Pp1[n][i]);  // |P| < 2^17
+            else S[n][i] += __mul24(sp[i], Pp[n][i]);
+          }
       }
-      const long A = (long)(((unsigned long)hi << 32) | lo);
-      if constexpr (T == 14) {
-        // int8 scales of row 4g+i, groups 2j and 2j+1: bytes 16i + 2j, +1 of the row group's 64
-        int s0[4], s1[4];
+      if (j < 8) {
+#pragma unroll
+        for (int n = 0; n < NB; ++n) {
+          Pp[n] = Pc[n];
+          if constexpr (T == 14) Pp1[n] = Pc1[n];
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const uint32_t sw = scw[4 * i + (j >> 1)];
-          s0[i] = (int)(int8_t)(sw >> (16 * (j & 1)));
-          s1[i] = (int)(int8_t)(sw >> (16 * (j & 1) + 8));
-        }
-        const long A0 = g < 2 ? A : 0l, A1 = g < 2 ? 0l : A;
-#pragma unroll
-        for (int n = 0; n < NB; ++n) {
-          const u32x4& xc = f.x[n][j >> 1];
-          const long B = (long)(((unsigned long)xc[2 * (j & 1) + 1] << 32) | xc[2 * (j & 1)]);
-          const i32x4 P0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(A0, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
-          const i32x4 P1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(A1, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) S[n][i] += __mul24(s0[i], P0[i]) + __mul24(s1[i], P1[i]);  // |P| < 2^17
-        }
-      } else {
-        int sc[4];  // 6-bit scales of row 4g+i, sub-block j: byte 8i + j of the row group's 32
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sc[i] = (int)((scw[2 * i + (j >> 2)] >> (8 * (j & 3))) & 0xFFu);
-#pragma unroll
-        for (int n = 0; n < NB; ++n) {
-          const u32x4& xc = f.x[n][j >> 1];
-          const long B = (long)(((unsigned long)xc[2 * (j & 1) + 1] << 32) | xc[2 * (j & 1)]);
-          const i32x4 P = __builtin_amdgcn_mfma_i32_16x16x32_i8(A, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) S[n][i] += __mul24(sc[i], P[i]);
+          sp[i] = sc[i];
+          if constexpr (T == 14) sp1[i] = sc1[i];
         }
       }
     }
@@ -989,8 +1049,10 @@ __global__ __launch_bounds__(64 * W) void mkq_wide_kernel(MMArgs a) {
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, tid = threadIdx.x;
   const int SB = a.K / 256;
+  // grid.y > 1 (EPI_SLAB): this work-group's K range of super-blocks [kb, kb + nsb)
+  const int kb = SB * blockIdx.y / gridDim.y, nsb = SB * (blockIdx.y + 1) / gridDim.y - kb;
   const int tile = blockIdx.x * W + w;
-  const uint8_t* Wr = reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[0] + (size_t)tile * SB * TB;
+  const uint8_t* Wr = reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[0] + ((size_t)tile * SB + kb) * TB;
 
   // staging: piece p < NQ = 16 B of q (token row p/16, segment p%16), else 16 B of the sums; tokens
   // >= M re-read token M-1 (outputs dropped); the ragged tail re-stages the last piece
@@ -1002,20 +1064,20 @@ __global__ __launch_bounds__(64 * W) void mkq_wide_kernel(MMArgs a) {
     const int p = min(tid + i * NT, PIECES - 1);
     if (p < NQ) {
       const int row = p / 16, rr = row < a.M ? row : a.M - 1;
-      xsrc[i] = reinterpret_cast<const u32x4*>(a.xq + (size_t)rr * a.K + (p % 16) * 16);
+      xsrc[i] = reinterpret_cast<const u32x4*>(a.xq + (size_t)rr * a.K + (size_t)kb * 256 + (p % 16) * 16);
       xstep[i] = 16;  // u32x4 per super-block
       xdst[i] = row * QP + (p % 16) * 16;
       xq_piece[i] = true;
     } else {
       const int q = p - NQ, row = q / 2, rr = row < a.M ? row : a.M - 1;
-      xsrc[i] = reinterpret_cast<const u32x4*>(a.xb + (size_t)rr * (a.K / 32) + (q % 2) * 4);
+      xsrc[i] = reinterpret_cast<const u32x4*>(a.xb + (size_t)rr * (a.K / 32) + kb * 8 + (q % 2) * 4);
       xstep[i] = 2;
       xdst[i] = row * 32 + (q % 2) * 16;
       xq_piece[i] = false;
     }
   }
   const int drow = tid < ROWS ? (tid < a.M ? tid : a.M - 1) : 0;
-  const float* dsrc = a.xd + (size_t)drow * SB;
+  const float* dsrc = a.xd + (size_t)drow * SB + kb;
   u32x4 xr[2][PPT];
   float xdr[2];
   auto load_x = [&](int set, int sb) {
@@ -1043,10 +1105,11 @@ __global__ __launch_bounds__(64 * W) void mkq_wide_kernel(MMArgs a) {
 #pragma unroll
   for (int n = 0; n < NB; ++n) acc[0][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // super-block indices below are relative to kb
   load_x(0, 0);
-  load_x(1, SB > 1 ? 1 : 0);
+  load_x(1, nsb > 1 ? 1 : 0);
 #pragma unroll
-  for (int u = 0; u < U; ++u) load_w(ring[u], u < SB ? u : SB - 1);
+  for (int u = 0; u < U; ++u) load_w(ring[u], u < nsb ? u : nsb - 1);
   store_x(0, 0);
   __syncthreads();
 
@@ -1055,7 +1118,7 @@ __global__ __launch_bounds__(64 * W) void mkq_wide_kernel(MMArgs a) {
     constexpr int H = decltype(Hc)::value;
     constexpr int R = decltype(Rc)::value;
     const int buf = sb & 1;
-    load_x(H, sb + 2 < SB ? sb + 2 : SB - 1);
+    load_x(H, sb + 2 < nsb ? sb + 2 : nsb - 1);
     Frag& f = ring[R];
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
@@ -1066,7 +1129,7 @@ __global__ __launch_bounds__(64 * W) void mkq_wide_kernel(MMArgs a) {
       if constexpr (T != 14) f.xb[n] = *reinterpret_cast<const f32x2*>(&ssb[buf][row][2 * g]);
     }
     kq_compute<T, 1, NB>(acc, f, g);
-    load_w(f, min(sb + U, SB - 1));  // past the end: re-read the last super-block (no branch)
+    load_w(f, min(sb + U, nsb - 1));  // past the end: re-read the last super-block (no branch)
     store_x(1 - H, buf ^ 1);
     __syncthreads();
     __builtin_amdgcn_sched_barrier(0);  // nothing moves across super-blocks (interleaving them spills)
@@ -1075,14 +1138,14 @@ __global__ __launch_bounds__(64 * W) void mkq_wide_kernel(MMArgs a) {
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
-  // SB % U == 0 (launch_kq_wide): no data-dependent branch in the loop -- at a branch join hipcc
-  // merges wait counts conservatively, which drains the weight ring
-  for (int sb = 0; sb < SB; sb += U) {
+  // (the ring refill is unconditional -- a refill behind a branch made hipcc drain the ring at the
+  // join -- while whole steps sit behind uniform guards, which keeps its register use in bounds)
+  for (int sb = 0; sb < nsb; sb += U) {
     step(I0{}, I0{}, sb);
-    if (sb + 1 < SB) step(I1{}, I1{}, sb + 1);
+    if (sb + 1 < nsb) step(I1{}, I1{}, sb + 1);
     if constexpr (U == 4) {
-      if (sb + 2 < SB) step(I0{}, I2{}, sb + 2);
-      if (sb + 3 < SB) step(I1{}, I3{}, sb + 3);
+      if (sb + 2 < nsb) step(I0{}, I2{}, sb + 2);
+      if (sb + 3 < nsb) step(I1{}, I3{}, sb + 3);
     }
   }
 
@@ -1097,14 +1160,17 @@ __global__ __launch_bounds__(64 * W) void mkq_wide_kernel(MMArgs a) {
     }
     const int col = n * 16 + (lane & 15);
     if (col >= a.M || (EPI == EPI_SWIGLU && lane >= 32)) continue;
-    epi_store<EPI>(a, tile, lane, col, s, up);
+    if constexpr (EPI == EPI_SLAB)  // partial over this K range: slab blockIdx.y [token][N]
+      *reinterpret_cast<f32x4*>(a.out + blockIdx.y * a.slab_stride + (size_t)col * a.ldo + tile * 16 + (lane >> 4) * 4) = s;
+    else
+      epi_store<EPI>(a, tile, lane, col, s, up);
   }
 }
 
 // two column tiles (17..32 tokens); ring 4 deep for Q4_K / Q5_K, 2 for Q6_K (its 4-deep ring spills)
 template <int T, int W, int EPI>
-static void launch_kq_wide_t(const MMArgs& a, int ntiles, hipStream_t s) {
-  mkq_wide_kernel<T, W, 2, EPI, T == 14 ? 2 : 4><<<ntiles / W, 64 * W, 0, s>>>(a);
+static void launch_kq_wide_t(const MMArgs& a, int ntiles, hipStream_t s, int ksplit = 1) {
+  mkq_wide_kernel<T, W, 2, EPI, T == 14 ? 2 : 4><<<dim3(ntiles / W, ksplit), 64 * W, 0, s>>>(a);
 }
 
 template <int EPI>
@@ -1131,6 +1197,29 @@ static int launch_kq_wide(int epi, const MMArgs& a, int ntiles, hipStream_t s) {
   if (epi == EPI_SWIGLU) return launch_kq_wide_epi<EPI_SWIGLU>(a, ntiles, s);
   if (epi == EPI_F32) return launch_kq_wide_epi<EPI_F32>(a, ntiles, s);
   return -1;
+}
+
+// 17..32 tokens, attn_output / ffn_down of a K-quant file (256 tiles for h 4096): 4-wave groups with K
+// split over grid.y until ~256 work-groups, partials into slabs [ksplit][token][N] that the next
+// RMS_NORM + Q8_K launch (launch_rmsnorm_q8k with slabs) folds into the residual stream in slab
+// order.  Returns the split, or -1 (the caller runs mkq_kernel's in-place EPI_RESID instead).
+int launch_mkq_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s) {
+  static const bool off = getenv("MX_NO_KQ_WIDE") != nullptr || getenv("MX_NO_KQ_SLAB") != nullptr;
+  if (off || a.M <= 16 || a.M > 32 || a.kq_n != 1 || !a.xq || !a.xd || !a.xb || a.K % 256 || a.N % 64) return -1;
+  const int ntiles = a.N / TILE_N, SB = a.K / 256;
+  int ks = 1;
+  while (ks < 8 && (ntiles / 4) * ks * 2 <= 256 && SB / (ks * 2) >= 4) ks *= 2;
+  if (ks < 2) return -1;
+  MMArgs p = a;
+  p.out = slabs;
+  p.ldo = a.N;
+  p.slab_stride = slab_stride;
+  const int t = a.kq_type[0];
+  if (t == 12) launch_kq_wide_t<12, 4, EPI_SLAB>(p, ntiles, s, ks);
+  else if (t == 13) launch_kq_wide_t<13, 4, EPI_SLAB>(p, ntiles, s, ks);
+  else if (t == 14) launch_kq_wide_t<14, 4, EPI_SLAB>(p, ntiles, s, ks);
+  else return -1;
+  return ks;
 }
 
 bool mkq_can_quantize_on_load(int M, int K, bool norm) {
