@@ -1185,8 +1185,18 @@ int mx_engine::enqueue_forward_kq(int M, const int* pos, const int* slot, void* 
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
     a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
     a.slot_stride = slot_stride;
-    if (launch_mkq(EPI_QKV, a, s)) return fail(MX_ERR_ARG, "kq qkv launch shape");
     AttnArgs at{};
+    // 17..32 rows: q|k|v as split-K slabs, finished by the attention kernel (distinct sequences) or
+    // by launch_qkv_finish
+    const int qs = (!ql && M > 16 && M <= 32) ? launch_mkq_qkv_slab(a, slabs, slab_stride, s) : -1;
+    if (qs > 0 && rows_distinct) {
+      at.slabs = slabs; at.nslab = qs; at.slab_stride = slab_stride; at.rope_cs = rope_cs; at.kc_w = kc;
+      at.vc_w = vc;
+    } else if (qs > 0) {
+      launch_qkv_finish(a, slabs, qs, slab_stride, s);
+    } else if (launch_mkq(EPI_QKV, a, s)) {
+      return fail(MX_ERR_ARG, "kq qkv launch shape");
+    }
     at.q = q; at.kc = kc; at.vc = vc; at.pos = pos; at.slot = slot;
     at.outf = attn_f; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
     at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;

@@ -201,6 +201,10 @@ int launch_mkq(int epi, const MMArgs& a, hipStream_t s);
 // 17..32 tokens, attn_output / ffn_down: split-K partials into slabs ([ks][token][N], slab_stride apart)
 // for launch_rmsnorm_q8k to fold; returns ks, or -1 when the shape has no such form (use launch_mkq)
 int launch_mkq_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s);
+// 17..32 tokens, q|k|v: split-K partial slabs for the attention's FIN path or launch_qkv_finish
+int launch_mkq_qkv_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s);
+// q/k/v split-K partial slabs -> sum in slab order -> RoPE + q / KV-cache stores (EPI_QKV's epilogue)
+void launch_qkv_finish(const MMArgs& a, const float* slabs, int nslab, size_t slab_stride, hipStream_t s);
 // packed K-quant matrix (segments as in MMArgs) -> packed bf16 tiles [N/16][K/32] x 1 KiB (prefill GEMM)
 int launch_dequant_kq(uint16_t* dst, const void* W, int K, int kq_n, const int* type, const int* tile_end,
                       const size_t* off, hipStream_t s);

@@ -909,6 +909,11 @@ __global__ __launch_bounds__(256) void qkv_finish_kernel(MMArgs a, const float* 
   }
 }
 
+void launch_qkv_finish(const MMArgs& a, const float* slabs, int nslab, size_t stride, hipStream_t s) {
+  const int total = a.M * (a.n_q + 2 * a.n_kv) / 4;
+  qkv_finish_kernel<<<(total + 255) / 256, 256, 0, s>>>(a, slabs, nslab, stride);
+}
+
 void launch_resid_norm(uint16_t* y, int ldy, float* x, const float* slabs, int nslab, size_t stride, const float* w,
                        int M, int n, float eps, hipStream_t s) {
   launch_norm_impl(y, ldy, x, slabs, nslab, stride, w, nullptr, M, n, eps, s);

@@ -1033,7 +1033,7 @@ static void launch_mkq_epi(const MMArgs& a, int ntiles, hipStream_t s) {
 // Single-type matrices (one segment): gate/up and the lm_head of a K-quant file.
 // ---------------------------------------------------------------------------
 template <int T, int W, int NB, int EPI, int U>
-__global__ __launch_bounds__(64 * W) void mkq_wide_kernel(MMArgs a) {
+__device__ __forceinline__ void mkq_wide_body(const MMArgs& a, int tile, const uint8_t* Wseg, int tile_in_seg) {
   constexpr int TB = KqTile<T>::BYTES;
   constexpr int ROWS = 16 * NB;
   constexpr int QP = 256 + 16;  // int8 per LDS row: +16 B keeps the 16 token rows' fragment reads conflict-free
@@ -1051,8 +1051,7 @@ __global__ __launch_bounds__(64 * W) void mkq_wide_kernel(MMArgs a) {
   const int SB = a.K / 256;
   // grid.y > 1 (EPI_SLAB): this work-group's K range of super-blocks [kb, kb + nsb)
   const int kb = SB * blockIdx.y / gridDim.y, nsb = SB * (blockIdx.y + 1) / gridDim.y - kb;
-  const int tile = blockIdx.x * W + w;
-  const uint8_t* Wr = reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[0] + ((size_t)tile * SB + kb) * TB;
+  const uint8_t* Wr = Wseg + ((size_t)tile_in_seg * SB + kb) * TB;
 
   // staging: piece p < NQ = 16 B of q (token row p/16, segment p%16), else 16 B of the sums; tokens
   // >= M re-read token M-1 (outputs dropped); the ragged tail re-stages the last piece
@@ -1167,6 +1166,30 @@ __global__ __launch_bounds__(64 * W) void mkq_wide_kernel(MMArgs a) {
   }
 }
 
+template <int T, int W, int NB, int EPI, int U>
+__global__ __launch_bounds__(64 * W) void mkq_wide_kernel(MMArgs a) {
+  const int tile = blockIdx.x * W + (threadIdx.x >> 6);
+  mkq_wide_body<T, W, NB, EPI, U>(a, tile, reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[0], tile);
+}
+
+// A matrix of up to 3 row segments of different types (q|k Q4_K + v Q6_K): every segment boundary is
+// a multiple of W, so a work-group's W tiles share one type, dispatched at run time (the kernel's
+// registers are those of its largest body, Q6_K)
+template <int W, int NB, int EPI>
+__global__ __launch_bounds__(64 * W) void mkq_wide_seg_kernel(MMArgs a) {
+  const int t0 = blockIdx.x * W;
+  int seg = 0;
+  while (seg < a.kq_n - 1 && t0 >= a.kq_tile_end[seg]) ++seg;
+  const int tb = seg ? a.kq_tile_end[seg - 1] : 0;
+  const int tile = t0 + (threadIdx.x >> 6);
+  const uint8_t* Ws = reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[seg];
+  switch (a.kq_type[seg]) {
+    case 12: mkq_wide_body<12, W, NB, EPI, 4>(a, tile, Ws, tile - tb); break;
+    case 13: mkq_wide_body<13, W, NB, EPI, 4>(a, tile, Ws, tile - tb); break;
+    case 14: mkq_wide_body<14, W, NB, EPI, 2>(a, tile, Ws, tile - tb); break;
+  }
+}
+
 // two column tiles (17..32 tokens); ring 4 deep for Q4_K / Q5_K, 2 for Q6_K (its 4-deep ring spills)
 template <int T, int W, int EPI>
 static void launch_kq_wide_t(const MMArgs& a, int ntiles, hipStream_t s, int ksplit = 1) {
@@ -1219,6 +1242,25 @@ int launch_mkq_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipStream
   else if (t == 13) launch_kq_wide_t<13, 4, EPI_SLAB>(p, ntiles, s, ks);
   else if (t == 14) launch_kq_wide_t<14, 4, EPI_SLAB>(p, ntiles, s, ks);
   else return -1;
+  return ks;
+}
+
+// 17..32 tokens, q|k|v of a K-quant file (segments of different types): 4-wave groups, K split in two,
+// partial slabs [2][token][N] that the decode attention (FIN) or launch_qkv_finish completes.
+// Returns the split or -1 (the caller runs mkq_kernel's EPI_QKV instead).
+int launch_mkq_qkv_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s) {
+  static const bool off = getenv("MX_NO_KQ_WIDE") != nullptr || getenv("MX_NO_KQ_SLAB") != nullptr;
+  if (off || a.M <= 16 || a.M > 32 || !a.xq || !a.xd || !a.xb || a.K % 256 || a.N % 64) return -1;
+  for (int i = 0; i < a.kq_n; ++i)
+    if (a.kq_tile_end[i] % 4) return -1;
+  const int ntiles = a.N / TILE_N, SB = a.K / 256;
+  int ks = 1;
+  while (ks < 8 && (ntiles / 4) * ks * 2 <= 256 && SB / (ks * 2) >= 4) ks *= 2;
+  MMArgs p = a;
+  p.out = slabs;
+  p.ldo = a.N;
+  p.slab_stride = slab_stride;
+  mkq_wide_seg_kernel<4, 2, EPI_SLAB><<<dim3(ntiles / 4, ks), 256, 0, s>>>(p);
   return ks;
 }
 

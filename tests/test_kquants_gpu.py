@@ -282,6 +282,14 @@ def test_kq_wide_lds_gemv_vs_grouped_and_oracle(mx, oracle_mod, monkeypatch, nam
     o = np.stack([om.context(64).eval(p, 0)[0] for p in prompts])
     assert_logits_close(got, o, f"{name} {ftype} wide M={M}")
     assert_tokens_match(got, o, f"{name} {ftype} wide M={M}")
+    # M rows of ONE sequence (a prompt chunk): the q|k|v slabs are finished by launch_qkv_finish
+    # before the attention (rows attend to each other's new K/V)
+    seq = np.concatenate([[1], rng.integers(3, shape.n_vocab, M - 1)]).astype(np.int32)
+    eng = mx.Engine(f"synthetic:{name}:seed=0:{ftype}", n_ctx=64, n_seq_max=2)
+    g1 = eng.forward_logits(seq, 0, slot=0)
+    eng.close()
+    o1 = om.context(64).eval(seq, 0, all_logits=True)
+    assert_logits_close(g1, o1, f"{name} {ftype} one-sequence chunk M={M}")
 
 
 @pytest.mark.parametrize("name,ftype,n_prompt", [("test-d128", "q4_k_m", 300), ("test-h4096", "q5_k_m", 200),
