@@ -2357,6 +2357,163 @@ static int launch_mq8_ql_epi(const MMArgs& a, hipStream_t s) {
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Q8_0 GEMV for 17..32 tokens with the activations shared through LDS (mkq_wide_kernel's scheme in
+// kquant.hip): each wave owns one 16-row tile over the whole K; the W waves of a work-group share
+// each staged 256-k chunk of Q8_0 activation rows (32 tokens x 256 q, k permuted within 64-k groups
+// as q8_perm; + the 8 block scales per token), double-buffered in LDS with the next-but-one chunk
+// in registers, and each wave keeps a U-chunk ring of its weight tiles (4 Q8 tiles per chunk) in
+// flight.  Per 64-k tile the arithmetic is mq8_kernel's (two exact int32 block products, each
+// scaled by d_w * d_x in f32); the whole K stays in one wave, so the epilogue runs from registers.
+// ---------------------------------------------------------------------------
+template <int W, int EPI, int U>
+__global__ __launch_bounds__(64 * W) void mq8_wide_kernel(MMArgs a) {
+  constexpr int NB = 2, ROWS = 32;
+  constexpr int QP = 256 + 16;     // int8 per LDS row (+16 B: conflict-free fragment reads)
+  constexpr int NQ = ROWS * 16;    // 16-B pieces of q per chunk
+  constexpr int ND = ROWS * 2;     // 16-B pieces of the block scales (8 floats per token)
+  constexpr int PIECES = NQ + ND;
+  constexpr int NT = 64 * W;
+  constexpr int PPT = (PIECES + NT - 1) / NT;
+  static_assert(U == 2 || U == 4, "ring depth");
+  __shared__ __attribute__((aligned(16))) int8_t sq[2][ROWS][QP];
+  __shared__ __attribute__((aligned(16))) float sd[2][ROWS][8];
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
+  const int KT = a.K / Q8_TILE_K, NCH = a.K / 256;
+  const int tile = blockIdx.x * W + w;
+  const uint8_t* Wt = reinterpret_cast<const uint8_t*>(a.W) + (size_t)tile * KT * Q8_TILE_BYTES;
+
+  const u32x4* xsrc[PPT];
+  int xstep[PPT], xdst[PPT];
+  bool xq_piece[PPT];
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int p = min(tid + i * NT, PIECES - 1);
+    if (p < NQ) {
+      const int row = p / 16, rr = row < a.M ? row : a.M - 1;
+      xsrc[i] = reinterpret_cast<const u32x4*>(a.xq + (size_t)rr * a.K + (p % 16) * 16);
+      xstep[i] = 16;
+      xdst[i] = row * QP + (p % 16) * 16;
+      xq_piece[i] = true;
+    } else {
+      const int q = p - NQ, row = q / 2, rr = row < a.M ? row : a.M - 1;
+      xsrc[i] = reinterpret_cast<const u32x4*>(a.xd + (size_t)rr * (a.K / 32) + (q % 2) * 4);
+      xstep[i] = 2;
+      xdst[i] = row * 32 + (q % 2) * 16;
+      xq_piece[i] = false;
+    }
+  }
+  u32x4 xr[2][PPT];
+  auto load_x = [&](int set, int ch) {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) xr[set][i] = xsrc[i][ch * xstep[i]];
+  };
+  auto store_x = [&](int set, int buf) {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      uint8_t* base = xq_piece[i] ? reinterpret_cast<uint8_t*>(&sq[buf][0][0]) : reinterpret_cast<uint8_t*>(&sd[buf][0][0]);
+      *reinterpret_cast<u32x4*>(base + xdst[i]) = xr[set][i];
+    }
+  };
+  struct Frag {
+    u32x4 q[4], d[4];  // the chunk's 4 Q8 tiles: int8 operands, f16 block scales of this lane's row group
+  };
+  Frag ring[U];
+  auto load_w = [&](Frag& f, int ch) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint8_t* t = Wt + (size_t)(ch * 4 + k) * Q8_TILE_BYTES;
+      f.q[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t) + lane);
+      f.d[k] = *reinterpret_cast<const u32x4*>(t + 1024 + 16 * (lane >> 4));
+    }
+  };
+  f32x4 acc[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_x(0, 0);
+  load_x(1, NCH > 1 ? 1 : 0);
+#pragma unroll
+  for (int u = 0; u < U; ++u) load_w(ring[u], u < NCH ? u : NCH - 1);
+  store_x(0, 0);
+  __syncthreads();
+
+  auto step = [&](auto Hc, auto Rc, int ch) {
+    constexpr int H = decltype(Hc)::value;
+    constexpr int R = decltype(Rc)::value;
+    const int buf = ch & 1;
+    load_x(H, ch + 2 < NCH ? ch + 2 : NCH - 1);
+    const Frag f = ring[R];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const long a0 = (long)(((unsigned long)f.q[k][1] << 32) | f.q[k][0]);
+      const long a1 = (long)(((unsigned long)f.q[k][3] << 32) | f.q[k][2]);
+      const f16x8 dw = __builtin_bit_cast(f16x8, f.d[k]);
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        const int row = n * 16 + (lane & 15);
+        const u32x4 xb = *reinterpret_cast<const u32x4*>(&sq[buf][row][k * 64 + (lane >> 4) * 16]);
+        const f32x2 dx = *reinterpret_cast<const f32x2*>(&sd[buf][row][2 * k]);
+        const long b0 = (long)(((unsigned long)xb[1] << 32) | xb[0]);
+        const long b1 = (long)(((unsigned long)xb[3] << 32) | xb[2]);
+        const i32x4 p0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, b0, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        const i32x4 p1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, b1, i32x4{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[n][i] = fmaf((float)dw[i] * dx[0], (float)p0[i], acc[n][i]);
+          acc[n][i] = fmaf((float)dw[4 + i] * dx[1], (float)p1[i], acc[n][i]);
+        }
+      }
+    }
+    load_w(ring[R], min(ch + U, NCH - 1));  // past the end: re-read the last chunk (no branch)
+    store_x(1 - H, buf ^ 1);
+    __syncthreads();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  for (int ch = 0; ch < NCH; ch += U) {
+    step(I0{}, I0{}, ch);
+    if (ch + 1 < NCH) step(I1{}, I1{}, ch + 1);
+    if constexpr (U == 4) {
+      if (ch + 2 < NCH) step(I0{}, I2{}, ch + 2);
+      if (ch + 3 < NCH) step(I1{}, I3{}, ch + 3);
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    const f32x4 sv = acc[n];
+    f32x4 up = sv;
+    if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(sv[i], 32);
+    }
+    const int col = n * 16 + (lane & 15);
+    if (col >= a.M || (EPI == EPI_SWIGLU && lane >= 32)) continue;
+    epi_store<EPI>(a, tile, lane, col, sv, up);
+  }
+}
+
+// 17..32 tokens, gate/up or lm_head of a Q8_0 file: the LDS-shared form (MX_NO_Q8_WIDE=1: mq8_kernel)
+static int launch_mq8_wide(int epi, const MMArgs& a, hipStream_t s) {
+  static const bool off = getenv("MX_NO_Q8_WIDE") != nullptr;
+  const int ntiles = a.N / TILE_N;
+  if (off || a.M <= 16 || a.M > 32 || !a.xq || !a.xd || a.K % 256) return -1;
+  if (epi != EPI_SWIGLU && epi != EPI_F32) return -1;
+  auto go = [&](auto wc) {
+    constexpr int W = decltype(wc)::value;
+    if (epi == EPI_SWIGLU) mq8_wide_kernel<W, EPI_SWIGLU, 2><<<ntiles / W, 64 * W, 0, s>>>(a);
+    else mq8_wide_kernel<W, EPI_F32, 2><<<ntiles / W, 64 * W, 0, s>>>(a);
+    return 0;
+  };
+  if (ntiles % 7 == 0 && ntiles / 7 >= 200) return go(std::integral_constant<int, 7>{});
+  if (ntiles % 8 == 0 && ntiles / 8 >= 200) return go(std::integral_constant<int, 8>{});
+  if (ntiles % 4 == 0) return go(std::integral_constant<int, 4>{});
+  return -1;
+}
+
 int launch_mq8(int epi, const MMArgs& a, hipStream_t s) {
   if (a.M < 1 || a.K % Q8_TILE_K || a.N % TILE_N) return -1;
   if (epi == EPI_SWIGLU && !a.actf && !a.act) return -1;
@@ -2373,6 +2530,7 @@ int launch_mq8(int epi, const MMArgs& a, hipStream_t s) {
     return -1;
   }
   if (!a.xd) return -1;
+  if (launch_mq8_wide(epi, a, s) == 0) return 0;
   switch (epi) {
     case EPI_F32: return launch_mq8_epi<EPI_F32>(a, s);
     case EPI_RESID: return launch_mq8_epi<EPI_RESID>(a, s);

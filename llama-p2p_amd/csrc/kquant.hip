@@ -284,35 +284,34 @@ __device__ __forceinline__ void q8k_row(const float (&v)[16], int t, int8_t* qsb
 // (resid_norm's order), the sum of squares taken over the folded row and the folded values written
 // back to x by the thread that quantises them.
 template <bool NORM, bool FOLD>
-__global__ __launch_bounds__(256) void q8k_kernel(int8_t* xq, float* xd, float* xb, const float* src, int ld,
-                                                  const float* w, const int* row_map, int n, float eps,
-                                                  const float* slabs, int nslab, size_t sstride) {
+__global__ __launch_bounds__(FOLD ? 1024 : 256) void q8k_kernel(int8_t* xq, float* xd, float* xb, const float* src,
+                                                                int ld, const float* w, const int* row_map, int n,
+                                                                float eps, const float* slabs, int nslab,
+                                                                size_t sstride) {
   const int c = blockIdx.y;
   const int r = row_map ? row_map[c] : c;
   const float* xr = src + (size_t)r * ld;
-  auto fold = [&](f32x4 v, int i) -> f32x4 {  // all slab loads issued before the adds (one round trip)
-    if constexpr (!FOLD) return v;
-    f32x4 sl[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (k < nslab) sl[k] = *reinterpret_cast<const f32x4*>(slabs + k * sstride + (size_t)c * n + i);
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (k < nslab) v += sl[k];
-    return v;
-  };
   float scale = 1.0f;
+  // FOLD (n <= 4096, 1024 threads, NORM): one 4-value piece per thread, x and every slab loaded at once,
+  // folded x written back to x and staged in LDS for the quantisation below
+  __shared__ __attribute__((aligned(16))) float xf[FOLD ? 4096 : 1];
   if constexpr (NORM) {
     double acc = 0.0;
-    if constexpr (FOLD) {  // n <= 4096: 4 pieces per thread, every load in flight at once
+    if constexpr (FOLD) {
+      const int i = threadIdx.x * 4;
+      if (i < n) {
+        f32x4 sl[8];
 #pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        const int i = threadIdx.x * 4 + 1024 * it;
-        if (i < n) {
-          const f32x4 v = fold(*reinterpret_cast<const f32x4*>(xr + i), i);
+        for (int k = 0; k < 8; ++k)
+          if (k < nslab) sl[k] = *reinterpret_cast<const f32x4*>(slabs + k * sstride + (size_t)c * n + i);
+        f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc += (double)(v[j] * v[j]);
-        }
+        for (int k = 0; k < 8; ++k)
+          if (k < nslab) v += sl[k];  // resid_norm's order
+        *reinterpret_cast<f32x4*>(const_cast<float*>(xr) + i) = v;
+        *reinterpret_cast<f32x4*>(xf + i) = v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc += (double)(v[j] * v[j]);
       }
     } else {
       for (int i = threadIdx.x * 4; i < n; i += 1024) {
@@ -322,10 +321,13 @@ __global__ __launch_bounds__(256) void q8k_kernel(int8_t* xq, float* xd, float* 
       }
     }
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-    __shared__ double part[4];
+    constexpr int NWV = FOLD ? 16 : 4;
+    __shared__ double part[NWV];
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
     __syncthreads();
-    const double sum = part[0] + part[1] + part[2] + part[3];
+    double sum = 0.0;
+#pragma unroll
+    for (int k = 0; k < NWV; ++k) sum += part[k];
     scale = 1.0f / sqrtf((float)(sum / n) + eps);
   }
   const int s = 16 * blockIdx.x + (threadIdx.x >> 4);
@@ -335,10 +337,9 @@ __global__ __launch_bounds__(256) void q8k_kernel(int8_t* xq, float* xd, float* 
 #pragma unroll
   for (int i = 0; i < 16; i += 4) {
     const int k = 256 * s + 16 * t + i;
-    const f32x4 x4 = fold(*reinterpret_cast<const f32x4*>(xr + k), k);
-    if constexpr (FOLD) *reinterpret_cast<f32x4*>(const_cast<float*>(xr) + k) = x4;  // every read of x is behind the barrier
+    const f32x4 x4 = FOLD ? *reinterpret_cast<const f32x4*>(xf + k) : *reinterpret_cast<const f32x4*>(xr + k);
     if constexpr (NORM) {
-      const f32x4 g4 = *reinterpret_cast<const f32x4*>(w + 256 * s + 16 * t + i);
+      const f32x4 g4 = *reinterpret_cast<const f32x4*>(w + k);
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[i + e] = (x4[e] * scale) * g4[e];
     } else {
@@ -354,7 +355,7 @@ int launch_rmsnorm_q8k(int8_t* xq, float* xd, float* xb, const float* x, const f
   if (n % 256 || M < 1) return -1;
   if (nslab && (row_map || n > 16 * 256 || !slabs)) return -1;  // the fold needs one work-group per row
   if (nslab)
-    q8k_kernel<true, true><<<dim3(1, M), 256, 0, s>>>(xq, xd, xb, x, n, w, row_map, n, eps, slabs, nslab, slab_stride);
+    q8k_kernel<true, true><<<dim3(1, M), 1024, 0, s>>>(xq, xd, xb, x, n, w, row_map, n, eps, slabs, nslab, slab_stride);
   else
     q8k_kernel<true, false><<<dim3((n / 256 + 15) / 16, M), 256, 0, s>>>(xq, xd, xb, x, n, w, row_map, n, eps,
                                                                         nullptr, 0, 0);

@@ -130,3 +130,37 @@ def test_q8_batch_greedy_loop_vs_oracle(mx, oracle_mod):
         assert check_greedy_chain(om.context(128), p, [first[i]] + toks[i].tolist(), f"q8 seq {i}") >= G
     b.close()
     eng.close()
+
+
+@pytest.mark.parametrize("name,M", [("test-8b-ffn", 32), ("test-8b-v128k", 24), ("test-d128", 17)])
+def test_q8_wide_lds_gemv_vs_grouped_and_oracle(mx, oracle_mod, monkeypatch, name, M):
+    """17-32 rows of a Q8_0 gate/up or lm_head (Llama-3-8B: 1792 gate/up tiles on 7-wave groups, 8016
+    lm_head tiles on 8-wave groups) run mq8_wide_kernel, a 256-k chunk of Q8_0 activation rows shared
+    by the group's waves through LDS.  Against mq8_kernel (MX_NO_Q8_WIDE=1): the same exact block
+    products and scales, summed over K in one wave instead of several K-slices -- within twice the
+    bf16 tolerance; against the oracle's Q8_0 forward within the bf16 tolerance."""
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES[name]
+    rng = np.random.default_rng(M)
+    prompts = [np.concatenate([[1], rng.integers(3, shape.n_vocab, int(rng.integers(3, 8)))]).astype(np.int32)
+               for _ in range(M)]
+
+    def run():
+        eng = mx.Engine(f"synthetic:{name}:seed=0:q8_0", n_ctx=64, n_seq_max=M)
+        for i, p in enumerate(prompts):
+            eng.forward_logits(p[:-1], 0, slot=i)
+        out = eng.forward_rows(list(range(M)), [len(p) - 1 for p in prompts], [int(p[-1]) for p in prompts])
+        eng.close()
+        return out
+
+    got = run()
+    monkeypatch.setenv("MX_NO_Q8_WIDE", "1")
+    ref = run()
+    monkeypatch.delenv("MX_NO_Q8_WIDE")
+    tol2 = 2 * (1e-2 * np.abs(ref) + 2e-2 * np.abs(ref).max(axis=-1, keepdims=True))
+    assert (np.abs(got - ref) <= tol2).all()
+    om = _oracle_q8(oracle_mod, shape, 0)
+    o = np.stack([om.context(64).eval(p, 0)[0] for p in prompts])
+    assert_logits_close(got, o, f"{name} q8_0 wide M={M}")
+    assert_tokens_match(got, o, f"{name} q8_0 wide M={M}")
