@@ -1073,14 +1073,30 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
   const bool ql = q8_on_load(M);
   static const int no_ql_mask = getenv("MX_Q8_NO_QL_MASK") ? atoi(getenv("MX_Q8_NO_QL_MASK")) : 0;  // probe
   int site = 0;  // 1 qkv, 2 attn_output, 4 gate/up, 8 down, 16 lm_head
+  // 17..32 rows: attn_output / ffn_down as split-K slabs (launch_mq8_slab) folded by the next
+  // RMS_NORM + quantise launch; nslab = partials not yet folded into x
+  int nslab = 0;
   auto operand = [&](MMArgs& m, const float* src, int K, const float* norm_w, int rows, const int* rmap) {
     if (ql && !rmap && !(no_ql_mask & site)) {
       m.xq = nullptr; m.xf = src; m.norm_w = norm_w; m.eps = eps; m.ssq = norm_w ? ssq : nullptr; m.np = K / 16;
     } else {
-      if (norm_w) launch_rmsnorm_q8(xq8, xqd, src, norm_w, rmap, rows, K, eps, s);
-      else launch_quantize_q8(xq8, xqd, src, K, rows, K, s);
+      if (norm_w && src == x && nslab) {
+        launch_rmsnorm_q8(xq8, xqd, src, norm_w, rmap, rows, K, eps, s, slabs, nslab, slab_stride);
+        nslab = 0;
+      } else if (norm_w) {
+        launch_rmsnorm_q8(xq8, xqd, src, norm_w, rmap, rows, K, eps, s);
+      } else {
+        launch_quantize_q8(xq8, xqd, src, K, rows, K, s);
+      }
       m.xq = xq8; m.xd = xqd;
     }
+  };
+  auto resid = [&](MMArgs& m) -> int {
+    if (!ql && M > 16 && M <= 32) {
+      const int ks = launch_mq8_slab(m, slabs, slab_stride, s);
+      if (ks > 0) return nslab = ks, 0;
+    }
+    return launch_mq8(EPI_RESID, m, s);
   };
   for (int li = 0; li < (int)layers.size(); li++) {
     const Layer& L = layers[li];
@@ -1093,8 +1109,16 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
     a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
     a.slot_stride = slot_stride;
-    if (launch_mq8(EPI_QKV, a, s)) return fail(MX_ERR_ARG, "q8 qkv launch shape");
     AttnArgs at{};
+    const int qs = (!ql && M > 16 && M <= 32) ? launch_mq8_slab(a, slabs, slab_stride, s) : -1;
+    if (qs > 0 && rows_distinct) {  // the attention kernel finishes q/k/v from the split-K slabs
+      at.slabs = slabs; at.nslab = qs; at.slab_stride = slab_stride; at.rope_cs = rope_cs; at.kc_w = kc;
+      at.vc_w = vc;
+    } else if (qs > 0) {
+      launch_qkv_finish(a, slabs, qs, slab_stride, s);
+    } else if (launch_mq8(EPI_QKV, a, s)) {
+      return fail(MX_ERR_ARG, "q8 qkv launch shape");
+    }
     at.q = q; at.kc = kc; at.vc = vc; at.pos = pos; at.slot = slot;
     at.outf = attn_f; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
     at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;
@@ -1106,7 +1130,7 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     site = 2;
     operand(b, attn_f, h, nullptr, M, nullptr);
     b.ssq = ql ? ssq : nullptr; b.np = h / 16;  // partials of the new residual for gate/up's norm
-    if (launch_mq8(EPI_RESID, b, s)) return fail(MX_ERR_ARG, "q8 attn_output launch shape");
+    if (resid(b)) return fail(MX_ERR_ARG, "q8 attn_output launch shape");
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.actf = act_f; c.lda = ff;
     site = 4;
@@ -1117,7 +1141,11 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     site = 8;
     operand(d, act_f, ff, nullptr, M, nullptr);
     d.ssq = ql ? ssq : nullptr; d.np = h / 16;  // for the next layer's qkv (or lm_head) norm
-    if (launch_mq8(EPI_RESID, d, s)) return fail(MX_ERR_ARG, "q8 ffn_down launch shape");
+    if (resid(d)) return fail(MX_ERR_ARG, "q8 ffn_down launch shape");
+  }
+  if (nslab && (x_out || !(head && !rowmap && n_out == M))) {  // x itself is read next: fold
+    launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);
+    nslab = 0;
   }
   if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
   if (head) {

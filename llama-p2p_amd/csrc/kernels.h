@@ -164,13 +164,17 @@ void launch_embed_q8(float* x, const uint8_t* tok_embd_blocks, const int* ids, i
                      hipStream_t s);
 // RMS_NORM + MUL, quantised to Q8_0 activation rows (xq [M][n], xd [M][n/32])
 void launch_rmsnorm_q8(int8_t* xq, float* xd, const float* x, const float* w, const int* row_map, int M, int n,
-                       float eps, hipStream_t s);
+                       float eps, hipStream_t s, const float* slabs = nullptr, int nslab = 0,
+                      size_t slab_stride = 0);  // nslab: fold the producer's split-K slabs into x first
 void launch_quantize_q8(int8_t* xq, float* xd, const float* src, int ld, int M, int n, hipStream_t s);
 // Q8_0 x Q8_0 products for any M (column groups of <= 64 tokens on grid.y), same epilogues.
 // a.xq == nullptr: quantise on load from f32 rows a.xf ([M][K]; RMS_NORM + MUL first when norm_w,
 // scale from the ssq partials), for mq8_can_quantize_on_load(M, K, norm_w != nullptr).  EPI_RESID writes ssq
 // partials when a.ssq.
 int launch_mq8(int epi, const MMArgs& a, hipStream_t s);
+// 17..32 tokens: split-K partial slabs ([ks][token][N]) for launch_rmsnorm_q8 to fold (attn_output /
+// ffn_down) or the attention / launch_qkv_finish to finish (q|k|v); ks, or -1 (use launch_mq8)
+int launch_mq8_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s);
 bool mq8_can_quantize_on_load(int M, int K, bool norm);
 
 // ---- K-quant weights (GGUF Q4_K 12, Q5_K 13, Q6_K 14), kquant.hip.  Packed tile =

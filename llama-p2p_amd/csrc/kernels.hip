@@ -2050,6 +2050,46 @@ __global__ __launch_bounds__(256) void norm_q8_kernel(int8_t* xq, float* xd, con
   }
 }
 
+// The same after folding the split-K slabs of the GEMV that wrote x (n <= 4096, 1024 threads, no
+// row_map): x += slab 0 + slab 1 + ... (resid_norm's order), written back; one 4-value piece per
+// thread with x and every slab loaded at once
+template <int NS>
+__global__ __launch_bounds__(1024) void norm_q8_fold_kernel(int8_t* xq, float* xd, float* x, const float* w, int n,
+                                                            float eps, const float* slabs, size_t sstride) {
+  const int c = blockIdx.x;
+  float* xr = x + (size_t)c * n;
+  const int i = threadIdx.x * 4;
+  f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+  double acc = 0.0;
+  if (i < n) {
+    f32x4 sl[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) sl[k] = *reinterpret_cast<const f32x4*>(slabs + k * sstride + (size_t)c * n + i);
+    v = *reinterpret_cast<const f32x4*>(xr + i);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) v += sl[k];
+    *reinterpret_cast<f32x4*>(xr + i) = v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc += (double)(v[j] * v[j]);
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  __shared__ double part[16];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  double sum = 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) sum += part[k];
+  const float scale = 1.0f / sqrtf((float)(sum / n) + eps);
+  if (i < n) {
+    const f32x4 g = *reinterpret_cast<const f32x4*>(w + i);
+    f32x4 y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = (v[j] * scale) * g[j];
+    q8_store_act(y, i, xq + (size_t)c * n, xd + (size_t)c * (n / 32));
+  }
+}
+
+
 __global__ __launch_bounds__(256) void quantize_q8_kernel(int8_t* xq, float* xd, const float* src, int ld, int n) {
   const int c = blockIdx.x;
   for (int i = threadIdx.x * 4; i < n; i += 1024)
@@ -2058,8 +2098,19 @@ __global__ __launch_bounds__(256) void quantize_q8_kernel(int8_t* xq, float* xd,
 }
 
 void launch_rmsnorm_q8(int8_t* xq, float* xd, const float* x, const float* w, const int* row_map, int M, int n,
-                       float eps, hipStream_t s) {
-  norm_q8_kernel<<<M, 256, 0, s>>>(xq, xd, x, w, row_map, n, eps);
+                       float eps, hipStream_t s, const float* slabs, int nslab, size_t slab_stride) {
+  if (nslab > 0 && (row_map || n > 4096 || (nslab != 1 && nslab != 2 && nslab != 4 && nslab != 8))) {  // fold first
+    launch_resid_norm(nullptr, 0, const_cast<float*>(x), slabs, nslab, slab_stride, nullptr, M, n, eps, s);
+    nslab = 0;
+  }
+  float* xw = const_cast<float*>(x);
+  switch (nslab) {  // (row_map / n > 4096 were folded above)
+    case 0: norm_q8_kernel<<<M, 256, 0, s>>>(xq, xd, x, w, row_map, n, eps); break;
+    case 1: norm_q8_fold_kernel<1><<<M, 1024, 0, s>>>(xq, xd, xw, w, n, eps, slabs, slab_stride); break;
+    case 2: norm_q8_fold_kernel<2><<<M, 1024, 0, s>>>(xq, xd, xw, w, n, eps, slabs, slab_stride); break;
+    case 4: norm_q8_fold_kernel<4><<<M, 1024, 0, s>>>(xq, xd, xw, w, n, eps, slabs, slab_stride); break;
+    default: norm_q8_fold_kernel<8><<<M, 1024, 0, s>>>(xq, xd, xw, w, n, eps, slabs, slab_stride); break;
+  }
 }
 void launch_quantize_q8(int8_t* xq, float* xd, const float* src, int ld, int M, int n, hipStream_t s) {
   quantize_q8_kernel<<<M, 256, 0, s>>>(xq, xd, src, ld, n);
@@ -2380,9 +2431,11 @@ __global__ __launch_bounds__(64 * W) void mq8_wide_kernel(MMArgs a) {
   __shared__ __attribute__((aligned(16))) float sd[2][ROWS][8];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
-  const int KT = a.K / Q8_TILE_K, NCH = a.K / 256;
+  const int KT = a.K / Q8_TILE_K;
+  // grid.y > 1 (EPI_SLAB): this work-group's K range of 256-k chunks [cb, cb + NCH)
+  const int NCHT = a.K / 256, cb = NCHT * blockIdx.y / gridDim.y, NCH = NCHT * (blockIdx.y + 1) / gridDim.y - cb;
   const int tile = blockIdx.x * W + w;
-  const uint8_t* Wt = reinterpret_cast<const uint8_t*>(a.W) + (size_t)tile * KT * Q8_TILE_BYTES;
+  const uint8_t* Wt = reinterpret_cast<const uint8_t*>(a.W) + ((size_t)tile * KT + cb * 4) * Q8_TILE_BYTES;
 
   const u32x4* xsrc[PPT];
   int xstep[PPT], xdst[PPT];
@@ -2392,13 +2445,13 @@ __global__ __launch_bounds__(64 * W) void mq8_wide_kernel(MMArgs a) {
     const int p = min(tid + i * NT, PIECES - 1);
     if (p < NQ) {
       const int row = p / 16, rr = row < a.M ? row : a.M - 1;
-      xsrc[i] = reinterpret_cast<const u32x4*>(a.xq + (size_t)rr * a.K + (p % 16) * 16);
+      xsrc[i] = reinterpret_cast<const u32x4*>(a.xq + (size_t)rr * a.K + (size_t)cb * 256 + (p % 16) * 16);
       xstep[i] = 16;
       xdst[i] = row * QP + (p % 16) * 16;
       xq_piece[i] = true;
     } else {
       const int q = p - NQ, row = q / 2, rr = row < a.M ? row : a.M - 1;
-      xsrc[i] = reinterpret_cast<const u32x4*>(a.xd + (size_t)rr * (a.K / 32) + (q % 2) * 4);
+      xsrc[i] = reinterpret_cast<const u32x4*>(a.xd + (size_t)rr * (a.K / 32) + cb * 8 + (q % 2) * 4);
       xstep[i] = 2;
       xdst[i] = row * 32 + (q % 2) * 16;
       xq_piece[i] = false;
@@ -2492,8 +2545,28 @@ __global__ __launch_bounds__(64 * W) void mq8_wide_kernel(MMArgs a) {
     }
     const int col = n * 16 + (lane & 15);
     if (col >= a.M || (EPI == EPI_SWIGLU && lane >= 32)) continue;
-    epi_store<EPI>(a, tile, lane, col, sv, up);
+    if constexpr (EPI == EPI_SLAB)  // partial over this K range: slab blockIdx.y [token][N]
+      *reinterpret_cast<f32x4*>(a.out + blockIdx.y * a.slab_stride + (size_t)col * a.ldo + tile * 16 + (lane >> 4) * 4) = sv;
+    else
+      epi_store<EPI>(a, tile, lane, col, sv, up);
   }
+}
+
+// 17..32 tokens, attn_output / ffn_down / q|k|v of a Q8_0 file: 4-wave groups, K split over grid.y
+// until ~256 work-groups, partial slabs [ks][token][N] (folded by launch_rmsnorm_q8's FOLD form, or
+// finished by the decode attention / launch_qkv_finish).  Returns ks, or -1 (use launch_mq8).
+int launch_mq8_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s) {
+  static const bool off = getenv("MX_NO_Q8_WIDE") != nullptr || getenv("MX_NO_Q8_SLAB") != nullptr;
+  if (off || a.M <= 16 || a.M > 32 || !a.xq || !a.xd || a.K % 256 || a.N % 64) return -1;
+  const int ntiles = a.N / TILE_N, NCH = a.K / 256;
+  int ks = 1;
+  while (ks < 8 && (ntiles / 4) * ks * 2 <= 256 && NCH / (ks * 2) >= 4) ks *= 2;
+  MMArgs p = a;
+  p.out = slabs;
+  p.ldo = a.N;
+  p.slab_stride = slab_stride;
+  mq8_wide_kernel<4, EPI_SLAB, 2><<<dim3(ntiles / 4, ks), 256, 0, s>>>(p);
+  return ks;
 }
 
 // 17..32 tokens, gate/up or lm_head of a Q8_0 file: the LDS-shared form (MX_NO_Q8_WIDE=1: mq8_kernel)

@@ -162,5 +162,17 @@ def test_q8_wide_lds_gemv_vs_grouped_and_oracle(mx, oracle_mod, monkeypatch, nam
     assert (np.abs(got - ref) <= tol2).all()
     om = _oracle_q8(oracle_mod, shape, 0)
     o = np.stack([om.context(64).eval(p, 0)[0] for p in prompts])
-    assert_logits_close(got, o, f"{name} q8_0 wide M={M}")
+    # Q8_0 rounding is discontinuous (module docstring): the engine's deviation is bounded by twice the
+    # oracle's own deviation under 1e-6 input noise, on top of twice the bf16 tolerance
+    oracle_mod.q8_jitter(1e-6)
+    try:
+        oj = _oracle_q8(oracle_mod, shape, 0)
+        jit = np.stack([oj.context(64).eval(p, 0)[0] for p in prompts])
+    finally:
+        oracle_mod.q8_jitter(0.0)
+    self_dev = np.abs(jit - o).max()
+    err = np.abs(got - o).max()
+    assert err <= 2 * self_dev + 1e-4 * np.abs(o).max(), (err, self_dev)
+    tol2o = 2 * (1e-2 * np.abs(o) + 2e-2 * np.abs(o).max(axis=-1, keepdims=True))
+    assert (np.abs(got - o) <= tol2o).all()
     assert_tokens_match(got, o, f"{name} q8_0 wide M={M}")
