@@ -246,7 +246,8 @@ def quant_bench(args, wtype: str, steps: int):
             kb = wbytes + m * h + m * h // 8 + m * shape.n_ff * 4   # int8 rows + scales in, f32 act out
         else:
             kb = wbytes + m * h + m * h // 64 + m * h // 8 + m * shape.n_ff * 4  # Q8_K rows, d, sub-block sums
-        kname = {"q8_0": "mq8_kernel", "q4_k_m": "mkq_pers_kernel" if m <= 16 else "mkq_wide_kernel"}[wtype]
+        kname = {"q8_0": "mq8_kernel" if m <= 16 else "mq8_wide_kernel",
+                 "q4_k_m": "mkq_pers_kernel" if m <= 16 else "mkq_wide_kernel"}[wtype]
         out[f"gate_up_M{m}"] = {"kernel": kname + "<EPI_SWIGLU>",
                                 "us_per_launch": round(us, 2), "bytes_per_launch": int(kb),
                                 "achieved_gbs": round(kb / us / 1e3, 1), "frac": round(kb / us / 1e3 / HBM_PEAK_GBS, 4)}
