@@ -856,8 +856,10 @@ __global__ __launch_bounds__(64 * KS) void mkq_kernel(MMArgs a) {
 // barrier that waits for the LDS writes only; wave 0 finishes tile i while the others stream tile
 // i+1).  Same K split (KS waves) and summation order per tile as mkq_kernel (hipcc's fma contraction
 // of the scale arithmetic may still differ by an ulp).
-template <int T, int KS, int NKW, int TPW, int NB, int EPI, int U, bool QL>
-__global__ __launch_bounds__(64 * KS) void mkq_pers_kernel(MMArgs a) {
+// CONTIG: the work-group's tiles are blockIdx.x*TPW + i (one segment of the matrix, starting at
+// tile tseg0, whose packed tiles start at Wseg) instead of blockIdx.x + i*G
+template <int T, int KS, int NKW, int TPW, int NB, int EPI, int U, bool QL, bool CONTIG = false>
+__device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Wseg, int tseg0) {
   constexpr int TB = KqTile<T>::BYTES;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -867,8 +869,9 @@ __global__ __launch_bounds__(64 * KS) void mkq_pers_kernel(MMArgs a) {
   const int G = gridDim.x;
   const int ntiles = a.N / TILE_N;
   __shared__ f32x4 red[2][KS][NB][64];
+  auto tile_of = [&](int i) { return CONTIG ? (int)blockIdx.x * TPW + i : (int)blockIdx.x + i * G; };
 
-  const uint8_t* W = reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[0];
+  const uint8_t* W = Wseg;
   const int8_t* Xq[NB];
   const float* Xd[NB];
   const float* Xb[NB];
@@ -896,7 +899,7 @@ __global__ __launch_bounds__(64 * KS) void mkq_pers_kernel(MMArgs a) {
   // end re-read the last tile; their outputs are dropped)
   auto load_w = [&](Frag& fr, int f) {
     const int i = f / NKW, k = f % NKW;
-    const int tile = min((int)blockIdx.x + i * G, ntiles - 1);
+    const int tile = min(tile_of(i), ntiles - 1) - tseg0;
     const uint8_t* Wt[1] = {W + ((size_t)tile * SB + kb + k) * TB};
     kq_load_w<T, 1, NB>(fr, Wt, lane, g);
   };
@@ -906,7 +909,7 @@ __global__ __launch_bounds__(64 * KS) void mkq_pers_kernel(MMArgs a) {
   };
   constexpr int LU = (EPI == EPI_SWIGLU) ? 32 : 64;
   auto finish = [&](int i) {
-    const int tile = blockIdx.x + i * G;
+    const int tile = tile_of(i);
     if (w != 0 || tile >= ntiles) return;
     f32x4 (*rb)[NB][64] = red[i & 1];
 #pragma unroll
@@ -958,6 +961,38 @@ __global__ __launch_bounds__(64 * KS) void mkq_pers_kernel(MMArgs a) {
     finish(i);
     __builtin_amdgcn_sched_barrier(0);  // no hoisting across tiles (it spilled the ring)
   }
+}
+
+template <int T, int KS, int NKW, int TPW, int NB, int EPI, int U, bool QL>
+__global__ __launch_bounds__(64 * KS) void mkq_pers_kernel(MMArgs a) {
+  mkq_pers_body<T, KS, NKW, TPW, NB, EPI, U, QL>(a, reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[0], 0);
+}
+
+// One token of a matrix with row segments of different types (q|k Q4_K + v Q6_K): TPW contiguous
+// tiles per work-group, every segment boundary a multiple of TPW, the body chosen per work-group
+template <int KS, int NKW, int TPW, int EPI, int U>
+__global__ __launch_bounds__(64 * KS) void mkq_pers_seg_kernel(MMArgs a) {
+  const int t0 = blockIdx.x * TPW;
+  int seg = 0;
+  while (seg < a.kq_n - 1 && t0 >= a.kq_tile_end[seg]) ++seg;
+  const int tb = seg ? a.kq_tile_end[seg - 1] : 0;
+  const uint8_t* Ws = reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[seg];
+  switch (a.kq_type[seg]) {
+    case 12: mkq_pers_body<12, KS, NKW, TPW, 1, EPI, U, true, true>(a, Ws, tb); break;
+    case 13: mkq_pers_body<13, KS, NKW, TPW, 1, EPI, U, true, true>(a, Ws, tb); break;
+    case 14: mkq_pers_body<14, KS, NKW, TPW, 1, EPI, U, true, true>(a, Ws, tb); break;
+  }
+}
+
+// one token, q|k|v of a K-quant file (K 4096: 16 super-blocks = 8 waves x 2): 2 tiles per
+// work-group (Llama-3-8B: 192 groups) quantising on load; -1 if the shape has no such form
+static int launch_kq_qkv_pers(const MMArgs& a, hipStream_t s) {
+  static const bool off = getenv("MX_NO_KQ_QKV_PERS") != nullptr;
+  if (off || a.M != 1 || a.xq != nullptr || a.K != 4096 || (a.N / TILE_N) % 2) return -1;
+  for (int i = 0; i < a.kq_n; ++i)
+    if (a.kq_tile_end[i] % 2) return -1;
+  mkq_pers_seg_kernel<8, 2, 2, EPI_QKV, 2><<<a.N / TILE_N / 2, 512, 8 * QL_WAVE_BYTES, s>>>(a);
+  return 0;
 }
 
 template <int T, int NKW, int TPW, int NB, int EPI, int U>
@@ -1283,6 +1318,7 @@ int launch_mkq(int epi, const MMArgs& a, hipStream_t s) {
     if (!kq_tile_bytes(a.kq_type[i]) || (i && a.kq_tile_end[i] <= a.kq_tile_end[i - 1])) return -1;
   if (epi == EPI_SWIGLU && !a.actf) return -1;
   const int ntiles = a.N / TILE_N;
+  if (epi == EPI_QKV && launch_kq_qkv_pers(a, s) == 0) return 0;
   if (launch_kq_pers(epi, a, ntiles, s) == 0) return 0;
   if (launch_kq_wide(epi, a, ntiles, s) == 0) return 0;
   switch (epi) {
