@@ -251,7 +251,9 @@ def quant_bench(args, wtype: str, steps: int):
         out[f"gate_up_M{m}"] = {"kernel": kname + "<EPI_SWIGLU>",
                                 "us_per_launch": round(us, 2), "bytes_per_launch": int(kb),
                                 "achieved_gbs": round(kb / us / 1e3, 1), "frac": round(kb / us / 1e3 / HBM_PEAK_GBS, 4)}
-    if wtype == "q4_k_m" and args.prefill_prompts > 0:  # > 64-row chunks: dequantised bf16 GEMMs
+    if args.prefill_prompts > 0:
+        # > 64-row chunks: K-quant as dequantised bf16 GEMMs; Q8_0 as grouped Q8_0 GEMVs (ggml's
+        # arithmetic), or dequantised bf16 GEMMs with MX_Q8_GEMM_PREFILL=1
         out["prefill"] = prefill_bench(eng, shape, args.prefill_prompts, args.prefill_len)
     eng.close()
     return out

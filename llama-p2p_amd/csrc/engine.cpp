@@ -192,6 +192,7 @@ struct mx_engine {
   bool norm_on_load = getenv("MX_NO_NORM_ON_LOAD") == nullptr;
   // gate/up as a row-tile-persistent GEMV with RMS_NORM on load (<= 4 rows); MX_NO_PERS=1 for A/B
   bool use_pers = getenv("MX_NO_PERS") == nullptr;
+  bool q8_gemm_prefill = getenv("MX_Q8_GEMM_PREFILL") != nullptr;  // see enqueue_forward
   float* ssq = nullptr;  // [MAX_ROWS][n_embd/16] per-tile sums of squares of x
   // rows of the next forward belong to distinct sequences (decode): no row attends to another row's
   // new K/V, so the wide path lets the attention kernel finish q/k/v from the split-K slabs
@@ -390,9 +391,9 @@ int mx_engine::init_common() {
   }
   slab_stride = (size_t)MAX_ROWS * (n_embd + 2 * n_embd_kv);
   if (int rc = alloc((void**)&slabs, slab_stride * 8 * 4)) return rc;
-  if (!wq8 && gemm_shapes())
+  if (gemm_shapes())
     if (int rc = alloc((void**)&gslabs, GSLAB_FLOATS * 4)) return rc;
-  if (wkq && gemm_shapes()) {
+  if ((wkq || (wq8 && q8_gemm_prefill)) && gemm_shapes()) {  // per-layer bf16 copies for the prefill GEMM
     const size_t h = n_embd, kv = n_embd_kv, ff = n_ff;
     if (int rc = alloc((void**)&kqd_qkv, (h + 2 * kv) * h * 2)) return rc;
     if (int rc = alloc((void**)&kqd_o, h * h * 2)) return rc;
@@ -901,6 +902,11 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
   }
   if (wkq && M > MAX_ROWS && kqd_qkv && !argmax && !(head && n_out > MAX_ROWS))
     return enqueue_forward_gemm(M, pos, slot, x_out, head, rowmap, n_out, s);  // dequantised bf16 GEMMs
+  // Q8_0 prefill chunks as dequantised bf16 GEMMs (llama.cpp's GPU-backend route for large batches):
+  // ~5x the default's rate, but bf16 activations instead of ggml's Q8_0 rows, so opt-in
+  // (MX_Q8_GEMM_PREFILL=1; tests/test_q8_gpu.py bounds its deviation)
+  if (wq8 && q8_gemm_prefill && M > MAX_ROWS && kqd_qkv && !argmax && !(head && n_out > MAX_ROWS))
+    return enqueue_forward_gemm(M, pos, slot, x_out, head, rowmap, n_out, s);
   if (wkq) return enqueue_forward_kq(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next, pos_next, hist,
                                      hist_stride, hist_count, max_hist, s);
   if (wq8) return enqueue_forward_q8(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next, pos_next, hist,
@@ -1289,6 +1295,14 @@ int mx_engine::enqueue_forward_gemm(int M, const int* pos, const int* slot, void
           dequant(kqd_down, L.kq_down, L.down, ff))
         return fail(MX_ERR_ARG, "K-quant dequantisation shape");
       Wqkv = kqd_qkv, Wo = kqd_o, Wgu = kqd_gu, Wdown = kqd_down;
+    } else if (wq8) {  // Q8_0: d * q per weight, rounded to bf16
+      auto dq = [&](uint16_t* dst, const uint16_t* w, int N, int K) {
+        return launch_dequant_q8_tiles(dst, reinterpret_cast<const uint8_t*>(w), N, K, s);
+      };
+      if (dq(kqd_qkv, L.qkv, h + 2 * kv, h) || dq(kqd_o, L.o, h, h) || dq(kqd_gu, L.gu, 2 * ff, h) ||
+          dq(kqd_down, L.down, h, ff))
+        return fail(MX_ERR_ARG, "Q8_0 dequantisation shape");
+      Wqkv = kqd_qkv, Wo = kqd_o, Wgu = kqd_gu, Wdown = kqd_down;
     }
     launch_resid_norm(xn, h, x, gslabs, nslab, gstride, L.attn_norm, M, h, eps, s);
     MMArgs a{};
@@ -1330,6 +1344,10 @@ int mx_engine::enqueue_forward_gemm(int M, const int* pos, const int* slot, void
       if (launch_rmsnorm_q8k(xq8, xqd, xkb, x, out_norm, rowmap, n_out, h, eps, s)) return fail(MX_ERR_ARG, "kq norm");
       g.xq = xq8; g.xd = xqd; g.xb = xkb;
       if (launch_mkq(EPI_F32, g, s)) return fail(MX_ERR_ARG, "kq lm_head launch shape");
+    } else if (wq8) {  // the Q8_0 head as at decode
+      launch_rmsnorm_q8(xq8, xqd, x, out_norm, rowmap, n_out, h, eps, s);
+      g.xq = xq8; g.xd = xqd;
+      if (launch_mq8(EPI_F32, g, s)) return fail(MX_ERR_ARG, "q8 lm_head launch shape");
     } else {
       launch_rmsnorm(xn, h, x, out_norm, rowmap, n_out, h, eps, s);
       g.X = xn; g.ldx = h;

@@ -153,6 +153,8 @@ constexpr int Q8_TILE_K = 64;
 constexpr int Q8_TILE_BYTES = 1088;
 inline size_t q8_matrix_bytes(int N, int K) { return (size_t)N / 16 * (K / Q8_TILE_K) * Q8_TILE_BYTES; }
 void launch_pack_q8(uint8_t* dst, const uint8_t* src_blocks, int N, int K, int mode, int row_offset, hipStream_t s);
+// packed Q8 tiles of a [N][K] matrix -> packed bf16 tiles (prefill GEMM operand), values d*q -> bf16
+int launch_dequant_q8_tiles(uint16_t* dst, const uint8_t* W, int N, int K, hipStream_t s);
 void launch_synth_q8_packed(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, int mode,
                             int row_offset, hipStream_t s);
 void launch_synth_q8_rowmajor(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, hipStream_t s);

@@ -1880,6 +1880,43 @@ __global__ void synth_q8_rowmajor_kernel(uint8_t* dst, int N, int K, uint64_t se
   }
 }
 
+// Packed Q8 tiles -> packed bf16 tiles (the prefill GEMM's A operand): ggml's dequantize_row_q8_0
+// value d * q in f32, rounded to bf16 like the bf16 path's weights.  One thread per (Q8 tile, lane):
+// its 16 bytes are row l&15's k 8(l>>4)..+8 of block 0 and of block 1, i.e. exactly lane l of the
+// two bf16 tiles (2kt, 2kt+1) of the same rows.
+__global__ void dequant_q8_tiles_kernel(uint16_t* dst, const uint8_t* W, int N, int K) {
+  const int KT = K / Q8_TILE_K;
+  const size_t total = (size_t)(N / TILE_N) * KT * 64;
+  for (size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x; u < total; u += (size_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(u & 63);
+    const size_t t = u >> 6;  // Q8 tile index, nt-major
+    const uint8_t* tile = W + t * Q8_TILE_BYTES;
+    const u32x4 q = *reinterpret_cast<const u32x4*>(tile + 16 * lane);
+    const int r = lane & 15;
+    const uint16_t* dh = reinterpret_cast<const uint16_t*>(tile + 1024 + 16 * (r >> 2));
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const float d = (float)__builtin_bit_cast(_Float16, dh[4 * b + (r & 3)]);
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t qw = q[2 * b + (j >> 1)];
+        const float lo = d * (float)(int8_t)(qw >> (16 * (j & 1)));
+        const float hi = d * (float)(int8_t)(qw >> (16 * (j & 1) + 8));
+        o[j] = f2bf(lo) | (f2bf(hi) << 16);
+      }
+      *reinterpret_cast<u32x4*>(dst + ((t * 2 + b) * 64 + lane) * 8) = o;
+    }
+  }
+}
+
+int launch_dequant_q8_tiles(uint16_t* dst, const uint8_t* W, int N, int K, hipStream_t s) {
+  if (N % TILE_N || K % Q8_TILE_K) return -1;
+  const size_t total = (size_t)(N / TILE_N) * (K / Q8_TILE_K) * 64;
+  dequant_q8_tiles_kernel<<<fill_grid(total), 256, 0, s>>>(dst, W, N, K);
+  return 0;
+}
+
 void launch_pack_q8(uint8_t* dst, const uint8_t* src, int N, int K, int mode, int offset, hipStream_t s) {
   pack_q8_kernel<<<fill_grid((size_t)N * K / 32), 256, 0, s>>>(dst, src, N, K, mode, offset);
 }

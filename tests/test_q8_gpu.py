@@ -176,3 +176,26 @@ def test_q8_wide_lds_gemv_vs_grouped_and_oracle(mx, oracle_mod, monkeypatch, nam
     tol2o = 2 * (1e-2 * np.abs(o) + 2e-2 * np.abs(o).max(axis=-1, keepdims=True))
     assert (np.abs(got - o) <= tol2o).all()
     assert_tokens_match(got, o, f"{name} q8_0 wide M={M}")
+
+
+def test_q8_dequantised_gemm_prefill_opt_in(mx, oracle_mod, monkeypatch):
+    """MX_Q8_GEMM_PREFILL=1: a > 64-row Q8_0 prompt chunk runs as bf16 GEMMs over weights dequantised
+    per layer (dequant_q8_tiles_kernel: d*q rounded to bf16).  Its activations are bf16, not ggml's
+    Q8_0 rows, so the next decode rows (attending to the K/V the GEMM path stored) are held to twice
+    the bf16 tolerance against the oracle, and the dequantised tiles are checked against the packed
+    Q8 tiles through the default path's logits on the same prompt."""
+    from llama_p2p_amd import synth
+
+    monkeypatch.setenv("MX_Q8_GEMM_PREFILL", "1")
+    name = "test-d128"
+    shape = synth.SHAPES[name]
+    om = _oracle_q8(oracle_mod, shape, 0)
+    eng = mx.Engine(f"synthetic:{name}:seed=0:q8_0", n_ctx=640, n_seq_max=2)
+    ids = _seq(shape, 610, seed=9)
+    assert eng.forward_rows([0] * 600, list(range(600)), ids[:600], want_logits=False) is None
+    got = eng.forward_logits(ids[600:610], 600, slot=0)
+    eng.close()
+    ref = om.context(640).eval(ids, 0, all_logits=True)[600:]
+    tol2 = 2 * (1e-2 * np.abs(ref) + 2e-2 * np.abs(ref).max(axis=-1, keepdims=True))
+    assert (np.abs(got - ref) <= tol2).all(), np.abs(got - ref).max()
+    assert_tokens_match(got, ref, "q8 dequantised GEMM prefill")
