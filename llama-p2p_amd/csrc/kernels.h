@@ -123,8 +123,6 @@ bool mm_can_norm_on_load(int M, int K);
 // <= 16 rows, row-tile-persistent gate/up: -1 if the shape has no instantiation
 bool mm_pers_supported(int epi, int M, int N, int K);
 int launch_mm_pers(int epi, const MMArgs& a, hipStream_t s);
-// one-token qkv as 2 split-K slabs with RMS_NORM on load (attention finishes): slab count or -1
-int launch_qkv_split(const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s);
 // 17..64 rows: activation chunks shared through LDS.  EPI_QKV / EPI_RESID run split-K into
 // `slabs` ([ksplit][MAX_ROWS][N] floats, slab_stride apart); returns the split used (the caller
 // folds RESID partials with launch_resid_norm; QKV partials are finished inside), or -1.
