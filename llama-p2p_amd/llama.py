@@ -133,6 +133,14 @@ class Llama:
         if cut >= 0:
             text = text[:cut]
             finish_reason = "stop"
+            # the cancel lands after the scheduler's current round (up to 8 greedy steps), so tokens past
+            # the stop may have been generated: count only those up to the one completing the stop
+            # string, as llama-cpp-python does (its check runs after every token)
+            for k in range(1, len(toks) + 1):
+                t = self.detokenize(toks[:k], prev_tokens=prompt_tokens).decode("utf-8", errors="ignore")
+                if any(s in t for s in stops):
+                    toks = toks[:k]
+                    break
         if echo:
             text = self.detokenize(prompt_tokens).decode("utf-8", errors="ignore") + text
         if suffix is not None:

@@ -45,6 +45,10 @@ class Timeout(Exception):
     """Raised by a reply transport's recv when nothing arrived (pynng.Timeout)."""
 
 
+class Closed(Exception):
+    """Raised by a reply context's recv once its socket is closed (pynng.Closed): the worker exits."""
+
+
 class LlamaP2PNode:
     def __init__(self, model_path, port, known_peers=None, cache_size=100, secret_key=None, *, model=None,
                  transport=None, llama_kwargs=None, n_contexts=64):
@@ -146,6 +150,8 @@ class LlamaP2PNode:
                 msg = ctx.recv(timeout=100)
             except Timeout:
                 continue
+            except Closed:
+                break
             except Exception as e:
                 log.error(f"Error handling request: {e}")
                 continue
@@ -331,14 +337,25 @@ class _NetTransport:
 
 
 class _NetContext:
-    def __init__(self, ctx, pynng):
-        self._ctx, self._pynng = ctx, pynng
+    """One REP context.  UNVERIFIED here (pynng is not importable in this container): the receive
+    timeout is set on the context itself where pynng exposes it, and otherwise inherited from the
+    socket's recv_timeout; ``close()`` of the socket is the shutdown path either way -- a blocked
+    recv then raises pynng.Closed, which ends the worker instead of being logged and retried."""
 
-    def recv(self, timeout=100):  # the socket's recv_timeout bounds the wait
+    def __init__(self, ctx, pynng, timeout_ms=100):
+        self._ctx, self._pynng = ctx, pynng
+        try:
+            ctx.recv_timeout = timeout_ms
+        except Exception:  # older pynng: contexts take the socket's option
+            pass
+
+    def recv(self, timeout=100):
         try:
             return self._ctx.recv()
         except self._pynng.Timeout:
             raise Timeout()
+        except self._pynng.Closed:
+            raise Closed()
 
     def send(self, data):
         self._ctx.send(data)

@@ -86,6 +86,58 @@ def test_tinyllama_32x128_gemm_prefill(mx, oracle_mod):
     eng.close()
 
 
+def test_8b_full_depth_32_sequences(mx, oracle_mod):
+    """Config 3 exactly as bench.py times it: the full 32-layer Llama-3-8B (bf16, V=128256) with 32
+    concurrent sequences.  Short prompts (8-16 tokens, so the CPU oracle stays cheap) prefilled
+    through the engine, then ONE 32-row decode step through the wide path (split-K slabs, FIN
+    attention) whose logits are compared with the oracle, then 4 steps of the device greedy loop
+    (hipGraph replay + device argmax over 128256) teacher-forced through the oracle."""
+    from llama_p2p_amd import synth
+
+    name = "llama3-8b"
+    shape = synth.SHAPES[name]
+    M, G = 32, 4
+    rng = np.random.default_rng(2)
+    prompts = [np.concatenate([[1], rng.integers(3, shape.n_vocab, int(rng.integers(7, 16)))]).astype(np.int32)
+               for _ in range(M)]
+    eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=64, n_seq_max=M)
+    assert eng.info.n_layer == 32 and eng.info.n_vocab == 128256
+    slots, pos, ids = [], [], []
+    for i, p in enumerate(prompts):
+        slots += [i] * (len(p) - 1)
+        pos += list(range(len(p) - 1))
+        ids += [int(t) for t in p[:-1]]
+    eng.forward_rows(slots, pos, ids, want_logits=False)
+    dslots, dpos, dids = list(range(M)), [len(p) - 1 for p in prompts], [int(p[-1]) for p in prompts]
+    got = eng.forward_rows(dslots, dpos, dids)  # one 32-row wide decode step
+    first = [int(np.argmax(got[i])) for i in range(M)]
+    b = eng.batch(slots=dslots, pos=[len(p) for p in prompts], ids=first, max_steps=G)
+    for _ in range(G):
+        b.step()
+    toks = b.tokens()
+    b.close()
+    eng.close()
+    om = oracle_mod.OracleModel(shape, seed=0)
+    exact, worst = 0, 0.0
+    for i, p in enumerate(prompts):
+        chain = [first[i]] + toks[i].tolist()
+        # one oracle evaluation per sequence: prompt + chain[:-1], logits of every row
+        lg = om.context(64).eval(np.concatenate([p, np.asarray(chain[:-1], np.int32)]), 0, all_logits=True)
+        ref = lg[len(p) - 1:len(p)]
+        assert_logits_close(got[i:i + 1], ref, f"seq {i}: 32-row step logits")
+        assert_tokens_match(got[i:i + 1], ref, f"seq {i}: 32-row step argmax")
+        worst = max(worst, float(np.abs(got[i] - ref[0]).max() / np.abs(ref).max()))
+        for k, t in enumerate(chain):
+            row = lg[len(p) - 1 + k]
+            tol = 2 * (1e-2 * abs(float(row.max())) + 2e-2 * float(np.abs(row).max()))
+            assert float(row.max() - row[t]) <= tol, f"seq {i} step {k}: picked {t}, oracle max at {int(row.argmax())}"
+            exact += int(t == int(row.argmax()))
+    om.close()
+    print(f"llama3-8b full depth, 32 sequences: max |d|/max|ref| {worst:.3g}; "
+          f"{exact}/{M * (G + 1)} greedy picks exact (the rest near ties)")
+    assert exact >= 0.9 * M * (G + 1)
+
+
 def test_8b_full_vocab_32_rows(mx, oracle_mod):
     """Config 3's step shape: Llama-3-8B layers with the 128256-token lm_head, exactly 32 rows (the
     17-64-row wide path).  Teacher-forced 32-row logits, the device top-k candidates of the sampler

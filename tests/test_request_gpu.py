@@ -1,0 +1,90 @@
+"""Request-path features of the scheduler through the C ABI (mx_submit / mx_poll / mx_cancel / mx_wait).
+
+  * penalties: llama.cpp's penalties sampler (repeat / frequency / presence over the last
+    repeat_last_n tokens of prompt + output) ahead of greedy -- engine.cpp sample_host -- pinned
+    against a numpy restatement applied to the engine's own teacher-forced logits;
+  * cancellation: a request cancelled before admission returns no tokens (finish STOP); one cancelled
+    while running ends at the next scheduler round with fewer tokens than max_tokens;
+  * mx_poll: incremental reads return growing prefixes of the final output.
+"""
+import numpy as np
+import pytest
+
+from conftest import logit_tol
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mx():
+    from llama_p2p_amd import engine
+
+    engine.lib()
+    return engine
+
+
+def penalise(logits, history, last_n, repeat, freq, presence):
+    """llama.cpp llama_sampler_penalties_apply (0.3.x): counts over the last last_n tokens; a counted
+    token's logit is divided by `repeat` when positive (multiplied when not), then count*freq and
+    presence are subtracted."""
+    out = logits.astype(np.float32).copy()
+    hist = list(history)[-last_n:] if last_n > 0 else list(history)
+    ids, counts = np.unique(np.asarray(hist, np.int64), return_counts=True)
+    for t, c in zip(ids, counts):
+        v = out[t]
+        if repeat != 1.0:
+            v = v * repeat if v <= 0 else v / repeat
+        out[t] = v - (c * freq + presence)
+    return out
+
+
+@pytest.mark.parametrize("repeat,freq,presence", [(1.3, 0.0, 0.0), (1.0, 0.4, 0.7), (1.15, 0.2, 0.3)])
+def test_penalised_greedy_vs_numpy_restatement(mx, repeat, freq, presence):
+    name = "test-tiny"
+    eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=128, n_seq_max=2)
+    rng = np.random.default_rng(11)
+    prompt = [1] + [int(t) for t in rng.integers(3, eng.n_vocab, 12)]
+    G, last_n = 24, 16
+    toks, fin = eng.generate(prompt, G, temperature=0.0, repeat_penalty=repeat, repeat_last_n=last_n,
+                             frequency_penalty=freq, presence_penalty=presence, ignore_eos=True)
+    assert len(toks) == G
+    # the same chain teacher-forced through the engine's parity hook (slot 1): logits of every row
+    seq = prompt + toks[:-1]
+    lg = eng.forward_logits(seq, 0, slot=1)[len(prompt) - 1:]
+    plain = 0
+    for k, t in enumerate(toks):
+        p = penalise(lg[k], prompt + toks[:k], last_n, repeat, freq, presence)
+        tol = 2 * logit_tol(lg[k]).max()
+        assert p.max() - p[t] <= tol, f"step {k}: picked {t}, penalised max {p.max():.4f} at {int(p.argmax())}"
+        plain += int(t == int(np.argmax(lg[k])))
+    # the penalties changed the chain (otherwise the test would not exercise them)
+    assert plain < G, "penalised greedy equals plain greedy at every step"
+    eng.close()
+
+
+def test_cancel_before_admission_returns_no_tokens(mx):
+    # TinyLlama-1.1B: the slot holder's 400 tokens take ~0.3 s, far longer than submit + cancel
+    eng = mx.Engine("synthetic:tinyllama-1.1b:seed=0", n_ctx=512, n_seq_max=1)
+    first = eng.submit([1, 5, 6, 7], 400, temperature=0.0, ignore_eos=True)  # holds the only slot
+    queued = eng.submit([1, 9, 9, 9], 50, temperature=0.0, ignore_eos=True)
+    eng.cancel(queued)
+    got, fin = eng.wait(queued)
+    assert got == [] and fin == mx.FINISH_STOP
+    toks, fin1 = eng.wait(first)
+    assert len(toks) == 400 and fin1 == mx.FINISH_LENGTH
+    eng.close()
+
+
+def test_cancel_running_request_and_poll_prefixes(mx):
+    eng = mx.Engine("synthetic:tinyllama-1.1b:seed=0", n_ctx=512, n_seq_max=2)
+    r = eng.submit([1, 4, 8, 15], 300, temperature=0.0, ignore_eos=True)
+    seen, n = [], 0
+    while n < 20:
+        part, done = eng.poll(r, n)
+        assert part[:len(seen)] == seen and len(part) > n and not done
+        seen, n = part, len(part)
+    eng.cancel(r)
+    got, fin = eng.wait(r)
+    assert fin == mx.FINISH_STOP and 20 <= len(got) < 300
+    assert got[:len(seen)] == seen  # what poll returned is a prefix of the final output
+    eng.close()
