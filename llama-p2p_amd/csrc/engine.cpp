@@ -782,16 +782,23 @@ int mx_engine::load_gguf(const std::string& path) {
           goto out;
         }
         weight_bytes += t->nbytes / V;
-      } else if (t->type == 30) {
-        if ((rc = alloc((void**)&tok_embd, t->nbytes))) goto out;
-        if (hipMemcpy(tok_embd, f.data(*t), t->nbytes, hipMemcpyHostToDevice) != hipSuccess) {
+      } else if (t->type == 30 || t->type == 8) {  // BF16 rows as stored; Q8_0 rows dequantised per lookup
+        void** dst = embd_q8 ? (void**)&tok_embd8 : (void**)&tok_embd;
+        if ((rc = alloc(dst, t->nbytes))) goto out;
+        if (hipMemcpy(*dst, f.data(*t), t->nbytes, hipMemcpyHostToDevice) != hipSuccess) {
+          rc = fail(MX_ERR_HIP, "upload token_embd");
+          goto out;
+        }
+        weight_bytes += t->nbytes / V;
+      } else {  // F32 / F16 / Q4_0 / ... (llama-quantize --token-embedding-type): a bf16 table once
+        if ((rc = alloc((void**)&tok_embd, (size_t)V * h * 2))) goto out;
+        if ((rc = to_bf16(t, (size_t)V * h))) goto out;
+        if (hipMemcpyAsync(tok_embd, stage, (size_t)V * h * 2, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
+            hipStreamSynchronize(stream) != hipSuccess) {
           rc = fail(MX_ERR_HIP, "upload token_embd");
           goto out;
         }
         weight_bytes += (size_t)h * 2;
-      } else {
-        rc = fail(MX_ERR_MODEL, "token_embd.weight: K-quant models take a Q4_K/Q5_K/Q6_K or BF16 token_embd");
-        goto out;
       }
     }
     if (has_head) {

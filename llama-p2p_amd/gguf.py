@@ -435,7 +435,7 @@ def _mixed_type(wtype: str, name: str) -> int:
 
 
 def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = None, wtype: str = "bf16",
-                         dequant_from: str = None, rope_freqs=None, rope_scaling=None):
+                         dequant_from: str = None, rope_freqs=None, rope_scaling=None, embd_type: int = None):
     """Write a LLaMA GGUF with the synthetic weights of synth.py: every matrix bf16, or (wtype
     "q8_0") the Q8_0 quantisation of those bf16 matrices; norms f32 either way.  wtype "q4_k_m",
     "q5_k_m", "q4_0", "f16": matrices in those per-tensor types (MIXED), with random valid blocks
@@ -443,7 +443,9 @@ def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = Non
     tensors take llama.cpp's per-layer recipe types with synth.kq_tensor's blocks.  dequant_from: a GGUF of the
     same shape whose matrices are written here dequantised (dequantize(), then bf16 RNE) as BF16.
     rope_freqs: a rope_freqs.weight tensor (head_dim/2 f32, Llama-3.1 style); rope_scaling:
-    (type, factor) written as llama.rope.scaling.type / .factor."""
+    (type, factor) written as llama.rope.scaling.type / .factor.  embd_type: token_embd.weight as this
+    type instead (GGML_Q8_0 or GGML_F16 of the synthetic bf16 table; llama-quantize
+    --token-embedding-type)."""
     from . import synth
 
     if wtype not in ("bf16", "q8_0") and wtype not in MIXED:
@@ -480,6 +482,11 @@ def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = Non
     arrays = []
     src = GGUFReader(dequant_from) if dequant_from else None
     for name, kind, arr in synth.synth_tensors(shape, seed):
+        if name == "token_embd.weight" and embd_type is not None:
+            w.add_tensor_info(name, arr.shape, embd_type)
+            arrays.append(synth_q8_0_tensor(arr) if embd_type == GGML_Q8_0
+                          else synth.bf16_bits_to_f32(arr).astype(np.float16))
+            continue
         if kind == "bf16" and src is not None:
             info = src.tensors[name]
             y = dequantize(info["type"], src.tensor(name), arr.shape)

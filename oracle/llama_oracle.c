@@ -251,7 +251,11 @@ int orc_set_tensor(orc_model *m, int layer, int kind, const void *src) {
     size_t h = m->hp.n_embd, kv = m->n_embd_kv, ff = m->hp.n_ff, V = m->hp.n_vocab;
     if (layer < 0) {
         switch (kind) {
-        case K_TOK_EMBD: memcpy(m->tok_embd, src, V * h * 2); return 0;
+        case K_TOK_EMBD: /* the table becomes bf16: drop any block representation set before */
+            memcpy(m->tok_embd, src, V * h * 2);
+            free(m->tok_embd_q8); m->tok_embd_q8 = NULL;
+            free(m->tok_embd_kq); m->tok_embd_kq = NULL;
+            return 0;
         case K_OUTPUT: memcpy(m->output, src, V * h * 2); return 0;
         case K_OUT_NORM: memcpy(m->out_norm, src, h * 4); return 0;
         }
@@ -324,6 +328,7 @@ int orc_set_tensor_q8(orc_model *m, int layer, int kind, const void *blocks) {
     if (!slot || cols % QK8_0) return -1;
     if (!*slot) *slot = (uint8_t *)malloc(q8_bytes(rows, cols));
     memcpy(*slot, blocks, q8_bytes(rows, cols));
+    if (layer < 0 && kind == K_TOK_EMBD) { free(m->tok_embd_kq); m->tok_embd_kq = NULL; } /* Q8_0 table wins */
     return 0;
 }
 

@@ -103,6 +103,35 @@ def test_kq_gguf_equals_synthetic(mx, tmp_path, ftype):
     b.close()
 
 
+@pytest.mark.parametrize("embd", ["q8_0", "f16"])
+def test_kq_gguf_with_other_token_embd_type(mx, oracle_mod, tmp_path, embd):
+    """A Q4_K_M file whose token_embd is Q8_0 or F16 (llama-quantize --token-embedding-type) loads on
+    the native K-quant path: Q8_0 rows are dequantised per lookup (ggml GET_ROWS), other types become a
+    bf16 table once.  Q8_0: logits vs the oracle with the same Q8_0 embedding; F16: vs the oracle with
+    the bf16 rounding of those f16 values (the table the engine keeps)."""
+    from llama_p2p_amd import gguf, synth
+
+    shape = synth.SHAPES["test-tiny"]
+    t = {"q8_0": gguf.GGML_Q8_0, "f16": gguf.GGML_F16}[embd]
+    path = str(tmp_path / f"tiny_q4_k_m_embd_{embd}.gguf")
+    gguf.write_synthetic_gguf(path, shape, seed=3, wtype="q4_k_m", embd_type=t)
+    eng = mx.Engine(path, n_ctx=64, n_seq_max=2)
+    assert eng.info.weight_type == synth.KQ_FTYPES["q4_k_m"]
+    ids = _seq(shape, 20)
+    got = eng.forward_logits(ids)
+    eng.close()
+    om = _oracle_kq(oracle_mod, shape, 3, "q4_k_m")
+    emb = next(a for n, k, a in synth.synth_tensors(shape, 3) if n == "token_embd.weight")
+    if embd == "q8_0":
+        om.set_tensor_q8(-1, 1, gguf.synth_q8_0_tensor(emb))
+    else:
+        f16 = synth.bf16_bits_to_f32(emb).astype(np.float16).astype(np.float32)
+        om.set_tensor(-1, 1, synth.f32_to_bf16_bits(f16))
+    ref = om.context(64).eval(ids, 0, all_logits=True)
+    assert_logits_close(got, ref, f"q4_k_m with {embd} token_embd")
+    assert_tokens_match(got, ref, f"q4_k_m with {embd} token_embd")
+
+
 @pytest.mark.parametrize("name,ftype", [("test-tiny", "q4_k_m"), ("test-d128", "q4_k_m"), ("test-d128", "q5_k_m"),
                                         ("test-h4096", "q4_k_m")])
 def test_kq_prefill_and_decode_vs_oracle(mx, oracle_mod, name, ftype):
