@@ -390,6 +390,108 @@ def prefill_bench(eng, shape, n_prompts: int, plen: int):
             "sample": f"{n_prompts} prompts x {plen} tokens, 4096-row GEMM chunks, no lm_head"}
 
 
+def make_text_prompts(n, tokenize, seed=2, lo=16, hi=256):
+    """n text prompts of about U[lo, hi] tokens (config 3's lengths): random words, trimmed by the
+    model's own tokenizer so that every prompt fits n_ctx 512 with the reference's 100 new tokens."""
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    words = ["node", "peer", "model", "layer", "cache", "token", "request", "the", "of", "and", "gossip",
+             "stage", "prompt", "answer", "question", "fast", "memory", "bandwidth", "graph", "stream"]
+    out = []
+    for i in range(n):
+        L = int(rng.integers(lo, hi + 1))
+        ws = [words[int(j)] for j in rng.integers(0, len(words), L)]
+        while len(ws) > 1 and len(tokenize(f"Request {i}: " + " ".join(ws))) > L:
+            ws = ws[:max(1, int(len(ws) * 0.9))]
+        out.append(f"Request {i}: " + " ".join(ws))
+    return out
+
+
+class _CountingModel:
+    """The node's ``self.model``: forwards to Llama (greedy, the parity setting) and counts completion
+    tokens (cached_inference itself returns text only)."""
+
+    def __init__(self, llm):
+        import threading
+
+        self.llm, self.tokens, self.calls, self.lock = llm, 0, 0, threading.Lock()
+
+    def __call__(self, prompt, **kw):
+        out = self.llm(prompt, temperature=0.0, **kw)
+        with self.lock:
+            self.tokens += out["usage"]["completion_tokens"]
+            self.calls += 1
+        return out
+
+
+def serving_bench(args, n: int = 32):
+    """BASELINE config 3 as worded -- Llama-3-8B bf16 serving 32 concurrent synthetic requests with the
+    result cache on -- through the drop-in node: n client threads send JSON inference requests at once
+    over an in-process REP transport with concurrent contexts (node.LocalTransport) ->
+    handle_requests (p2p:84-98) -> cached_inference (p2p:120-133) -> Llama(prompt, max_tokens=100)
+    (p2p:125; greedy) -> mx_submit/mx_wait.  A warm-up wave of other prompts runs first (the serving
+    engine is long-lived: its decode graphs exist); then wave 1 (n new prompts: tokenize, batched
+    prefill, micro-batched decode, detokenize, cache insert) is timed, then the same n prompts again
+    (all hits).  tok/s = generated tokens of wave 1 / its wall time, prefill included."""
+    import json as _json
+    import threading
+
+    from llama_p2p_amd.llama import Llama
+    from llama_p2p_amd.node import LlamaP2PNode, LocalTransport
+
+    path = f"synthetic:{args.model}"
+    llm = Llama(model_path=path, verbose=False, n_seq_max=max(n, 1), n_ctx=args.n_ctx)
+    model = _CountingModel(llm)
+    tr = LocalTransport()
+    node = LlamaP2PNode(path, 5000, cache_size=100, secret_key="k", model=model, transport=tr, n_contexts=n)
+    threading.Thread(target=node.handle_requests, daemon=True).start()
+    tok = lambda t: llm.tokenize(t.encode(), add_bos=True, special=True)  # noqa: E731
+
+    def wave(ps):
+        lat = [0.0] * len(ps)
+        err = []
+
+        def run(i):
+            t = time.perf_counter()
+            reply = _json.loads(tr.request(_json.dumps({"type": "inference", "prompt": ps[i],
+                                                        "secret_key": "k"}).encode()))
+            if "result" not in reply:
+                err.append(reply)
+            lat[i] = time.perf_counter() - t
+
+        th = [threading.Thread(target=run, args=(i,)) for i in range(len(ps))]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if err:
+            raise RuntimeError(f"serving: error replies {err[:2]}")
+        return time.perf_counter() - t0, lat
+
+    wave(make_text_prompts(n, tok, seed=11))  # warm-up (distinct prompts: no cache hits later)
+    prompts = make_text_prompts(n, tok, seed=2)
+    n_prompt_tok = sum(len(tok(p)) for p in prompts)
+    tok0, calls0 = model.tokens, model.calls
+    dt1, lat1 = wave(prompts)
+    gen1 = model.tokens - tok0
+    calls1 = model.calls
+    dt2, lat2 = wave(prompts)
+    hits = n - (model.calls - calls1)
+    node.active = False
+    llm.close()
+    lat1.sort()
+    return {"workload": f"config 3: {path} bf16, {n} concurrent requests through handle_requests (REP contexts) "
+                        f"-> cached_inference -> Llama(prompt, max_tokens=100), greedy; then the same {n} again",
+            "wave1": {"requests": n, "calls": calls1 - calls0, "prompt_tokens": n_prompt_tok,
+                      "generated_tokens": gen1, "wall_s": round(dt1, 4), "tok_s": round(gen1 / dt1, 1),
+                      "p50_latency_s": round(lat1[len(lat1) // 2], 4), "max_latency_s": round(lat1[-1], 4)},
+            "wave2": {"requests": n, "hit_rate": round(hits / n, 3), "wall_s": round(dt2, 4),
+                      "max_latency_ms": round(max(lat2) * 1e3, 3)},
+            "overall_hit_rate": round(hits / (2 * n), 3)}
+
+
 class Sections:
     """Runs the bench sections in order with wall-clock timings on stderr.  The headline section
     raises on failure; optional ones report their error in the line, and are skipped once the
@@ -434,6 +536,8 @@ def main():
     ap.add_argument("--tiny-tokens", type=int, default=128,
                     help="TinyLlama-1.1B batch-1 tokens (config 2; 0: skip the section)")
     ap.add_argument("--big-steps", type=int, default=8, help="Llama-3-70B decode steps (0: skip the section)")
+    ap.add_argument("--serve-requests", type=int, default=32,
+                    help="config 3 through the node's handler: concurrent requests (0: skip the section)")
     ap.add_argument("--budget", type=float, default=360.0,
                     help="seconds after which optional sections are skipped")
     ap.add_argument("--force-pipeline", action="store_true", help="run the torch.distributed pipeline path even at N=1")
@@ -472,6 +576,11 @@ def main():
     for k in ("batch1", "prefill"):
         if k in res:
             line[k] = res[k]
+    if args.serve_requests > 0:
+        sv = sec.run("serving", lambda: serving_bench(args, args.serve_requests))
+        if "wave1" in sv:
+            sv["ratio_to_value"] = round(sv["wave1"]["tok_s"] / line["value"], 4)
+        line["serving"] = sv
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = sec.run("cpu_baseline", lambda: cpu_baseline(args.model))
     if args.tiny_tokens > 0:

@@ -59,6 +59,8 @@ typedef struct {
   int32_t device;      /* HIP device ordinal, -1 = current device */
   int32_t use_graphs;  /* capture decode steps as hipGraphs (1) */
   uint64_t seed;       /* weights seed for "synthetic:<shape>" model paths */
+  int32_t handoff_bf16;/* pipeline stage hand-off: x_in / x_out of mx_batch_step, mx_stage_rows and
+                          mx_stage_rows_pick are bf16 [rows][n_embd] (1) instead of f32 (0) */
 } mx_opts;
 
 typedef struct {
@@ -83,6 +85,19 @@ typedef struct {
   float frequency_penalty; /* 0.0 = off: logit -= count * frequency_penalty (llama.cpp penalties sampler) */
   float presence_penalty;  /* 0.0 = off: logit -= (count > 0) * presence_penalty */
 } mx_sampling;
+
+/* One row's sampler for the device sampling chain (pipeline lanes, mx_batch_reset / mx_stage_rows_pick):
+ * the settings, the request's sampler stream (seed; the n-th sampled token of a request uses draw n),
+ * how many tokens it sampled so far, and its penalty window -- the last n_win (<= 64) tokens of
+ * prompt + output.  temperature <= 0 without penalties = greedy argmax.  Device-sampleable settings:
+ * top_k in 1..64 and, with penalties, repeat_last_n in 0..64 (otherwise MX_ERR_ARG). */
+typedef struct {
+  mx_sampling s;
+  uint64_t seed;
+  int32_t n_drawn;
+  int32_t n_win;
+  int32_t win[64];
+} mx_row_sampler;
 
 void mx_opts_default(mx_opts* o);
 void mx_sampling_default(mx_sampling* s);
@@ -150,12 +165,24 @@ int32_t* mx_batch_ids_device(mx_batch* b);
  * (int32[M], e.g. a torch tensor that RCCL receives into); current ids are copied over. */
 int mx_batch_bind_ids(mx_engine* e, mx_batch* b, int32_t* ids_device);
 int mx_batch_tokens(mx_engine* e, mx_batch* b, int32_t* out, int cap, int* n_steps);
+/* Re-arm a batch for its next run without re-capturing its graphs (pipeline lanes): positions of all
+ * M rows, next ids (NULL: keep the device ids), per-row samplers (NULL: greedy argmax over the last
+ * stage's logits), token history restarted; the copies are ordered on `stream` (NULL: engine stream). */
+int mx_batch_reset(mx_engine* e, mx_batch* b, const int32_t* pos, const int32_t* ids, const mx_row_sampler* rows,
+                   void* stream);
 void mx_batch_destroy(mx_engine* e, mx_batch* b);
 
 /* Stage forward of arbitrary rows (pipelined prefill): like mx_forward_rows but
  * with device x_in / x_out as in mx_batch_step; logits_out (host) only on the last stage. */
 int mx_stage_rows(mx_engine* e, int n, const int32_t* slots, const int32_t* pos, const int32_t* ids,
                   const void* x_in, void* x_out, float* logits_out, void* stream);
+/* Pipelined prefill of n rows (any count: GEMM chunks as mx_forward_rows; x_in / x_out device
+ * [n][n_embd] in the hand-off dtype).  On the last stage, rows rowmap[0..n_out) (increasing) each pick
+ * a token -- the device sampling chain with samp[i], or greedy argmax when samp is NULL -- copied to
+ * tok_out (host int32[n_out]); the first token of each prompt in the pipeline server. */
+int mx_stage_rows_pick(mx_engine* e, int n, const int32_t* slots, const int32_t* pos, const int32_t* ids,
+                       const void* x_in, void* x_out, int n_out, const int32_t* rowmap, const mx_row_sampler* samp,
+                       int32_t* tok_out, void* stream);
 
 /* Time `iters` passes of one layer-kernel kind over this stage's layers with
  * HIP events on the engine stream (benchmark roofline); kind: 0 qkv, 1 attn_output,

@@ -149,7 +149,7 @@ struct Request {
   int pos = 0;     // next position to write
   int reuse = 0;   // leading prompt positions whose K/V the slot already holds (prefix reuse)
   int32_t next_tok = 0;
-  std::mt19937_64 rng;
+  uint64_t seed = 0;  // sampler stream: the n-th sampled token draws samp_u01(seed, n) (kernels.h)
   std::string error;
 };
 
@@ -158,10 +158,12 @@ struct GraphKey {
   const void* xin;
   void* xout;
   hipStream_t stream;
+  int ktop;  // 0: greedy argmax tail; k: the device sampling chain with top-k k
   bool operator<(const GraphKey& o) const {
     if (M != o.M) return M < o.M;
     if (xin != o.xin) return xin < o.xin;
     if (xout != o.xout) return xout < o.xout;
+    if (ktop != o.ktop) return ktop < o.ktop;
     return stream < o.stream;
   }
 };
@@ -169,6 +171,8 @@ struct GraphKey {
 
 struct mx_batch {
   int M = 0, max_steps = 0;
+  SampRow* d_samp = nullptr;  // per-row device sampler settings (mx_batch_reset); null: greedy argmax
+  int ktop = 0;               // top-k of the device sampling chain, 0 = greedy argmax
   bool distinct = false;  // every row its own slot (decode); see mx_engine::rows_distinct
   int max_pos = 0;  // host mirror of the largest position, so steps never run past n_ctx
   int *d_ids = nullptr, *d_pos = nullptr, *d_slot = nullptr, *d_hist = nullptr, *d_hist_count = nullptr;
@@ -247,8 +251,33 @@ struct mx_engine {
   int *d_ids = nullptr, *d_pos = nullptr, *d_slot = nullptr, *d_rowmap = nullptr;
   std::vector<void*> allocations;
 
-  // graphs for the scheduler's decode steps, by M
-  std::map<int, hipGraphExec_t> sched_graphs;
+  // graphs for the scheduler's decode steps, by (M, top-k of the device sampling chain or 0 = argmax)
+  std::map<std::pair<int, int>, hipGraphExec_t> sched_graphs;
+  // pipeline stage hand-off dtype: x_in / x_out are bf16 [M][n_embd] instead of f32 (mx_opts.handoff_bf16)
+  bool handoff_bf16 = false;
+  // token pick at the end of a forward with `argmax` set: greedy argmax, or (pick_samp) the device
+  // sampling chain with top-k pick_k over the rows' SampRow settings
+  const SampRow* pick_samp = nullptr;
+  int pick_k = 0;
+  SampRow* d_samp = nullptr;  // [MAX_ROWS] the scheduler's rows
+  void pick(int n_out, int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count, int max_hist,
+            hipStream_t s) {
+    if (pick_samp)
+      launch_sample_chain(logits, n_vocab, n_out, n_vocab, pick_samp, pick_k, tk_ws_val, tk_ws_idx, tk_val, tk_idx,
+                          d_tok, ids_next, pos_next, hist, hist_stride, hist_count, max_hist, s);
+    else
+      launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, ids_next, pos_next, hist, hist_stride,
+                    hist_count, max_hist, s);
+  }
+  int copy_out(void* x_out, int M, hipStream_t s) {  // the residual stream to the next stage
+    if (handoff_bf16) launch_f32_to_bf16((uint16_t*)x_out, x, (size_t)M * n_embd, s);
+    else HIPC(hipMemcpyAsync(x_out, x, (size_t)M * n_embd * 4, hipMemcpyDeviceToDevice, s));
+    return 0;
+  }
+  // SampRow of a request for a run that starts now (draw index and penalty window at this point)
+  void samp_row(const Request* r, SampRow* o) const;
+  // true when the device sampling chain can serve this request (top_k 1..64, window <= 64)
+  static bool device_sampleable(const mx_sampling& sp);
 
   // scheduler
   std::mutex gpu_mu;  // serialises all GPU work issued through the API
@@ -416,6 +445,7 @@ int mx_engine::init_common() {
   if (int rc = alloc((void**)&d_rowmap, (size_t)R * 4)) return rc;
   if (int rc = alloc((void**)&sched_hist, (size_t)MAX_ROWS * SCHED_KMAX * 4)) return rc;
   if (int rc = alloc((void**)&sched_hist_count, (size_t)MAX_ROWS * 4)) return rc;
+  if (int rc = alloc((void**)&d_samp, (size_t)MAX_ROWS * sizeof(SampRow))) return rc;
   if (wq8 || wkq) {
     const size_t kmax = std::max(n_embd, n_ff);
     if (int rc = alloc((void**)&xq8, (size_t)R * kmax)) return rc;
@@ -894,8 +924,12 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
   const bool nol = !wide && !wq8 && !wkq && norm_on_load && mm_can_norm_on_load(M, h);
   const bool qql = q8_on_load(M) || kq_on_load(M);  // residual-stream Σx² partials wanted
   if (x_in) {
-    HIPC(hipMemcpyAsync(x, x_in, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
-    if (nol || qql) launch_ssq(x, M, h, ssq, s);
+    if (handoff_bf16) {  // bf16 hand-off from the previous stage: widen, with the Σx² partials on the way
+      launch_bf16_to_f32(x, (const uint16_t*)x_in, M, h, (nol || qql) ? ssq : nullptr, s);
+    } else {
+      HIPC(hipMemcpyAsync(x, x_in, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
+      if (nol || qql) launch_ssq(x, M, h, ssq, s);
+    }
   } else {
     if (!has_embed) return fail(MX_ERR_STATE, "this stage has no token embedding: x_in required");
     if (embd_kq_type) {
@@ -977,9 +1011,8 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
         launch_mm(EPI_RESID, d, s))
       return fail(MX_ERR_ARG, "ffn_down launch shape");
   }
-  if (x_out) {
-    HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
-  }
+  if (x_out)
+    if (int rc = copy_out(x_out, M, s)) return rc;
   if (head) {
     if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
     MMArgs g{};
@@ -995,7 +1028,7 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     if ((pers_head ? launch_mm_pers(EPI_F32, g, s) : -1) != 0 && launch_mm(EPI_F32, g, s))
       return fail(MX_ERR_ARG, "lm_head launch shape");
     if (argmax)
-      launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, ids_next, pos_next, hist, hist_stride,
+      pick(n_out, ids_next, pos_next, hist, hist_stride,
                     hist_count, max_hist, s);
   }
   HIPC(hipGetLastError());
@@ -1050,7 +1083,8 @@ int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void
     launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);
     nslab = 0;
   }
-  if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
+  if (x_out)
+    if (int rc = copy_out(x_out, M, s)) return rc;
   if (head) {
     if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
     if (rowmap || n_out != M) {
@@ -1064,7 +1098,7 @@ int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void
     const int rc = n_out > 16 ? launch_mm_wide(EPI_F32, g, slabs, slab_stride, s) : launch_mm(EPI_F32, g, s);
     if (rc < 0) return fail(MX_ERR_ARG, "lm_head launch shape");
     if (argmax)
-      launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, ids_next, pos_next, hist, hist_stride,
+      pick(n_out, ids_next, pos_next, hist, hist_stride,
                     hist_count, max_hist, s);
   } else if (nslab) {
     launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);
@@ -1160,7 +1194,8 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);
     nslab = 0;
   }
-  if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
+  if (x_out)
+    if (int rc = copy_out(x_out, M, s)) return rc;
   if (head) {
     if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
     MMArgs g{};
@@ -1169,7 +1204,7 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     operand(g, x, h, out_norm, n_out, (rowmap || n_out != M) ? rowmap : nullptr);
     if (launch_mq8(EPI_F32, g, s)) return fail(MX_ERR_ARG, "q8 lm_head launch shape");
     if (argmax)
-      launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, ids_next, pos_next, hist, hist_stride,
+      pick(n_out, ids_next, pos_next, hist, hist_stride,
                     hist_count, max_hist, s);
   }
   HIPC(hipGetLastError());
@@ -1263,7 +1298,8 @@ int mx_engine::enqueue_forward_kq(int M, const int* pos, const int* slot, void* 
     launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);
     nslab = 0;
   }
-  if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
+  if (x_out)
+    if (int rc = copy_out(x_out, M, s)) return rc;
   if (head) {
     if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
     MMArgs g{};
@@ -1272,7 +1308,7 @@ int mx_engine::enqueue_forward_kq(int M, const int* pos, const int* slot, void* 
         launch_mkq(EPI_F32, g, s))
       return fail(MX_ERR_ARG, "kq lm_head launch shape");
     if (argmax)
-      launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, ids_next, pos_next, hist, hist_stride,
+      pick(n_out, ids_next, pos_next, hist, hist_stride,
                     hist_count, max_hist, s);
   }
   HIPC(hipGetLastError());
@@ -1340,7 +1376,8 @@ int mx_engine::enqueue_forward_gemm(int M, const int* pos, const int* slot, void
       return fail(MX_ERR_ARG, "prefill ffn_down GEMM shape");
   }
   if (nslab) launch_resid_norm(nullptr, 0, x, gslabs, nslab, gstride, nullptr, M, h, eps, s);
-  if (x_out) HIPC(hipMemcpyAsync(x_out, x, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
+  if (x_out)
+    if (int rc = copy_out(x_out, M, s)) return rc;
   if (head) {
     if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
     if (!rowmap) return fail(MX_ERR_ARG, "prefill head needs a row map");
@@ -1467,38 +1504,42 @@ int32_t mx_engine::sample_host(Request* r, const float* lg) {
 }
 
 int32_t mx_engine::sample_chain(Request* r, std::vector<std::pair<float, int>>& c) {
+  // the device sampling chain's code (kernels.h samp_pick), over candidates of any count
   const mx_sampling& sp = r->samp;
   const int k = (int)c.size();
-  std::vector<double> p(k);
-  double mx = c[0].first, sum = 0;
-  for (int i = 0; i < k; i++) sum += (p[i] = exp(c[i].first - mx));
-  for (auto& v : p) v /= sum;
-  if (sp.top_p < 1.0f) {
-    double cum = 0;
-    int keep = k;
-    for (int i = 0; i < k; i++) {
-      cum += p[i];
-      if (cum >= sp.top_p) { keep = i + 1; break; }
-    }
-    c.resize(keep);
-    p.resize(keep);
+  std::vector<float> v(k);
+  std::vector<int> id(k);
+  for (int i = 0; i < k; i++) v[i] = c[i].first, id[i] = c[i].second;
+  std::vector<double> p(k), w(k);
+  return samp_pick(v.data(), id.data(), k, sp.temperature, sp.top_p, sp.min_p, samp_u01(r->seed, r->out.size()),
+                   p.data(), w.data());
+}
+
+bool mx_engine::device_sampleable(const mx_sampling& sp) {
+  if (sp.top_k < 1 || sp.top_k > TOPK_MAX) return false;
+  if (has_penalties(sp) && (sp.repeat_last_n < 0 || sp.repeat_last_n > SAMP_WIN)) return false;
+  return true;
+}
+
+void mx_engine::samp_row(const Request* r, SampRow* o) const {
+  const mx_sampling& sp = r->samp;
+  memset(o, 0, sizeof(*o));
+  o->temp = sp.temperature;
+  o->top_p = sp.top_p;
+  o->min_p = sp.min_p;
+  o->repeat = sp.repeat_penalty;
+  o->freq = sp.frequency_penalty;
+  o->presence = sp.presence_penalty;
+  o->top_k = std::max(1, std::min(sp.top_k, TOPK_MAX));
+  o->last_n = has_penalties(sp) ? std::min(sp.repeat_last_n, SAMP_WIN) : 0;
+  o->seed = r->seed;
+  o->draw0 = (int)r->out.size();
+  const int np = (int)r->prompt.size(), no = (int)r->out.size();
+  o->n_win = std::min(o->last_n, np + no);
+  for (int j = 0; j < o->n_win; j++) {
+    const int t = np + no - o->n_win + j;
+    o->win[j] = t < np ? r->prompt[t] : r->out[t - np];
   }
-  if (sp.min_p > 0.f) {
-    int keep = 1;
-    for (int i = 1; i < (int)c.size(); i++)
-      if (p[i] >= sp.min_p * p[0]) keep = i + 1;
-    c.resize(keep);
-  }
-  std::vector<double> w(c.size());
-  double m0 = c[0].first / sp.temperature, s2 = 0;
-  for (size_t i = 0; i < c.size(); i++) s2 += (w[i] = exp(c[i].first / sp.temperature - m0));
-  std::uniform_real_distribution<double> U(0.0, s2);
-  double u = U(r->rng), acc = 0;
-  for (size_t i = 0; i < c.size(); i++) {
-    acc += w[i];
-    if (u < acc) return c[i].second;
-  }
-  return c.back().second;
 }
 
 // Prefill of every newly admitted request together (llama.cpp's eval of the prompt, SURVEY §3.2,
@@ -1601,18 +1642,27 @@ int mx_engine::prefill_batch(std::vector<Request*>& reqs) {
 int mx_engine::sched_step(std::vector<Request*>& rows) {
   const int M = (int)rows.size();
   std::vector<int32_t> ids(M), pos(M), slots(M);
-  bool all_greedy = true;
-  int room = SCHED_KMAX, need = 1;
+  bool all_greedy = true, all_dev = true;
+  int room = SCHED_KMAX, need = 1, ktop = 0;
   for (int i = 0; i < M; i++) {
     ids[i] = rows[i]->next_tok;
     pos[i] = rows[i]->pos;
     slots[i] = rows[i]->slot;
-    if (rows[i]->samp.temperature > 0.f || has_penalties(rows[i]->samp)) all_greedy = false;
+    const mx_sampling& sp = rows[i]->samp;
+    if (sp.temperature > 0.f || has_penalties(sp)) {
+      all_greedy = false;
+      if (use_dev_topk && device_sampleable(sp)) ktop = std::max(ktop, std::min(sp.top_k, n_vocab));
+      else all_dev = false;
+    }
     room = std::min(room, n_ctx - rows[i]->pos);
     need = std::max(need, rows[i]->max_tokens - (int)rows[i]->out.size());
   }
+  // greedy rows: argmax on the device; every row sampleable on the device: the device sampling chain
+  // (penalties, top-k, top-p, min-p, temperature, draw); either way K steps run back to back on the
+  // device.  Otherwise one step, sampled on the host.
+  const bool dev_chain = !all_greedy && all_dev && ktop > 0;
   int K = 1;
-  if (all_greedy) {
+  if (all_greedy || dev_chain) {
     K = std::max(1, std::min(room, need));
     std::lock_guard<std::mutex> lk(mu);
     if (!pending.empty() && !free_slots.empty()) K = 1;  // admit waiting requests at the next round
@@ -1622,8 +1672,19 @@ int mx_engine::sched_step(std::vector<Request*>& rows) {
   HIPC(hipMemcpyAsync(d_pos, pos.data(), M * 4, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(d_slot, slots.data(), M * 4, hipMemcpyHostToDevice, s));
   HIPC(hipMemsetAsync(sched_hist_count, 0, M * 4, s));
+  std::vector<SampRow> sr;
+  if (dev_chain) {
+    sr.resize(M);
+    for (int i = 0; i < M; i++) samp_row(rows[i], &sr[i]);
+    HIPC(hipMemcpyAsync(d_samp, sr.data(), M * sizeof(SampRow), hipMemcpyHostToDevice, s));
+  }
   rows_distinct = true;  // one row per active request, each its own slot
-  struct Reset { bool& f; ~Reset() { f = false; } } reset_distinct{rows_distinct};
+  pick_samp = dev_chain ? d_samp : nullptr;
+  pick_k = dev_chain ? ktop : 0;
+  struct Reset {
+    mx_engine* e;
+    ~Reset() { e->rows_distinct = false; e->pick_samp = nullptr; e->pick_k = 0; }
+  } reset_flags{this};
   auto step = [&]() -> int {
     return enqueue_forward(M, d_ids, d_pos, d_slot, nullptr, nullptr, true, nullptr, M, true, d_ids, d_pos,
                            sched_hist, SCHED_KMAX, sched_hist_count, SCHED_KMAX, s);
@@ -1631,7 +1692,8 @@ int mx_engine::sched_step(std::vector<Request*>& rows) {
   static const bool trace = getenv("MX_SCHED_TRACE") != nullptr;  // per-round timing on stderr
   const auto t0 = std::chrono::steady_clock::now();
   bool captured = false;
-  auto it = sched_graphs.find(M);
+  const std::pair<int, int> gkey(M, pick_k);
+  auto it = sched_graphs.find(gkey);
   if (use_graphs && it == sched_graphs.end()) {
     captured = true;
     hipGraph_t g;
@@ -1643,7 +1705,7 @@ int mx_engine::sched_step(std::vector<Request*>& rows) {
     hipGraphExec_t ex;
     HIPC(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
     hipGraphDestroy(g);
-    it = sched_graphs.emplace(M, ex).first;
+    it = sched_graphs.emplace(gkey, ex).first;
   }
   for (int k = 0; k < K; k++) {
     if (use_graphs) HIPC(hipGraphLaunch(it->second, s));
@@ -1656,7 +1718,7 @@ int mx_engine::sched_step(std::vector<Request*>& rows) {
   // sampling rows: the top-k candidates come from the device (k <= TOPK_MAX, no penalties, which
   // would reorder logits first); otherwise the whole logits rows go to the host
   int TK = 0;
-  bool dev_topk = !all_greedy && use_dev_topk;
+  bool dev_topk = !all_greedy && !dev_chain && use_dev_topk;
   for (int i = 0; i < M && dev_topk; i++) {
     const mx_sampling& sp = rows[i]->samp;
     if (sp.temperature <= 0.f && !has_penalties(sp)) continue;
@@ -1670,14 +1732,15 @@ int mx_engine::sched_step(std::vector<Request*>& rows) {
     tki.resize((size_t)M * TK);
     HIPC(hipMemcpyAsync(tkv.data(), tk_val, (size_t)M * TK * 4, hipMemcpyDeviceToHost, s));
     HIPC(hipMemcpyAsync(tki.data(), tk_idx, (size_t)M * TK * 4, hipMemcpyDeviceToHost, s));
-  } else if (!all_greedy) {
+  } else if (!all_greedy && !dev_chain) {
     lg.resize((size_t)M * n_vocab);
     HIPC(hipMemcpyAsync(lg.data(), logits, (size_t)M * n_vocab * 4, hipMemcpyDeviceToHost, s));
   }
   HIPC(hipStreamSynchronize(s));
   if (trace) {
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    fprintf(stderr, "sched: decode M=%d K=%d %s%.3f ms\n", M, K, captured ? "(graph captured) " : "", ms);
+    fprintf(stderr, "sched: decode M=%d K=%d %s%s%.3f ms\n", M, K, dev_chain ? "(device sampling) " : "",
+            captured ? "(graph captured) " : "", ms);
   }
   std::lock_guard<std::mutex> lk(mu);
   for (int i = 0; i < M; i++) {
@@ -1685,7 +1748,7 @@ int mx_engine::sched_step(std::vector<Request*>& rows) {
     for (int k = 0; k < K && !r->done; k++) {
       r->pos++;
       int32_t t = hist[(size_t)i * SCHED_KMAX + k];
-      if (r->samp.temperature > 0.f || has_penalties(r->samp)) {
+      if (!dev_chain && (r->samp.temperature > 0.f || has_penalties(r->samp))) {
         if (!tkv.empty()) {
           std::vector<std::pair<float, int>> c(std::min(r->samp.top_k, n_vocab));
           for (size_t j = 0; j < c.size(); j++) c[j] = {tkv[(size_t)i * TK + j], tki[(size_t)i * TK + j]};
@@ -1793,6 +1856,7 @@ void mx_opts_default(mx_opts* o) {
   o->device = -1;
   o->use_graphs = 1;
   o->seed = 0;
+  o->handoff_bf16 = 0;
 }
 
 void mx_sampling_default(mx_sampling* s) {
@@ -1823,6 +1887,7 @@ int mx_engine_create(const char* model_path, const mx_opts* opts, mx_engine** ou
   e->lb = o.layer_begin;
   e->le = o.layer_end;
   e->use_graphs = o.use_graphs != 0 && getenv("MX_NO_GRAPHS") == nullptr;  // rocprofv3 runs set MX_NO_GRAPHS
+  e->handoff_bf16 = o.handoff_bf16 != 0;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MX_ERR_HIP, "no HIP device visible");
   if (o.device >= 0) HIPC(hipSetDevice(o.device));
@@ -1946,7 +2011,8 @@ static int make_request(mx_engine* e, const int32_t* ids, int n, const mx_sampli
   mx_sampling_default(&r->samp);
   if (s) r->samp = *s;
   r->max_tokens = max_tokens <= 0 ? e->n_ctx - n : std::min(max_tokens, e->n_ctx - n);
-  r->rng.seed(r->samp.seed == 0xFFFFFFFFull ? std::random_device{}() : r->samp.seed);
+  r->seed = r->samp.seed == 0xFFFFFFFFull ? ((uint64_t)std::random_device{}() << 32 | std::random_device{}())
+                                           : r->samp.seed;
   *out = std::move(r);
   return 0;
 }
@@ -2099,7 +2165,12 @@ int mx_batch_step(mx_engine* e, mx_batch* b, const void* x_in, void* x_out, void
   if (!x_in && !e->has_embed) return fail(MX_ERR_STATE, "x_in is required on a non-first pipeline stage");
   auto body = [&]() -> int {
     e->rows_distinct = b->distinct;
-    struct Reset { bool& f; ~Reset() { f = false; } } reset_distinct{e->rows_distinct};
+    e->pick_samp = head && b->ktop > 0 ? b->d_samp : nullptr;
+    e->pick_k = head ? b->ktop : 0;
+    struct Reset {
+      mx_engine* e;
+      ~Reset() { e->rows_distinct = false; e->pick_samp = nullptr; e->pick_k = 0; }
+    } reset_flags{e};
     if (int rc = e->enqueue_forward(b->M, b->d_ids, b->d_pos, b->d_slot, x_in, x_out, head, nullptr, b->M, head,
                                     b->d_ids, b->d_pos, b->d_hist, b->max_steps, b->d_hist_count, b->max_steps, s))
       return rc;
@@ -2107,7 +2178,7 @@ int mx_batch_step(mx_engine* e, mx_batch* b, const void* x_in, void* x_out, void
     return 0;
   };
   if (!e->use_graphs) return body();
-  GraphKey key{b->M, x_in, x_out, s};
+  GraphKey key{b->M, x_in, x_out, s, head ? b->ktop : 0};
   auto it = b->graphs.find(key);
   if (it == b->graphs.end()) {
     hipGraph_t g;
@@ -2155,7 +2226,127 @@ void mx_batch_destroy(mx_engine* e, mx_batch* b) {
   hipFree(b->d_slot);
   hipFree(b->d_hist);
   hipFree(b->d_hist_count);
+  if (b->d_samp) hipFree(b->d_samp);
   delete b;
+}
+
+static int fill_samp_rows(mx_engine* e, int n, const mx_row_sampler* rows, std::vector<SampRow>& out, int* ktop) {
+  out.assign(n, SampRow{});
+  *ktop = 0;
+  for (int i = 0; i < n; i++) {
+    const mx_sampling& sp = rows[i].s;
+    const bool sampling = sp.temperature > 0.f || has_penalties(sp);
+    if (sampling && !mx_engine::device_sampleable(sp))
+      return fail(MX_ERR_ARG, "row " + std::to_string(i) + ": sampling settings need the host sampler "
+                                  "(top_k outside 1..64 or a penalty window over 64 tokens)");
+    if (rows[i].n_win < 0 || rows[i].n_win > SAMP_WIN) return fail(MX_ERR_ARG, "penalty window over 64 tokens");
+    SampRow& o = out[i];
+    o.temp = sp.temperature; o.top_p = sp.top_p; o.min_p = sp.min_p; o.repeat = sp.repeat_penalty;
+    o.freq = sp.frequency_penalty; o.presence = sp.presence_penalty;
+    o.top_k = std::max(1, std::min(sp.top_k, TOPK_MAX));
+    o.last_n = has_penalties(sp) ? std::min(sp.repeat_last_n, SAMP_WIN) : 0;
+    o.seed = rows[i].seed;
+    o.draw0 = rows[i].n_drawn;
+    o.n_win = std::min(rows[i].n_win, o.last_n);
+    for (int j = 0; j < o.n_win; j++) o.win[j] = rows[i].win[rows[i].n_win - o.n_win + j];
+    if (sampling) *ktop = std::max(*ktop, std::min(o.top_k, e->n_vocab));
+  }
+  return 0;
+}
+
+int mx_batch_reset(mx_engine* e, mx_batch* b, const int32_t* pos, const int32_t* ids, const mx_row_sampler* rows,
+                   void* stream) {
+  if (!e || !b || !pos) return fail(MX_ERR_ARG, "null argument");
+  int max_pos = 0;
+  for (int i = 0; i < b->M; i++) {
+    if (pos[i] < 0 || pos[i] >= e->n_ctx) return fail(MX_ERR_CTX, "position outside n_ctx");
+    if (ids && (ids[i] < 0 || ids[i] >= e->n_vocab)) return fail(MX_ERR_ARG, "token id out of range");
+    max_pos = std::max(max_pos, (int)pos[i]);
+  }
+  std::vector<SampRow> sr;
+  int ktop = 0;
+  if (rows)
+    if (int rc = fill_samp_rows(e, b->M, rows, sr, &ktop)) return rc;
+  std::lock_guard<std::mutex> lk(e->gpu_mu);
+  hipSetDevice(e->device);
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  HIPC(hipMemcpyAsync(b->d_pos, pos, b->M * 4, hipMemcpyHostToDevice, s));
+  if (ids) HIPC(hipMemcpyAsync(b->d_ids, ids, b->M * 4, hipMemcpyHostToDevice, s));
+  HIPC(hipMemsetAsync(b->d_hist_count, 0, b->M * 4, s));
+  if (ktop > 0) {
+    if (!b->d_samp) HIPC(hipMalloc((void**)&b->d_samp, (size_t)MAX_ROWS * sizeof(SampRow)));
+    HIPC(hipMemcpyAsync(b->d_samp, sr.data(), b->M * sizeof(SampRow), hipMemcpyHostToDevice, s));
+  }
+  HIPC(hipStreamSynchronize(s));  // the host arrays may go away when this returns
+  b->ktop = ktop;
+  b->max_pos = max_pos;
+  return 0;
+}
+
+int mx_stage_rows_pick(mx_engine* e, int n, const int32_t* slots, const int32_t* pos, const int32_t* ids,
+                       const void* x_in, void* x_out, int n_out, const int32_t* rowmap, const mx_row_sampler* samp,
+                       int32_t* tok_out, void* stream) {
+  if (!e || n < 1 || !slots || !pos || n_out < 0 || (n_out && (!rowmap || !tok_out)))
+    return fail(MX_ERR_ARG, "mx_stage_rows_pick: bad arguments");
+  if (!x_in && (!e->has_embed || !ids)) return fail(MX_ERR_STATE, "x_in is required on a non-first pipeline stage");
+  if (n_out && (x_out || !e->has_head)) return fail(MX_ERR_STATE, "tokens are picked on the last stage only");
+  for (int k = 0; k < n_out; k++)
+    if (rowmap[k] < 0 || rowmap[k] >= n || (k && rowmap[k] <= rowmap[k - 1]))
+      return fail(MX_ERR_ARG, "rowmap must be increasing row indices");
+  std::vector<SampRow> sr;
+  int ktop = 0;
+  if (samp && n_out)
+    if (int rc = fill_samp_rows(e, n_out, samp, sr, &ktop)) return rc;
+  std::lock_guard<std::mutex> lk(e->gpu_mu);
+  hipSetDevice(e->device);
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  const size_t xb = (size_t)e->n_embd * (e->handoff_bf16 ? 2 : 4);  // hand-off bytes per row
+  const int chunk = e->gemm_ok() ? PREFILL_ROWS : MAX_ROWS;
+  int k0 = 0;  // first rowmap entry not yet produced
+  for (int i = 0; i < n;) {
+    int end = std::min(n, i + chunk), k1 = k0;
+    while (k1 < n_out && rowmap[k1] < end && k1 - k0 < MAX_ROWS) k1++;
+    if (k1 - k0 == MAX_ROWS && k1 < n_out && rowmap[k1] < end) end = rowmap[k1 - 1] + 1;
+    const int m = end - i, no = k1 - k0;
+    for (int r = i; r < end; r++) {
+      if (slots[r] < 0 || slots[r] >= e->n_seq_max) return fail(MX_ERR_ARG, "slot out of range");
+      if (pos[r] < 0 || pos[r] >= e->n_ctx) return fail(MX_ERR_CTX, "position outside n_ctx");
+      if (!x_in && (ids[r] < 0 || ids[r] >= e->n_vocab)) return fail(MX_ERR_ARG, "token id out of range");
+    }
+    if (!x_in) HIPC(hipMemcpyAsync(e->d_ids, ids + i, m * 4, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(e->d_pos, pos + i, m * 4, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(e->d_slot, slots + i, m * 4, hipMemcpyHostToDevice, s));
+    std::vector<int32_t> rm(no);
+    for (int k = 0; k < no; k++) rm[k] = rowmap[k0 + k] - i;
+    if (no) HIPC(hipMemcpyAsync(e->d_rowmap, rm.data(), no * 4, hipMemcpyHostToDevice, s));
+    if (no && ktop > 0) HIPC(hipMemcpyAsync(e->d_samp, sr.data() + k0, no * sizeof(SampRow), hipMemcpyHostToDevice, s));
+    {
+      std::lock_guard<std::mutex> lk2(e->mu);
+      for (int r = i; r < end; r++) e->slot_tokens[slots[r]].clear();
+    }
+    e->rows_distinct = false;
+    e->rows_blocked = true;
+    for (int r = 0; r < m && e->rows_blocked; r++)
+      if (r % 16 && (slots[i + r] != slots[i + r - r % 16] || pos[i + r] != pos[i + r - r % 16] + r % 16))
+        e->rows_blocked = false;
+    e->pick_samp = ktop > 0 ? e->d_samp : nullptr;
+    e->pick_k = ktop;
+    const char* xi = (const char*)x_in;
+    char* xo = (char*)x_out;
+    const int frc = e->enqueue_forward(m, e->d_ids, e->d_pos, e->d_slot, xi ? xi + i * xb : nullptr,
+                                       xo ? xo + i * xb : nullptr, no > 0, no ? e->d_rowmap : nullptr, no, false,
+                                       nullptr, nullptr, nullptr, 0, nullptr, 0, s);
+    e->rows_blocked = false;
+    if (!frc && no) e->pick(no, nullptr, nullptr, nullptr, 0, nullptr, 0, s);  // logits rows [no][V]
+    e->pick_samp = nullptr;
+    e->pick_k = 0;
+    if (frc) return frc;
+    if (no) HIPC(hipMemcpyAsync(tok_out + k0, e->d_tok, no * 4, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    k0 = k1;
+    i = end;
+  }
+  return 0;
 }
 
 int mx_engine_stats(mx_engine* e, mx_stats* out) {

@@ -221,6 +221,71 @@ void launch_argmax(const float* logits, int ldl, int M, int V, float* ws_val, in
                    int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count, int max_hist,
                    hipStream_t s);
 
+// ---- device sampling chain (llama-cpp-python 0.3's create_completion chain as
+// engine.cpp restates it): penalties over the last last_n tokens -> top_k -> top_p -> min_p ->
+// temperature -> draw; temperature <= 0 = greedy (after the penalties).  One SampRow per logits row.
+constexpr int SAMP_WIN = 64;
+struct SampRow {
+  float temp, top_p, min_p, repeat, freq, presence;
+  int top_k;    // 1..TOPK_MAX on the device path
+  int last_n;   // penalty window (0..SAMP_WIN); 0 = no penalties
+  uint64_t seed;
+  int draw0;    // index of the row's next random draw = tokens the request sampled before this run
+  int n_win;    // penalty window at the start of the run: the last n_win tokens of prompt + output
+  int win[SAMP_WIN];
+};
+// counter-based uniform draw in [0, 1) (splitmix64 of seed and draw index): host and device agree
+__host__ __device__ inline double samp_u01(uint64_t seed, uint64_t draw) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (draw + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (double)(z >> 11) * (1.0 / 9007199254740992.0);
+}
+// top_p / min_p / temperature / draw over k candidates sorted by value (descending, ties lower id
+// first); p and w are scratch of k doubles.  The host sampler and sample_kernel both call this.
+__host__ __device__ inline int samp_pick(const float* vals, const int* ids, int k, float temp, float top_p,
+                                         float min_p, double u01, double* p, double* w) {
+  if (temp <= 0.f || k <= 1) return ids[0];
+  const double mx = vals[0];
+  double sum = 0;
+  for (int i = 0; i < k; i++) sum += (p[i] = exp((double)vals[i] - mx));
+  for (int i = 0; i < k; i++) p[i] /= sum;
+  int keep = k;
+  if (top_p < 1.0f) {
+    double cum = 0;
+    for (int i = 0; i < k; i++) {
+      cum += p[i];
+      if (cum >= top_p) { keep = i + 1; break; }
+    }
+  }
+  if (min_p > 0.f) {
+    int kk = 1;
+    for (int i = 1; i < keep; i++)
+      if (p[i] >= min_p * p[0]) kk = i + 1;
+    keep = kk;
+  }
+  const double m0 = (double)vals[0] / temp;
+  double s2 = 0;
+  for (int i = 0; i < keep; i++) s2 += (w[i] = exp((double)vals[i] / temp - m0));
+  const double u = u01 * s2;
+  double acc = 0;
+  for (int i = 0; i < keep; i++) {
+    acc += w[i];
+    if (u < acc) return ids[i];
+  }
+  return ids[keep - 1];
+}
+// penalties (in place on the logits rows), top-k of K = max top_k of the rows, the draw, then the
+// same token bookkeeping as launch_argmax (tok_out, ids_next, pos_next, history)
+int launch_sample_chain(float* logits, int ldl, int M, int V, const SampRow* samp, int K, float* ws_val, int* ws_idx,
+                        float* tk_val, int* tk_idx, int* tok_out, int* ids_next, int* pos_next, int* hist,
+                        int hist_stride, int* hist_count, int max_hist, hipStream_t s);
+// hand-off conversions of the residual stream (pipeline stages): f32 <-> bf16 rows (RNE), and the
+// per-16-element sums of squares of the f32 rows made from bf16 (RMS_NORM-on-load consumers)
+void launch_f32_to_bf16(uint16_t* dst, const float* src, size_t n, hipStream_t s);
+void launch_bf16_to_f32(float* dst, const uint16_t* src, int M, int n, float* ssq, hipStream_t s);
+
 // HBM streaming probes: variant v of probe_variants() (loads in flight, grid, non-temporal) of a
 // read-only (XOR fold) or copy stream over n16 16-byte words (n16 % 4096 == 0); desc describes it
 int probe_variants();

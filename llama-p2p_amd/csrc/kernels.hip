@@ -1418,6 +1418,120 @@ void launch_argmax(const float* logits, int ldl, int M, int V, float* ws_val, in
                                  max_hist);
 }
 
+// ---------------------------------------------------------------------------
+// Device sampling chain.  penalty_kernel: llama.cpp's penalties sampler over the row's window (the
+// last last_n tokens of prompt + output: the n_win tokens given at the start of the run, then the
+// tokens this run generated, hist[0..hist_count)).  Lane j holds window token j; the lane holding a
+// token's first occurrence counts its occurrences and rewrites that one logit: divided by `repeat`
+// when positive (multiplied otherwise), then count*freq + presence subtracted -- engine.cpp
+// sample_host's arithmetic, in the same order.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void penalty_kernel(float* logits, int ldl, const SampRow* samp, const int* hist,
+                                                     int hist_stride, const int* hist_count) {
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const SampRow& sp = samp[c];
+  if (sp.last_n <= 0 || (sp.repeat == 1.0f && sp.freq == 0.0f && sp.presence == 0.0f)) return;
+  const int nh = hist ? hist_count[c] : 0;
+  const int total = sp.n_win + nh;
+  const int n = min(sp.last_n, total);
+  const int j = total - n + lane;
+  int t = -1;
+  if (lane < n) t = j < sp.n_win ? sp.win[j] : hist[(size_t)c * hist_stride + (j - sp.n_win)];
+  int count = 0;
+  bool first = lane < n;
+  for (int o = 0; o < 64; ++o) {
+    const int u = __shfl(t, o);
+    count += (u == t && t >= 0) ? 1 : 0;
+    if (o < lane && u == t) first = false;
+  }
+  if (first && t >= 0) {
+    float* lp = logits + (size_t)c * ldl + t;
+    float v = *lp;
+    if (sp.repeat != 1.0f) v = v <= 0.f ? v * sp.repeat : v / sp.repeat;
+    *lp = v - ((float)count * sp.freq + sp.presence);
+  }
+}
+
+// one wave per row over its top-k candidates: lane 0 runs samp_pick (the host sampler's code) on
+// the k <= 64 candidates; draw index = draw0 + tokens this run already generated for the row
+__global__ __launch_bounds__(64) void sample_kernel(const float* tk_val, const int* tk_idx, int K, const SampRow* samp,
+                                                    int* tok_out, int* ids_next, int* pos_next, int* hist,
+                                                    int hist_stride, int* hist_count, int max_hist) {
+  const int c = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  const SampRow& sp = samp[c];
+  const int nh = hist ? hist_count[c] : 0;
+  double p[TOPK_MAX], w[TOPK_MAX];
+  const int k = max(1, min(sp.top_k, K));
+  const int tok = samp_pick(tk_val + (size_t)c * K, tk_idx + (size_t)c * K, k, sp.temp, sp.top_p, sp.min_p,
+                            samp_u01(sp.seed, (uint64_t)(sp.draw0 + nh)), p, w);
+  if (tok_out) tok_out[c] = tok;
+  if (ids_next) ids_next[c] = tok;
+  if (pos_next) pos_next[c] += 1;
+  if (hist) {
+    if (nh < max_hist) hist[(size_t)c * hist_stride + nh] = tok;
+    hist_count[c] = nh + 1;
+  }
+}
+
+int launch_sample_chain(float* logits, int ldl, int M, int V, const SampRow* samp, int K, float* ws_val, int* ws_idx,
+                        float* tk_val, int* tk_idx, int* tok_out, int* ids_next, int* pos_next, int* hist,
+                        int hist_stride, int* hist_count, int max_hist, hipStream_t s) {
+  if (K < 1 || K > TOPK_MAX || M < 1) return -1;
+  penalty_kernel<<<M, 64, 0, s>>>(logits, ldl, samp, hist, hist_stride, hist_count);
+  if (launch_topk(logits, ldl, M, V, K, ws_val, ws_idx, tk_val, tk_idx, s)) return -1;
+  sample_kernel<<<M, 64, 0, s>>>(tk_val, tk_idx, K, samp, tok_out, ids_next, pos_next, hist, hist_stride, hist_count,
+                                 max_hist);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// pipeline hand-off of the residual stream in bf16 (half the bytes of f32 per stage boundary)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void f32_to_bf16_kernel(uint16_t* dst, const float* src, size_t n4) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(src)[i];
+    u32x2 o;
+    o[0] = f2bf(v[0]) | (f2bf(v[1]) << 16);
+    o[1] = f2bf(v[2]) | (f2bf(v[3]) << 16);
+    reinterpret_cast<u32x2*>(dst)[i] = o;
+  }
+}
+
+// one work-group per row; ssq as embed_kernel / ssq_kernel (per 16-element tile, double sum)
+__global__ __launch_bounds__(256) void bf16_to_f32_kernel(float* x, const uint16_t* src, int n, float* ssq) {
+  const int c = blockIdx.x;
+  const u32x4* s4 = reinterpret_cast<const u32x4*>(src + (size_t)c * n);
+  f32x4* dst = reinterpret_cast<f32x4*>(x + (size_t)c * n);
+  for (int t = threadIdx.x; t < n / 16; t += blockDim.x) {
+    double q = 0.0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const u32x4 v = s4[2 * t + h];
+      f32x4 lo, hi;
+      lo[0] = __uint_as_float(v[0] << 16); lo[1] = __uint_as_float(v[0] & 0xffff0000u);
+      lo[2] = __uint_as_float(v[1] << 16); lo[3] = __uint_as_float(v[1] & 0xffff0000u);
+      hi[0] = __uint_as_float(v[2] << 16); hi[1] = __uint_as_float(v[2] & 0xffff0000u);
+      hi[2] = __uint_as_float(v[3] << 16); hi[3] = __uint_as_float(v[3] & 0xffff0000u);
+      dst[4 * t + 2 * h] = lo;
+      dst[4 * t + 2 * h + 1] = hi;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) q += (double)(lo[i] * lo[i]) + (double)(hi[i] * hi[i]);
+    }
+    if (ssq) ssq[(size_t)c * (n / 16) + t] = (float)q;
+  }
+}
+
+void launch_f32_to_bf16(uint16_t* dst, const float* src, size_t n, hipStream_t s) {
+  const size_t n4 = n / 4;
+  const int grid = (int)std::min<size_t>(1024, (n4 + 255) / 256);
+  f32_to_bf16_kernel<<<std::max(grid, 1), 256, 0, s>>>(dst, src, n4);
+}
+
+void launch_bf16_to_f32(float* dst, const uint16_t* src, int M, int n, float* ssq, hipStream_t s) {
+  bf16_to_f32_kernel<<<M, 256, 0, s>>>(dst, src, n, ssq);
+}
+
 }  // namespace mx
 
 namespace mx {

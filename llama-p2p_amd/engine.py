@@ -26,7 +26,7 @@ EXPORTS = [
     "mx_opts_default", "mx_sampling_default", "mx_last_error", "mx_engine_create", "mx_engine_destroy", "mx_gguf_check",
     "mx_engine_info", "mx_forward_logits", "mx_forward_rows", "mx_forward_topk", "mx_submit", "mx_wait", "mx_submit_batch", "mx_poll", "mx_cancel", "mx_batch_create",
     "mx_batch_step", "mx_batch_ids_device", "mx_batch_bind_ids", "mx_batch_tokens", "mx_batch_destroy", "mx_stage_rows",
-    "mx_profile_kernel", "mx_sync", "mx_device_count", "mx_engine_stats",
+    "mx_profile_kernel", "mx_sync", "mx_device_count", "mx_engine_stats", "mx_batch_reset", "mx_stage_rows_pick",
     "mx_probe_copy", "mx_probe_read",
 ]
 
@@ -40,7 +40,7 @@ class MxError(RuntimeError):
 class MxOpts(ctypes.Structure):
     _fields_ = [("n_ctx", ctypes.c_int32), ("n_seq_max", ctypes.c_int32), ("layer_begin", ctypes.c_int32),
                 ("layer_end", ctypes.c_int32), ("device", ctypes.c_int32), ("use_graphs", ctypes.c_int32),
-                ("seed", ctypes.c_uint64)]
+                ("seed", ctypes.c_uint64), ("handoff_bf16", ctypes.c_int32)]
 
 
 class MxModelInfo(ctypes.Structure):
@@ -57,6 +57,39 @@ class MxSampling(ctypes.Structure):
                 ("min_p", ctypes.c_float), ("repeat_penalty", ctypes.c_float), ("repeat_last_n", ctypes.c_int32),
                 ("seed", ctypes.c_uint64), ("ignore_eos", ctypes.c_int32),
                 ("frequency_penalty", ctypes.c_float), ("presence_penalty", ctypes.c_float)]
+
+
+class MxRowSampler(ctypes.Structure):
+    _fields_ = [("s", MxSampling), ("seed", ctypes.c_uint64), ("n_drawn", ctypes.c_int32), ("n_win", ctypes.c_int32),
+                ("win", ctypes.c_int32 * 64)]
+
+
+def sampling(temperature: float = 0.0, top_k: int = 40, top_p: float = 0.95, min_p: float = 0.05,
+             repeat_penalty: float = 1.0, repeat_last_n: int = 64, seed: Optional[int] = None,
+             ignore_eos: bool = False, frequency_penalty: float = 0.0, presence_penalty: float = 0.0) -> MxSampling:
+    """An mx_sampling with llama-cpp-python's defaults for the unspecified fields."""
+    s = MxSampling()
+    lib().mx_sampling_default(ctypes.byref(s))
+    s.temperature, s.top_k, s.top_p, s.min_p = temperature, top_k, top_p, min_p
+    s.repeat_penalty, s.repeat_last_n, s.ignore_eos = repeat_penalty, repeat_last_n, int(ignore_eos)
+    s.frequency_penalty, s.presence_penalty = frequency_penalty, presence_penalty
+    if seed is not None and seed >= 0:
+        s.seed = seed
+    return s
+
+
+def row_samplers(rows) -> "ctypes.Array":
+    """rows: [(MxSampling, seed, n_drawn, window tokens)] -> mx_row_sampler[len(rows)]."""
+    arr = (MxRowSampler * len(rows))()
+    for i, (smp, seed, n_drawn, win) in enumerate(rows):
+        win = list(win)[-64:]
+        arr[i].s = smp
+        arr[i].seed = seed
+        arr[i].n_drawn = n_drawn
+        arr[i].n_win = len(win)
+        for j, t in enumerate(win):
+            arr[i].win[j] = int(t)
+    return arr
 
 
 _lib = None
@@ -104,6 +137,8 @@ def lib() -> ctypes.CDLL:
         L.mx_probe_read.argtypes = [i32, ctypes.c_size_t, i32, P(ctypes.c_double), ctypes.c_char_p, i32]
         L.mx_device_count.argtypes = [P(i32)]
         L.mx_engine_stats.argtypes = [vp, P(MxStats)]
+        L.mx_batch_reset.argtypes = [vp, vp, vp, vp, vp, vp]
+        L.mx_stage_rows_pick.argtypes = [vp, i32, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp]
         for name in EXPORTS:
             if name not in ("mx_opts_default", "mx_sampling_default", "mx_last_error", "mx_engine_destroy",
                             "mx_batch_destroy", "mx_batch_ids_device"):
@@ -151,13 +186,16 @@ class Engine:
     """One engine instance = one GPU, one model (or one pipeline stage of it)."""
 
     def __init__(self, model_path: str, n_ctx: int = 512, n_seq_max: int = 64, layer_begin: int = 0,
-                 layer_end: int = -1, device: int = -1, use_graphs: bool = True, seed: int = 0):
+                 layer_end: int = -1, device: int = -1, use_graphs: bool = True, seed: int = 0,
+                 handoff_bf16: bool = False):
         L = lib()
         opts = MxOpts()
         L.mx_opts_default(ctypes.byref(opts))
         opts.n_ctx, opts.n_seq_max = n_ctx, n_seq_max
         opts.layer_begin, opts.layer_end, opts.device = layer_begin, layer_end, device
         opts.use_graphs, opts.seed = int(use_graphs), seed
+        opts.handoff_bf16 = int(handoff_bf16)
+        self.handoff_bf16 = bool(handoff_bf16)
         h = ctypes.c_void_p()
         _check(L.mx_engine_create(model_path.encode(), ctypes.byref(opts), ctypes.byref(h)))
         self._h = h
@@ -204,6 +242,20 @@ class Engine:
                                    x_in or None, x_out or None, out.ctypes.data if out is not None else None,
                                    stream or None))
         return out
+
+    def stage_rows_pick(self, slots, pos, ids, x_in: int = 0, x_out: int = 0, rowmap=(), samplers=None,
+                        stream: int = 0):
+        """Pipelined prefill of any number of rows; on the last stage the rows in `rowmap` pick a token
+        each (samplers: row_samplers() array or None for greedy).  Returns the tokens (list)."""
+        slots, pos = _i32(slots), _i32(pos)
+        ids_a = _i32(ids) if ids is not None else None
+        rm = _i32(rowmap)
+        tok = np.zeros(max(1, len(rm)), dtype=np.int32)
+        _check(lib().mx_stage_rows_pick(self._h, len(slots), slots.ctypes.data, pos.ctypes.data,
+                                        ids_a.ctypes.data if ids_a is not None else None, x_in or None, x_out or None,
+                                        len(rm), rm.ctypes.data if len(rm) else None, samplers,
+                                        tok.ctypes.data if len(rm) else None, stream or None))
+        return tok[:len(rm)].tolist()
 
     # -- request API ---------------------------------------------------------
     def submit(self, ids: Sequence[int], max_tokens: int, temperature: float = 0.0, top_k: int = 40,
@@ -333,6 +385,14 @@ class Batch:
 
     def step(self, x_in: int = 0, x_out: int = 0, stream: int = 0):
         _check(lib().mx_batch_step(self.eng._h, self._h, x_in or None, x_out or None, stream or None))
+
+    def reset(self, pos, ids=None, samplers=None, stream: int = 0):
+        """Re-arm for the next run (graphs kept): positions, optional next ids, per-row samplers
+        (row_samplers() array; None = greedy argmax); the token history restarts."""
+        pos = _i32(pos)
+        ids_a = _i32(ids) if ids is not None else None
+        _check(lib().mx_batch_reset(self.eng._h, self._h, pos.ctypes.data,
+                                    ids_a.ctypes.data if ids_a is not None else None, samplers, stream or None))
 
     def bind_ids(self, ids_device_ptr: int):
         _check(lib().mx_batch_bind_ids(self.eng._h, self._h, ids_device_ptr))

@@ -385,7 +385,8 @@ static float dot_q8_0(const uint8_t *w, const int8_t *q, const float *d, int n) 
 }
 
 /* Sensitivity probe for tests: a relative perturbation of up to q8_jitter (deterministic hash
- * noise) on every activation before it is quantised (Q8_0 and Q8_K).  0 = off (the restatement proper).  The
+ * noise) on every activation before it is quantised (Q8_0 and Q8_K) or rounded to bf16 for a bf16
+ * weight product.  0 = off (the restatement proper).  The
  * Q8_0 forward is discontinuous in its inputs (x*id crossing a rounding boundary moves q by one
  * step), so the tests bound the engine's deviation by the oracle's own under 1e-6 noise. */
 static float q8_jitter = 0.0f;
@@ -765,7 +766,16 @@ static float dot_bf16_f32(const uint16_t *w, const float *x, int n) {
 static void matmul_bf16(float *y, const uint16_t *W, const float *x, int T, int n_in, int n_out, int exact,
                         uint16_t *scratch /* T*n_in */) {
     if (!exact) {
-        for (size_t i = 0; i < (size_t)T * n_in; i++) scratch[i] = f32_to_bf16(x[i]);
+        if (q8_jitter != 0.0f) { /* sensitivity probe (tests): noise before the bf16 rounding too */
+            float *xj = (float *)malloc(sizeof(float) * n_in);
+            for (int t = 0; t < T; t++) {
+                jitter_row(x + (size_t)t * n_in, xj, n_in, t, n_out);
+                for (int i = 0; i < n_in; i++) scratch[(size_t)t * n_in + i] = f32_to_bf16(xj[i]);
+            }
+            free(xj);
+        } else {
+            for (size_t i = 0; i < (size_t)T * n_in; i++) scratch[i] = f32_to_bf16(x[i]);
+        }
 #pragma omp parallel for schedule(static)
         for (int o = 0; o < n_out; o++)
             for (int t = 0; t < T; t++)
