@@ -45,18 +45,30 @@ class Llama:
         self._engine = _engine.Engine(model_path, n_ctx=n_ctx, n_seq_max=n_seq_max, device=device,
                                       seed=synthetic_seed)
         self._n_ctx = n_ctx
-        info = self._engine.info
-        if syn is None:
+        self._init_tokenizer(model_path, self._engine.info.n_vocab)
+
+    @classmethod
+    def from_engine(cls, model_path: str, engine, n_ctx: int = 512, seed: int = LLAMA_DEFAULT_SEED,
+                    verbose: bool = True) -> "Llama":
+        """A Llama over another engine object with Engine's request methods (submit / poll / cancel /
+        wait, n_vocab, n_embd) -- the pipeline server's rank-0 front (pipeserve.py)."""
+        self = cls.__new__(cls)
+        self.model_path, self.verbose, self._seed = model_path, verbose, seed
+        self._engine, self._n_ctx = engine, n_ctx
+        self._init_tokenizer(model_path, engine.n_vocab)
+        return self
+
+    def _init_tokenizer(self, model_path: str, n_vocab: int):
+        if _synth.parse_synthetic_path(model_path) is None:
             from .gguf import GGUFReader
 
-            self.metadata = {k: v for k, v in GGUFReader(model_path).metadata.items()
-                             if not isinstance(v, list)}
             md = GGUFReader(model_path).metadata
+            self.metadata = {k: v for k, v in md.items() if not isinstance(v, list)}
             self.tokenizer_ = Tokenizer.from_gguf_metadata(md)
         else:
             from .gguf import synthetic_spm_vocab
 
-            toks, scores, types = synthetic_spm_vocab(info.n_vocab)
+            toks, scores, types = synthetic_spm_vocab(n_vocab)
             self.tokenizer_ = Tokenizer(toks, scores, types, "llama", bos_id=1, eos_id=2)
             self.metadata = {"general.architecture": "llama", "general.name": model_path}
         self._lock = threading.Lock()

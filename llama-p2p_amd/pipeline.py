@@ -97,11 +97,29 @@ class TorchComm:
     together have to share a group (see ``Stage.decode_steps``).
     """
 
-    def __init__(self, rank: int, world: int):
+    def __init__(self, rank: int, world: int, obj_group=None):
         import torch.distributed as dist
 
         self.dist, self.rank, self.world = dist, rank, world
         self._pending = []
+        # control-plane objects (round plans, token lists) go over a gloo group: host data, no device
+        # round trip; on a gloo default group that group is reused
+        if obj_group is None and world > 1 and dist.get_backend() != "gloo":
+            obj_group = dist.new_group(backend="gloo")
+        self.obj_group = obj_group
+
+    def bcast_obj(self, obj, src: int = 0):
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=src, group=self.obj_group)
+        return box[0]
+
+    def send_obj(self, obj, dst: int):
+        self.dist.send_object_list([obj], dst=dst, group=self.obj_group)
+
+    def recv_obj(self, src: int):
+        box = [None]
+        self.dist.recv_object_list(box, src=src, group=self.obj_group)
+        return box[0]
 
     def send(self, t, dst: int):
         w = self.dist.isend(t, dst)

@@ -1,0 +1,754 @@
+"""Pipeline serving: the reference's request path on a model sharded over S GPU stages.
+
+The reference node answers a request with ``self.model(prompt, max_tokens=100)`` on a model it
+holds whole (/root/reference/llama_p2p_network.py:125, :19) and scales by forwarding whole
+requests to peers (:135-154).  On one 8xMI355X node the peers are GPUs holding contiguous layer
+shards (pipeline.py), and this module puts the same request API on top of that sharded model:
+
+  * ``PipelineLlama`` (rank 0) has ``Llama``'s contract (llama.py: create_completion, tokenize, the
+    completion dict), so ``cached_inference`` / ``handle_requests`` (p2p:84-133) run unchanged on a
+    sharded model; ranks 1..S-1 run ``serve_stage``.
+  * Requests are admitted into S micro-batch *lanes* of M rows (KV slot = lane*M + row); the lane is
+    chosen by the reference's peer scoreboard (placement.PeerScoreboard: p2p:156-168's score, or the
+    score-aware policy), so the gossip scores drive request placement onto the pipeline.
+  * Rounds: rank 0 broadcasts a plan (admissions, every active lane's positions and samplers, K);
+    the admitted prompts are prefilled through all stages in GEMM chunks (hand-off per chunk) and
+    the last stage picks each first token; then K decode steps of every active lane run around the
+    ring with grouped send/recv (pipeline.Stage's deadlock-free schedule) while the tokens stay on
+    the device (last stage -> stage 0); the last stage returns the K tokens per row to rank 0.
+  * Token picks are on the device (greedy argmax, or the device sampling chain: penalties, top-k,
+    top-p, min-p, temperature, counter-based draws), so sampling requests run K steps per round too.
+  * Hidden states cross stage boundaries in bf16 (``handoff_bf16``: half the bytes of f32).
+  * Per-stage busy time is reported to rank 0 every few rounds into a second scoreboard whose mean
+    times give ``proposed_partition`` (stage placement from measured scores).
+
+Transport- and executor-agnostic like pipeline.Stage: tests drive it on CPU over gloo (and an
+in-process rendezvous) with a toy executor, and on one GPU with in-process stage engines.
+"""
+from __future__ import annotations
+
+import collections
+import itertools
+import threading
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from .placement import PeerScoreboard
+
+FINISH_LENGTH, FINISH_STOP = 0, 1
+
+
+class PRequest:
+    __slots__ = ("id", "prompt", "samp", "seed", "max_tokens", "out", "done", "finish", "cancel", "lane", "row",
+                 "pos", "t0", "error")
+
+    def __init__(self, rid, prompt, samp, seed, max_tokens):
+        self.id, self.prompt, self.samp, self.seed, self.max_tokens = rid, list(prompt), samp, seed, max_tokens
+        self.out: List[int] = []
+        self.done, self.finish, self.cancel = False, None, False
+        self.lane = self.row = -1
+        self.pos = 0
+        self.t0 = time.perf_counter()
+        self.error = None
+
+
+def _sampling_rows(reqs, firsts=None):
+    """Per-row sampler specs for the last stage: (settings, seed, tokens sampled so far, penalty window)."""
+    rows = []
+    for i, r in enumerate(reqs):
+        if r is None:
+            rows.append(None)
+            continue
+        out = r.out if firsts is None else r.out + [firsts[i]]
+        hist = (r.prompt + out)[-64:]
+        rows.append((dict(r.samp), r.seed, len(out), hist))
+    return rows
+
+
+class Scheduler:
+    """Rank 0: pending queue, lane table, placement, round plans, token bookkeeping."""
+
+    def __init__(self, lanes: int, rows: int, n_ctx: int, eos: int, kmax: int = 8, policy: str = "score_aware",
+                 seed: Optional[int] = None):
+        self.S, self.M, self.n_ctx, self.eos, self.kmax = lanes, rows, n_ctx, eos, kmax
+        self.table: List[List[Optional[PRequest]]] = [[None] * rows for _ in range(lanes)]
+        self.pending: collections.deque = collections.deque()
+        self.reqs: Dict[int, PRequest] = {}
+        self.cv = threading.Condition()
+        self.ids = itertools.count(1)
+        self.board = PeerScoreboard(list(range(lanes)), policy=policy, seed=seed)
+        self.stop = False
+        self.rounds = 0
+
+    # ---- request side (any thread)
+    def submit(self, prompt, max_tokens, samp, seed):
+        with self.cv:
+            if self.stop:
+                raise RuntimeError("pipeline server shutting down")
+            r = PRequest(next(self.ids), prompt, samp, seed, max_tokens)
+            self.reqs[r.id] = r
+            self.pending.append(r)
+            self.cv.notify_all()
+            return r.id
+
+    def wait(self, rid):
+        with self.cv:
+            r = self.reqs[rid]
+            self.cv.wait_for(lambda: r.done)
+            del self.reqs[rid]
+        if r.error:
+            raise RuntimeError(f"request failed: {r.error}")
+        return list(r.out), r.finish
+
+    def poll(self, rid, n_have):
+        with self.cv:
+            r = self.reqs[rid]
+            self.cv.wait_for(lambda: r.done or len(r.out) > n_have)
+            return list(r.out), r.done
+
+    def cancel(self, rid):
+        with self.cv:
+            self.reqs[rid].cancel = True
+
+    def shutdown(self):
+        with self.cv:
+            self.stop = True
+            self.cv.notify_all()
+
+    # ---- server side (the round loop)
+    def _free_lanes(self):
+        return [l for l in range(self.S) if any(x is None for x in self.table[l])]
+
+    def _active(self):
+        return [l for l in range(self.S) if any(x is not None for x in self.table[l])]
+
+    def next_plan(self, idle_s: float = 1.0):
+        """Block until there is work (or idle_s passed: a heartbeat plan keeps the peers' collectives
+        alive); admit pending requests into lanes; return the round plan."""
+        with self.cv:
+            self.cv.wait_for(lambda: self.stop or self.pending or self._active(), timeout=idle_s)
+            if self.stop:
+                for r in list(self.pending) + [x for ln in self.table for x in ln if x is not None]:
+                    r.error, r.done = "pipeline server shutting down", True
+                self.cv.notify_all()
+                return {"stop": True}
+            admit = []
+            while self.pending:
+                r = self.pending[0]
+                if r.cancel:  # cancelled before admission: no tokens
+                    self.pending.popleft()
+                    r.done, r.finish = True, FINISH_STOP
+                    continue
+                free = self._free_lanes()
+                if not free:
+                    break
+                self.pending.popleft()
+                lane = self.board.select(candidates=free)
+                row = self.table[lane].index(None)
+                r.lane, r.row, r.pos = lane, row, len(r.prompt)
+                self.table[lane][row] = r
+                admit.append(r)
+            self.cv.notify_all()
+            active = self._active()
+            if not admit and not active:
+                return {"idle": True}
+            room, need = self.kmax, 1
+            for l in active:
+                for r in self.table[l]:
+                    if r is not None and r not in admit:
+                        room = min(room, self.n_ctx - r.pos)
+                        need = max(need, r.max_tokens - len(r.out))
+                    elif r is not None:
+                        room = min(room, self.n_ctx - r.pos)
+                        need = max(need, r.max_tokens - 1)
+            K = max(1, min(room, need))
+            if self.pending and self._free_lanes():
+                K = 1
+            lanes = []
+            for l in active:
+                pos, ids, new = [], [], []
+                for row, r in enumerate(self.table[l]):
+                    if r is None:
+                        pos.append(0), ids.append(0), new.append(False)
+                    else:
+                        pos.append(r.pos), ids.append(r.out[-1] if r.out else -1), new.append(r in admit)
+                lanes.append({"lane": l, "pos": pos, "ids": ids, "new": new,
+                              "samp": _sampling_rows(self.table[l])})
+            self.rounds += 1
+            return {"admit": [{"lane": r.lane, "row": r.row, "ids": r.prompt, "samp": dict(r.samp), "seed": r.seed}
+                              for r in admit],
+                    "lanes": lanes, "K": K}
+
+    def apply_first(self, plan, firsts):
+        """First tokens of the admitted requests (prefill picks), in plan["admit"] order."""
+        with self.cv:
+            for a, t in zip(plan["admit"], firsts):
+                r = self.table[a["lane"]][a["row"]]
+                r.out.append(int(t))
+            self.cv.notify_all()
+        return {(a["lane"], a["row"]): int(t) for a, t in zip(plan["admit"], firsts)}
+
+    def apply_round(self, plan, tokens):
+        """tokens[lane] = int array [M][K] (the K decode tokens of every row of that lane).  A row stops
+        at EOS, max_tokens, n_ctx or a cancel; tokens after that within the round are discarded."""
+        now = time.perf_counter()
+        with self.cv:
+            for ln in plan["lanes"]:
+                l = ln["lane"]
+                tk = tokens[l]
+                for row, r in enumerate(self.table[l]):
+                    if r is None:
+                        continue
+                    if self._finished(r):  # finished by its first token (prefill pick)
+                        self._release(r, now)
+                        continue
+                    for k in range(plan["K"]):
+                        r.pos += 1
+                        r.out.append(int(tk[row][k]))
+                        if self._finished(r):
+                            break
+                    if r.done:
+                        self._release(r, now)
+            self.cv.notify_all()
+
+    def _finished(self, r):
+        if r.done:
+            return True
+        t = r.out[-1] if r.out else None
+        if (t == self.eos and not r.samp.get("ignore_eos", False)) or r.cancel:
+            r.done, r.finish = True, FINISH_STOP
+        elif len(r.out) >= r.max_tokens or r.pos >= self.n_ctx:
+            r.done, r.finish = True, FINISH_LENGTH
+        return r.done
+
+    def _release(self, r, now):
+        self.table[r.lane][r.row] = None
+        self.board.update(r.lane, True, now - r.t0)
+
+
+class StageRunner:
+    """Executes round plans on one stage: pipelined prefill of admissions, lane resets, the K-step
+    decode ring, and (last stage) the token return to rank 0."""
+
+    def __init__(self, executor, comm, rank: int, world: int, lanes: int, rows: int, kmax: int, device,
+                 stage_time_every: int = 8):
+        import torch
+
+        self.ex, self.comm, self.rank, self.world = executor, comm, rank, world
+        self.first, self.last = rank == 0, rank == world - 1
+        self.S, self.M, self.kmax, self.device = lanes, rows, kmax, device
+        self.torch = torch
+        self.stage_time_every = stage_time_every
+        self.busy_s, self.rounds = 0.0, 0
+        self._events = []  # (start, end) CUDA events around this stage's lane steps
+        self.lanes, self.x_in, self.x_out, self.tok = [], [], [], []
+        for l in range(lanes):
+            b = executor.make_lane([l * rows + i for i in range(rows)], kmax)
+            t = torch.zeros(rows, dtype=torch.int32, device=device)
+            if self.first or self.last:
+                b.bind_ids_tensor(t)
+            self.lanes.append(b)
+            self.tok.append(t)
+            self.x_in.append(executor.alloc_x(rows))
+            self.x_out.append(executor.alloc_x(rows))
+        self.chunk = executor.prefill_chunk
+        self.buf_in = executor.alloc_x(self.chunk)
+        self.buf_out = executor.alloc_x(self.chunk)
+
+    # ---- prefill of the admitted prompts: rows of every prompt back to back (each padded to a
+    # multiple of 16 positions inside n_ctx so chunks form 16-position blocks), in hand-off chunks
+    def _prefill(self, admit, M, n_ctx):
+        slots, pos, ids, ends = [], [], [], []
+        for a in admit:
+            sl = a["lane"] * M + a["row"]
+            n = len(a["ids"])
+            slots += [sl] * n
+            pos += list(range(n))
+            ids += a["ids"]
+            ends.append(len(slots) - 1)
+            pad = (16 - n % 16) % 16
+            if n + pad <= n_ctx:
+                slots += [sl] * pad
+                pos += list(range(n, n + pad))
+                ids += [a["ids"][-1]] * pad
+        samp = [(a["samp"], a["seed"], 0, a["ids"][-64:]) for a in admit]
+        firsts: List[int] = []
+        k0 = 0
+        for i in range(0, len(slots), self.chunk):
+            n = min(self.chunk, len(slots) - i)
+            xin = xout = None
+            if not self.first:
+                self.comm.recv(self.buf_in[:n], self.rank - 1)
+                xin = self.buf_in[:n]
+            if not self.last:
+                xout = self.buf_out[:n]
+            k1 = k0
+            while k1 < len(ends) and ends[k1] < i + n:
+                k1 += 1
+            rowmap = [e - i for e in ends[k0:k1]] if self.last else []
+            toks = self.ex.prefill(slots[i:i + n], pos[i:i + n], ids[i:i + n] if self.first else None, xin, xout,
+                                   rowmap, samp[k0:k1] if self.last else None)
+            firsts += toks
+            k0 = k1
+            if not self.last:
+                self.comm.send(xout, self.rank + 1)
+                self.comm.drain()  # buf_out is reused by the next chunk
+        return firsts
+
+    def _step(self, b, x_in=None, x_out=None):
+        """One lane step, bracketed by events on the work stream (after the hand-off waits were
+        enqueued, so the pair times this stage's kernels only): the stage's busy time."""
+        if self.device.type == "cuda":
+            e0, e1 = self.torch.cuda.Event(enable_timing=True), self.torch.cuda.Event(enable_timing=True)
+            e0.record()
+            b.step_tensors(x_in, x_out)
+            e1.record()
+            self._events.append((e0, e1))
+        else:
+            t = time.perf_counter()
+            b.step_tensors(x_in, x_out)
+            self.busy_s += time.perf_counter() - t
+
+    def take_busy(self):
+        """Seconds this stage spent in its lane steps since the last call (synchronises)."""
+        if self._events:
+            self._events[-1][1].synchronize()
+            self.busy_s += sum(a.elapsed_time(b) for a, b in self._events) / 1e3
+            self._events.clear()
+        t, self.busy_s = self.busy_s, 0.0
+        return t
+
+    def _ring(self, active, K):
+        """K decode steps of the active lanes around the ring (pipeline.Stage.decode_steps' grouped
+        schedule: the send of micro-step k is posted with the receive of micro-step k+1)."""
+        if self.world == 1:
+            for _ in range(K):
+                for l in active:
+                    self._step(self.lanes[l])
+            return
+        deferred, pending_tokens = [], False
+        for _ in range(K):
+            for l in active:
+                b = self.lanes[l]
+                if self.first:
+                    recvs = [(self.tok[l], self.world - 1)] if pending_tokens else []
+                else:
+                    recvs = [(self.x_in[l], self.rank - 1)]
+                self.comm.exchange(deferred, recvs)
+                if self.first:
+                    self._step(b, None, self.x_out[l])
+                    deferred = [(self.x_out[l], 1)]
+                elif self.last:
+                    self._step(b, self.x_in[l], None)
+                    deferred = [(self.tok[l], 0)]
+                else:
+                    self._step(b, self.x_in[l], self.x_out[l])
+                    deferred = [(self.x_out[l], self.rank + 1)]
+            pending_tokens = True
+        recvs = [(self.tok[l], self.world - 1) for l in active] if self.first else []
+        self.comm.exchange(deferred, recvs)
+
+    def run_round(self, plan, sched: Optional[Scheduler] = None, n_ctx: int = 512):
+        """One round on this stage.  Rank 0 passes its Scheduler (bookkeeping)."""
+        firsts = {}
+        if plan["admit"]:
+            toks = self._prefill(plan["admit"], self.M, n_ctx)
+            if self.last and not self.first:
+                self.comm.send_obj(toks, 0)
+            if self.first and not self.last:
+                toks = self.comm.recv_obj(self.world - 1)
+            if self.first:
+                firsts = sched.apply_first(plan, toks)
+            elif self.last:
+                firsts = {(a["lane"], a["row"]): t for a, t in zip(plan["admit"], toks)}
+        active = [ln["lane"] for ln in plan["lanes"]]
+        for ln in plan["lanes"]:
+            l = ln["lane"]
+            ids = None
+            if self.first:  # next token per row: the prefill pick for rows admitted now, else the last one
+                ids = [firsts[(l, r)] if (l, r) in firsts else max(0, t) for r, t in enumerate(ln["ids"])]
+            samplers = None
+            if self.last:
+                rows = []
+                for r, spec in enumerate(ln["samp"]):
+                    if spec is None:
+                        rows.append(({"temperature": 0.0}, 0, 0, []))
+                    elif ln["new"][r]:  # its first token was just picked: one draw used, window grows
+                        s, seed, nd, win = spec
+                        rows.append((s, seed, nd + 1, (list(win) + [firsts[(l, r)]])[-64:]))
+                    else:
+                        rows.append(spec)
+                samplers = self.ex.samplers(rows)
+            self.lanes[l].reset(ln["pos"], ids, samplers)
+        self._ring(active, plan["K"])
+        tokens = None
+        if self.last:
+            tokens = {l: self.lanes[l].tokens()[:, :plan["K"]] for l in active}
+            if not self.first:
+                self.comm.send_obj(tokens, 0)
+        if self.first and not self.last:
+            tokens = self.comm.recv_obj(self.world - 1)
+        if self.first:
+            sched.apply_round(plan, tokens)
+        self.rounds += 1
+        return tokens
+
+    def close(self):
+        for b in self.lanes:
+            b.close()
+
+
+def serve_loop(runner: StageRunner, comm, sched: Optional[Scheduler], n_ctx: int, stage_board=None):
+    """The round loop of every rank: rank 0 plans (sched) and broadcasts, every rank runs the plan.
+    Per-stage busy time is gathered every runner.stage_time_every rounds into stage_board (rank 0)."""
+    while True:
+        plan = sched.next_plan() if runner.first else None
+        if runner.world > 1:
+            plan = comm.bcast_obj(plan, 0)
+        if plan.get("stop"):
+            return
+        if plan.get("idle"):
+            continue
+        try:
+            runner.run_round(plan, sched, n_ctx)
+        except Exception as e:  # a failed round fails its requests (rank 0) and ends the loop
+            if sched is not None:
+                with sched.cv:
+                    for ln in sched.table:
+                        for r in ln:
+                            if r is not None:
+                                r.error, r.done = repr(e), True
+                    sched.table = [[None] * sched.M for _ in range(sched.S)]
+                    sched.cv.notify_all()
+            raise
+        if runner.world > 1 and runner.rounds % runner.stage_time_every == 0:
+            busy = runner.take_busy()
+            if runner.first:
+                times = [busy] + [comm.recv_obj(r) for r in range(1, runner.world)]
+                if stage_board is not None:
+                    for s, t in enumerate(times):
+                        stage_board.update(s, True, t / runner.stage_time_every)
+            else:
+                comm.send_obj(busy, 0)
+
+
+def proposed_partition(stage_board: PeerScoreboard, parts, head_layers: float = 0.0):
+    """Stage placement from measured scores: each stage's mean round time / its layer count gives a
+    per-layer cost on that GPU; layers are re-split (pipeline.partition_layers' DP, per-stage cost
+    weights) so that the slowest stage's predicted time is minimal.  Returns the new ranges."""
+    st = stage_board.stats()
+    S = len(parts)
+    speeds = []
+    for s, (lb, le) in enumerate(parts):
+        t = st.get(s, {}).get("avg_time", 0.0) or 0.0
+        n = le - lb + (head_layers if s == S - 1 else 0.0)
+        speeds.append(t / n if t > 0 else None)
+    known = [v for v in speeds if v]
+    if not known:
+        return list(parts)
+    mean = sum(known) / len(known)
+    w = [v / mean if v else 1.0 for v in speeds]
+    n_layer = parts[-1][1]
+    best = None
+
+    def rec(s, lb, acc):
+        nonlocal best
+        if s == S - 1:
+            c = w[s] * (n_layer - lb + head_layers)
+            cand = (max(acc + [c]), acc + [c])
+            bounds.append((lb, n_layer))
+            if best is None or cand[0] < best[0] - 1e-12:
+                best = (cand[0], list(bounds))
+            bounds.pop()
+            return
+        for le in range(lb + 1, n_layer - (S - 1 - s) + 1):
+            c = w[s] * (le - lb)
+            if best is not None and c >= best[0]:
+                break
+            bounds.append((lb, le))
+            rec(s + 1, le, acc + [c])
+            bounds.pop()
+
+    bounds: List = []
+    rec(0, 0, [])
+    return best[1]
+
+
+# ------------------------------------------------------------------------------ engine executor
+class EngineExecutor:
+    """The MI355X engine as a pipeline-serving stage (engine.Engine with a layer range)."""
+
+    def __init__(self, eng, device, prefill_chunk: int = 1024):
+        import torch
+
+        from .engine import row_samplers, sampling, torch_stream_handle
+
+        self.eng, self.device, self.torch = eng, device, torch
+        self._row_samplers, self._sampling, self._stream = row_samplers, sampling, torch_stream_handle
+        self.first, self.last = bool(eng.info.has_embed), bool(eng.info.has_head)
+        self.n_embd = eng.n_embd
+        self.dtype = torch.bfloat16 if eng.handoff_bf16 else torch.float32
+        self.prefill_chunk = prefill_chunk
+
+    def alloc_x(self, rows):
+        return self.torch.empty((rows, self.n_embd), dtype=self.dtype, device=self.device)
+
+    def prefill(self, slots, pos, ids, x_in, x_out, rowmap, samp):
+        samplers = self.samplers(samp) if samp else None
+        return self.eng.stage_rows_pick(slots, pos, ids, x_in.data_ptr() if x_in is not None else 0,
+                                        x_out.data_ptr() if x_out is not None else 0, rowmap, samplers,
+                                        self._stream())
+
+    def make_lane(self, slots, kmax):
+        return _EngineLane(self.eng.batch(slots, [0] * len(slots), [0] * len(slots) if self.first else None,
+                                          max_steps=kmax), self._stream)
+
+    def samplers(self, rows):
+        return self._row_samplers([(self._sampling(**s), seed, nd, win) for s, seed, nd, win in rows])
+
+
+class _EngineLane:
+    def __init__(self, batch, stream):
+        self.b, self._stream = batch, stream
+
+    def reset(self, pos, ids=None, samplers=None):
+        self.b.reset(pos, ids, samplers, self._stream())
+
+    def step_tensors(self, x_in=None, x_out=None):
+        self.b.step_tensors(x_in, x_out)
+
+    def bind_ids_tensor(self, t):
+        self.b.bind_ids_tensor(t)
+
+    def tokens(self):
+        return self.b.tokens()
+
+    def close(self):
+        self.b.close()
+
+
+# ------------------------------------------------------------------------------ request front
+SAMPLING_KEYS = ("temperature", "top_k", "top_p", "min_p", "repeat_penalty", "repeat_last_n", "ignore_eos",
+                 "frequency_penalty", "presence_penalty")
+
+
+class PipelineFront:
+    """Rank 0's request API with engine.Engine's method names (submit / poll / cancel / wait), so
+    llama.Llama.create_completion drives the pipeline unchanged.  The round loop runs on a thread."""
+
+    def __init__(self, runner: StageRunner, comm, sched: Scheduler, n_ctx: int, n_vocab: int, n_embd: int,
+                 stage_board: Optional[PeerScoreboard] = None):
+        self.runner, self.comm, self.sched, self.n_ctx = runner, comm, sched, n_ctx
+        self.n_vocab, self.n_embd = n_vocab, n_embd
+        self.stage_board = stage_board
+        self.engine = None  # this stage's engine, closed with the front
+        self.error = None
+        self._thread = threading.Thread(target=self._loop, daemon=True)
+        self._thread.start()
+
+    def _loop(self):
+        try:
+            dev = self.runner.device
+            if dev.type == "cuda":  # the round loop's own (non-default) stream: engine calls and hand-offs
+                import torch
+
+                torch.cuda.set_device(dev)
+                torch.cuda.set_stream(torch.cuda.Stream(device=dev))
+            serve_loop(self.runner, self.comm, self.sched, self.n_ctx, self.stage_board)
+        except Exception as e:  # noqa: BLE001 -- surfaced to callers through their requests
+            self.error = e
+
+    def submit(self, ids, max_tokens, seed=None, **kw):
+        import random
+
+        samp = {k: kw[k] for k in SAMPLING_KEYS if k in kw}
+        samp.setdefault("temperature", 0.0)
+        tk, rl = samp.get("top_k", 40), samp.get("repeat_last_n", 64)
+        sampling = samp["temperature"] > 0 or samp.get("repeat_penalty", 1.0) != 1.0 or \
+            samp.get("frequency_penalty", 0.0) != 0.0 or samp.get("presence_penalty", 0.0) != 0.0
+        if sampling and not (1 <= tk <= 64 and 0 <= rl <= 64):
+            raise ValueError("pipeline serving samples on the device: top_k must be 1..64 and repeat_last_n 0..64")
+        if self.error is not None:
+            raise RuntimeError(f"pipeline server failed: {self.error!r}")
+        s = seed if seed is not None and seed >= 0 else random.getrandbits(63)
+        mt = max_tokens if max_tokens and max_tokens > 0 else self.n_ctx - len(ids)
+        return self.sched.submit(list(map(int, ids)), min(mt, self.n_ctx - len(ids)), samp, s)
+
+    def poll(self, rid, n_have=0):
+        return self.sched.poll(rid, n_have)
+
+    def cancel(self, rid):
+        self.sched.cancel(rid)
+
+    def wait(self, rid, cap=None):
+        return self.sched.wait(rid)
+
+    def generate(self, ids, max_tokens, **kw):
+        return self.wait(self.submit(ids, max_tokens, **kw))
+
+    def close(self):
+        self.sched.shutdown()
+        self._thread.join(timeout=60)
+        self.runner.close()
+        if self.engine is not None:
+            self.engine.close()
+            self.engine = None
+
+
+def _stage_setup(model_path, rank, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts=None):
+    """Engine holding this rank's byte-balanced layer range, its executor and runner pieces."""
+    from . import engine as E
+    from .pipeline import partition_layers
+
+    if parts is None:
+        from . import synth
+
+        syn = synth.parse_synthetic_path(model_path)
+        if syn is None:
+            raise ValueError("pipeline serving of a GGUF needs explicit stage ranges (parts=...)")
+        sh = syn[0]
+        layer = 2 * (2 * sh.n_embd ** 2 + 2 * sh.n_embd * sh.n_embd_kv + 3 * sh.n_embd * sh.n_ff)
+        parts = partition_layers(sh.n_layer, layer, 2 * sh.n_vocab * sh.n_embd, world)
+    lb, le = parts[rank]
+    eng = E.Engine(model_path, n_ctx=n_ctx, n_seq_max=lanes * rows, layer_begin=lb, layer_end=le,
+                   device=device.index if device.type == "cuda" else -1, handoff_bf16=handoff_bf16)
+    return eng, parts
+
+
+def serve_stage(model_path: str, comm, rank: int, world: int, lanes: int, rows: int = 32, n_ctx: int = 512,
+                kmax: int = 8, device=None, handoff_bf16: bool = True, parts=None):
+    """Ranks 1..S-1: hold a stage and execute rank 0's round plans until it stops."""
+    import torch
+
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    eng, parts = _stage_setup(model_path, rank, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts)
+    runner = StageRunner(EngineExecutor(eng, device), comm, rank, world, lanes, rows, kmax, device)
+    try:
+        serve_loop(runner, comm, None, n_ctx)
+    finally:
+        runner.close()
+        eng.close()
+
+
+def pipeline_llama(model_path: str, comm, world: int, lanes: Optional[int] = None, rows: int = 32,
+                   n_ctx: int = 512, kmax: int = 8, device=None, handoff_bf16: bool = True, parts=None,
+                   policy: str = "score_aware", seed: Optional[int] = None, verbose: bool = False):
+    """Rank 0: a Llama-compatible object whose completions run on the S-stage pipeline (ranks 1..S-1
+    run serve_stage with the same arguments)."""
+    import torch
+
+    from .llama import Llama
+
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    lanes = lanes or world
+    eng, parts = _stage_setup(model_path, 0, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts)
+    runner = StageRunner(EngineExecutor(eng, device), comm, 0, world, lanes, rows, kmax, device)
+    sched = Scheduler(lanes, rows, n_ctx, eng.info.eos_id, kmax, policy=policy, seed=seed)
+    stage_board = PeerScoreboard(list(range(world)), policy="score_aware")
+    # vocabulary size from the model (stage 0 has no head: n_vocab comes from the model info)
+    front = PipelineFront(runner, comm, sched, n_ctx, eng.info.n_vocab, eng.info.n_embd, stage_board)
+    llm = Llama.from_engine(model_path, front, n_ctx=n_ctx, verbose=verbose)
+    front.engine = eng
+    llm.parts, llm.stage_board, llm.scheduler = parts, stage_board, sched
+    return llm
+
+
+# ------------------------------------------------------------------------------ in-process stages
+class LocalHub:
+    """Mailboxes between in-process stages (one queue per ordered (src, dst) pair)."""
+
+    def __init__(self):
+        import queue
+
+        self._q = collections.defaultdict(queue.Queue)
+        self.lock = threading.Lock()
+
+    def q(self, src, dst):
+        with self.lock:
+            return self._q[(src, dst)]
+
+
+class LocalComm:
+    """Hand-offs between stages living in ONE process (S stage engines on one GPU, each stage a
+    thread with its own stream): a send snapshots the tensor (clone on the sender's stream, then
+    that stream is synchronised) into the receiver's mailbox, a receive copies it in on the
+    receiver's stream; sends never block, so the grouped ring schedule cannot deadlock.  Control
+    objects travel through the same mailboxes."""
+
+    def __init__(self, hub: LocalHub, rank: int, world: int, timeout: float = 120.0):
+        self.hub, self.rank, self.world, self.timeout = hub, rank, world, timeout
+
+    def send(self, t, dst):
+        import torch
+
+        c = t.clone()
+        if c.is_cuda:
+            torch.cuda.current_stream().synchronize()
+        self.hub.q(self.rank, dst).put(("t", c))
+
+    def recv(self, t, src):
+        kind, c = self.hub.q(src, self.rank).get(timeout=self.timeout)
+        assert kind == "t", "hand-off order mismatch: expected a tensor"
+        t.copy_(c)
+
+    def exchange(self, sends, recvs):
+        for t, d in sends:
+            self.send(t, d)
+        for t, s in recvs:
+            self.recv(t, s)
+
+    def drain(self):
+        pass
+
+    def send_obj(self, obj, dst):
+        self.hub.q(self.rank, dst).put(("o", obj))
+
+    def recv_obj(self, src):
+        kind, obj = self.hub.q(src, self.rank).get(timeout=self.timeout)
+        assert kind == "o", "hand-off order mismatch: expected an object"
+        return obj
+
+    def bcast_obj(self, obj, src=0):
+        if self.rank == src:
+            for r in range(self.world):
+                if r != src:
+                    self.send_obj(obj, r)
+            return obj
+        return self.recv_obj(src)
+
+
+def local_pipeline_llama(model_path: str, parts, lanes: int = 2, rows: int = 8, n_ctx: int = 512, kmax: int = 8,
+                         device=None, handoff_bf16: bool = True, policy: str = "score_aware",
+                         seed: Optional[int] = None):
+    """S = len(parts) stage engines of one model in THIS process (one GPU), each served by its own
+    thread and stream, behind one Llama-compatible front: the pipeline server end to end without a
+    multi-GPU launch (tests; a 1-GPU rehearsal of the S-GPU layout)."""
+    import torch
+
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    world = len(parts)
+    hub = LocalHub()
+    comms = [LocalComm(hub, r, world) for r in range(world)]
+    ready, errors, threads = threading.Barrier(world), [], []
+
+    def stage(r):
+        try:
+            torch.cuda.set_device(device)
+            torch.cuda.set_stream(torch.cuda.Stream(device=device))
+            ready.wait()
+            serve_stage(model_path, comms[r], r, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    for r in range(1, world):
+        th = threading.Thread(target=stage, args=(r,), daemon=True)
+        th.start()
+        threads.append(th)
+    torch.cuda.set_stream(torch.cuda.Stream(device=device))
+    ready.wait()
+    llm = pipeline_llama(model_path, comms[0], world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts,
+                         policy=policy, seed=seed)
+    llm._stage_threads, llm._stage_errors = threads, errors
+    return llm

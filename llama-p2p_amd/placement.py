@@ -44,25 +44,32 @@ class PeerScoreboard:
         """p2p:159: success / (success + failure + 1)."""
         return p["success"] / (p["success"] + p["failure"] + 1)
 
-    def select(self):
+    def select(self, candidates: Optional[Sequence] = None):
+        """The next target.  candidates: the targets able to take a request now (e.g. pipeline lanes
+        with a free row); default all.  The reference policy picks among the candidates that have
+        stats exactly as p2p:156-159 does among its peers, and a random candidate when none has."""
         with self.lock:
+            cands = list(self.targets) if candidates is None else list(candidates)
+            if not cands:
+                raise ValueError("no placement target available")
             if self.policy == "reference":
-                if not self.perf:
-                    t = self.rng.choice(self.targets)
+                known = [x for x in self.perf if x in cands]
+                if not known:
+                    t = self.rng.choice(cands)
                 else:
-                    t = max(self.perf, key=lambda x: self.score(self.perf[x]))
+                    t = max(known, key=lambda x: self.score(self.perf[x]))
             else:
-                untried = [t for t in self.targets if t not in self.perf and self.inflight[t] == 0]
+                untried = [t for t in cands if t not in self.perf and self.inflight[t] == 0]
                 if untried:
                     t = untried[0]
                 else:
                     def value(x):
                         p = self.perf[x] if x in self.perf else {"success": 0, "failure": 0, "avg_time": 0}
                         if p["success"] == 0:  # never answered (or only failed): last resort
-                            return 0.0 if p["failure"] else 1e-12
+                            return (0.0 if p["failure"] else 1e-12) / (1 + self.inflight[x])
                         return self.score(p) / (max(p["avg_time"], 1e-6) * (1 + self.inflight[x]))
 
-                    t = max(self.targets, key=value)
+                    t = max(cands, key=value)
             self.inflight[t] += 1
             return t
 
