@@ -148,7 +148,7 @@ class TorchComm:
 class Stage:
     """One pipeline stage: S micro-batches of M sequences, greedy decode."""
 
-    def __init__(self, eng, comm, rank: int, world: int, n_embd: int, device, micro_batches: int):
+    def __init__(self, eng, comm, rank: int, world: int, n_embd: int, device, micro_batches: int, dtype=None):
         import torch
 
         self.eng, self.comm, self.rank, self.world = eng, comm, rank, world
@@ -157,6 +157,7 @@ class Stage:
         self.n_embd = n_embd
         self.device = device
         self.torch = torch
+        self.dtype = dtype or torch.float32  # hand-off dtype (the engine's handoff_bf16)
         self.batches = []
         self.x_in, self.x_out, self.tok = [], [], []
         self.pending_tokens = False  # stage 0 has not yet received the last step's tokens
@@ -166,8 +167,8 @@ class Stage:
     def prefill(self, mb_rows: Sequence[Tuple[List[int], List[int], List[int]]], chunk: int = 64):
         """mb_rows[mb] = (slots, positions, ids) of every prompt row of micro-batch mb."""
         torch = self.torch
-        buf_in = torch.empty((chunk, self.n_embd), dtype=torch.float32, device=self.device)
-        buf_out = torch.empty((chunk, self.n_embd), dtype=torch.float32, device=self.device)
+        buf_in = torch.empty((chunk, self.n_embd), dtype=self.dtype, device=self.device)
+        buf_out = torch.empty((chunk, self.n_embd), dtype=self.dtype, device=self.device)
         for slots, pos, ids in mb_rows:
             for i in range(0, len(slots), chunk):
                 n = min(chunk, len(slots) - i)
@@ -193,8 +194,8 @@ class Stage:
                 b.bind_ids_tensor(t)
             self.batches.append(b)
             self.tok.append(t)
-            self.x_in.append(torch.empty((M, self.n_embd), dtype=torch.float32, device=self.device))
-            self.x_out.append(torch.empty((M, self.n_embd), dtype=torch.float32, device=self.device))
+            self.x_in.append(torch.empty((M, self.n_embd), dtype=self.dtype, device=self.device))
+            self.x_out.append(torch.empty((M, self.n_embd), dtype=self.dtype, device=self.device))
 
     def decode_steps(self, n_steps: int, step0: int = 0):
         """n_steps greedy tokens for every micro-batch, micro-batches interleaved.
@@ -267,11 +268,12 @@ def bench_main(args, metric: str, make_prompts):
     lb, le = parts[rank]
     S, M = world, args.seqs
     eng = Engine(f"synthetic:{args.model}:seed=0", n_ctx=args.n_ctx, n_seq_max=S * M, layer_begin=lb,
-                 layer_end=le, device=local)
+                 layer_end=le, device=local, handoff_bf16=True)
     comm = TorchComm(rank, world)
     work_stream = torch.cuda.Stream(device=local)  # engine kernels and RCCL hand-offs are ordered on it
     torch.cuda.set_stream(work_stream)
-    stage = Stage(EngineAdapter(eng), comm, rank, world, shape.n_embd, torch.device("cuda", local), S)
+    stage = Stage(EngineAdapter(eng), comm, rank, world, shape.n_embd, torch.device("cuda", local), S,
+                  dtype=torch.bfloat16)  # hidden states cross stage boundaries in bf16
     prompts = make_prompts(shape.n_vocab, S * M)
     mb_rows, mb_state = [], []
     for mb in range(S):
@@ -320,7 +322,7 @@ def bench_main(args, metric: str, make_prompts):
             "config": {"workload": f"{args.model} greedy decode, {world}-stage pipeline, {S} micro-batches x {M} "
                                    f"sequences in flight, prompts U[16,256] (seed 2), n_ctx {args.n_ctx}",
                        "model": args.model, "stages": world, "micro_batches": S, "seqs_per_micro_batch": M,
-                       "layer_ranges": parts, "parallelism": f"pp{world}"},
+                       "layer_ranges": parts, "parallelism": f"pp{world}", "handoff": "bf16"},
             "step_hbm_gbs": round(step_bytes / dt * args.steps / 1e9, 1),
             "step_hbm_frac": round(step_bytes / (dt / args.steps) / 1e9 / 8000.0 / world, 4),
             "roofline": {"bound": "hbm", "achieved": round(kbytes / us / 1e3, 1), "peak": 8000.0, "unit": "GB/s",

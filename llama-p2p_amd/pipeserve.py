@@ -81,6 +81,8 @@ class Scheduler:
         self.board = PeerScoreboard(list(range(lanes)), policy=policy, seed=seed)
         self.stop = False
         self.rounds = 0
+        # placement decisions: (request id, lane, candidate lanes, scoreboard snapshot before the pick)
+        self.placements = collections.deque(maxlen=100000)
 
     # ---- request side (any thread)
     def submit(self, prompt, max_tokens, samp, seed):
@@ -145,7 +147,9 @@ class Scheduler:
                 if not free:
                     break
                 self.pending.popleft()
+                snap = {t: (p["success"], p["failure"]) for t, p in self.board.stats().items()}
                 lane = self.board.select(candidates=free)
+                self.placements.append((r.id, lane, free, snap))
                 row = self.table[lane].index(None)
                 r.lane, r.row, r.pos = lane, row, len(r.prompt)
                 self.table[lane][row] = r

@@ -12,6 +12,7 @@ An in-process strict-rendezvous transport (test_pipeline_cpu._Hub) shows the ser
 cannot deadlock under RCCL's blocking-send semantics.
 """
 import os
+import time
 import queue
 import threading
 
@@ -313,3 +314,58 @@ def test_proposed_partition_follows_stage_scores():
     for s in range(4):
         b2.update(s, True, 1.0)
     assert P.proposed_partition(b2, parts) == parts
+
+
+def _p2p159(snap, cands):
+    """select_peer (p2p:156-159) over the candidate lanes that have stats: argmax success/(s+f+1)."""
+    known = [t for t in snap if t in cands]
+    if not known:
+        return None  # random among the candidates
+    return max(known, key=lambda t: snap[t][0] / (snap[t][0] + snap[t][1] + 1))
+
+
+@pytest.mark.parametrize("policy", ["reference", "score_aware"])
+def test_poisson_stream_placed_on_lanes(policy):
+    """Config 5's driver shape on the toy pipeline (world 4 in-process, strict rendezvous): a Poisson
+    stream (compressed clock) whose requests the peer scoreboard places onto the pipeline's lanes.
+    Under the reference policy every placement is p2p:159's pick among the lanes with a free row."""
+    from collections import defaultdict
+
+    from llama_p2p_amd.placement import poisson_schedule
+    from test_pipeline_cpu import _Hub
+
+    world, lanes, rows = 4, 4, 2
+    parts = partition_layers(L, 1.0, 1.5, world)
+    hub, boxes = _Hub(30), defaultdict(queue.Queue)
+    comms = [_RdvComm(hub, r, world, boxes) for r in range(world)]
+    sched = P.Scheduler(lanes, rows, N_CTX, -1, kmax=4, policy=policy, seed=3)
+    runners = [P.StageRunner(ToyServeEngine(*parts[r], lanes * rows), comms[r], r, world, lanes, rows, 4,
+                             torch.device("cpu")) for r in range(world)]
+    th = [threading.Thread(target=P.serve_loop, args=(runners[r], comms[r], None, N_CTX), daemon=True)
+          for r in range(1, world)]
+    for t in th:
+        t.start()
+    front = P.PipelineFront(runners[0], comms[0], sched, N_CTX, V, H)
+    stream = poisson_schedule(2.0, 24, seed=3, prompt_lo=4, prompt_hi=30, vocab=V, bos=1)
+    t0, out, workers = time.perf_counter(), [None] * len(stream), []
+    for i, (ta, prompt) in enumerate(stream):
+        d = ta * 0.02 - (time.perf_counter() - t0)  # clock compressed 50x
+        if d > 0:
+            time.sleep(d)
+        w = threading.Thread(target=lambda i=i, p=prompt: out.__setitem__(i, front.generate(p.tolist(), 6)))
+        w.start()
+        workers.append(w)
+    for w in workers:
+        w.join()
+    front.close()
+    for t in th:
+        t.join(timeout=30)
+    assert all(o is not None and len(o[0]) == 6 for o in out)
+    placements = list(sched.placements)
+    assert len(placements) == len(stream)
+    if policy == "reference":
+        for rid, lane, cands, snap in placements:
+            want = _p2p159(snap, cands)
+            assert lane in cands and (want is None or lane == want)
+    used = {lane for _, lane, _, _ in placements}
+    assert used <= set(range(lanes))

@@ -1,53 +1,142 @@
 #!/usr/bin/env python3
-"""Config 5 driver: a Poisson request stream placed by the gossip scoreboard
-(llama-p2p_amd/placement.py, the reference's p2p:156-168 bookkeeping) onto engine replicas, one
-per visible GPU (several per GPU with --per-gpu).  Each replica micro-batches whatever it is given.
+"""Config 5 driver: a Poisson request stream (rate λ, seed 3, prompt lengths
+U[lo, hi], `gen` new tokens) placed by the reference's peer scoreboard (placement.PeerScoreboard,
+p2p:156-168) onto serving targets:
 
-    python tools/serve_poisson.py --model llama3-8b --rate 2 --n 64 --gen 128 [--policy reference]
+  --stages S (default): the pipeline server (pipeserve.py) -- S stages, S micro-batch lanes; the
+      scoreboard places every request on a lane with a free row, per-stage busy times feed a second
+      scoreboard whose scores propose the next layer split.  Under torch.distributed.run (WORLD_SIZE
+      > 1) every rank holds one stage on its own GPU with RCCL hand-offs; otherwise the S stages
+      live in this process on one GPU (the 1-GPU rehearsal of the 8-GPU layout).
+  --replicas: whole-model engine replicas, one per visible GPU (the reference's own scaling).
+
+    python tools/serve_poisson.py --model llama3-70b --stages 8 --rate 2 --n 256 --time-scale 0.25
+    python -m torch.distributed.run --nproc-per-node 8 tools/serve_poisson.py --model llama3-70b
+One JSON line (rank 0).
 """
 import argparse
 import json
 import os
 import sys
+import threading
+import time
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def drive(generate, schedule, gen, time_scale):
+    """Replay the arrivals in (scaled) real time; each request on its own thread."""
+    import numpy as np
+
+    t0, lat, toks, workers = time.perf_counter(), [0.0] * len(schedule), [0] * len(schedule), []
+
+    def one(i, prompt):
+        ts = time.perf_counter()
+        out, _ = generate(prompt, gen)
+        lat[i], toks[i] = time.perf_counter() - ts, len(out)
+
+    for i, (ta, prompt) in enumerate(schedule):
+        d = ta * time_scale - (time.perf_counter() - t0)
+        if d > 0:
+            time.sleep(d)
+        w = threading.Thread(target=one, args=(i, prompt.tolist()), daemon=True)
+        w.start()
+        workers.append(w)
+    for w in workers:
+        w.join()
+    wall = time.perf_counter() - t0
+    a = np.array(lat)
+    return {"requests": len(schedule), "tokens": int(sum(toks)), "wall_s": round(wall, 3),
+            "tok_s": round(sum(toks) / wall, 1), "p50_s": round(float(np.percentile(a, 50)), 3),
+            "p99_s": round(float(np.percentile(a, 99)), 3)}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--rate", type=float, default=2.0, help="requests per second")
-    ap.add_argument("--n", type=int, default=64)
+    ap.add_argument("--n", type=int, default=256)
     ap.add_argument("--gen", type=int, default=128)
     ap.add_argument("--prompt-lo", type=int, default=32)
     ap.add_argument("--prompt-hi", type=int, default=512)
-    ap.add_argument("--n-ctx", type=int, default=1024)
-    ap.add_argument("--per-gpu", type=int, default=1)
+    ap.add_argument("--n-ctx", type=int, default=640)
+    ap.add_argument("--stages", type=int, default=8)
+    ap.add_argument("--rows", type=int, default=32, help="rows per pipeline lane")
+    ap.add_argument("--replicas", action="store_true")
     ap.add_argument("--policy", default="score_aware", choices=["score_aware", "reference"])
     ap.add_argument("--time-scale", type=float, default=1.0, help="<1 compresses the arrival clock")
     args = ap.parse_args()
     from llama_p2p_amd import synth
-    from llama_p2p_amd.engine import Engine, device_count
     from llama_p2p_amd.placement import PeerScoreboard, poisson_schedule, serve
 
     shape = synth.SHAPES[args.model]
-    ngpu = max(1, device_count())
-    engines = {f"gpu{d}.{k}": Engine(f"synthetic:{args.model}:seed=0", n_ctx=args.n_ctx, n_seq_max=64, device=d)
-               for d in range(ngpu) for k in range(args.per_gpu)}
+    path = f"synthetic:{args.model}:seed=0"
     sched = poisson_schedule(args.rate, args.n, seed=3, prompt_lo=args.prompt_lo, prompt_hi=args.prompt_hi,
                              vocab=shape.n_vocab)
+    if args.replicas:
+        from llama_p2p_amd.engine import Engine, device_count
 
-    def run(tgt, prompt, gen):
-        toks, _ = engines[tgt].generate(prompt, gen, temperature=0.0, ignore_eos=True)
-        return len(toks)
+        engines = {f"gpu{d}": Engine(path, n_ctx=args.n_ctx, n_seq_max=64, device=d)
+                   for d in range(max(1, device_count()))}
+        board = PeerScoreboard(list(engines), policy=args.policy, seed=0)
+        res = serve(board, lambda t, p, g: len(engines[t].generate(p, g, temperature=0.0, ignore_eos=True)[0]),
+                    sched, args.gen, time_scale=args.time_scale)
+        res.pop("records")
+        res.update({"model": args.model, "mode": "replicas", "replicas": len(engines), "policy": args.policy})
+        print(json.dumps(res), flush=True)
+        for e in engines.values():
+            e.close()
+        return
 
-    board = PeerScoreboard(list(engines), policy=args.policy, seed=0)
-    res = serve(board, run, sched, args.gen, time_scale=args.time_scale)
-    res.pop("records")
-    res.update({"model": args.model, "replicas": len(engines), "rate": args.rate, "policy": args.policy})
+    import torch
+
+    from llama_p2p_amd import pipeserve
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:  # one stage per rank/GPU, RCCL hand-offs
+        import torch.distributed as dist
+
+        from llama_p2p_amd.pipeline import TorchComm
+
+        rank, local = int(os.environ["RANK"]), int(os.environ.get("LOCAL_RANK", os.environ["RANK"]))
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        comm = TorchComm(rank, world)
+        torch.cuda.set_stream(torch.cuda.Stream())
+        dev = torch.device("cuda", local)
+        if rank != 0:
+            pipeserve.serve_stage(path, comm, rank, world, world, args.rows, args.n_ctx, device=dev)
+            dist.destroy_process_group()
+            return
+        llm = pipeserve.pipeline_llama(path, comm, world, world, args.rows, args.n_ctx, device=dev,
+                                       policy=args.policy, seed=0)
+        mode = f"{world} stages, one GPU each (RCCL)"
+    else:
+        from llama_p2p_amd.pipeline import partition_layers
+
+        h, kv, ff = shape.n_embd, shape.n_embd_kv, shape.n_ff
+        parts = partition_layers(shape.n_layer, 2 * (2 * h * h + 2 * h * kv + 3 * h * ff), 2 * shape.n_vocab * h,
+                                 args.stages)
+        llm = pipeserve.local_pipeline_llama(path, parts, lanes=args.stages, rows=args.rows, n_ctx=args.n_ctx,
+                                             policy=args.policy, seed=0)
+        mode = f"{args.stages} stages in one process on one GPU"
+    front = llm._engine
+    res = drive(lambda p, g: front.generate(p, g, temperature=0.0, ignore_eos=True), sched, args.gen,
+                args.time_scale)
+    lanes = {}
+    for _, lane, _, _ in llm.scheduler.placements:
+        lanes[lane] = lanes.get(lane, 0) + 1
+    res.update({"model": args.model, "mode": mode, "policy": args.policy, "rate": args.rate,
+                "time_scale": args.time_scale, "prompt_len": [args.prompt_lo, args.prompt_hi], "gen": args.gen,
+                "layer_ranges": llm.parts, "requests_per_lane": lanes, "lane_scores": llm.scheduler.board.stats(),
+                "stage_scores": llm.stage_board.stats(),
+                "proposed_partition": pipeserve.proposed_partition(llm.stage_board, llm.parts),
+                "rounds": llm.scheduler.rounds})
+    llm.close()
     print(json.dumps(res), flush=True)
-    for e in engines.values():
-        e.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":
