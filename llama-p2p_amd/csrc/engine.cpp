@@ -223,6 +223,10 @@ struct mx_engine {
   // Q8_0 model: layer matrices as packed Q8 tiles; token_embd / output may each
   // be Q8_0 (tok_embd8: GGUF blocks, row-major) or BF16
   bool wq8 = false, embd_q8 = false, out_q8 = false;
+  // Q4_0 model (llama.cpp Q4_0 files): the layer matrices are Q4 tiles on the Q8_0 path (Q8_0 activation
+  // rows, ggml_vec_dot_q4_0_q8_0); the head is Q8_0 / Q4_0 tiles (out_q4) or, as llama-quantize writes it,
+  // a K-quant output (out_kq_head: kq_out segments, Q8_K activation rows)
+  bool wq4 = false, out_q4 = false, out_kq_head = false;
   bool q8_ql = getenv("MX_NO_Q8_QL") == nullptr;  // Q8_0 GEMVs of <= 4 rows quantise their operand on load
   uint8_t* tok_embd8 = nullptr;
   // K-quant model (Q4_K / Q5_K / Q6_K matrices: llama.cpp's Q4_K_M / Q5_K_M; kquant.hip): packed
@@ -303,7 +307,7 @@ struct mx_engine {
     return 0;
   }
   int init_common();
-  int load_synthetic(const Shape& s, uint64_t seed, bool q8 = false, int kq_base = 0);
+  int load_synthetic(const Shape& s, uint64_t seed, bool q8 = false, int kq_base = 0, bool q4 = false);
   int load_gguf(const std::string& path);
   int enqueue_forward(int M, const int* ids, const int* pos, const int* slot, const void* x_in, void* x_out,
                       bool head, const int* rowmap, int n_out, bool argmax, int* ids_next, int* pos_next, int* hist,
@@ -422,7 +426,7 @@ int mx_engine::init_common() {
   if (int rc = alloc((void**)&slabs, slab_stride * 8 * 4)) return rc;
   if (gemm_shapes())
     if (int rc = alloc((void**)&gslabs, GSLAB_FLOATS * 4)) return rc;
-  if ((wkq || (wq8 && q8_gemm_prefill)) && gemm_shapes()) {  // per-layer bf16 copies for the prefill GEMM
+  if ((wkq || (wq8 && !wq4 && q8_gemm_prefill)) && gemm_shapes()) {  // per-layer bf16 copies for the prefill GEMM
     const size_t h = n_embd, kv = n_embd_kv, ff = n_ff;
     if (int rc = alloc((void**)&kqd_qkv, (h + 2 * kv) * h * 2)) return rc;
     if (int rc = alloc((void**)&kqd_o, h * h * 2)) return rc;
@@ -452,7 +456,7 @@ int mx_engine::init_common() {
     if (int rc = alloc((void**)&xqd, (size_t)R * (kmax / 32) * 4)) return rc;
     if (int rc = alloc((void**)&attn_f, (size_t)R * n_embd * 4)) return rc;
     if (int rc = alloc((void**)&act_f, (size_t)R * n_ff * 4)) return rc;
-    if (wkq)
+    if (wkq || out_kq_head)
       if (int rc = alloc((void**)&xkb, (size_t)R * (kmax / 32) * 4)) return rc;
   }
   // poison-free start: zero activations so padded MFMA columns never read uninitialised memory
@@ -467,8 +471,8 @@ int mx_engine::init_common() {
 static int alloc_layer(mx_engine* e, Layer& L) {
   const size_t h = e->n_embd, kv = e->n_embd_kv, ff = e->n_ff;
   if (e->wq8) {
-    const size_t bq = q8_matrix_bytes(h + 2 * kv, h), bo = q8_matrix_bytes(h, h), bg = q8_matrix_bytes(2 * ff, h),
-                 bd = q8_matrix_bytes(h, ff);
+    auto qb = e->wq4 ? q4_matrix_bytes : q8_matrix_bytes;
+    const size_t bq = qb(h + 2 * kv, h), bo = qb(h, h), bg = qb(2 * ff, h), bd = qb(h, ff);
     if (int rc = e->alloc((void**)&L.qkv, bq)) return rc;
     if (int rc = e->alloc((void**)&L.o, bo)) return rc;
     if (int rc = e->alloc((void**)&L.gu, bg)) return rc;
@@ -518,11 +522,12 @@ static int pack_kq_rows(const KqMat& km, uint16_t* base, const uint8_t* blocks, 
   return launch_pack_kq((uint8_t*)base + km.off[sg], blocks, type, rows, K, mode, in_seg, s);
 }
 
-int mx_engine::load_synthetic(const Shape& s, uint64_t seed, bool q8, int kq_base) {
+int mx_engine::load_synthetic(const Shape& s, uint64_t seed, bool q8, int kq_base, bool q4) {
   n_embd = s.n_embd; n_layer = s.n_layer; n_head = s.n_head; n_head_kv = s.n_head_kv; n_ff = s.n_ff;
   n_vocab = s.n_vocab; rope_base = s.rope_base; eps = s.eps; n_ctx_train = s.n_ctx_train;
   if (le < 0 || le > n_layer) le = n_layer;
-  wq8 = embd_q8 = out_q8 = q8;
+  wq8 = embd_q8 = out_q8 = q8 || q4;
+  wq4 = q4;  // layer matrices Q4_0 (quantize_row_q4_0_ref of the bf16 synthetic values); embd / output Q8_0
   wkq = kq_base != 0;
   if (int rc = init_common()) return rc;
   const float ws = std_scale(0.02), ns = std_scale(0.1);
@@ -576,7 +581,7 @@ int mx_engine::load_synthetic(const Shape& s, uint64_t seed, bool q8, int kq_bas
     HIPC(hipGetLastError());
     return 0;
   }
-  if (q8) {  // the Q8_0 quantisation of the bf16 synthetic model (what llama-quantize makes of it)
+  if (wq8) {  // the Q8_0 (Q4_0) quantisation of the bf16 synthetic model (what llama-quantize makes of it)
     if (has_embed) {
       if (int rc = alloc((void**)&tok_embd8, (size_t)V * (h / 32) * 34)) return rc;
       launch_synth_q8_rowmajor(tok_embd8, V, h, seed, TID_TOK_EMBD, ws, stream);
@@ -595,13 +600,14 @@ int mx_engine::load_synthetic(const Shape& s, uint64_t seed, bool q8, int kq_bas
       uint8_t *qkv = (uint8_t*)L.qkv, *o = (uint8_t*)L.o, *gu = (uint8_t*)L.gu, *dn = (uint8_t*)L.down;
       launch_synth_norm(L.attn_norm, h, seed, layer_tid(l, L_ATTN_NORM), ns, stream);
       launch_synth_norm(L.ffn_norm, h, seed, layer_tid(l, L_FFN_NORM), ns, stream);
-      launch_synth_q8_packed(qkv, h, h, seed, layer_tid(l, L_Q), ws, PACK_ROWS, 0, stream);
-      launch_synth_q8_packed(qkv, kv, h, seed, layer_tid(l, L_K), ws, PACK_ROWS, h, stream);
-      launch_synth_q8_packed(qkv, kv, h, seed, layer_tid(l, L_V), ws, PACK_ROWS, h + kv, stream);
-      launch_synth_q8_packed(o, h, h, seed, layer_tid(l, L_O), ws, PACK_ROWS, 0, stream);
-      launch_synth_q8_packed(gu, ff, h, seed, layer_tid(l, L_GATE), ws, PACK_GATE, 0, stream);
-      launch_synth_q8_packed(gu, ff, h, seed, layer_tid(l, L_UP), ws, PACK_UP, 0, stream);
-      launch_synth_q8_packed(dn, h, ff, seed, layer_tid(l, L_DOWN), ws, PACK_ROWS, 0, stream);
+      auto syn = q4 ? launch_synth_q4_packed : launch_synth_q8_packed;
+      syn(qkv, h, h, seed, layer_tid(l, L_Q), ws, PACK_ROWS, 0, stream);
+      syn(qkv, kv, h, seed, layer_tid(l, L_K), ws, PACK_ROWS, h, stream);
+      syn(qkv, kv, h, seed, layer_tid(l, L_V), ws, PACK_ROWS, h + kv, stream);
+      syn(o, h, h, seed, layer_tid(l, L_O), ws, PACK_ROWS, 0, stream);
+      syn(gu, ff, h, seed, layer_tid(l, L_GATE), ws, PACK_GATE, 0, stream);
+      syn(gu, ff, h, seed, layer_tid(l, L_UP), ws, PACK_UP, 0, stream);
+      syn(dn, h, ff, seed, layer_tid(l, L_DOWN), ws, PACK_ROWS, 0, stream);
     }
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(stream));
@@ -694,7 +700,7 @@ int mx_engine::load_gguf(const std::string& path) {
     for (int l = b0; l < e0; l++)
       for (const char* k : kinds) mats.push_back("blk." + std::to_string(l) + "." + k + ".weight");
     if (e0 == n_layer) mats.push_back(f.tensor("output.weight") ? "output.weight" : "token_embd.weight");
-    int n8 = 0, n30 = 0, nkq = 0;
+    int n8 = 0, n30 = 0, nkq = 0, n4 = 0;
     for (const std::string& nm : mats) {
       const GGUFTensor* t = f.tensor(nm);
       if (!t) return fail(MX_ERR_MODEL, "missing tensor " + nm);
@@ -702,11 +708,23 @@ int mx_engine::load_gguf(const std::string& path) {
         return fail(MX_ERR_MODEL, "tensor " + nm + ": ggml type " + std::to_string(t->type) +
                                       " is not supported (F32, F16, BF16, Q4_0, Q8_0, Q4_K, Q5_K, Q6_K are)");
       n8 += t->type == 8;
+      n4 += t->type == 2 && nm != mats.back();  // layer matrices only (the head is checked below)
       n30 += t->type == 30;
       nkq += t->type == 12 || t->type == 13 || t->type == 14;
       raw_max = std::max(raw_max, (size_t)t->nbytes);
     }
     wq8 = out_q8 = n8 == (int)mats.size();
+    if (!wq8 && n4 == (int)mats.size() - (e0 == n_layer ? 1 : 0) && n4 > 0) {
+      // Q4_0 layers; the head: Q8_0 / Q4_0 tiles, or a K-quant output (llama-quantize's Q6_K) on the
+      // K-quant kernels -- anything else dequantises the whole model as before
+      const int ot = e0 == n_layer ? f.tensor(mats.back())->type : 8;
+      if (ot == 8 || ot == 2 || ((ot == 12 || ot == 13 || ot == 14) && n_embd % 256 == 0)) {
+        wq8 = wq4 = true;
+        out_q8 = ot == 8 || ot == 2;
+        out_q4 = ot == 2;
+        out_kq_head = !out_q8;
+      }
+    }
     wkq = nkq == (int)mats.size() && n_embd % 256 == 0 && n_ff % 256 == 0;
     for (int l = b0; l < e0 && wkq; l++) {
       const std::string p = "blk." + std::to_string(l) + ".";
@@ -714,6 +732,7 @@ int mx_engine::load_gguf(const std::string& path) {
     }
     if (wkq) kq_main_type = f.tensor("blk." + std::to_string(b0) + ".ffn_gate.weight")->type;
     deq = !wq8 && !wkq && n30 != (int)mats.size();
+    if (wq8 && !out_q8) deq = false;
     embd_q8 = te->type == 8;
     if (wkq && (te->type == 12 || te->type == 13 || te->type == 14)) embd_kq_type = te->type;
     if (te->type != 30 && te->type != 8) {
@@ -724,14 +743,14 @@ int mx_engine::load_gguf(const std::string& path) {
   }
   if (int rc = init_common()) return rc;
   const int h = n_embd, kv = n_embd_kv, ff = n_ff, V = n_vocab;
-  const int mat_type = wq8 ? 8 : 30;
+  const int mat_type = wq4 ? 2 : wq8 ? 8 : 30;
 
   // staging buffer for the largest matrix (bf16), and for the raw blocks of dequantised tensors
   size_t stage_bytes = std::max({(size_t)V * h * 2, (size_t)ff * h * 2, (size_t)(h + 2 * kv) * h * 2});
   uint16_t* stage = nullptr;
   uint8_t* stage_raw = nullptr;
   HIPC(hipMalloc((void**)&stage, stage_bytes));
-  if (raw_max && (deq || wkq || (te->type != 30 && te->type != 8))) {
+  if (raw_max && (deq || wkq || out_kq_head || (te->type != 30 && te->type != 8))) {
     if (hipMalloc((void**)&stage_raw, raw_max) != hipSuccess) {
       hipFree(stage);
       return fail(MX_ERR_HIP, "staging buffer");
@@ -754,7 +773,8 @@ int mx_engine::load_gguf(const std::string& path) {
       return fail(MX_ERR_MODEL, "tensor " + name + " has unexpected shape");
     if (t->type != type && !(deq && type == 30))
       return fail(MX_ERR_MODEL, "tensor " + name + ": expected ggml type " + std::to_string(type) +
-                                    (type == 8 ? " (Q8_0, like the other matrices)" : " (BF16, like the other matrices)") +
+                                    (type == 8 ? " (Q8_0, like the other matrices)"
+                                     : type == 2 ? " (Q4_0, like the other matrices)" : " (BF16, like the other matrices)") +
                                     ", got type " + std::to_string(t->type));
     *out = t;
     return 0;
@@ -765,7 +785,8 @@ int mx_engine::load_gguf(const std::string& path) {
     if (int rc = get_mat(name, rows, cols, &t, mat_type)) return rc;
     if (wq8) {
       HIPC(hipMemcpy(stage, f.data(*t), t->nbytes, hipMemcpyHostToDevice));
-      launch_pack_q8((uint8_t*)dst, (const uint8_t*)stage, rows, cols, mode, offset, stream);
+      if (t->type == 2) launch_pack_q4((uint8_t*)dst, (const uint8_t*)stage, rows, cols, mode, offset, stream);
+      else launch_pack_q8((uint8_t*)dst, (const uint8_t*)stage, rows, cols, mode, offset, stream);
     } else {
       if (int rc = to_bf16(t, (size_t)rows * cols)) return rc;
       launch_pack(dst, stage, rows, cols, mode, offset, stream);
@@ -885,12 +906,37 @@ int mx_engine::load_gguf(const std::string& path) {
     }
   }
   if (has_head) {
-    if ((rc = alloc((void**)&output, wq8 ? q8_matrix_bytes(V, h) : (size_t)V * h * 2))) goto out;
-    if ((rc = alloc((void**)&out_norm, (size_t)h * 4))) goto out;
     const char* oname = f.tensor("output.weight") ? "output.weight" : "token_embd.weight";  // tied embeddings
-    if ((rc = upload_packed(oname, V, h, output, PACK_ROWS, 0))) goto out;
+    if ((rc = alloc((void**)&out_norm, (size_t)h * 4))) goto out;
     if ((rc = upload_norm("output_norm.weight", out_norm))) goto out;
-    weight_bytes += (wq8 ? q8_matrix_bytes(V, h) : (size_t)V * h * 2) + h * 4;
+    if (out_kq_head) {  // Q4_0 model with a K-quant output: packed K-quant tiles for mkq
+      kq_out = KqMat();
+      kq_out.add(f.tensor(oname)->type, V, h);
+      if ((rc = alloc((void**)&output, kq_out.bytes))) goto out;
+      if ((rc = upload_kq(oname, V, h, kq_out, output, PACK_ROWS, 0))) goto out;
+      weight_bytes += kq_out.bytes + h * 4;
+    } else {
+      const size_t ob = out_q4 ? q4_matrix_bytes(V, h) : wq8 ? q8_matrix_bytes(V, h) : (size_t)V * h * 2;
+      if ((rc = alloc((void**)&output, ob))) goto out;
+      const GGUFTensor* ot = nullptr;
+      if (wq8) {  // the head keeps its own block type (Q8_0 or Q4_0 tiles)
+        ot = f.tensor(oname);
+        if (!ot || ot->ne.size() != 2 || (int)ot->ne[0] != h || (int)ot->ne[1] != V) {
+          rc = fail(MX_ERR_MODEL, "tensor output.weight has unexpected shape");
+          goto out;
+        }
+        if (hipMemcpy(stage, f.data(*ot), ot->nbytes, hipMemcpyHostToDevice) != hipSuccess) {
+          rc = fail(MX_ERR_HIP, "upload output");
+          goto out;
+        }
+        if (out_q4) launch_pack_q4((uint8_t*)output, (const uint8_t*)stage, V, h, PACK_ROWS, 0, stream);
+        else launch_pack_q8((uint8_t*)output, (const uint8_t*)stage, V, h, PACK_ROWS, 0, stream);
+        hipStreamSynchronize(stream);
+      } else if ((rc = upload_packed(oname, V, h, output, PACK_ROWS, 0))) {
+        goto out;
+      }
+      weight_bytes += ob + h * 4;
+    }
   }
   for (int l = lb; l < le; l++) {
     Layer& L = layers[l - lb];
@@ -946,7 +992,7 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
   // Q8_0 prefill chunks as dequantised bf16 GEMMs (llama.cpp's GPU-backend route for large batches):
   // ~5x the default's rate, but bf16 activations instead of ggml's Q8_0 rows, so opt-in
   // (MX_Q8_GEMM_PREFILL=1; tests/test_q8_gpu.py bounds its deviation)
-  if (wq8 && q8_gemm_prefill && M > MAX_ROWS && kqd_qkv && !argmax && !(head && n_out > MAX_ROWS))
+  if (wq8 && !wq4 && q8_gemm_prefill && M > MAX_ROWS && kqd_qkv && !argmax && !(head && n_out > MAX_ROWS))
     return enqueue_forward_gemm(M, pos, slot, x_out, head, rowmap, n_out, s);
   if (wkq) return enqueue_forward_kq(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next, pos_next, hist,
                                      hist_stride, hist_count, max_hist, s);
@@ -1150,7 +1196,7 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     _Float16* kc = kcache + layer_kv_stride * li;
     _Float16* vc = vcache + layer_kv_stride * li;
     MMArgs a{};
-    a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M;
+    a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M; a.wq4 = wq4;
     site = 1;
     operand(a, x, h, L.attn_norm, M, nullptr);
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
@@ -1173,18 +1219,18 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     if (M > MAX_ROWS && rows_blocked) launch_attention_prefill(at, s);
     else launch_attention(at, s);
     MMArgs b{};
-    b.W = L.o; b.N = h; b.K = h; b.M = M; b.out = x; b.ldo = h;
+    b.W = L.o; b.N = h; b.K = h; b.M = M; b.out = x; b.ldo = h; b.wq4 = wq4;
     site = 2;
     operand(b, attn_f, h, nullptr, M, nullptr);
     b.ssq = ql ? ssq : nullptr; b.np = h / 16;  // partials of the new residual for gate/up's norm
     if (resid(b)) return fail(MX_ERR_ARG, "q8 attn_output launch shape");
     MMArgs c{};
-    c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.actf = act_f; c.lda = ff;
+    c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.actf = act_f; c.lda = ff; c.wq4 = wq4;
     site = 4;
     operand(c, x, h, L.ffn_norm, M, nullptr);
     if (launch_mq8(EPI_SWIGLU, c, s)) return fail(MX_ERR_ARG, "q8 gate/up launch shape");
     MMArgs d{};
-    d.W = L.down; d.N = h; d.K = ff; d.M = M; d.out = x; d.ldo = h;
+    d.W = L.down; d.N = h; d.K = ff; d.M = M; d.out = x; d.ldo = h; d.wq4 = wq4;
     site = 8;
     operand(d, act_f, ff, nullptr, M, nullptr);
     d.ssq = ql ? ssq : nullptr; d.np = h / 16;  // for the next layer's qkv (or lm_head) norm
@@ -1201,8 +1247,21 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     MMArgs g{};
     g.W = output; g.N = n_vocab; g.K = h; g.M = n_out; g.out = logits; g.ldo = n_vocab;
     site = 16;
-    operand(g, x, h, out_norm, n_out, (rowmap || n_out != M) ? rowmap : nullptr);
-    if (launch_mq8(EPI_F32, g, s)) return fail(MX_ERR_ARG, "q8 lm_head launch shape");
+    if (out_kq_head) {  // K-quant output (Q4_0 files): Q8_K rows of the normed rows, ggml's q6_K.q8_K
+      if (nslab) {
+        launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);
+        nslab = 0;
+      }
+      kq_out.set(g);
+      if (launch_rmsnorm_q8k(xq8, xqd, xkb, x, out_norm, (rowmap || n_out != M) ? rowmap : nullptr, n_out, h, eps, s))
+        return fail(MX_ERR_ARG, "kq head norm");
+      g.xq = xq8; g.xd = xqd; g.xb = xkb;
+      if (launch_mkq(EPI_F32, g, s)) return fail(MX_ERR_ARG, "kq lm_head launch shape");
+    } else {
+      g.wq4 = out_q4;
+      operand(g, x, h, out_norm, n_out, (rowmap || n_out != M) ? rowmap : nullptr);
+      if (launch_mq8(EPI_F32, g, s)) return fail(MX_ERR_ARG, "q8 lm_head launch shape");
+    }
     if (argmax)
       pick(n_out, ids_next, pos_next, hist, hist_stride,
                     hist_count, max_hist, s);
@@ -1383,14 +1442,14 @@ int mx_engine::enqueue_forward_gemm(int M, const int* pos, const int* slot, void
     if (!rowmap) return fail(MX_ERR_ARG, "prefill head needs a row map");
     MMArgs g{};
     g.W = output; g.N = n_vocab; g.K = h; g.M = n_out; g.out = logits; g.ldo = n_vocab;
-    if (wkq) {  // the K-quant head as at decode: Q8_K rows of the normed last rows
+    if (wkq || out_kq_head) {  // the K-quant head as at decode: Q8_K rows of the normed last rows
       kq_out.set(g);
       if (launch_rmsnorm_q8k(xq8, xqd, xkb, x, out_norm, rowmap, n_out, h, eps, s)) return fail(MX_ERR_ARG, "kq norm");
       g.xq = xq8; g.xd = xqd; g.xb = xkb;
       if (launch_mkq(EPI_F32, g, s)) return fail(MX_ERR_ARG, "kq lm_head launch shape");
     } else if (wq8) {  // the Q8_0 head as at decode
       launch_rmsnorm_q8(xq8, xqd, x, out_norm, rowmap, n_out, h, eps, s);
-      g.xq = xq8; g.xd = xqd;
+      g.xq = xq8; g.xd = xqd; g.wq4 = out_q4;
       if (launch_mq8(EPI_F32, g, s)) return fail(MX_ERR_ARG, "q8 lm_head launch shape");
     } else {
       launch_rmsnorm(xn, h, x, out_norm, rowmap, n_out, h, eps, s);
@@ -1898,7 +1957,7 @@ int mx_engine_create(const char* model_path, const mx_opts* opts, mx_engine** ou
   if (path.rfind("synthetic:", 0) == 0) {
     std::string rest = path.substr(10), name = rest;
     uint64_t seed = o.seed;
-    bool q8 = false;
+    bool q8 = false, q4 = false;
     int kq = 0;
     size_t c = rest.find(':');
     if (c != std::string::npos) {
@@ -1909,6 +1968,7 @@ int mx_engine_create(const char* model_path, const mx_opts* opts, mx_engine** ou
         const std::string part = tail.substr(0, e2);
         if (part.rfind("seed=", 0) == 0) seed = strtoull(part.c_str() + 5, nullptr, 10);
         else if (part == "q8_0") q8 = true;
+        else if (part == "q4_0") q4 = true;
         else if (part == "q4_k_m") kq = 12;
         else if (part == "q5_k_m") kq = 13;
         else if (part != "bf16") return fail(MX_ERR_MODEL, "unknown synthetic option '" + part + "'");
@@ -1919,7 +1979,7 @@ int mx_engine_create(const char* model_path, const mx_opts* opts, mx_engine** ou
     for (const Shape& k : kShapes)
       if (name == k.name) s = &k;
     if (!s) return fail(MX_ERR_MODEL, "unknown synthetic shape '" + name + "'");
-    rc = e->load_synthetic(*s, seed, q8, kq);
+    rc = e->load_synthetic(*s, seed, q8, kq, q4);
   } else {
     rc = e->load_gguf(path);
   }
@@ -1944,7 +2004,7 @@ int mx_engine_info(const mx_engine* e, mx_model_info* o) {
   o->eps = e->eps; o->rope_base = e->rope_base; o->bos_id = e->bos; o->eos_id = e->eos;
   o->n_ctx = e->n_ctx; o->n_seq_max = e->n_seq_max; o->layer_begin = e->lb; o->layer_end = e->le;
   o->has_embed = e->has_embed; o->has_head = e->has_head; o->weight_bytes = e->weight_bytes;
-  o->weight_type = e->wq8 ? 8 : e->wkq ? e->kq_main_type : 30;
+  o->weight_type = e->wq4 ? 2 : e->wq8 ? 8 : e->wkq ? e->kq_main_type : 30;
   return 0;
 }
 
@@ -2461,27 +2521,29 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
     MMArgs a{};
     a.M = M;
     if (e->wq8 && kind <= 4) {  // Q8_0 weights: the activations are Q8_0 rows in xq8/xqd
-      a.xq = e->xq8; a.xd = e->xqd;
+      a.xq = e->xq8; a.xd = e->xqd; a.wq4 = e->wq4;
+      auto qb = e->wq4 ? q4_matrix_bytes : q8_matrix_bytes;
       switch (kind) {
         case 0:
           a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.out = e->q; a.ldo = h; a.n_q = h; a.n_kv = kv;
           a.head_dim = e->head_dim; a.pos = e->d_pos; a.slot = e->d_slot; a.rope_cs = e->rope_cs;
           a.kc = e->kcache + e->layer_kv_stride * li; a.vc = e->vcache + e->layer_kv_stride * li;
           a.n_ctx = e->n_ctx; a.ctx_stride = e->ctx_stride; a.n_head_kv = e->n_head_kv; a.slot_stride = e->slot_stride;
-          per = q8_matrix_bytes(h + 2 * kv, h);
+          per = qb(h + 2 * kv, h);
           return launch_mq8(EPI_QKV, a, s);
         case 1: case 3:
           a.W = kind == 1 ? L.o : L.down; a.N = h; a.K = kind == 1 ? h : ff; a.out = e->x; a.ldo = h;
-          per = q8_matrix_bytes(h, a.K);
+          per = qb(h, a.K);
           return launch_mq8(EPI_RESID, a, s);
         case 2:
           a.W = L.gu; a.N = 2 * ff; a.K = h; a.actf = e->act_f; a.lda = ff;
-          per = q8_matrix_bytes(2 * ff, h);
+          per = qb(2 * ff, h);
           return launch_mq8(EPI_SWIGLU, a, s);
         case 4:
-          if (!e->has_head) return -1;
+          if (!e->has_head || e->out_kq_head) return -1;
+          a.wq4 = e->out_q4;
           a.W = e->output; a.N = e->n_vocab; a.K = h; a.out = e->logits; a.ldo = e->n_vocab;
-          per = q8_matrix_bytes(e->n_vocab, h);
+          per = e->out_q4 ? q4_matrix_bytes(e->n_vocab, h) : q8_matrix_bytes(e->n_vocab, h);
           return launch_mq8(EPI_F32, a, s);
       }
     }

@@ -94,6 +94,7 @@ struct MMArgs {
   // as up to 3 row segments of one ggml type each (e.g. q|k Q4_K, v Q6_K): segment i holds packed
   // tiles [kq_tile_end[i-1], kq_tile_end[i]) at byte offset kq_off[i] from W
   const float* xb;
+  int wq4;             // Q8_0-path GEMVs: W holds Q4_0 tiles (Q4_TILE_BYTES) instead of Q8 tiles
   int kq_n;
   int kq_type[3];
   int kq_tile_end[3];
@@ -151,6 +152,18 @@ constexpr int Q8_TILE_K = 64;
 constexpr int Q8_TILE_BYTES = 1088;
 inline size_t q8_matrix_bytes(int N, int K) { return (size_t)N / 16 * (K / Q8_TILE_K) * Q8_TILE_BYTES; }
 void launch_pack_q8(uint8_t* dst, const uint8_t* src_blocks, int N, int K, int mode, int row_offset, hipStream_t s);
+// ---- Q4_0 weights (GGUF type 2: 32 weights = f16 d + 16 bytes, q - 8) on the Q8_0
+// path: a packed Q4 tile = 16 rows x 64 k in Q4_TILE_BYTES: [0,512) lane l = row l&15 holds 4 bytes of
+// block 0 then 4 of block 1, its 8 values k 8(l>>4)..+8 as low nibbles (first 4) and high nibbles (last
+// 4) of those bytes -- unpacked (and shifted by -8) into the int8 A operand of the same
+// v_mfma_i32_16x16x32_i8 as a Q8 tile; [512,576): the f16 block scales as in a Q8 tile.  The activations
+// are Q8_0 rows: ggml's ggml_vec_dot_q4_0_q8_0 (exact int32 block sums, scaled by d_w * d_x in f32).
+constexpr int Q4_TILE_BYTES = 576;
+inline size_t q4_matrix_bytes(int N, int K) { return (size_t)N / 16 * (K / Q8_TILE_K) * Q4_TILE_BYTES; }
+void launch_pack_q4(uint8_t* dst, const uint8_t* src_blocks, int N, int K, int mode, int row_offset, hipStream_t s);
+// synthetic Q4_0 matrix: ggml quantize_row_q4_0_ref of the bf16 synthetic values, packed
+void launch_synth_q4_packed(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, int mode,
+                            int row_offset, hipStream_t s);
 // packed Q8 tiles of a [N][K] matrix -> packed bf16 tiles (prefill GEMM operand), values d*q -> bf16
 int launch_dequant_q8_tiles(uint16_t* dst, const uint8_t* W, int N, int K, hipStream_t s);
 void launch_synth_q8_packed(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, int mode,

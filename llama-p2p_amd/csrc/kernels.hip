@@ -1958,6 +1958,85 @@ __global__ void pack_q8_kernel(uint8_t* dst, const uint8_t* src, int N, int K, i
   }
 }
 
+// ---- Q4_0 tiles (kernels.h): one lane's 4 bytes of a block -> the int8 A operand of its 8 values,
+// q - 8 bytewise (q in 0..15: ((q | 0x80) - 8) ^ 0x80 is the int8 q - 8 without a borrow between bytes)
+__device__ __forceinline__ long q4_operand(uint32_t d) {
+  uint32_t lo = d & 0x0F0F0F0Fu, hi = (d >> 4) & 0x0F0F0F0Fu;
+  lo = ((lo | 0x80808080u) - 0x08080808u) ^ 0x80808080u;
+  hi = ((hi | 0x80808080u) - 0x08080808u) ^ 0x80808080u;
+  return (long)(((unsigned long)hi << 32) | lo);
+}
+
+// place one Q4_0 block (row, block b; q = the 32 unsigned nibble values) into its packed tile
+__device__ __forceinline__ void q4_place(uint8_t* dst, int P, int b, int KT2, uint16_t dbits, const uint8_t (&q)[32]) {
+  uint8_t* tile = dst + ((size_t)(P >> 4) * KT2 + (b >> 1)) * Q4_TILE_BYTES;
+  const int r = P & 15, half = b & 1;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w |= (uint32_t)((q[8 * g + j] & 15) | ((q[8 * g + 4 + j] & 15) << 4)) << (8 * j);
+    *reinterpret_cast<uint32_t*>(tile + 8 * (g * 16 + r) + 4 * half) = w;
+  }
+  *reinterpret_cast<uint16_t*>(tile + 512 + 16 * (r >> 2) + 8 * half + 2 * (r & 3)) = dbits;
+}
+
+// GGUF block_q4_0 {f16 d; uint8 qs[16]}: qs[j] low nibble = weight j, high nibble = weight j + 16
+__global__ void pack_q4_kernel(uint8_t* dst, const uint8_t* src, int N, int K, int mode, int offset) {
+  const int nb = K / 32;
+  const size_t total = (size_t)N * nb;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int row = (int)(i / nb), b = (int)(i % nb);
+    const uint8_t* blk = src + i * 18;
+    const uint16_t dbits = (uint16_t)(blk[0] | (blk[1] << 8));
+    uint8_t q[32];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) q[j] = blk[2 + j] & 15, q[16 + j] = blk[2 + j] >> 4;
+    q4_place(dst, packed_row(row, mode, offset), b, K / Q8_TILE_K, dbits, q);
+  }
+}
+
+// ggml quantize_row_q4_0_ref: d = (the value of largest magnitude) / -8, q = min(15, (int8)(x / d + 8.5))
+// with x / d as x * (1 / d); no contraction (the oracle's C does the same operations)
+__device__ __forceinline__ void q4_quant_ref(const float (&v)[32], uint16_t& dbits, uint8_t (&q)[32]) {
+  float amax = 0.f, mx = 0.f;
+#pragma unroll
+  for (int j = 0; j < 32; ++j)
+    if (amax < fabsf(v[j])) amax = fabsf(v[j]), mx = v[j];
+  const float d = __fdiv_rn(mx, -8.0f);
+  const float id = d != 0.f ? __fdiv_rn(1.0f, d) : 0.0f;
+  dbits = __builtin_bit_cast(uint16_t, (_Float16)d);
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const int qi = (int)(int8_t)__fadd_rn(__fmul_rn(v[j], id), 8.5f);
+    q[j] = (uint8_t)min(15, qi);
+  }
+}
+
+__global__ void synth_q4_packed_kernel(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, int mode,
+                                       int offset) {
+  const int nb = K / 32;
+  const size_t total = (size_t)N * nb;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int row = (int)(i / nb), b = (int)(i % nb);
+    float v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = bf2f(f2bf(synth_value(seed, tid, (size_t)row * K + 32 * b + j, scale)));
+    uint16_t dbits;
+    uint8_t q[32];
+    q4_quant_ref(v, dbits, q);
+    q4_place(dst, packed_row(row, mode, offset), b, K / Q8_TILE_K, dbits, q);
+  }
+}
+
+void launch_pack_q4(uint8_t* dst, const uint8_t* src, int N, int K, int mode, int offset, hipStream_t s) {
+  pack_q4_kernel<<<fill_grid((size_t)N * (K / 32)), 256, 0, s>>>(dst, src, N, K, mode, offset);
+}
+void launch_synth_q4_packed(uint8_t* dst, int N, int K, uint64_t seed, uint64_t tid, float scale, int mode,
+                            int offset, hipStream_t s) {
+  synth_q4_packed_kernel<<<fill_grid((size_t)N * (K / 32)), 256, 0, s>>>(dst, N, K, seed, tid, scale, mode, offset);
+}
+
 // synthetic Q8_0 matrix: the quantisation of the bf16 synthetic matrix (synth.py values -> bf16 -> f32)
 __device__ __forceinline__ void q8_synth_block(uint64_t seed, uint64_t tid, size_t i0, float scale, uint16_t& dbits,
                                                int8_t (&q)[32]) {
@@ -2275,8 +2354,9 @@ void launch_quantize_q8(int8_t* xq, float* xd, const float* src, int ld, int M, 
 // the scale from the residual writers' ssq partials, as mm_kernel's XS path -- into registers
 // BEFORE issuing its weight ring (QP float4 per lane and row: slice <= 256*QP), then quantises
 // them to Q8_0 (8 lanes per block) into a wave-private LDS image its B fragments are read from.
-template <int KS, int RT, int NB, int EPI, int U, int QP, int QM>
+template <int KS, int RT, int NB, int EPI, int U, int QP, int QM, bool Q4>
 __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
+  constexpr int TB = Q4 ? Q4_TILE_BYTES : Q8_TILE_BYTES, SO = Q4 ? 512 : 1024;  // tile bytes, scale offset
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int KT = a.K / Q8_TILE_K;
@@ -2289,7 +2369,7 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
 
   const uint8_t* Wr[RT];
 #pragma unroll
-  for (int r = 0; r < RT; ++r) Wr[r] = reinterpret_cast<const uint8_t*>(a.W) + (size_t)(tile0 + r) * KT * Q8_TILE_BYTES;
+  for (int r = 0; r < RT; ++r) Wr[r] = reinterpret_cast<const uint8_t*>(a.W) + (size_t)(tile0 + r) * KT * TB;
   const int8_t* Xq[NB];
   const float* Xd[NB];
   // QP image: rows of QB bytes (slice + 16 pad), then QM*QS floats of block scales
@@ -2348,9 +2428,14 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
   auto load_w = [&](Frag& f, int kt) {
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
-      const uint8_t* t = Wr[r] + (size_t)kt * Q8_TILE_BYTES;
-      f.q[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t) + lane);
-      f.d[r] = *reinterpret_cast<const u32x4*>(t + 1024 + 16 * (lane >> 4));
+      const uint8_t* t = Wr[r] + (size_t)kt * TB;
+      if constexpr (Q4) {
+        const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(t) + lane);
+        f.q[r] = u32x4{v[0], v[1], 0u, 0u};
+      } else {
+        f.q[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t) + lane);
+      }
+      f.d[r] = *reinterpret_cast<const u32x4*>(t + SO + 16 * (lane >> 4));
     }
     if constexpr (QP == 0) {
 #pragma unroll
@@ -2376,8 +2461,8 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
       const long b1 = (long)(((unsigned long)xb[3] << 32) | xb[2]);
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
-        const long a0 = (long)(((unsigned long)f.q[r][1] << 32) | f.q[r][0]);
-        const long a1 = (long)(((unsigned long)f.q[r][3] << 32) | f.q[r][2]);
+        const long a0 = Q4 ? q4_operand(f.q[r][0]) : (long)(((unsigned long)f.q[r][1] << 32) | f.q[r][0]);
+        const long a1 = Q4 ? q4_operand(f.q[r][1]) : (long)(((unsigned long)f.q[r][3] << 32) | f.q[r][2]);
         const i32x4 p0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, b0, i32x4{0, 0, 0, 0}, 0, 0, 0);
         const i32x4 p1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, b1, i32x4{0, 0, 0, 0}, 0, 0, 0);
         const f16x8 dw = __builtin_bit_cast(f16x8, f.d[r]);
@@ -2491,23 +2576,19 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
 }
 
 // quantise-on-load launch: 8 waves (the slice of K per wave <= 256*QP), QM row slots
-template <int EPI, int QP, int QM>
+template <int EPI, int QP, int QM, bool Q4>
 static void launch_mq8_ql(const MMArgs& a, hipStream_t s) {
   const int KT = a.K / Q8_TILE_K;
   const int QB = (KT + 7) / 8 * Q8_TILE_K + 16, QS = (KT + 7) / 8 * 2;
   const size_t lds = (size_t)8 * QM * (QB + 4 * QS);
-  static const int rt = getenv("MX_Q8_QL_RT") ? atoi(getenv("MX_Q8_QL_RT")) : 1;  // geometry probe
-  if (rt == 2 && (a.N / TILE_N) % 2 == 0)
-    mq8_kernel<8, 2, 1, EPI, 2, QP, QM><<<dim3(a.N / TILE_N / 2, 1), 512, lds, s>>>(a);
-  else
-    mq8_kernel<8, 1, 1, EPI, 4, QP, QM><<<dim3(a.N / TILE_N, 1), 512, lds, s>>>(a);
+  mq8_kernel<8, 1, 1, EPI, 4, QP, QM, Q4><<<dim3(a.N / TILE_N, 1), 512, lds, s>>>(a);
 }
 
-template <int EPI, int QP>
+template <int EPI, int QP, bool Q4>
 static void launch_mq8_ql_m(const MMArgs& a, hipStream_t s) {
-  if (a.M == 1) launch_mq8_ql<EPI, QP, 1>(a, s);
-  else if (a.M == 2) launch_mq8_ql<EPI, QP, 2>(a, s);
-  else launch_mq8_ql<EPI, QP, 4>(a, s);
+  if (a.M == 1) launch_mq8_ql<EPI, QP, 1, Q4>(a, s);
+  else if (a.M == 2) launch_mq8_ql<EPI, QP, 2, Q4>(a, s);
+  else launch_mq8_ql<EPI, QP, 4, Q4>(a, s);
 }
 
 bool mq8_can_quantize_on_load(int M, int K, bool norm) {
@@ -2515,47 +2596,31 @@ bool mq8_can_quantize_on_load(int M, int K, bool norm) {
   return M >= 1 && M <= XS_MAX_M && K % Q8_TILE_K == 0 && slice <= 2048 && (!norm || K / 16 <= 512);
 }
 
-// one column tile: 16 waves split K (as mm_kernel); two or four tiles: 8 waves (the B fragments and
-// block scales of every tile stay in registers: 16 waves would spill)
-template <int EPI>
+// <= 16 tokens: 8 waves split K, one row tile each (tools/gpu/q8_probe.sh); 17..32 tokens: per
+// epilogue, from tools/gpu/q8_probe32.sh (Llama-3-8B, 32 rows): more row tiles per wave for the wide
+// matrices (each B fragment loaded from L2 feeds RT MFMAs), one for the 4096-row ones; more: 4 tiles
+template <int EPI, bool Q4>
 static int launch_mq8_epi(const MMArgs& a, hipStream_t s) {
   const int ntiles = a.N / TILE_N;
   if (a.M <= 16) {
-    static const int cfg = getenv("MX_Q8_CFG") ? atoi(getenv("MX_Q8_CFG")) : 1;  // geometry probe
-    switch (ntiles % 2 ? 1 : cfg) {  // 1 (default): 8 waves, best of tools/gpu/q8_probe.sh
-      case 0: mq8_kernel<16, 1, 1, EPI, 4, 0, 1><<<dim3(ntiles, 1), 1024, 0, s>>>(a); return 0;
-      case 2: mq8_kernel<16, 2, 1, EPI, 2, 0, 1><<<dim3(ntiles / 2, 1), 1024, 0, s>>>(a); return 0;
-      case 3: mq8_kernel<8, 2, 1, EPI, 4, 0, 1><<<dim3(ntiles / 2, 1), 512, 0, s>>>(a); return 0;
-      case 4: mq8_kernel<4, 1, 1, EPI, 8, 0, 1><<<dim3(ntiles, 1), 256, 0, s>>>(a); return 0;
-      case 5: mq8_kernel<16, 1, 1, EPI, 2, 0, 1><<<dim3(ntiles, 1), 1024, 0, s>>>(a); return 0;
-      case 6: mq8_kernel<8, 2, 1, EPI, 2, 0, 1><<<dim3(ntiles / 2, 1), 512, 0, s>>>(a); return 0;
-    }
-    mq8_kernel<8, 1, 1, EPI, 4, 0, 1><<<dim3(ntiles, 1), 512, 0, s>>>(a);
+    mq8_kernel<8, 1, 1, EPI, 4, 0, 1, Q4><<<dim3(ntiles, 1), 512, 0, s>>>(a);
   } else if (a.M <= 32) {
-    // per epilogue, from tools/gpu/q8_probe32.sh (Llama-3-8B, 32 rows): more row tiles per wave for
-    // the wide matrices (each B fragment loaded from L2 feeds RT MFMAs), one for the 4096-row ones
-    const int dflt = EPI == EPI_QKV ? 1 : (EPI == EPI_SWIGLU || EPI == EPI_F32) ? 3 : 0;
-    static const int cfg2e = getenv("MX_Q8_CFG2") ? atoi(getenv("MX_Q8_CFG2")) : -1;  // geometry probe
-    const int cfg2 = cfg2e >= 0 ? cfg2e : dflt;
-    switch (ntiles % 4 ? 0 : cfg2) {
-      case 1: mq8_kernel<8, 2, 2, EPI, 2, 0, 1><<<dim3(ntiles / 2, 1), 512, 0, s>>>(a); return 0;
-      case 2: mq8_kernel<8, 4, 2, EPI, 2, 0, 1><<<dim3(ntiles / 4, 1), 512, 0, s>>>(a); return 0;
-      case 3: mq8_kernel<4, 4, 2, EPI, 2, 0, 1><<<dim3(ntiles / 4, 1), 256, 0, s>>>(a); return 0;
-      case 4: mq8_kernel<16, 2, 2, EPI, 1, 0, 1><<<dim3(ntiles / 2, 1), 1024, 0, s>>>(a); return 0;
-    }
-    mq8_kernel<8, 1, 2, EPI, 4, 0, 1><<<dim3(ntiles, 1), 512, 0, s>>>(a);
+    const int cfg = ntiles % 4 ? 0 : EPI == EPI_QKV ? 1 : (EPI == EPI_SWIGLU || EPI == EPI_F32) ? 3 : 0;
+    if (cfg == 1) mq8_kernel<8, 2, 2, EPI, 2, 0, 1, Q4><<<dim3(ntiles / 2, 1), 512, 0, s>>>(a);
+    else if (cfg == 3) mq8_kernel<4, 4, 2, EPI, 2, 0, 1, Q4><<<dim3(ntiles / 4, 1), 256, 0, s>>>(a);
+    else mq8_kernel<8, 1, 2, EPI, 4, 0, 1, Q4><<<dim3(ntiles, 1), 512, 0, s>>>(a);
   } else {
-    mq8_kernel<8, 1, 4, EPI, 2, 0, 1><<<dim3(ntiles, (a.M + 63) / 64), 512, 0, s>>>(a);
+    mq8_kernel<8, 1, 4, EPI, 2, 0, 1, Q4><<<dim3(ntiles, (a.M + 63) / 64), 512, 0, s>>>(a);
   }
   return 0;
 }
 
-template <int EPI>
+template <int EPI, bool Q4>
 static int launch_mq8_ql_epi(const MMArgs& a, hipStream_t s) {
   const int slice = (a.K / Q8_TILE_K + 7) / 8 * Q8_TILE_K;
-  if (slice <= 512) launch_mq8_ql_m<EPI, 2>(a, s);
-  else if (slice <= 1024) launch_mq8_ql_m<EPI, 4>(a, s);
-  else launch_mq8_ql_m<EPI, 8>(a, s);
+  if (slice <= 512) launch_mq8_ql_m<EPI, 2, Q4>(a, s);
+  else if (slice <= 1024) launch_mq8_ql_m<EPI, 4, Q4>(a, s);
+  else launch_mq8_ql_m<EPI, 8, Q4>(a, s);
   return 0;
 }
 
@@ -2568,8 +2633,9 @@ static int launch_mq8_ql_epi(const MMArgs& a, hipStream_t s) {
 // flight.  Per 64-k tile the arithmetic is mq8_kernel's (two exact int32 block products, each
 // scaled by d_w * d_x in f32); the whole K stays in one wave, so the epilogue runs from registers.
 // ---------------------------------------------------------------------------
-template <int W, int EPI, int U>
+template <int W, int EPI, int U, bool Q4>
 __global__ __launch_bounds__(64 * W) void mq8_wide_kernel(MMArgs a) {
+  constexpr int TB = Q4 ? Q4_TILE_BYTES : Q8_TILE_BYTES, SO = Q4 ? 512 : 1024;  // tile bytes, scale offset
   constexpr int NB = 2, ROWS = 32;
   constexpr int QP = 256 + 16;     // int8 per LDS row (+16 B: conflict-free fragment reads)
   constexpr int NQ = ROWS * 16;    // 16-B pieces of q per chunk
@@ -2586,7 +2652,7 @@ __global__ __launch_bounds__(64 * W) void mq8_wide_kernel(MMArgs a) {
   // grid.y > 1 (EPI_SLAB): this work-group's K range of 256-k chunks [cb, cb + NCH)
   const int NCHT = a.K / 256, cb = NCHT * blockIdx.y / gridDim.y, NCH = NCHT * (blockIdx.y + 1) / gridDim.y - cb;
   const int tile = blockIdx.x * W + w;
-  const uint8_t* Wt = reinterpret_cast<const uint8_t*>(a.W) + ((size_t)tile * KT + cb * 4) * Q8_TILE_BYTES;
+  const uint8_t* Wt = reinterpret_cast<const uint8_t*>(a.W) + ((size_t)tile * KT + cb * 4) * TB;
 
   const u32x4* xsrc[PPT];
   int xstep[PPT], xdst[PPT];
@@ -2627,9 +2693,14 @@ __global__ __launch_bounds__(64 * W) void mq8_wide_kernel(MMArgs a) {
   auto load_w = [&](Frag& f, int ch) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const uint8_t* t = Wt + (size_t)(ch * 4 + k) * Q8_TILE_BYTES;
-      f.q[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t) + lane);
-      f.d[k] = *reinterpret_cast<const u32x4*>(t + 1024 + 16 * (lane >> 4));
+      const uint8_t* t = Wt + (size_t)(ch * 4 + k) * TB;
+      if constexpr (Q4) {
+        const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(t) + lane);
+        f.q[k] = u32x4{v[0], v[1], 0u, 0u};
+      } else {
+        f.q[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t) + lane);
+      }
+      f.d[k] = *reinterpret_cast<const u32x4*>(t + SO + 16 * (lane >> 4));
     }
   };
   f32x4 acc[NB];
@@ -2651,8 +2722,8 @@ __global__ __launch_bounds__(64 * W) void mq8_wide_kernel(MMArgs a) {
     const Frag f = ring[R];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const long a0 = (long)(((unsigned long)f.q[k][1] << 32) | f.q[k][0]);
-      const long a1 = (long)(((unsigned long)f.q[k][3] << 32) | f.q[k][2]);
+      const long a0 = Q4 ? q4_operand(f.q[k][0]) : (long)(((unsigned long)f.q[k][1] << 32) | f.q[k][0]);
+      const long a1 = Q4 ? q4_operand(f.q[k][1]) : (long)(((unsigned long)f.q[k][3] << 32) | f.q[k][2]);
       const f16x8 dw = __builtin_bit_cast(f16x8, f.d[k]);
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
@@ -2707,7 +2778,7 @@ __global__ __launch_bounds__(64 * W) void mq8_wide_kernel(MMArgs a) {
 // until ~256 work-groups, partial slabs [ks][token][N] (folded by launch_rmsnorm_q8's FOLD form, or
 // finished by the decode attention / launch_qkv_finish).  Returns ks, or -1 (use launch_mq8).
 int launch_mq8_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s) {
-  static const bool off = getenv("MX_NO_Q8_WIDE") != nullptr || getenv("MX_NO_Q8_SLAB") != nullptr;
+  static const bool off = getenv("MX_NO_Q8_WIDE") != nullptr;
   if (off || a.M <= 16 || a.M > 32 || !a.xq || !a.xd || a.K % 256 || a.N % 64) return -1;
   const int ntiles = a.N / TILE_N, NCH = a.K / 256;
   int ks = 1;
@@ -2716,7 +2787,8 @@ int launch_mq8_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipStream
   p.out = slabs;
   p.ldo = a.N;
   p.slab_stride = slab_stride;
-  mq8_wide_kernel<4, EPI_SLAB, 2><<<dim3(ntiles / 4, ks), 256, 0, s>>>(p);
+  if (a.wq4) mq8_wide_kernel<4, EPI_SLAB, 2, true><<<dim3(ntiles / 4, ks), 256, 0, s>>>(p);
+  else mq8_wide_kernel<4, EPI_SLAB, 2, false><<<dim3(ntiles / 4, ks), 256, 0, s>>>(p);
   return ks;
 }
 
@@ -2728,8 +2800,13 @@ static int launch_mq8_wide(int epi, const MMArgs& a, hipStream_t s) {
   if (epi != EPI_SWIGLU && epi != EPI_F32) return -1;
   auto go = [&](auto wc) {
     constexpr int W = decltype(wc)::value;
-    if (epi == EPI_SWIGLU) mq8_wide_kernel<W, EPI_SWIGLU, 2><<<ntiles / W, 64 * W, 0, s>>>(a);
-    else mq8_wide_kernel<W, EPI_F32, 2><<<ntiles / W, 64 * W, 0, s>>>(a);
+    if (a.wq4) {
+      if (epi == EPI_SWIGLU) mq8_wide_kernel<W, EPI_SWIGLU, 2, true><<<ntiles / W, 64 * W, 0, s>>>(a);
+      else mq8_wide_kernel<W, EPI_F32, 2, true><<<ntiles / W, 64 * W, 0, s>>>(a);
+    } else {
+      if (epi == EPI_SWIGLU) mq8_wide_kernel<W, EPI_SWIGLU, 2, false><<<ntiles / W, 64 * W, 0, s>>>(a);
+      else mq8_wide_kernel<W, EPI_F32, 2, false><<<ntiles / W, 64 * W, 0, s>>>(a);
+    }
     return 0;
   };
   if (ntiles % 7 == 0 && ntiles / 7 >= 200) return go(std::integral_constant<int, 7>{});
@@ -2745,23 +2822,31 @@ int launch_mq8(int epi, const MMArgs& a, hipStream_t s) {
     if (!a.xf || !mq8_can_quantize_on_load(a.M, a.K, a.norm_w != nullptr) ||
         (a.norm_w && (!a.ssq || a.np * 16 != a.K)))
       return -1;
-    switch (epi) {
-      case EPI_F32: return launch_mq8_ql_epi<EPI_F32>(a, s);
-      case EPI_RESID: return launch_mq8_ql_epi<EPI_RESID>(a, s);
-      case EPI_QKV: return launch_mq8_ql_epi<EPI_QKV>(a, s);
-      case EPI_SWIGLU: return launch_mq8_ql_epi<EPI_SWIGLU>(a, s);
-    }
-    return -1;
+    auto ql = [&](auto q4c) {
+      constexpr bool Q4 = decltype(q4c)::value;
+      switch (epi) {
+        case EPI_F32: return launch_mq8_ql_epi<EPI_F32, Q4>(a, s);
+        case EPI_RESID: return launch_mq8_ql_epi<EPI_RESID, Q4>(a, s);
+        case EPI_QKV: return launch_mq8_ql_epi<EPI_QKV, Q4>(a, s);
+        case EPI_SWIGLU: return launch_mq8_ql_epi<EPI_SWIGLU, Q4>(a, s);
+      }
+      return -1;
+    };
+    return a.wq4 ? ql(std::true_type{}) : ql(std::false_type{});
   }
   if (!a.xd) return -1;
   if (launch_mq8_wide(epi, a, s) == 0) return 0;
-  switch (epi) {
-    case EPI_F32: return launch_mq8_epi<EPI_F32>(a, s);
-    case EPI_RESID: return launch_mq8_epi<EPI_RESID>(a, s);
-    case EPI_QKV: return launch_mq8_epi<EPI_QKV>(a, s);
-    case EPI_SWIGLU: return launch_mq8_epi<EPI_SWIGLU>(a, s);
-  }
-  return -1;
+  auto go = [&](auto q4c) {
+    constexpr bool Q4 = decltype(q4c)::value;
+    switch (epi) {
+      case EPI_F32: return launch_mq8_epi<EPI_F32, Q4>(a, s);
+      case EPI_RESID: return launch_mq8_epi<EPI_RESID, Q4>(a, s);
+      case EPI_QKV: return launch_mq8_epi<EPI_QKV, Q4>(a, s);
+      case EPI_SWIGLU: return launch_mq8_epi<EPI_SWIGLU, Q4>(a, s);
+    }
+    return -1;
+  };
+  return a.wq4 ? go(std::true_type{}) : go(std::false_type{});
 }
 
 }  // namespace mx

@@ -71,6 +71,7 @@ typedef struct {
     float *attn_norm, *ffn_norm;
     uint8_t *q8[9]; /* Q8_0 blocks by L_* kind (NULL: the bf16 matrix is used) */
     uint8_t *kq[9]; /* K-quant blocks by L_* kind (NULL: not a K-quant matrix) */
+    uint8_t *q4[9]; /* Q4_0 blocks by L_* kind (NULL: not a Q4_0 matrix) */
     int kq_type[9];
 } orc_layer;
 
@@ -81,6 +82,7 @@ typedef struct {
     uint16_t *tok_embd, *output; /* bf16 [V][h] */
     uint8_t *tok_embd_q8, *output_q8; /* Q8_0 blocks or NULL */
     uint8_t *tok_embd_kq, *output_kq; /* K-quant blocks or NULL */
+    uint8_t *output_q4;               /* Q4_0 blocks or NULL */
     int tok_embd_kq_type, output_kq_type;
     float *out_norm;
     orc_layer *layers;
@@ -202,9 +204,9 @@ void orc_free(orc_model *m) {
         orc_layer *L = &m->layers[l];
         free(L->wq); free(L->wk); free(L->wv); free(L->wo); free(L->wg); free(L->wu); free(L->wd);
         free(L->attn_norm); free(L->ffn_norm);
-        for (int k = 0; k < 9; k++) { free(L->q8[k]); free(L->kq[k]); }
+        for (int k = 0; k < 9; k++) { free(L->q8[k]); free(L->kq[k]); free(L->q4[k]); }
     }
-    free(m->tok_embd_q8); free(m->output_q8); free(m->tok_embd_kq); free(m->output_kq);
+    free(m->tok_embd_q8); free(m->output_q8); free(m->tok_embd_kq); free(m->output_kq); free(m->output_q4);
     free(m->rope_ff);
     free(m->layers); free(m->tok_embd); free(m->output); free(m->out_norm); free(m);
 }
@@ -421,6 +423,138 @@ static void matmul_q8(float *y, const uint8_t *W, const float *x, int T, int n_i
     free(xd);
 }
 
+
+/* ------------------------------------------------------------------ Q4_0 */
+/* ggml block_q4_0 {f16 d; uint8 qs[16]}: weight j = (qs[j] & 15) - 8, weight j+16 = (qs[j] >> 4) - 8 */
+#define Q4_0_BLOCK 18
+
+/* ggml quantize_row_q4_0_ref: d = (signed value of largest magnitude) / -8, q = min(15, (int8)(x*id + 8.5)) */
+static void quantize_row_q4_0_ref(const float *x, uint8_t *y, int k) {
+    for (int b = 0; b < k / 32; b++) {
+        const float *xb = x + (size_t)b * 32;
+        float amax = 0.f, max = 0.f;
+        for (int j = 0; j < 32; j++)
+            if (amax < fabsf(xb[j])) { amax = fabsf(xb[j]); max = xb[j]; }
+        const float d = max / -8;
+        const float id = d ? 1.0f / d : 0.0f;
+        uint8_t *yb = y + (size_t)b * Q4_0_BLOCK;
+        const uint16_t dh = f32_to_f16(d);
+        memcpy(yb, &dh, 2);
+        for (int j = 0; j < 16; j++) {
+            const float x0 = xb[j] * id, x1 = xb[16 + j] * id;
+            int xi0 = (int8_t)(x0 + 8.5f), xi1 = (int8_t)(x1 + 8.5f);
+            if (xi0 > 15) xi0 = 15;
+            if (xi1 > 15) xi1 = 15;
+            yb[2 + j] = (uint8_t)(xi0 | (xi1 << 4));
+        }
+    }
+}
+
+/* ggml_vec_dot_q4_0_q8_0 (generic): exact int block sums, scaled by d_w * d_x */
+static float dot_q4_0(const uint8_t *w, const int8_t *q, const float *d, int n) {
+    float s = 0.f;
+    for (int b = 0; b < n / 32; b++) {
+        const uint8_t *wb = w + (size_t)b * Q4_0_BLOCK;
+        uint16_t dh;
+        memcpy(&dh, wb, 2);
+        int sumi = 0;
+        for (int j = 0; j < 16; j++) {
+            sumi += ((wb[2 + j] & 15) - 8) * (int)q[(size_t)b * 32 + j];
+            sumi += ((wb[2 + j] >> 4) - 8) * (int)q[(size_t)b * 32 + 16 + j];
+        }
+        s += (f16_to_f32(dh) * d[b]) * (float)sumi;
+    }
+    return s;
+}
+
+static void jitter_row(const float *xr, float *xj, int n_in, int t, int n_out);
+
+static void matmul_q4_0(float *y, const uint8_t *W, const float *x, int T, int n_in, int n_out) {
+    int8_t *xq = (int8_t *)malloc((size_t)T * n_in);
+    float *xd = (float *)malloc(sizeof(float) * (size_t)T * (n_in / 32));
+    float *xj = (float *)malloc(sizeof(float) * n_in);
+    for (int t = 0; t < T; t++) {
+        jitter_row(x + (size_t)t * n_in, xj, n_in, t, n_out);
+        quantize_act_q8_0(xj, n_in, xq + (size_t)t * n_in, xd + (size_t)t * (n_in / 32));
+    }
+    free(xj);
+    const size_t rb = (size_t)(n_in / 32) * Q4_0_BLOCK;
+#pragma omp parallel for schedule(static)
+    for (int o = 0; o < n_out; o++)
+        for (int t = 0; t < T; t++)
+            y[(size_t)t * n_out + o] = dot_q4_0(W + (size_t)o * rb, xq + (size_t)t * n_in, xd + (size_t)t * (n_in / 32), n_in);
+    free(xq);
+    free(xd);
+}
+
+static uint8_t **q4_slot(orc_model *m, int layer, int kind, size_t *rows, size_t *cols, uint16_t **bf) {
+    if (layer < 0) {
+        if (kind != K_OUTPUT) return NULL;
+        *rows = m->hp.n_vocab; *cols = m->hp.n_embd; *bf = m->output;
+        return &m->output_q4;
+    }
+    uint8_t **q8 = q8_slot(m, layer, kind, rows, cols, bf);
+    return q8 ? &m->layers[layer].q4[kind] : NULL;
+}
+
+/* Make one matrix Q4_0 from GGUF block bytes (rows x cols/32 blocks of 18 bytes). */
+int orc_set_tensor_q4_0(orc_model *m, int layer, int kind, const void *blocks) {
+    size_t rows, cols;
+    uint16_t *bf;
+    uint8_t **slot = q4_slot(m, layer, kind, &rows, &cols, &bf);
+    if (!slot || cols % 32) return -1;
+    const size_t nb = rows * (cols / 32) * Q4_0_BLOCK;
+    if (!*slot) *slot = (uint8_t *)malloc(nb);
+    memcpy(*slot, blocks, nb);
+    return 0;
+}
+
+/* The synthetic "q4_0" model: every layer matrix -> quantize_row_q4_0_ref of its bf16 values, token_embd
+ * and output -> Q8_0 (as the engine's synthetic:<shape>:q4_0). */
+int orc_quantize_q4_0(orc_model *m) {
+    static const int kinds[] = {L_Q, L_K, L_V, L_O, L_GATE, L_UP, L_DOWN};
+    for (int l = -1; l < m->hp.n_layer; l++) {
+        int nk = l < 0 ? 2 : 7;
+        for (int i = 0; i < nk; i++) {
+            int kind = l < 0 ? (i ? K_OUTPUT : K_TOK_EMBD) : kinds[i];
+            size_t rows, cols;
+            uint16_t *bf;
+            uint8_t **slot = l < 0 ? q8_slot(m, l, kind, &rows, &cols, &bf) : q4_slot(m, l, kind, &rows, &cols, &bf);
+            if (!slot || cols % 32) return -1;
+            const size_t bb = l < 0 ? Q8_0_BLOCK : Q4_0_BLOCK;
+            if (!*slot) *slot = (uint8_t *)malloc(rows * (cols / 32) * bb);
+            uint8_t *dst = *slot;
+#pragma omp parallel for schedule(static)
+            for (size_t r = 0; r < rows; r++) {
+                float *v = (float *)malloc(sizeof(float) * cols);
+                for (size_t c = 0; c < cols; c++) v[c] = bf16_to_f32(bf[r * cols + c]);
+                if (l < 0) {
+                    quantize_row_q8_0_ref(v, dst + r * (cols / 32) * Q8_0_BLOCK, (int)cols);
+                } else {
+                    quantize_row_q4_0_ref(v, dst + r * (cols / 32) * Q4_0_BLOCK, (int)cols);
+                }
+                free(v);
+            }
+        }
+    }
+    return 0;
+}
+
+/* test hooks: one Q4_0 row of a float row, and its dot product with the Q8_0 image of x */
+int orc_q4_0_quantize_row(const float *x, int k, uint8_t *out) {
+    if (k % 32) return -1;
+    quantize_row_q4_0_ref(x, out, k);
+    return 0;
+}
+float orc_q4_0_vec_dot(const uint8_t *w, const float *x, int n) {
+    int8_t *q = (int8_t *)malloc(n);
+    float *d = (float *)malloc(sizeof(float) * (n / 32));
+    quantize_act_q8_0(x, n, q, d);
+    const float r = dot_q4_0(w, q, d, n);
+    free(q);
+    free(d);
+    return r;
+}
 
 /* ------------------------------------------------------------------ K-quants */
 #define QK_K 256
@@ -789,8 +923,9 @@ static void matmul_bf16(float *y, const uint16_t *W, const float *x, int T, int 
 }
 
 static void matmul(float *y, const uint16_t *W, const uint8_t *Wq8, const uint8_t *Wkq, int kq_type, const float *x,
-                   int T, int n_in, int n_out, int exact, uint16_t *scratch) {
-    if (Wkq) matmul_kq(y, kq_type, Wkq, x, T, n_in, n_out);
+                   int T, int n_in, int n_out, int exact, uint16_t *scratch, const uint8_t *Wq4) {
+    if (Wq4) matmul_q4_0(y, Wq4, x, T, n_in, n_out);
+    else if (Wkq) matmul_kq(y, kq_type, Wkq, x, T, n_in, n_out);
     else if (Wq8) matmul_q8(y, Wq8, x, T, n_in, n_out);
     else matmul_bf16(y, W, x, T, n_in, n_out, exact, scratch);
 }
@@ -854,9 +989,9 @@ int orc_eval(orc_ctx *c, const int32_t *ids, int n, int pos0, float *logits, int
     for (int l = 0; l < hp->n_layer; l++) {
         orc_layer *L = &m->layers[l];
         for (int t = 0; t < T; t++) rmsnorm(cur + (size_t)t * h, x + (size_t)t * h, L->attn_norm, h, hp->eps);
-        matmul(q, L->wq, L->q8[L_Q], L->kq[L_Q], L->kq_type[L_Q], cur, T, h, h, exact, scratch);
-        matmul(k, L->wk, L->q8[L_K], L->kq[L_K], L->kq_type[L_K], cur, T, h, kvd, exact, scratch);
-        matmul(v, L->wv, L->q8[L_V], L->kq[L_V], L->kq_type[L_V], cur, T, h, kvd, exact, scratch);
+        matmul(q, L->wq, L->q8[L_Q], L->kq[L_Q], L->kq_type[L_Q], cur, T, h, h, exact, scratch, L->q4[L_Q]);
+        matmul(k, L->wk, L->q8[L_K], L->kq[L_K], L->kq_type[L_K], cur, T, h, kvd, exact, scratch, L->q4[L_K]);
+        matmul(v, L->wv, L->q8[L_V], L->kq[L_V], L->kq_type[L_V], cur, T, h, kvd, exact, scratch, L->q4[L_V]);
         for (int t = 0; t < T; t++) {
             const float *cs = c->rope_cs + (size_t)(pos0 + t) * (d / 2) * 2;
             rope_rows(q + (size_t)t * h, nh, d, cs);
@@ -926,23 +1061,23 @@ int orc_eval(orc_ctx *c, const int32_t *ids, int n, int pos0, float *logits, int
                 free(s);
             }
         }
-        matmul(tmp, L->wo, L->q8[L_O], L->kq[L_O], L->kq_type[L_O], att, T, h, h, exact, scratch);
+        matmul(tmp, L->wo, L->q8[L_O], L->kq[L_O], L->kq_type[L_O], att, T, h, h, exact, scratch, L->q4[L_O]);
         for (size_t i = 0; i < (size_t)T * h; i++) x[i] += tmp[i];
         /* ffn */
         for (int t = 0; t < T; t++) rmsnorm(cur + (size_t)t * h, x + (size_t)t * h, L->ffn_norm, h, hp->eps);
-        matmul(u, L->wu, L->q8[L_UP], L->kq[L_UP], L->kq_type[L_UP], cur, T, h, ff, exact, scratch);
-        matmul(g, L->wg, L->q8[L_GATE], L->kq[L_GATE], L->kq_type[L_GATE], cur, T, h, ff, exact, scratch);
+        matmul(u, L->wu, L->q8[L_UP], L->kq[L_UP], L->kq_type[L_UP], cur, T, h, ff, exact, scratch, L->q4[L_UP]);
+        matmul(g, L->wg, L->q8[L_GATE], L->kq[L_GATE], L->kq_type[L_GATE], cur, T, h, ff, exact, scratch, L->q4[L_GATE]);
         for (size_t i = 0; i < (size_t)T * ff; i++) {
             float gg = g[i];
             g[i] = (gg / (1.0f + expf(-gg))) * u[i];
         }
-        matmul(tmp, L->wd, L->q8[L_DOWN], L->kq[L_DOWN], L->kq_type[L_DOWN], g, T, ff, h, exact, scratch);
+        matmul(tmp, L->wd, L->q8[L_DOWN], L->kq[L_DOWN], L->kq_type[L_DOWN], g, T, ff, h, exact, scratch, L->q4[L_DOWN]);
         for (size_t i = 0; i < (size_t)T * h; i++) x[i] += tmp[i];
     }
     int t0 = all_logits ? 0 : T - 1;
     int nt = T - t0;
     for (int t = 0; t < nt; t++) rmsnorm(cur + (size_t)t * h, x + (size_t)(t0 + t) * h, m->out_norm, h, hp->eps);
-    matmul(logits, m->output, m->output_q8, m->output_kq, m->output_kq_type, cur, nt, h, V, exact, scratch);
+    matmul(logits, m->output, m->output_q8, m->output_kq, m->output_kq_type, cur, nt, h, V, exact, scratch, m->output_q4);
 
     free(x); free(cur); free(q); free(k); free(v); free(att); free(g); free(u); free(tmp); free(scratch);
     return 0;

@@ -53,6 +53,14 @@ def lib():
         L.orc_quantize_q8.argtypes = [vp]
         L.orc_quantize_q8.restype = i32
         L.orc_set_q8_jitter.argtypes = [ctypes.c_float]
+        L.orc_set_tensor_q4_0.argtypes = [vp, i32, i32, vp]
+        L.orc_set_tensor_q4_0.restype = i32
+        L.orc_quantize_q4_0.argtypes = [vp]
+        L.orc_quantize_q4_0.restype = i32
+        L.orc_q4_0_quantize_row.argtypes = [vp, i32, vp]
+        L.orc_q4_0_quantize_row.restype = i32
+        L.orc_q4_0_vec_dot.argtypes = [vp, vp, i32]
+        L.orc_q4_0_vec_dot.restype = ctypes.c_float
         L.orc_set_tensor_kq.argtypes = [vp, i32, i32, i32, vp]
         L.orc_set_tensor_kq.restype = i32
         L.orc_kq_synth_blocks.argtypes = [i32, ctypes.c_int64, u64, u64, vp]
@@ -107,6 +115,18 @@ class OracleModel:
         blocks = np.ascontiguousarray(blocks, dtype=np.uint8)
         if lib().orc_set_tensor_q8(self._m, layer, kind, blocks.ctypes.data):
             raise ValueError(f"orc_set_tensor_q8({layer},{kind}) failed")
+
+    def set_tensor_q4_0(self, layer: int, kind: int, blocks: np.ndarray):
+        """Make one matrix Q4_0 from GGUF block bytes (uint8 [rows][cols/32*18]); output: layer -1 kind 3."""
+        blocks = np.ascontiguousarray(blocks, dtype=np.uint8)
+        if lib().orc_set_tensor_q4_0(self._m, layer, kind, blocks.ctypes.data):
+            raise ValueError(f"orc_set_tensor_q4_0({layer},{kind}) failed")
+
+    def quantize_q4_0(self):
+        """Layer matrices -> Q4_0 of their bf16 values (ggml quantize_row_q4_0_ref), token_embd and
+        output -> Q8_0: the engine's synthetic:<shape>:q4_0 model."""
+        if lib().orc_quantize_q4_0(self._m):
+            raise ValueError("orc_quantize_q4_0 failed")
 
     def set_tensor_kq(self, layer: int, kind: int, ggml_type: int, blocks: np.ndarray):
         """Make one matrix a K-quant (Q4_K 12, Q5_K 13, Q6_K 14) from GGUF block bytes."""
@@ -197,6 +217,22 @@ class OracleContext:
 def q8_jitter(eps: float):
     """Relative activation noise before every Q8_0 quantisation (sensitivity probe; 0 = off)."""
     lib().orc_set_q8_jitter(eps)
+
+
+def q4_0_quantize_row(x: np.ndarray) -> np.ndarray:
+    """ggml quantize_row_q4_0_ref of one f32 row -> block_q4_0 bytes (uint8 [n/32*18])."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty(x.size // 32 * 18, np.uint8)
+    if lib().orc_q4_0_quantize_row(x.ctypes.data, x.size, out.ctypes.data):
+        raise ValueError("orc_q4_0_quantize_row failed")
+    return out
+
+
+def q4_0_vec_dot(blocks: np.ndarray, x: np.ndarray) -> float:
+    """ggml_vec_dot_q4_0_q8_0 of one Q4_0 row with the Q8_0 image of x."""
+    blocks = np.ascontiguousarray(blocks, dtype=np.uint8)
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    return float(lib().orc_q4_0_vec_dot(blocks.ctypes.data, x.ctypes.data, x.size))
 
 
 def kq_synth_blocks(ggml_type: int, nblocks: int, seed: int, tid: int) -> np.ndarray:

@@ -7,9 +7,10 @@ tests/test_kquants.py) for every row regime, the device greedy loop, the GGUF lo
 synthesis, and Llama-3-8B Q4_K_M at full size.  Tolerance as tests/test_q8_gpu.py: the bf16 one, and
 2x the oracle's own deviation under 1e-6 relative input noise (Q8_K rounding is discontinuous).
 
-Other block types (Q4_0, F16 files): the engine dequantises every matrix at load
+Other block types (F16 files, mixes without a native path): the engine dequantises every matrix at load
 (dequant_bf16_kernel) and runs the bf16 path -- bit-identical to a BF16 file holding numpy's
-dequantisation of the same blocks, and close to the CPU oracle built from those bf16 weights."""
+dequantisation of the same blocks, and close to the CPU oracle built from those bf16 weights.  (Q4_0
+files run natively: tests/test_q4_0_gpu.py.)"""
 import numpy as np
 import pytest
 
@@ -40,7 +41,7 @@ def _oracle_from_gguf(oracle_mod, path, shape):
     return om
 
 
-@pytest.mark.parametrize("wtype", ["q4_0", "f16"])
+@pytest.mark.parametrize("wtype", ["f16"])
 def test_dequantised_file_equals_bf16_file_and_oracle(oracle_mod, tmp_path, wtype):
     from llama_p2p_amd import engine, gguf, synth
 
