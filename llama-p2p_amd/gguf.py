@@ -73,6 +73,25 @@ def quantize_q8_0(x: np.ndarray) -> np.ndarray:
     return out.reshape(x.shape[:-1] + (K // QK8_0 * Q8_0_BLOCK,))
 
 
+def quantize_q4_0(x: np.ndarray) -> np.ndarray:
+    """ggml quantize_row_q4_0_ref over rows of f32 [rows][K] -> block_q4_0 bytes [rows][K/32*18]:
+    d = (first value of largest magnitude) / -8, id = 1/d, q = min(15, (int8)(x*id + 8.5)), f32 steps."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    rows, K = x.shape
+    xb = x.reshape(rows, K // 32, 32)
+    idx = np.abs(xb).argmax(axis=2)
+    mx = np.take_along_axis(xb, idx[..., None], axis=2)[..., 0]
+    d = (mx / np.float32(-8)).astype(np.float32)
+    with np.errstate(divide="ignore"):
+        idv = np.where(d != 0, np.float32(1) / d, np.float32(0)).astype(np.float32)
+    v = ((xb * idv[..., None]).astype(np.float32) + np.float32(8.5)).astype(np.float32)
+    q = np.minimum(15, np.trunc(v).astype(np.int32)).astype(np.uint8)
+    out = np.empty((rows, K // 32, 18), np.uint8)
+    out[..., :2] = d.astype(np.float16).view(np.uint8).reshape(rows, K // 32, 2)
+    out[..., 2:] = q[..., :16] | (q[..., 16:] << 4)
+    return out.reshape(rows, K // 32 * 18)
+
+
 def dequantize_q8_0(blocks: np.ndarray, K: int) -> np.ndarray:
     """ggml dequantize_row_q8_0: y = q * f32(d)."""
     b = np.ascontiguousarray(blocks, dtype=np.uint8).reshape(-1, K // QK8_0, Q8_0_BLOCK)
@@ -448,7 +467,7 @@ def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = Non
     --token-embedding-type)."""
     from . import synth
 
-    if wtype not in ("bf16", "q8_0") and wtype not in MIXED:
+    if wtype not in ("bf16", "q8_0", "q4_0_synth") and wtype not in MIXED:
         raise ValueError(f"unknown wtype {wtype!r}")
     rng = np.random.default_rng(1000 + seed)
 
@@ -456,7 +475,7 @@ def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = Non
     w.add_string("general.architecture", "llama")
     w.add_string("general.name", f"synthetic-{shape.name}-seed{seed}")
     w.add_uint32("general.file_type", {"bf16": 32, "q8_0": 7, "q4_k_m": 15, "q5_k_m": 17, "q4_0": 2,
-                                        "f16": 1}[wtype])  # llama_ftype
+                                        "q4_0_synth": 2, "f16": 1}[wtype])  # llama_ftype
     w.add_uint32("llama.context_length", n_ctx_train or shape.n_ctx_train)
     w.add_uint32("llama.embedding_length", shape.n_embd)
     w.add_uint32("llama.block_count", shape.n_layer)
@@ -492,9 +511,12 @@ def write_synthetic_gguf(path: str, shape, seed: int = 0, n_ctx_train: int = Non
             y = dequantize(info["type"], src.tensor(name), arr.shape)
             w.add_tensor_info(name, arr.shape, GGML_BF16)
             arrays.append(synth.f32_to_bf16_bits(y))
-        elif kind == "bf16" and wtype == "q8_0":
+        elif kind == "bf16" and (wtype == "q8_0" or (wtype == "q4_0_synth" and name.count(".") == 1)):
             w.add_tensor_info(name, arr.shape, GGML_Q8_0)
             arrays.append(synth_q8_0_tensor(arr))
+        elif kind == "bf16" and wtype == "q4_0_synth":  # the engine's synthetic:<shape>:q4_0 model
+            w.add_tensor_info(name, arr.shape, GGML_Q4_0)
+            arrays.append(quantize_q4_0(synth.bf16_bits_to_f32(arr)))
         elif kind == "bf16" and wtype in synth.KQ_FTYPES:
             # llama.cpp's recipe types per tensor, the synthetic K-quant blocks of synth.kq_tensor
             # (the same bytes the engine's "synthetic:<shape>:<wtype>" model packs)

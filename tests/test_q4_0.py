@@ -95,3 +95,15 @@ def test_q4_0_dot_and_dequant(orc):
                                           (bl[i, 2:] >> 4).astype(np.float32) - 8]) * d[i] for i in range(len(bl))])
     assert np.array_equal(deq, ref)
     assert np.abs(deq - w).max() <= np.abs(w).max() / 8 + 1e-6  # within one step of the 4-bit grid
+
+
+def test_numpy_q4_0_quantiser_equals_oracle(orc):
+    """gguf.quantize_q4_0 (vectorised, writes the synthetic q4_0 GGUF) == the oracle's quantiser."""
+    from llama_p2p_amd.gguf import quantize_q4_0
+
+    rng = np.random.default_rng(2)
+    x = (rng.standard_normal((7, 32 * 8)) * 0.03).astype(np.float32)
+    x[3, 40] = -1.0
+    got = quantize_q4_0(x)
+    for r in range(x.shape[0]):
+        assert np.array_equal(got[r], orc.q4_0_quantize_row(x[r]))
