@@ -296,6 +296,48 @@ def tiny_bench(args):
     return out
 
 
+def geometry_bench(args, name: str = "llama2-7b", steps: int = 16):
+    """A non-Llama-3 geometry (Llama-2-7B: MHA, ff 11008, V 32000) at batch 1 and 32 rows: the
+    shape-specialised fast paths (row-tile-persistent GEMVs for K 2048/4096/8192 with Llama-3 tile
+    counts) do not apply to its gate/up (1376 tiles) and ffn_down (K 11008), so this measures the
+    generic GEMV fallbacks against the same HBM roofline."""
+    from llama_p2p_amd import synth
+    from llama_p2p_amd.engine import Engine
+
+    shape = synth.SHAPES[name]
+    M = args.seqs
+    eng = Engine(f"synthetic:{name}:seed=0", n_ctx=512, n_seq_max=M)
+    prompts = make_prompts(shape.n_vocab, M, lo=16, hi=128)
+    slots, pos, ids = [], [], []
+    for i, p in enumerate(prompts):
+        slots += [i] * (len(p) - 1)
+        pos += list(range(len(p) - 1))
+        ids += [int(t) for t in p[:-1]]
+    eng.forward_rows(slots, pos, ids, want_logits=False)
+    out = {"model": f"{name} bf16 (synthetic weights, seed 0)", "weight_bytes": int(eng.info.weight_bytes)}
+    for m in (1, M):
+        b = eng.batch(slots=list(range(m)), pos=[len(p) - 1 for p in prompts[:m]],
+                      ids=[int(p[-1]) for p in prompts[:m]], max_steps=steps + 2)
+        for _ in range(2):
+            b.step()
+        eng.sync()
+        t1 = time.perf_counter()
+        for _ in range(steps):
+            b.step()
+        eng.sync()
+        dt = (time.perf_counter() - t1) / steps
+        b.close()
+        ctx_sum = sum(len(p) + 2 + steps / 2 for p in prompts[:m])
+        by = eng.info.weight_bytes + ctx_sum * shape.kv_bytes_per_pos() + m * shape.n_vocab * 4
+        out[f"decode_M{m}"] = {"tok_s": round(m / dt, 2), "ms_per_step": round(dt * 1e3, 3),
+                               "hbm_frac": round(by / dt / 1e9 / HBM_PEAK_GBS, 4)}
+        us, wbytes = eng.profile_kernel(2, m, iters=2)
+        kb = wbytes + m * shape.n_embd * 2 + m * shape.n_ff * 2
+        out[f"gate_up_M{m}"] = {"us_per_launch": round(us, 2), "frac": round(kb / us / 1e3 / HBM_PEAK_GBS, 4)}
+    eng.close()
+    return out
+
+
 def big_bench(args):
     """BASELINE config 5's model on ONE MI355X (141 GB of bf16 weights fit in 288 GB): Llama-3-70B
     synthetic, batch-1 and M-sequence greedy decode tok/s against the HBM roofline, and its gate/up
@@ -536,6 +578,8 @@ def main():
     ap.add_argument("--tiny-tokens", type=int, default=128,
                     help="TinyLlama-1.1B batch-1 tokens (config 2; 0: skip the section)")
     ap.add_argument("--big-steps", type=int, default=8, help="Llama-3-70B decode steps (0: skip the section)")
+    ap.add_argument("--geometry-steps", type=int, default=16,
+                    help="Llama-2-7B-geometry decode steps (generic GEMV paths; 0: skip the section)")
     ap.add_argument("--serve-requests", type=int, default=32,
                     help="config 3 through the node's handler: concurrent requests (0: skip the section)")
     ap.add_argument("--budget", type=float, default=360.0,
@@ -592,6 +636,8 @@ def main():
         line["q4_k_m"] = sec.run("q4_k_m", lambda: quant_bench(args, "q4_k_m", args.kq_steps))
     if args.big_steps > 0:
         line["llama3_70b"] = sec.run("llama3_70b", lambda: big_bench(args))
+    if args.geometry_steps > 0:
+        line["llama2_7b_geometry"] = sec.run("llama2_7b_geometry", lambda: geometry_bench(args, steps=args.geometry_steps))
     line["section_seconds"] = sec.seconds
     print(json.dumps(line), flush=True)
 

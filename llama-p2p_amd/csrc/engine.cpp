@@ -69,6 +69,8 @@ const Shape kShapes[] = {
     {"test-70b-ffn", 8192, 1, 64, 8, 28672, 1024, 500000.f, 1e-5f, 2048},
     {"test-tiny-ffn", 2048, 1, 32, 4, 5632, 32000, 10000.f, 1e-5f, 2048},
     {"test-8b-v128k", 4096, 2, 32, 8, 14336, 128256, 500000.f, 1e-5f, 8192},
+    // a non-Llama-3 geometry (Llama-2-7B: MHA, ff 11008, V 32000): the generic GEMV fallbacks' cost
+    {"llama2-7b", 4096, 32, 32, 32, 11008, 32000, 10000.f, 1e-5f, 4096},
 };
 
 // decode steps the scheduler runs on the device between host syncs when every active row is greedy
@@ -191,9 +193,9 @@ struct mx_engine {
   int bos = 1, eos = 2;
   int n_ctx = 512, n_seq_max = 64, lb = 0, le = 0, device = 0;
   bool has_embed = true, has_head = true, use_graphs = true;
-  // <= 16 rows: RMS_NORM applied while loading the GEMV's B operand, from per-tile sums of squares
-  // written by the residual-stream producer (no norm launches); MX_NO_NORM_ON_LOAD=1 for A/B runs
-  bool norm_on_load = getenv("MX_NO_NORM_ON_LOAD") == nullptr;
+  // <= 4 rows: RMS_NORM applied while loading the GEMV's B operand, from per-tile sums of squares
+  // written by the residual-stream producer (no norm launches)
+  static constexpr bool norm_on_load = true;
   // gate/up as a row-tile-persistent GEMV with RMS_NORM on load (<= 4 rows); MX_NO_PERS=1 for A/B
   bool use_pers = getenv("MX_NO_PERS") == nullptr;
   bool q8_gemm_prefill = getenv("MX_Q8_GEMM_PREFILL") != nullptr;  // see enqueue_forward
@@ -204,7 +206,7 @@ struct mx_engine {
   // rows of the next forward come in blocks of 16 consecutive positions of one sequence (prefill):
   // attention runs as attn_prefill_kernel, 16 queries per K/V pass
   bool rows_blocked = false;
-  bool use_wide = getenv("MX_NO_WIDE") == nullptr;  // 17..64-row forward through mm_wide (LDS-shared activations)
+  static constexpr bool use_wide = true;  // 17..64-row forward through mm_wide (LDS-shared activations)
   float* slabs = nullptr;                           // split-K partials [8][MAX_ROWS][n_embd + 2 n_embd_kv]
   size_t slab_stride = 0;
   float* gslabs = nullptr;  // split-K partials of small-M prefill GEMMs, [S][M][N] (launch_gemm_split)
@@ -227,7 +229,7 @@ struct mx_engine {
   // rows, ggml_vec_dot_q4_0_q8_0); the head is Q8_0 / Q4_0 tiles (out_q4) or, as llama-quantize writes it,
   // a K-quant output (out_kq_head: kq_out segments, Q8_K activation rows)
   bool wq4 = false, out_q4 = false, out_kq_head = false;
-  bool q8_ql = getenv("MX_NO_Q8_QL") == nullptr;  // Q8_0 GEMVs of <= 4 rows quantise their operand on load
+  static constexpr bool q8_ql = true;  // Q8_0 GEMVs of <= 4 rows quantise their operand on load
   uint8_t* tok_embd8 = nullptr;
   // K-quant model (Q4_K / Q5_K / Q6_K matrices: llama.cpp's Q4_K_M / Q5_K_M; kquant.hip): packed
   // K-quant tiles, activations as Q8_K rows (q in xq8, d in xqd, sub-block sums in xkb)
@@ -315,11 +317,9 @@ struct mx_engine {
   bool q8_on_load(int M) const {
     return wq8 && q8_ql && mq8_can_quantize_on_load(M, n_embd, true) && mq8_can_quantize_on_load(M, n_ff, false);
   }
-  // one-token K-quant GEMVs quantise their Q8_K operand on load (no norm / quantise launches);
-  // MX_KQ_NO_QL=1: separate launches (A/B)
+  // one-token K-quant GEMVs quantise their Q8_K operand on load (no norm / quantise launches)
   bool kq_on_load(int M) const {
-    return wkq && getenv("MX_KQ_NO_QL") == nullptr && mkq_can_quantize_on_load(M, n_embd, true) &&
-           mkq_can_quantize_on_load(M, n_ff, false);
+    return wkq && mkq_can_quantize_on_load(M, n_embd, true) && mkq_can_quantize_on_load(M, n_ff, false);
   }
   int enqueue_forward_q8(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap, int n_out,
                          bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride, int* hist_count,
@@ -1164,13 +1164,11 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
   // <= 4 rows: every GEMV quantises its operand on load (RMS_NORM from the ssq partials the
   // residual writers leave); more rows: Q8_0 rows made once per GEMV by a norm / quantise launch
   const bool ql = q8_on_load(M);
-  static const int no_ql_mask = getenv("MX_Q8_NO_QL_MASK") ? atoi(getenv("MX_Q8_NO_QL_MASK")) : 0;  // probe
-  int site = 0;  // 1 qkv, 2 attn_output, 4 gate/up, 8 down, 16 lm_head
   // 17..32 rows: attn_output / ffn_down as split-K slabs (launch_mq8_slab) folded by the next
   // RMS_NORM + quantise launch; nslab = partials not yet folded into x
   int nslab = 0;
   auto operand = [&](MMArgs& m, const float* src, int K, const float* norm_w, int rows, const int* rmap) {
-    if (ql && !rmap && !(no_ql_mask & site)) {
+    if (ql && !rmap) {
       m.xq = nullptr; m.xf = src; m.norm_w = norm_w; m.eps = eps; m.ssq = norm_w ? ssq : nullptr; m.np = K / 16;
     } else {
       if (norm_w && src == x && nslab) {
@@ -1197,7 +1195,6 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     _Float16* vc = vcache + layer_kv_stride * li;
     MMArgs a{};
     a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M; a.wq4 = wq4;
-    site = 1;
     operand(a, x, h, L.attn_norm, M, nullptr);
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
     a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
@@ -1220,18 +1217,15 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     else launch_attention(at, s);
     MMArgs b{};
     b.W = L.o; b.N = h; b.K = h; b.M = M; b.out = x; b.ldo = h; b.wq4 = wq4;
-    site = 2;
     operand(b, attn_f, h, nullptr, M, nullptr);
     b.ssq = ql ? ssq : nullptr; b.np = h / 16;  // partials of the new residual for gate/up's norm
     if (resid(b)) return fail(MX_ERR_ARG, "q8 attn_output launch shape");
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.actf = act_f; c.lda = ff; c.wq4 = wq4;
-    site = 4;
     operand(c, x, h, L.ffn_norm, M, nullptr);
     if (launch_mq8(EPI_SWIGLU, c, s)) return fail(MX_ERR_ARG, "q8 gate/up launch shape");
     MMArgs d{};
     d.W = L.down; d.N = h; d.K = ff; d.M = M; d.out = x; d.ldo = h; d.wq4 = wq4;
-    site = 8;
     operand(d, act_f, ff, nullptr, M, nullptr);
     d.ssq = ql ? ssq : nullptr; d.np = h / 16;  // for the next layer's qkv (or lm_head) norm
     if (resid(d)) return fail(MX_ERR_ARG, "q8 ffn_down launch shape");
@@ -1246,7 +1240,6 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
     MMArgs g{};
     g.W = output; g.N = n_vocab; g.K = h; g.M = n_out; g.out = logits; g.ldo = n_vocab;
-    site = 16;
     if (out_kq_head) {  // K-quant output (Q4_0 files): Q8_K rows of the normed rows, ggml's q6_K.q8_K
       if (nslab) {
         launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);

@@ -633,28 +633,20 @@ static int launch_pers_cfg(const MMArgs& a, hipStream_t s) {
 }
 
 // Row-tile-persistent GEMVs for <= 16 tokens; -1 when the shape has no instantiation (callers
-// fall back to launch_mm).  gate/up: Llama-3-8B (K 4096, 1792 tiles = 256 x 7), -70B (K 8192,
-// 3584 = 256 x 14), TinyLlama (K 2048, 704 tiles = 235 groups x <= 3); attn_output / ffn_down of
-// h 4096 (one tile per group, whole K-slice in flight); lm_head (<= 32 / 8 tiles per group).
-static const bool pers_resid = getenv("MX_NO_PERS_RESID") == nullptr;  // attn_output / ffn_down too
-// lm_head with the output norm on load: correct but neutral at batch 1 (8B 2.804 vs 2.809 ms,
-// TinyLlama 0.750 vs 0.751; tools/gpu/pers_ab4.sh), so opt-in (MX_PERS_HEAD=1)
-static const bool pers_head = getenv("MX_PERS_HEAD") != nullptr;
-// q|k|v of Llama-3-8B (384 tiles: 1.5 rounds of mm_kernel work-groups) as 192 groups x 2 tiles
-// (MX_PERS_QKV=2, default), 128 x 3 (=3) or mm_kernel (=0); read per call (A/B across runs)
-static int qkv_pers_tpw() {
-  const char* v = getenv("MX_PERS_QKV");
-  return v ? atoi(v) : 2;
-}
-
+// fall back to launch_mm).  gate/up: K 4096 with 1025..1792 tiles (Llama-3-8B: 1792 = 256 x 7;
+// Llama-2-7B's ff 11008: 1376 = 230 x 6), K 8192 with 3584 (Llama-3-70B, 256 x 14), K 2048 with 704
+// (TinyLlama, 235 groups x <= 3); attn_output / ffn_down of h 4096 with K 4096 or 14336 (one tile per
+// group, whole K-slice in flight); q|k|v of Llama-3-8B (384 tiles as 192 groups x 2).  The tile-count
+// template (TPW, fully unrolled) and the K-slice per wave (NKW, the ring) are compile-time, so other
+// geometries take mm_kernel (measured: bench.py llama2_7b_geometry).  The lm_head as a persistent
+// GEMV with the output norm on load measured neutral at batch 1 (8B 2.804 vs 2.809 ms) and is not used.
 bool mm_pers_supported(int epi, int M, int N, int K) {
   if (M < 1 || M > 16) return false;
   const int nt = N / TILE_N;
-  if (epi == EPI_SWIGLU) return (K == 4096 && nt == 1792) || (K == 8192 && nt == 3584) || (K == 2048 && nt == 704);
-  if (epi == EPI_RESID && pers_resid)
-    return N == 4096 && (K == 4096 || K == 14336);
-  if (epi == EPI_F32 && pers_head) return (K == 4096 && nt <= 256 * 32) || (K == 2048 && nt <= 256 * 8);
-  if (epi == EPI_QKV) return K == 4096 && nt == 384 && qkv_pers_tpw() > 0;  // Llama-3-8B q|k|v
+  if (epi == EPI_SWIGLU)
+    return (K == 4096 && nt > 1024 && nt <= 1792) || (K == 8192 && nt == 3584) || (K == 2048 && nt == 704);
+  if (epi == EPI_RESID) return N == 4096 && (K == 4096 || K == 14336);
+  if (epi == EPI_QKV) return K == 4096 && nt == 384;  // Llama-3-8B q|k|v
   return false;
 }
 
@@ -662,18 +654,20 @@ int launch_mm_pers(int epi, const MMArgs& a, hipStream_t s) {
   if (!mm_pers_supported(epi, a.M, a.N, a.K)) return -1;
   const int ntiles = a.N / TILE_N;
   if (epi == EPI_SWIGLU) {
-    if (a.K == 4096 && ntiles == 1792) return launch_pers_cfg<16, 8, 7, EPI_SWIGLU, 8>(a, s);
+    if (a.K == 4096) {
+      switch ((ntiles + 255) / 256) {  // tiles per work-group
+        case 5: return launch_pers_cfg<16, 8, 5, EPI_SWIGLU, 8>(a, s);
+        case 6: return launch_pers_cfg<16, 8, 6, EPI_SWIGLU, 8>(a, s);
+        case 7: return launch_pers_cfg<16, 8, 7, EPI_SWIGLU, 8>(a, s);
+      }
+    }
     if (a.K == 8192 && ntiles == 3584) return launch_pers_cfg<16, 16, 14, EPI_SWIGLU, 4>(a, s);
     if (a.K == 2048 && ntiles == 704) return launch_pers_cfg<16, 4, 3, EPI_SWIGLU, 4>(a, s);
   } else if (epi == EPI_RESID) {
     if (a.K == 4096) return launch_pers_cfg<16, 8, 1, EPI_RESID, 8>(a, s);
     if (a.K == 14336) return launch_pers_cfg<16, 28, 1, EPI_RESID, 14>(a, s);
   } else if (epi == EPI_QKV) {
-    if (qkv_pers_tpw() == 3) return launch_pers_cfg<16, 8, 3, EPI_QKV, 8>(a, s);
     return launch_pers_cfg<16, 8, 2, EPI_QKV, 8>(a, s);
-  } else if (epi == EPI_F32) {
-    if (a.K == 4096) return launch_pers_cfg<16, 8, 32, EPI_F32, 8>(a, s);  // 8B: 251 groups
-    if (a.K == 2048) return launch_pers_cfg<16, 4, 8, EPI_F32, 4>(a, s);   // TinyLlama: 250 groups
   }
   return -1;
 }
@@ -687,22 +681,6 @@ int launch_mm(int epi, const MMArgs& a, hipStream_t s) {
   const int ntiles = a.N / TILE_N;
   const int nb = (a.M + 15) / 16;
   if (nb == 1 || a.X == nullptr) {
-    // RMS_NORM-on-load geometries under evaluation (tools/kernel_probe.py with MX_XS_CFG=n)
-    static const int xs_cfg = getenv("MX_XS_CFG") ? atoi(getenv("MX_XS_CFG")) : 0;
-    if (a.X == nullptr && xs_cfg) {
-      if (epi == EPI_SWIGLU && ntiles % 7 == 0) {
-        if (xs_cfg == 1) return launch_mm_cfg<8, 7, EPI_SWIGLU, 4>(a, s);
-        if (xs_cfg == 2) return launch_mm_cfg<16, 7, EPI_SWIGLU, 2>(a, s);
-        if (xs_cfg == 3) return launch_mm_cfg<8, 7, EPI_SWIGLU, 2>(a, s);
-        if (xs_cfg == 4) return launch_mm_cfg<16, 1, EPI_SWIGLU, 8>(a, s);
-      }
-      if (epi == EPI_QKV && ntiles % 3 == 0) {
-        if (xs_cfg == 1) return launch_mm_cfg<8, 1, EPI_QKV, 4>(a, s);
-        if (xs_cfg == 2) return launch_mm_cfg<8, 3, EPI_QKV, 4>(a, s);
-        if (xs_cfg == 3) return launch_mm_cfg<16, 3, EPI_QKV, 2>(a, s);
-        if (xs_cfg == 4) return launch_mm_cfg<16, 1, EPI_QKV, 8>(a, s);
-      }
-    }
     // (TinyLlama: deeper rings -- U = 11 for ffn_down, 8 for q|k|v and gate/up -- measured within
     // +-3 % of these, tools/gpu/r2ah.sh: the one-token launches there are latency-, not ring-bound)
     switch (epi) {

@@ -987,7 +987,7 @@ __global__ __launch_bounds__(64 * KS) void mkq_pers_seg_kernel(MMArgs a) {
 // one token, q|k|v of a K-quant file (K 4096: 16 super-blocks = 8 waves x 2): 2 tiles per
 // work-group (Llama-3-8B: 192 groups) quantising on load; -1 if the shape has no such form
 static int launch_kq_qkv_pers(const MMArgs& a, hipStream_t s) {
-  static const bool off = getenv("MX_NO_KQ_QKV_PERS") != nullptr;
+  constexpr bool off = false;
   if (off || a.M != 1 || a.xq != nullptr || a.K != 4096 || (a.N / TILE_N) % 2) return -1;
   for (int i = 0; i < a.kq_n; ++i)
     if (a.kq_tile_end[i] % 2) return -1;
@@ -1022,7 +1022,8 @@ static int launch_kq_pers_ty(const MMArgs& a, int ntiles, hipStream_t s) {
 
 static int launch_kq_pers(int epi, const MMArgs& a, int ntiles, hipStream_t s) {
   // MX_NO_KQ_PERS: the one-tile-per-work-group kernel (read per launch: tests compare the two)
-  if (getenv("MX_NO_KQ_PERS") || a.kq_n != 1 || a.M > 16) return -1;  // 17-32 rows (two column tiles): spills
+  static const bool off = getenv("MX_NO_KQ_PERS") != nullptr;  // tests: the grouped kernel's path
+  if (off || a.kq_n != 1 || a.M > 16) return -1;  // 17-32 rows (two column tiles): spills
   const int t = a.kq_type[0];
   auto by_nb = [&](auto nb) -> int {
     constexpr int NB = decltype(nb)::value;
@@ -1263,7 +1264,7 @@ static int launch_kq_wide(int epi, const MMArgs& a, int ntiles, hipStream_t s) {
 // RMS_NORM + Q8_K launch (launch_rmsnorm_q8k with slabs) folds into the residual stream in slab
 // order.  Returns the split, or -1 (the caller runs mkq_kernel's in-place EPI_RESID instead).
 int launch_mkq_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s) {
-  static const bool off = getenv("MX_NO_KQ_WIDE") != nullptr || getenv("MX_NO_KQ_SLAB") != nullptr;
+  static const bool off = getenv("MX_NO_KQ_WIDE") != nullptr;
   if (off || a.M <= 16 || a.M > 32 || a.kq_n != 1 || !a.xq || !a.xd || !a.xb || a.K % 256 || a.N % 64) return -1;
   const int ntiles = a.N / TILE_N, SB = a.K / 256;
   int ks = 1;
@@ -1285,7 +1286,7 @@ int launch_mkq_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipStream
 // partial slabs [2][token][N] that the decode attention (FIN) or launch_qkv_finish completes.
 // Returns the split or -1 (the caller runs mkq_kernel's EPI_QKV instead).
 int launch_mkq_qkv_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s) {
-  static const bool off = getenv("MX_NO_KQ_WIDE") != nullptr || getenv("MX_NO_KQ_SLAB") != nullptr;
+  static const bool off = getenv("MX_NO_KQ_WIDE") != nullptr;
   if (off || a.M <= 16 || a.M > 32 || !a.xq || !a.xd || !a.xb || a.K % 256 || a.N % 64) return -1;
   for (int i = 0; i < a.kq_n; ++i)
     if (a.kq_tile_end[i] % 4) return -1;

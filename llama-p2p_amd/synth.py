@@ -97,6 +97,8 @@ SHAPES = {
     # Llama-3-8B layers (2 of 32) with the full 128256-token vocabulary: the bench's lm_head / argmax /
     # top-k instantiations at the real width
     "test-8b-v128k": LlamaShape("test-8b-v128k", 4096, 2, 32, 8, 14336, 128256, 500000.0, 1e-5, 8192),
+    # a non-Llama-3 geometry (Llama-2-7B: multi-head attention, ff 11008): the generic GEMV paths
+    "llama2-7b": LlamaShape("llama2-7b", 4096, 32, 32, 32, 11008, 32000, 10000.0, 1e-5, 4096),
 }
 
 _M64 = (1 << 64) - 1
