@@ -198,7 +198,7 @@ def quant_bench(args, wtype: str, steps: int):
     shape = synth.SHAPES[args.model]
     M = args.seqs
     eng = Engine(f"synthetic:{args.model}:seed=0:{wtype}", n_ctx=args.n_ctx, n_seq_max=max(M, 1))
-    assert eng.info.weight_type == {"q8_0": 8, "q4_k_m": 12}[wtype]
+    assert eng.info.weight_type == {"q8_0": 8, "q4_k_m": 12, "q4_0": 2}[wtype]
     prompts = make_prompts(shape.n_vocab, M)
     slots, pos, ids = [], [], []
     for i, p in enumerate(prompts):
@@ -207,7 +207,8 @@ def quant_bench(args, wtype: str, steps: int):
         ids += [int(t) for t in p[:-1]]
     eng.forward_rows(slots, pos, ids, want_logits=False)
     desc = {"q8_0": "Q8_0 (quantisation of the same synthetic bf16 weights)",
-            "q4_k_m": "Q4_K_M (llama.cpp recipe types, synthetic K-quant blocks; native int8-MFMA K-quant path)"}
+            "q4_k_m": "Q4_K_M (llama.cpp recipe types, synthetic K-quant blocks; native int8-MFMA K-quant path)",
+            "q4_0": "Q4_0 layers (quantize_row_q4_0_ref of the same synthetic bf16 weights), Q8_0 embd/output"}
     out = {"model": f"{args.model} {desc[wtype]}", "weight_bytes": int(eng.info.weight_bytes)}
     b = eng.batch(slots=list(range(M)), pos=[len(p) - 1 for p in prompts], ids=[int(p[-1]) for p in prompts],
                   max_steps=4 + steps)
@@ -242,11 +243,12 @@ def quant_bench(args, wtype: str, steps: int):
     h = shape.n_embd
     for m in (1, M):
         us, wbytes = eng.profile_kernel(2, m, iters=3)
-        if wtype == "q8_0":
+        if wtype in ("q8_0", "q4_0"):
             kb = wbytes + m * h + m * h // 8 + m * shape.n_ff * 4   # int8 rows + scales in, f32 act out
         else:
             kb = wbytes + m * h + m * h // 64 + m * h // 8 + m * shape.n_ff * 4  # Q8_K rows, d, sub-block sums
         kname = {"q8_0": "mq8_kernel" if m <= 16 else "mq8_wide_kernel",
+                 "q4_0": "mq8_kernel<Q4>" if m <= 16 else "mq8_wide_kernel<Q4>",
                  "q4_k_m": "mkq_pers_kernel" if m <= 16 else "mkq_wide_kernel"}[wtype]
         out[f"gate_up_M{m}"] = {"kernel": kname + "<EPI_SWIGLU>",
                                 "us_per_launch": round(us, 2), "bytes_per_launch": int(kb),
@@ -575,6 +577,7 @@ def main():
     ap.add_argument("--prefill-len", type=int, default=128)
     ap.add_argument("--q8-steps", type=int, default=32, help="Q8_0 decode steps (0: skip the Q8_0 section)")
     ap.add_argument("--kq-steps", type=int, default=32, help="Q4_K_M decode steps (0: skip the Q4_K_M section)")
+    ap.add_argument("--q40-steps", type=int, default=32, help="Q4_0 decode steps (0: skip the Q4_0 section)")
     ap.add_argument("--tiny-tokens", type=int, default=128,
                     help="TinyLlama-1.1B batch-1 tokens (config 2; 0: skip the section)")
     ap.add_argument("--big-steps", type=int, default=8, help="Llama-3-70B decode steps (0: skip the section)")
@@ -634,6 +637,8 @@ def main():
         line["q8_0"] = sec.run("q8_0", lambda: quant_bench(args, "q8_0", args.q8_steps))
     if args.kq_steps > 0:
         line["q4_k_m"] = sec.run("q4_k_m", lambda: quant_bench(args, "q4_k_m", args.kq_steps))
+    if args.q40_steps > 0:
+        line["q4_0"] = sec.run("q4_0", lambda: quant_bench(args, "q4_0", args.q40_steps))
     if args.big_steps > 0:
         line["llama3_70b"] = sec.run("llama3_70b", lambda: big_bench(args))
     if args.geometry_steps > 0:

@@ -1975,18 +1975,21 @@ __global__ void pack_q4_kernel(uint8_t* dst, const uint8_t* src, int N, int K, i
 }
 
 // ggml quantize_row_q4_0_ref: d = (the value of largest magnitude) / -8, q = min(15, (int8)(x / d + 8.5))
-// with x / d as x * (1 / d); no contraction (the oracle's C does the same operations)
+// with x / d as x * (1 / d); no contraction (the oracle's C does the same operations: the pragma covers
+// only operators written here -- HIP's __fmul_rn / __fadd_rn carry the header's contract flag and fuse)
 __device__ __forceinline__ void q4_quant_ref(const float (&v)[32], uint16_t& dbits, uint8_t (&q)[32]) {
+#pragma clang fp contract(off)
   float amax = 0.f, mx = 0.f;
 #pragma unroll
   for (int j = 0; j < 32; ++j)
     if (amax < fabsf(v[j])) amax = fabsf(v[j]), mx = v[j];
-  const float d = __fdiv_rn(mx, -8.0f);
-  const float id = d != 0.f ? __fdiv_rn(1.0f, d) : 0.0f;
+  const float d = mx / -8.0f;
+  const float id = d != 0.f ? 1.0f / d : 0.0f;
   dbits = __builtin_bit_cast(uint16_t, (_Float16)d);
 #pragma unroll
   for (int j = 0; j < 32; ++j) {
-    const int qi = (int)(int8_t)__fadd_rn(__fmul_rn(v[j], id), 8.5f);
+    const float t = v[j] * id;
+    const int qi = (int)(int8_t)(t + 8.5f);
     q[j] = (uint8_t)min(15, qi);
   }
 }

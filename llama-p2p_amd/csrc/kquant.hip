@@ -745,49 +745,58 @@ __device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int 
   };
   auto compute = [&](const Frag& f) { kq_compute<T, RT, NB>(acc, f, g); };
 
-  Frag ring[U];
-  int sb = kb;
-  const int nfull = (ke - kb) / U;
-  QlRegs qr;
-  if constexpr (QL) ql_load(qr, a, kb, ke - kb, lane);
-  if (nfull > 0) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if constexpr (QL) {
-        const uint8_t* Wt[RT];
-#pragma unroll
-        for (int r = 0; r < RT; ++r) Wt[r] = Wr[r] + (size_t)(sb + u) * TB;
-        kq_load_w<T, RT, NB>(ring[u], Wt, lane, g);
-      } else {
-        load(ring[u], sb + u);
-      }
-    }
-  }
   if constexpr (QL) {
-    ql_build(qr, a, ke - kb, lane, iq, id, ib);
+    // one token: at most QL_SB_MAX super-blocks per wave, unrolled with wave-uniform guards; the
+    // ring holds the weight parts, the activations come from the LDS image one position ahead
+    const int n = ke - kb;
+    auto load_w = [&](Frag& f, int sb) {
+      const uint8_t* Wt[RT];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) Wt[r] = Wr[r] + (size_t)sb * TB;
+      kq_load_w<T, RT, NB>(f, Wt, lane, g);
+    };
+    Frag ring[U];
+    QlRegs qr;
+    ql_load(qr, a, kb, n, lane);
+#pragma unroll
+    for (int f = 0; f < U; ++f)
+      if (f < n) load_w(ring[f], kb + f);
+    ql_build(qr, a, n, lane, iq, id, ib);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
     __builtin_amdgcn_wave_barrier();
-    if (nfull > 0)
+    if (n > 0) kq_load_x<T, RT, NB>(ring[0], Xq, Xd, Xb, kb);
 #pragma unroll
-      for (int u = 0; u < U; ++u) kq_load_x<T, RT, NB>(ring[u], Xq, Xd, Xb, sb + u);
-  }
-  if (nfull > 0) {
-    for (int ch = 1; ch < nfull; ++ch) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        compute(ring[u]);
-        load(ring[u], sb + U + u);
+    for (int f = 0; f < QL_SB_MAX; ++f) {
+      if (f < n) {
+        compute(ring[f % U]);
+        if (f + U < n) load_w(ring[f % U], kb + f + U);
+        if (f + 1 < n) kq_load_x<T, RT, NB>(ring[(f + 1) % U], Xq, Xd, Xb, kb + f + 1);
       }
+    }
+  } else {
+    Frag ring[U];
+    int sb = kb;
+    const int nfull = (ke - kb) / U;
+    if (nfull > 0) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) load(ring[u], sb + u);
+      for (int ch = 1; ch < nfull; ++ch) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          compute(ring[u]);
+          load(ring[u], sb + U + u);
+        }
+        sb += U;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) compute(ring[u]);
       sb += U;
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) compute(ring[u]);
-    sb += U;
-  }
-  for (; sb < ke; ++sb) {
-    Frag f;
-    load(f, sb);
-    compute(f);
+    for (; sb < ke; ++sb) {
+      Frag f;
+      load(f, sb);
+      compute(f);
+    }
   }
 
 #pragma unroll
@@ -926,11 +935,14 @@ __device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Ws
     }
   };
 
-  Frag ring[U];
+  // QL: the ring holds the weight parts only; each position's activations come from the wave's LDS
+  // image one position ahead (they would otherwise hold U x 19 VGPRs, which is what bounded U)
+  constexpr int NF = TPW * NKW, UR = U < NF ? U : NF;
+  Frag ring[UR];
   QlRegs qr;
   if constexpr (QL) ql_load(qr, a, kb, NKW, lane);  // once per work-group: the slice is the same for every tile
 #pragma unroll
-  for (int f = 0; f < U; ++f) {
+  for (int f = 0; f < UR; ++f) {
     if constexpr (QL) load_w(ring[f], f);
     else load(ring[f], f);
   }
@@ -938,8 +950,7 @@ __device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Ws
     ql_build(qr, a, NKW, lane, iq, id, ib);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
     __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int f = 0; f < U; ++f) kq_load_x<T, 1, NB>(ring[f], Xq, Xd, Xb, kb + f % NKW);
+    kq_load_x<T, 1, NB>(ring[0], Xq, Xd, Xb, kb);
   }
   // fully unrolled over the TPW tiles (a loop back-edge renames the ring with moves that wait for
   // the loads, draining it)
@@ -951,8 +962,13 @@ __device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Ws
 #pragma unroll
     for (int k = 0; k < NKW; ++k) {
       const int f = i * NKW + k;
-      kq_compute<T, 1, NB>(acc, ring[f % U], g);
-      if (f + U < TPW * NKW) load(ring[f % U], f + U);
+      kq_compute<T, 1, NB>(acc, ring[f % UR], g);
+      if (f + UR < NF) {
+        if constexpr (QL) load_w(ring[f % UR], f + UR);
+        else load(ring[f % UR], f + UR);
+      }
+      if constexpr (QL)
+        if (f + 1 < NF) kq_load_x<T, 1, NB>(ring[(f + 1) % UR], Xq, Xd, Xb, kb + (f + 1) % NKW);
     }
 #pragma unroll
     for (int n = 0; n < NB; ++n) red[i & 1][w][n][lane] = acc[0][n];
@@ -984,6 +1000,8 @@ __global__ __launch_bounds__(64 * KS) void mkq_pers_seg_kernel(MMArgs a) {
   }
 }
 
+constexpr int KQ_UQ = 4;  // one-token ring depth (weight parts only; Q6_K's larger scale part: 3)
+
 // one token, q|k|v of a K-quant file (K 4096: 16 super-blocks = 8 waves x 2): 2 tiles per
 // work-group (Llama-3-8B: 192 groups) quantising on load; -1 if the shape has no such form
 static int launch_kq_qkv_pers(const MMArgs& a, hipStream_t s) {
@@ -991,15 +1009,17 @@ static int launch_kq_qkv_pers(const MMArgs& a, hipStream_t s) {
   if (off || a.M != 1 || a.xq != nullptr || a.K != 4096 || (a.N / TILE_N) % 2) return -1;
   for (int i = 0; i < a.kq_n; ++i)
     if (a.kq_tile_end[i] % 2) return -1;
-  mkq_pers_seg_kernel<8, 2, 2, EPI_QKV, 2><<<a.N / TILE_N / 2, 512, 8 * QL_WAVE_BYTES, s>>>(a);
+  mkq_pers_seg_kernel<8, 2, 2, EPI_QKV, KQ_UQ><<<a.N / TILE_N / 2, 512, 8 * QL_WAVE_BYTES, s>>>(a);
   return 0;
 }
 
-template <int T, int NKW, int TPW, int NB, int EPI, int U>
+// U: ring depth with activations in the ring (2..16 tokens); one token (QL) keeps only the weight
+// parts in flight and runs UQ deep
+template <int T, int NKW, int TPW, int NB, int EPI, int U, int UQ>
 static void launch_kq_pers_t(const MMArgs& a, int ntiles, hipStream_t s) {
   const int grid = (ntiles + TPW - 1) / TPW;
   if (a.xq == nullptr)
-    mkq_pers_kernel<T, 8, NKW, TPW, NB, EPI, U, true><<<grid, 512, 8 * QL_WAVE_BYTES, s>>>(a);
+    mkq_pers_kernel<T, 8, NKW, TPW, NB, EPI, UQ, true><<<grid, 512, 8 * QL_WAVE_BYTES, s>>>(a);
   else
     mkq_pers_kernel<T, 8, NKW, TPW, NB, EPI, U, false><<<grid, 512, 0, s>>>(a);
 }
@@ -1011,11 +1031,11 @@ template <int T, int NB, int EPI>
 static int launch_kq_pers_ty(const MMArgs& a, int ntiles, hipStream_t s) {
   const int SB = a.K / 256;
   if constexpr (EPI == EPI_SWIGLU) {
-    if (SB == 16 && ntiles == 1792) return launch_kq_pers_t<T, 2, 7, NB, EPI, 2>(a, ntiles, s), 0;
-    if (SB == 8 && ntiles == 704) return launch_kq_pers_t<T, 1, 3, NB, EPI, 2>(a, ntiles, s), 0;
+    if (SB == 16 && ntiles == 1792) return launch_kq_pers_t<T, 2, 7, NB, EPI, 2, T == 14 ? 3 : KQ_UQ>(a, ntiles, s), 0;
+    if (SB == 8 && ntiles == 704) return launch_kq_pers_t<T, 1, 3, NB, EPI, 2, T == 14 ? 3 : KQ_UQ>(a, ntiles, s), 0;
   } else {
-    if (SB == 16 && ntiles > 256 * 8) return launch_kq_pers_t<T, 2, 8, NB, EPI, 2>(a, ntiles, s), 0;  // 16: spills
-    if (SB == 8 && ntiles > 256 * 4) return launch_kq_pers_t<T, 1, 8, NB, EPI, 2>(a, ntiles, s), 0;
+    if (SB == 16 && ntiles > 256 * 8) return launch_kq_pers_t<T, 2, 8, NB, EPI, 2, T == 14 ? 3 : KQ_UQ>(a, ntiles, s), 0;  // 16: spills
+    if (SB == 8 && ntiles > 256 * 4) return launch_kq_pers_t<T, 1, 8, NB, EPI, 2, T == 14 ? 3 : KQ_UQ>(a, ntiles, s), 0;
   }
   return -1;
 }
@@ -1045,7 +1065,7 @@ static int launch_kq_pers(int epi, const MMArgs& a, int ntiles, hipStream_t s) {
 template <int EPI>
 static void launch_mkq_epi(const MMArgs& a, int ntiles, hipStream_t s) {
   if (a.xq == nullptr) {  // one token, quantised on load (launch_mkq checked the slice fits)
-    mkq_kernel<8, 1, 1, EPI, 2, true><<<dim3(ntiles, 1), 512, 8 * QL_WAVE_BYTES, s>>>(a);
+    mkq_kernel<8, 1, 1, EPI, 3, true><<<dim3(ntiles, 1), 512, 8 * QL_WAVE_BYTES, s>>>(a);  // ring 3: 4 spills
   } else if (a.M <= 16) {
     mkq_kernel<8, 1, 1, EPI, 2, false><<<dim3(ntiles, 1), 512, 0, s>>>(a);
   } else if (a.M <= 32) {  // (a 2-deep ring spills ~460 B/lane at two column tiles: U = 1)
