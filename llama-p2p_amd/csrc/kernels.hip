@@ -272,19 +272,23 @@ struct XsRegs {
   f32x4 q[MM][2], x[MM][2], g[2];
 };
 
+// Every load is unconditional, at a clamped address (lanes / rows past the end re-read valid data
+// that xs_build ignores): a load behind a branch left hipcc's wait counts at the merge at zero, and
+// each conditional load then waited for itself -- up to 2 + 4·MM serialised L2 round trips before
+// the weight ring was even issued.
 template <int MM>
 __device__ __forceinline__ void xs_load(XsRegs<MM>& r, const MMArgs& a, int kbase, int nk, int lane) {
   const int i0 = lane * 4;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     const int i = i0 + 256 * p;
-    if (i < nk) r.g[p] = *reinterpret_cast<const f32x4*>(a.norm_w + kbase + i);
+    const int ik = min(i, nk - 4), iq = min(i, a.np - 4);
+    r.g[p] = *reinterpret_cast<const f32x4*>(a.norm_w + kbase + ik);
 #pragma unroll
     for (int c = 0; c < MM; ++c) {
-      if (c < a.M) {
-        if (i < a.np) r.q[c][p] = *reinterpret_cast<const f32x4*>(a.ssq + (size_t)c * a.np + i);
-        if (i < nk) r.x[c][p] = *reinterpret_cast<const f32x4*>(a.xf + (size_t)c * a.K + kbase + i);
-      }
+      const size_t cc = (size_t)min(c, a.M - 1);
+      r.q[c][p] = *reinterpret_cast<const f32x4*>(a.ssq + cc * a.np + iq);
+      r.x[c][p] = *reinterpret_cast<const f32x4*>(a.xf + cc * a.K + kbase + ik);
     }
   }
 }
@@ -635,18 +639,24 @@ static int launch_pers_cfg(const MMArgs& a, hipStream_t s) {
 // Row-tile-persistent GEMVs for <= 16 tokens; -1 when the shape has no instantiation (callers
 // fall back to launch_mm).  gate/up: K 4096 with 1025..1792 tiles (Llama-3-8B: 1792 = 256 x 7;
 // Llama-2-7B's ff 11008: 1376 = 230 x 6), K 8192 with 3584 (Llama-3-70B, 256 x 14), K 2048 with 704
-// (TinyLlama, 235 groups x <= 3); attn_output / ffn_down of h 4096 with K 4096 or 14336 (one tile per
-// group, whole K-slice in flight); q|k|v of Llama-3-8B (384 tiles as 192 groups x 2).  The tile-count
-// template (TPW, fully unrolled) and the K-slice per wave (NKW, the ring) are compile-time, so other
-// geometries take mm_kernel (measured: bench.py llama2_7b_geometry).  The lm_head as a persistent
+// (TinyLlama, 235 groups x <= 3); attn_output / ffn_down of h 4096 with K 4096 or 14336 and of
+// TinyLlama's h 2048 (one tile per group, whole K-slice in flight); q|k|v of Llama-3-8B (384 tiles as
+// 192 groups x 2), TinyLlama (160 x 1) and Llama-3-70B (640 as 214 x 3).  The tile-count template
+// (TPW, fully unrolled) and the K-slice per wave (NKW, the ring) are compile-time; mm_kernel's K loop
+// has a run-time trip count, and hipcc renames its ring across the back-edge with moves that wait for
+// the loads (1-3 of its 4-deep ring in flight).  Other geometries take mm_kernel (measured: bench.py
+// llama2_7b_geometry).  70B: attn_output's 16 B fragments per wave spill at 16 waves, ffn_down's 56
+// do not fit.  The lm_head as a persistent
 // GEMV with the output norm on load measured neutral at batch 1 (8B 2.804 vs 2.809 ms) and is not used.
 bool mm_pers_supported(int epi, int M, int N, int K) {
   if (M < 1 || M > 16) return false;
   const int nt = N / TILE_N;
   if (epi == EPI_SWIGLU)
     return (K == 4096 && nt > 1024 && nt <= 1792) || (K == 8192 && nt == 3584) || (K == 2048 && nt == 704);
-  if (epi == EPI_RESID) return N == 4096 && (K == 4096 || K == 14336);
-  if (epi == EPI_QKV) return K == 4096 && nt == 384;  // Llama-3-8B q|k|v
+  if (epi == EPI_RESID)
+    return (N == 4096 && (K == 4096 || K == 14336)) || (N == 2048 && (K == 2048 || K == 5632));
+  if (epi == EPI_QKV)  // q|k|v of Llama-3-8B, TinyLlama, Llama-3-70B
+    return (K == 4096 && nt == 384) || (K == 2048 && nt == 160) || (K == 8192 && nt == 640);
   return false;
 }
 
@@ -664,10 +674,14 @@ int launch_mm_pers(int epi, const MMArgs& a, hipStream_t s) {
     if (a.K == 8192 && ntiles == 3584) return launch_pers_cfg<16, 16, 14, EPI_SWIGLU, 4>(a, s);
     if (a.K == 2048 && ntiles == 704) return launch_pers_cfg<16, 4, 3, EPI_SWIGLU, 4>(a, s);
   } else if (epi == EPI_RESID) {
-    if (a.K == 4096) return launch_pers_cfg<16, 8, 1, EPI_RESID, 8>(a, s);
-    if (a.K == 14336) return launch_pers_cfg<16, 28, 1, EPI_RESID, 14>(a, s);
+    if (a.N == 4096 && a.K == 4096) return launch_pers_cfg<16, 8, 1, EPI_RESID, 8>(a, s);
+    if (a.N == 4096 && a.K == 14336) return launch_pers_cfg<16, 28, 1, EPI_RESID, 14>(a, s);
+    if (a.N == 2048 && a.K == 2048) return launch_pers_cfg<16, 4, 1, EPI_RESID, 4>(a, s);
+    if (a.N == 2048 && a.K == 5632) return launch_pers_cfg<16, 11, 1, EPI_RESID, 11>(a, s);
   } else if (epi == EPI_QKV) {
-    return launch_pers_cfg<16, 8, 2, EPI_QKV, 8>(a, s);
+    if (a.K == 4096) return launch_pers_cfg<16, 8, 2, EPI_QKV, 8>(a, s);
+    if (a.K == 2048) return launch_pers_cfg<16, 4, 1, EPI_QKV, 4>(a, s);
+    if (a.K == 8192) return launch_pers_cfg<16, 16, 3, EPI_QKV, 4>(a, s);
   }
   return -1;
 }
@@ -2381,23 +2395,25 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
   f32x4 xv[QMn][QPn], gv[QPn], sv[QMn][2];
   const int nk = (ke - kb) * Q8_TILE_K, kbase = kb * Q8_TILE_K;
   if constexpr (QP > 0) {
+    // unconditional loads at clamped addresses (values past the slice / rows are never used): a
+    // branch around any of them leaves the compiler's wait counts at the merge conservative, and the
+    // image build below then waited for the whole weight ring (vmcnt(0)) instead of these loads
+    const float* gsrc = a.norm_w ? a.norm_w : a.xf;
 #pragma unroll
     for (int p = 0; p < QP; ++p) {
-      const int i = lane * 4 + 256 * p;
-      if (i < nk) {
-        if (a.norm_w) gv[p] = *reinterpret_cast<const f32x4*>(a.norm_w + kbase + i);
-#pragma unroll
-        for (int c = 0; c < QM; ++c)
-          if (c < a.M) xv[c][p] = *reinterpret_cast<const f32x4*>(a.xf + (size_t)c * a.K + kbase + i);
-      }
-    }
-    if (a.norm_w)
+      const int i = min(lane * 4 + 256 * p, nk - 4);
+      gv[p] = *reinterpret_cast<const f32x4*>(gsrc + kbase + i);
 #pragma unroll
       for (int c = 0; c < QM; ++c)
+        xv[c][p] = *reinterpret_cast<const f32x4*>(a.xf + (size_t)min(c, a.M - 1) * a.K + kbase + i);
+    }
+    const float* ssrc = a.norm_w ? a.ssq : a.xf;
+    const int np = a.norm_w ? a.np : 4;
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
-          if (c < a.M && lane * 4 + 256 * p < a.np)
-            sv[c][p] = *reinterpret_cast<const f32x4*>(a.ssq + (size_t)c * a.np + lane * 4 + 256 * p);
+    for (int c = 0; c < QM; ++c)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        sv[c][p] = *reinterpret_cast<const f32x4*>(ssrc + (size_t)min(c, a.M - 1) * np + min(lane * 4 + 256 * p, np - 4));
   }
 
   // one ring slot = one 64-k tile: RT weight tiles (int8 operands + scales) and, from global
@@ -2459,10 +2475,8 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
   Frag ring[U];
   int kt = kb;
   const int nfull = (ke - kb) / U;
-  if (nfull > 0) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) load_w(ring[u], kt + u);
-  }
+  for (int u = 0; u < U; ++u) load_w(ring[u], min(kt + u, ke - 1));  // unconditional (see xs_load); unused when nfull == 0
   if constexpr (QP > 0) {  // build the image while the ring is in flight
 #pragma unroll
     for (int c = 0; c < QM; ++c) {

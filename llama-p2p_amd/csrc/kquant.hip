@@ -526,24 +526,25 @@ __device__ __forceinline__ void kq_load(KqFrag<RT, NB>& f, const uint8_t* const 
 struct QlRegs {
   f32x4 x[2][4], w[2][4], sq[2];
 };
+// every load unconditional at a clamped address (ql_build ignores the extra values): a load behind a
+// branch left hipcc's wait counts at the merge at zero, serialising the prologue (xs_load's note)
 __device__ __forceinline__ void ql_load(QlRegs& r, const MMArgs& a, int kb, int nsb, int lane) {
   const int t = lane & 15, rr = lane >> 4;
+  const float* wsrc = a.norm_w ? a.norm_w : a.xf;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    const int it = rr + 4 * q;
-    if (it < nsb) {
-      const size_t k0 = (size_t)(kb + it) * 256 + 16 * t;
+    const int it = min(rr + 4 * q, nsb - 1);
+    const size_t k0 = (size_t)(kb + it) * 256 + 16 * t;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        r.x[q][i] = *reinterpret_cast<const f32x4*>(a.xf + k0 + 4 * i);
-        if (a.norm_w) r.w[q][i] = *reinterpret_cast<const f32x4*>(a.norm_w + k0 + 4 * i);
-      }
+    for (int i = 0; i < 4; ++i) {
+      r.x[q][i] = *reinterpret_cast<const f32x4*>(a.xf + k0 + 4 * i);
+      r.w[q][i] = *reinterpret_cast<const f32x4*>(wsrc + k0 + 4 * i);
     }
   }
-  if (a.norm_w)
+  const float* qsrc = a.norm_w ? a.ssq : a.xf;
+  const int np = a.norm_w ? a.np : 4;
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
-      if (lane * 4 + 256 * p < a.np) r.sq[p] = *reinterpret_cast<const f32x4*>(a.ssq + lane * 4 + 256 * p);
+  for (int p = 0; p < 2; ++p) r.sq[p] = *reinterpret_cast<const f32x4*>(qsrc + min(lane * 4 + 256 * p, np - 4));
 }
 __device__ __forceinline__ void ql_build(const QlRegs& r, const MMArgs& a, int nsb, int lane, int8_t* iq, float* id,
                                          float* ib) {
@@ -745,58 +746,49 @@ __device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int 
   };
   auto compute = [&](const Frag& f) { kq_compute<T, RT, NB>(acc, f, g); };
 
+  Frag ring[U];
+  int sb = kb;
+  const int nfull = (ke - kb) / U;
+  QlRegs qr;
+  if constexpr (QL) ql_load(qr, a, kb, ke - kb, lane);
+  if (nfull > 0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (QL) {
+        const uint8_t* Wt[RT];
+#pragma unroll
+        for (int r = 0; r < RT; ++r) Wt[r] = Wr[r] + (size_t)(sb + u) * TB;
+        kq_load_w<T, RT, NB>(ring[u], Wt, lane, g);
+      } else {
+        load(ring[u], sb + u);
+      }
+    }
+  }
   if constexpr (QL) {
-    // one token: at most QL_SB_MAX super-blocks per wave, unrolled with wave-uniform guards; the
-    // ring holds the weight parts, the activations come from the LDS image one position ahead
-    const int n = ke - kb;
-    auto load_w = [&](Frag& f, int sb) {
-      const uint8_t* Wt[RT];
-#pragma unroll
-      for (int r = 0; r < RT; ++r) Wt[r] = Wr[r] + (size_t)sb * TB;
-      kq_load_w<T, RT, NB>(f, Wt, lane, g);
-    };
-    Frag ring[U];
-    QlRegs qr;
-    ql_load(qr, a, kb, n, lane);
-#pragma unroll
-    for (int f = 0; f < U; ++f)
-      if (f < n) load_w(ring[f], kb + f);
-    ql_build(qr, a, n, lane, iq, id, ib);
+    ql_build(qr, a, ke - kb, lane, iq, id, ib);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
     __builtin_amdgcn_wave_barrier();
-    if (n > 0) kq_load_x<T, RT, NB>(ring[0], Xq, Xd, Xb, kb);
+    if (nfull > 0)
 #pragma unroll
-    for (int f = 0; f < QL_SB_MAX; ++f) {
-      if (f < n) {
-        compute(ring[f % U]);
-        if (f + U < n) load_w(ring[f % U], kb + f + U);
-        if (f + 1 < n) kq_load_x<T, RT, NB>(ring[(f + 1) % U], Xq, Xd, Xb, kb + f + 1);
+      for (int u = 0; u < U; ++u) kq_load_x<T, RT, NB>(ring[u], Xq, Xd, Xb, sb + u);
+  }
+  if (nfull > 0) {
+    for (int ch = 1; ch < nfull; ++ch) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        compute(ring[u]);
+        load(ring[u], sb + U + u);
       }
-    }
-  } else {
-    Frag ring[U];
-    int sb = kb;
-    const int nfull = (ke - kb) / U;
-    if (nfull > 0) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) load(ring[u], sb + u);
-      for (int ch = 1; ch < nfull; ++ch) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          compute(ring[u]);
-          load(ring[u], sb + U + u);
-        }
-        sb += U;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) compute(ring[u]);
       sb += U;
     }
-    for (; sb < ke; ++sb) {
-      Frag f;
-      load(f, sb);
-      compute(f);
-    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) compute(ring[u]);
+    sb += U;
+  }
+  for (; sb < ke; ++sb) {
+    Frag f;
+    load(f, sb);
+    compute(f);
   }
 
 #pragma unroll
@@ -935,14 +927,11 @@ __device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Ws
     }
   };
 
-  // QL: the ring holds the weight parts only; each position's activations come from the wave's LDS
-  // image one position ahead (they would otherwise hold U x 19 VGPRs, which is what bounded U)
-  constexpr int NF = TPW * NKW, UR = U < NF ? U : NF;
-  Frag ring[UR];
+  Frag ring[U];
   QlRegs qr;
   if constexpr (QL) ql_load(qr, a, kb, NKW, lane);  // once per work-group: the slice is the same for every tile
 #pragma unroll
-  for (int f = 0; f < UR; ++f) {
+  for (int f = 0; f < U; ++f) {
     if constexpr (QL) load_w(ring[f], f);
     else load(ring[f], f);
   }
@@ -950,7 +939,8 @@ __device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Ws
     ql_build(qr, a, NKW, lane, iq, id, ib);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
     __builtin_amdgcn_wave_barrier();
-    kq_load_x<T, 1, NB>(ring[0], Xq, Xd, Xb, kb);
+#pragma unroll
+    for (int f = 0; f < U; ++f) kq_load_x<T, 1, NB>(ring[f], Xq, Xd, Xb, kb + f % NKW);
   }
   // fully unrolled over the TPW tiles (a loop back-edge renames the ring with moves that wait for
   // the loads, draining it)
@@ -962,13 +952,11 @@ __device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Ws
 #pragma unroll
     for (int k = 0; k < NKW; ++k) {
       const int f = i * NKW + k;
-      kq_compute<T, 1, NB>(acc, ring[f % UR], g);
-      if (f + UR < NF) {
-        if constexpr (QL) load_w(ring[f % UR], f + UR);
-        else load(ring[f % UR], f + UR);
-      }
-      if constexpr (QL)
-        if (f + 1 < NF) kq_load_x<T, 1, NB>(ring[(f + 1) % UR], Xq, Xd, Xb, kb + (f + 1) % NKW);
+      kq_compute<T, 1, NB>(acc, ring[f % U], g);
+      if (f + U < TPW * NKW) load(ring[f % U], f + U);
+      // issue the refill here: left to itself the scheduler sinks a tile's refills below its last
+      // compute, which then waits for vmcnt(0) (the ring empty once per tile)
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int n = 0; n < NB; ++n) red[i & 1][w][n][lane] = acc[0][n];
@@ -1000,8 +988,6 @@ __global__ __launch_bounds__(64 * KS) void mkq_pers_seg_kernel(MMArgs a) {
   }
 }
 
-constexpr int KQ_UQ = 4;  // one-token ring depth (weight parts only; Q6_K's larger scale part: 3)
-
 // one token, q|k|v of a K-quant file (K 4096: 16 super-blocks = 8 waves x 2): 2 tiles per
 // work-group (Llama-3-8B: 192 groups) quantising on load; -1 if the shape has no such form
 static int launch_kq_qkv_pers(const MMArgs& a, hipStream_t s) {
@@ -1009,17 +995,15 @@ static int launch_kq_qkv_pers(const MMArgs& a, hipStream_t s) {
   if (off || a.M != 1 || a.xq != nullptr || a.K != 4096 || (a.N / TILE_N) % 2) return -1;
   for (int i = 0; i < a.kq_n; ++i)
     if (a.kq_tile_end[i] % 2) return -1;
-  mkq_pers_seg_kernel<8, 2, 2, EPI_QKV, KQ_UQ><<<a.N / TILE_N / 2, 512, 8 * QL_WAVE_BYTES, s>>>(a);
+  mkq_pers_seg_kernel<8, 2, 2, EPI_QKV, 2><<<a.N / TILE_N / 2, 512, 8 * QL_WAVE_BYTES, s>>>(a);
   return 0;
 }
 
-// U: ring depth with activations in the ring (2..16 tokens); one token (QL) keeps only the weight
-// parts in flight and runs UQ deep
-template <int T, int NKW, int TPW, int NB, int EPI, int U, int UQ>
+template <int T, int NKW, int TPW, int NB, int EPI, int U>
 static void launch_kq_pers_t(const MMArgs& a, int ntiles, hipStream_t s) {
   const int grid = (ntiles + TPW - 1) / TPW;
   if (a.xq == nullptr)
-    mkq_pers_kernel<T, 8, NKW, TPW, NB, EPI, UQ, true><<<grid, 512, 8 * QL_WAVE_BYTES, s>>>(a);
+    mkq_pers_kernel<T, 8, NKW, TPW, NB, EPI, U, true><<<grid, 512, 8 * QL_WAVE_BYTES, s>>>(a);
   else
     mkq_pers_kernel<T, 8, NKW, TPW, NB, EPI, U, false><<<grid, 512, 0, s>>>(a);
 }
@@ -1031,11 +1015,11 @@ template <int T, int NB, int EPI>
 static int launch_kq_pers_ty(const MMArgs& a, int ntiles, hipStream_t s) {
   const int SB = a.K / 256;
   if constexpr (EPI == EPI_SWIGLU) {
-    if (SB == 16 && ntiles == 1792) return launch_kq_pers_t<T, 2, 7, NB, EPI, 2, T == 14 ? 3 : KQ_UQ>(a, ntiles, s), 0;
-    if (SB == 8 && ntiles == 704) return launch_kq_pers_t<T, 1, 3, NB, EPI, 2, T == 14 ? 3 : KQ_UQ>(a, ntiles, s), 0;
+    if (SB == 16 && ntiles == 1792) return launch_kq_pers_t<T, 2, 7, NB, EPI, 2>(a, ntiles, s), 0;
+    if (SB == 8 && ntiles == 704) return launch_kq_pers_t<T, 1, 3, NB, EPI, 2>(a, ntiles, s), 0;
   } else {
-    if (SB == 16 && ntiles > 256 * 8) return launch_kq_pers_t<T, 2, 8, NB, EPI, 2, T == 14 ? 3 : KQ_UQ>(a, ntiles, s), 0;  // 16: spills
-    if (SB == 8 && ntiles > 256 * 4) return launch_kq_pers_t<T, 1, 8, NB, EPI, 2, T == 14 ? 3 : KQ_UQ>(a, ntiles, s), 0;
+    if (SB == 16 && ntiles > 256 * 8) return launch_kq_pers_t<T, 2, 8, NB, EPI, 2>(a, ntiles, s), 0;  // 16: spills
+    if (SB == 8 && ntiles > 256 * 4) return launch_kq_pers_t<T, 1, 8, NB, EPI, 2>(a, ntiles, s), 0;
   }
   return -1;
 }
@@ -1065,7 +1049,7 @@ static int launch_kq_pers(int epi, const MMArgs& a, int ntiles, hipStream_t s) {
 template <int EPI>
 static void launch_mkq_epi(const MMArgs& a, int ntiles, hipStream_t s) {
   if (a.xq == nullptr) {  // one token, quantised on load (launch_mkq checked the slice fits)
-    mkq_kernel<8, 1, 1, EPI, 3, true><<<dim3(ntiles, 1), 512, 8 * QL_WAVE_BYTES, s>>>(a);  // ring 3: 4 spills
+    mkq_kernel<8, 1, 1, EPI, 2, true><<<dim3(ntiles, 1), 512, 8 * QL_WAVE_BYTES, s>>>(a);
   } else if (a.M <= 16) {
     mkq_kernel<8, 1, 1, EPI, 2, false><<<dim3(ntiles, 1), 512, 0, s>>>(a);
   } else if (a.M <= 32) {  // (a 2-deep ring spills ~460 B/lane at two column tiles: U = 1)

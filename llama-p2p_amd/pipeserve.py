@@ -548,6 +548,7 @@ class PipelineFront:
         self.n_vocab, self.n_embd = n_vocab, n_embd
         self.stage_board = stage_board
         self.engine = None  # this stage's engine, closed with the front
+        self.stage_threads = []  # in-process stages (local_pipeline_llama): joined on close
         self.error = None
         self._thread = threading.Thread(target=self._loop, daemon=True)
         self._thread.start()
@@ -599,6 +600,11 @@ class PipelineFront:
         if self.engine is not None:
             self.engine.close()
             self.engine = None
+        # in-process stages leave serve_loop on the stop plan and free their engines: wait for them,
+        # or the interpreter may finalise while a stage thread is still inside the HIP runtime
+        for th in self.stage_threads:
+            th.join(timeout=120)
+        self.stage_threads = []
 
 
 def _stage_setup(model_path, rank, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts=None):
@@ -754,5 +760,6 @@ def local_pipeline_llama(model_path: str, parts, lanes: int = 2, rows: int = 8, 
     ready.wait()
     llm = pipeline_llama(model_path, comms[0], world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts,
                          policy=policy, seed=seed)
+    llm._engine.stage_threads = threads
     llm._stage_threads, llm._stage_errors = threads, errors
     return llm

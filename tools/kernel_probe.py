@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel timing on the GPU (HIP events, rotating through every layer's weights).
 
-    python tools/kernel_probe.py [--model llama3-8b] [--rows 1,32] [--pos 255]
+    python tools/kernel_probe.py [--model llama3-8b] [--rows 1,32] [--pos 255] [--wtype q4_k_m] [--kinds 0,2,3]
 """
 import argparse
 import os
@@ -19,16 +19,22 @@ def main():
     ap.add_argument("--rows", default="1,32")
     ap.add_argument("--pos", type=int, default=255)
     ap.add_argument("--q8", action="store_true", help="the Q8_0 quantisation of the model")
+    ap.add_argument("--wtype", default="", help="q8_0 / q4_0 / q4_k_m / q5_k_m (default bf16)")
+    ap.add_argument("--kinds", default="", help="comma list of kernel kinds (default all)")
+    ap.add_argument("--iters", type=int, default=3)
     args = ap.parse_args()
     os.environ["MX_PROF_POS"] = str(args.pos)
     from llama_p2p_amd.engine import Engine
 
-    eng = Engine(f"synthetic:{args.model}:seed=0" + (":q8_0" if args.q8 else ""), n_ctx=512, n_seq_max=64)
+    wtype = "q8_0" if args.q8 else args.wtype
+    eng = Engine(f"synthetic:{args.model}:seed=0" + (f":{wtype}" if wtype else ""), n_ctx=512, n_seq_max=64)
+    kinds = [int(x) for x in args.kinds.split(",")] if args.kinds else list(KINDS)
     for M in [int(x) for x in args.rows.split(",")]:
-        for k, name in KINDS.items():
-            if k in (5, 6) and (M > 4 or args.q8):
+        for k in kinds:
+            name = KINDS[k]
+            if k in (5, 6) and (M > 4 or wtype):
                 continue
-            us, b = eng.profile_kernel(k, M, iters=3)
+            us, b = eng.profile_kernel(k, M, iters=args.iters)
             print(f"M={M:<3d} {name:14s} {us:9.2f} us  {b / us / 1e3:8.1f} GB/s", flush=True)
     eng.close()
 

@@ -62,6 +62,8 @@ def main():
     ap.add_argument("--n-ctx", type=int, default=640)
     ap.add_argument("--stages", type=int, default=8)
     ap.add_argument("--rows", type=int, default=32, help="rows per pipeline lane")
+    ap.add_argument("--lanes", type=int, default=0, help="micro-batch lanes (default: one per stage; on one GPU "
+                    "the in-process stages run one after another, so every extra lane streams the weights again)")
     ap.add_argument("--replicas", action="store_true")
     ap.add_argument("--policy", default="score_aware", choices=["score_aware", "reference"])
     ap.add_argument("--time-scale", type=float, default=1.0, help="<1 compresses the arrival clock")
@@ -118,9 +120,9 @@ def main():
         h, kv, ff = shape.n_embd, shape.n_embd_kv, shape.n_ff
         parts = partition_layers(shape.n_layer, 2 * (2 * h * h + 2 * h * kv + 3 * h * ff), 2 * shape.n_vocab * h,
                                  args.stages)
-        llm = pipeserve.local_pipeline_llama(path, parts, lanes=args.stages, rows=args.rows, n_ctx=args.n_ctx,
+        llm = pipeserve.local_pipeline_llama(path, parts, lanes=args.lanes or args.stages, rows=args.rows, n_ctx=args.n_ctx,
                                              policy=args.policy, seed=0)
-        mode = f"{args.stages} stages in one process on one GPU"
+        mode = f"{args.stages} stages in one process on one GPU, {args.lanes or args.stages} lanes"
     front = llm._engine
     res = drive(lambda p, g: front.generate(p, g, temperature=0.0, ignore_eos=True), sched, args.gen,
                 args.time_scale)
