@@ -76,17 +76,27 @@ __device__ __forceinline__ size_t kv_v_off(int pos, int d, int D) {
   return (((size_t)(pos >> 5) * (D >> 4) + (d >> 4)) * 64 + (d & 15) + 16 * ((pos & 31) >> 3)) * 8 + (pos & 7);
 }
 
+// The RoPE (cos, sin) pairs of rows [row, row+4) at `pos` (clamped into the table: rows that take
+// no RoPE, or positions that are not stored, load a valid entry and ignore it).  Callers that can
+// issue it early (the persistent GEMVs, with pos / slot loaded once per kernel) pass it to
+// qkv_store_pre: qkv_store's own chain pos -> (cs, slot) is two dependent round trips at the tail.
+__device__ __forceinline__ f32x4 qkv_cs(const MMArgs& a, int row, int pos) {
+  const int d = a.head_dim;
+  const int rl = row < a.n_q ? row : row - a.n_q;
+  const int p = min(max(pos, 0), a.n_ctx - 1);
+  return *reinterpret_cast<const f32x4*>(a.rope_cs + ((size_t)p * (d / 2) + (rl % d) / 2) * 2);
+}
+
 // q/k/v rows [row, row+4) of token column `col`: RoPE (mode NORM, adjacent pairs) on q and k,
 // q -> f32 buffer, k / v -> the f16 K / V caches (layout above).
-__device__ __forceinline__ void qkv_store(const MMArgs& a, int row, int col, f32x4 s) {
+__device__ __forceinline__ void qkv_store_pre(const MMArgs& a, int row, int col, f32x4 s, int pos, int slot,
+                                              f32x4 csv) {
   const int d = a.head_dim;
-  const int pos = a.pos[col];
   if (pos < 0 || pos >= a.n_ctx) return;  // never write outside the slot's KV rows
   if (row < a.n_q + a.n_kv) {
     const bool is_q = row < a.n_q;
     const int rl = is_q ? row : row - a.n_q;
     const int dd = rl % d;  // multiple of 4
-    const f32x4 csv = *reinterpret_cast<const f32x4*>(a.rope_cs + ((size_t)pos * (d / 2) + dd / 2) * 2);
     f32x4 o;
     o[0] = s[0] * csv[0] - s[1] * csv[1];
     o[1] = s[0] * csv[1] + s[1] * csv[0];
@@ -95,15 +105,19 @@ __device__ __forceinline__ void qkv_store(const MMArgs& a, int row, int col, f32
     if (is_q) {
       *reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + row) = o;
     } else {
-      _Float16* kp = a.kc + (size_t)a.slot[col] * a.slot_stride + (size_t)(rl / d) * a.ctx_stride * d + kv_k_off(pos, dd, d);
+      _Float16* kp = a.kc + (size_t)slot * a.slot_stride + (size_t)(rl / d) * a.ctx_stride * d + kv_k_off(pos, dd, d);
       *reinterpret_cast<f16x4*>(kp) = f16x4{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
     }
   } else {
     const int rl = row - a.n_q - a.n_kv;
-    _Float16* vh = a.vc + (size_t)a.slot[col] * a.slot_stride + (size_t)(rl / d) * a.ctx_stride * d;
+    _Float16* vh = a.vc + (size_t)slot * a.slot_stride + (size_t)(rl / d) * a.ctx_stride * d;
 #pragma unroll
     for (int i = 0; i < 4; ++i) vh[kv_v_off(pos, rl % d + i, d)] = (_Float16)s[i];
   }
+}
+__device__ __forceinline__ void qkv_store(const MMArgs& a, int row, int col, f32x4 s) {
+  const int pos = a.pos[col], slot = a.slot[col];
+  qkv_store_pre(a, row, col, s, pos, slot, qkv_cs(a, row, pos));
 }
 
 // One C-layout unit of a finished 16-row tile: rows 16*tile + 4*(l>>4) + i (i < 4) of token

@@ -142,11 +142,14 @@ __global__ __launch_bounds__(1024) void norm_kernel(uint16_t* y, int ldy, float*
   float* xr = x + (size_t)r * n;
   const int tid = threadIdx.x;
   f32x4 v[IT], g[IT], sl[IT][NS > 0 ? NS : 1];
+  // the norm weight is loaded unconditionally (x stands in without y): behind `if (y)` the load made
+  // hipcc wait for it alone (vmcnt(0)) before issuing x and the slabs -- two round trips, not one
+  const float* wp = y ? w : xr;
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int i = (it * 1024 + tid) * 4;
     v[it] = *reinterpret_cast<const f32x4*>(xr + i);
-    if (y) g[it] = *reinterpret_cast<const f32x4*>(w + i);
+    g[it] = *reinterpret_cast<const f32x4*>(wp + i);
 #pragma unroll
     for (int k = 0; k < NS; ++k) sl[it][k] = *reinterpret_cast<const f32x4*>(slabs + k * stride + (size_t)r * n + i);
   }
@@ -559,6 +562,19 @@ __global__ __launch_bounds__(64 * KS) void mm_pers_kernel(MMArgs a) {
     for (int k = 0; k < NKW; ++k) xb[k] = xp[(kb + k) * 4];
   }
 
+  // the epilogue's own loads -- the residual rows (RESID), the RoPE pairs of the q|k rows with pos /
+  // slot (QKV) -- are issued when the tile starts, with its weight loads, so the tile's tail is one
+  // barrier and the stores (loaded there, they were up to three dependent round trips long)
+  int qpos = 0, qslot = 0;
+  if constexpr (EPI == EPI_QKV) qpos = a.pos[col], qslot = a.slot[col];
+  f32x4 pre[TPW];
+  auto prefetch = [&](int i) {
+    const int tile = min((int)blockIdx.x + i * G, ntiles - 1);
+    if constexpr (EPI == EPI_QKV) pre[i] = qkv_cs(a, tile * 16 + (lane >> 4) * 4, qpos);
+    if constexpr (EPI == EPI_RESID)
+      pre[i] = *reinterpret_cast<const f32x4*>(a.out + (size_t)col * a.ldo + tile * 16 + (lane >> 4) * 4);
+  };
+
   constexpr int LU = (EPI == EPI_SWIGLU) ? 32 : 64;
   auto finish = [&](int i) {  // after the barrier of tile i: wave 0 sums the KS partials, epilogue
     const int tile = blockIdx.x + i * G;
@@ -572,7 +588,7 @@ __global__ __launch_bounds__(64 * KS) void mm_pers_kernel(MMArgs a) {
       double q = 0.0;
       if (col_raw < a.M) {
         f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col_raw * a.ldo + tile * 16 + (l >> 4) * 4);
-        const f32x4 xv = *px + s;
+        const f32x4 xv = pre[i] + s;
         *px = xv;
 #pragma unroll
         for (int j = 0; j < 4; ++j) q += (double)(xv[j] * xv[j]);
@@ -593,7 +609,8 @@ __global__ __launch_bounds__(64 * KS) void mm_pers_kernel(MMArgs a) {
         s += rb[ww][l];
         if constexpr (EPI == EPI_SWIGLU) up += rb[ww][l + 32];
       }
-      epi_store<EPI>(a, tile, l, col_raw, s, up);
+      if constexpr (EPI == EPI_QKV) qkv_store_pre(a, tile * 16 + (l >> 4) * 4, col_raw, s, qpos, qslot, pre[i]);
+      else epi_store<EPI>(a, tile, l, col_raw, s, up);
     }
   };
   auto publish = [&](int i, f32x4 acc) {
@@ -608,6 +625,7 @@ __global__ __launch_bounds__(64 * KS) void mm_pers_kernel(MMArgs a) {
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    prefetch(i);
 #pragma unroll
     for (int k = 0; k < NKW; ++k) {
       const int f = i * NKW + k;  // flat ring position (compile-time after unrolling)
@@ -1008,6 +1026,8 @@ constexpr float LOG2E = 1.4426950408889634f;
 // still as the wide path's split-K slabs (finished here, see below).  Everything that only the
 // chunk holding `pos` (FIN) or the partial last chunk needs sits behind a wave-uniform branch, so
 // the full chunks run the bare MFMA + softmax stream.
+constexpr int ATTN_FIN_MAXSLAB = 8;  // split-K slabs the FIN path can sum (the wide launchers split K at most 8 ways)
+
 template <int D, int G, int NW, bool FIN>
 __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int c) {
   constexpr int CH = ATTN_CHUNK;
@@ -1019,10 +1039,10 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
   auto stamp = [&](int k) {
     if (tr && lane == 0) tr[k] = __builtin_amdgcn_s_memrealtime();
   };
-  stamp(0);
   const int pos = a.pos[c];
-  const int ctx = min(pos + 1, a.n_ctx);
   const int slot = a.slot[c];
+  stamp(0);
+  const int ctx = min(pos + 1, a.n_ctx);
 
   __shared__ __attribute__((aligned(16))) _Float16 Ps[NW][16][CH + 8];
   __shared__ float Om[NW][G][D];
@@ -1061,16 +1081,30 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
       const int i = u * 4;  // qs index
       const int row = i < G * D ? kvh * G * D + i : i < G * D + D ? nq + kvh * D + (i - G * D)
                                                                    : nq + nkv + kvh * D + (i - G * D - D);
-      f32x4 v = *reinterpret_cast<const f32x4*>(a.slabs + (size_t)c * N + row);
-      for (int k = 1; k < a.nslab; ++k) v += *reinterpret_cast<const f32x4*>(a.slabs + k * a.slab_stride + (size_t)c * N + row);
+      // all slab and RoPE loads issued together (clamped: extra reads repeat the last slab): a run-time
+      // slab loop or a load behind the RoPE branch made each load wait for itself
+      f32x4 sv[ATTN_FIN_MAXSLAB];
+#pragma unroll
+      for (int k = 0; k < ATTN_FIN_MAXSLAB; ++k)
+        sv[k] = *reinterpret_cast<const f32x4*>(a.slabs + min(k, a.nslab - 1) * a.slab_stride + (size_t)c * N + row);
       const int dd = i % D;
-      if (i < G * D + D && pos < a.n_ctx) {  // RoPE (mode NORM: adjacent pairs) on q and k
-        const f32x4 csv = *reinterpret_cast<const f32x4*>(a.rope_cs + ((size_t)pos * (D / 2) + dd / 2) * 2);
+      const f32x4 csv =
+          *reinterpret_cast<const f32x4*>(a.rope_cs + ((size_t)min(pos, a.n_ctx - 1) * (D / 2) + dd / 2) * 2);
+      // slab order, as qkv_finish_kernel; the slabs past nslab add exact zeros (a branch per slab
+      // would pull its load into the branch again)
+      f32x4 v = sv[0];
+#pragma unroll
+      for (int k = 1; k < ATTN_FIN_MAXSLAB; ++k) v += sv[k] * (k < a.nslab ? 1.0f : 0.0f);
+      {  // RoPE (mode NORM: adjacent pairs) on q and k, as selects (a branch would pull csv's load into it)
+        const bool rope = i < G * D + D && pos < a.n_ctx;
         const f32x4 s = v;
-        v[0] = s[0] * csv[0] - s[1] * csv[1];
-        v[1] = s[0] * csv[1] + s[1] * csv[0];
-        v[2] = s[2] * csv[2] - s[3] * csv[3];
-        v[3] = s[2] * csv[3] + s[3] * csv[2];
+        f32x4 rv;
+        rv[0] = s[0] * csv[0] - s[1] * csv[1];
+        rv[1] = s[0] * csv[1] + s[1] * csv[0];
+        rv[2] = s[2] * csv[2] - s[3] * csv[3];
+        rv[3] = s[2] * csv[3] + s[3] * csv[2];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = rope ? rv[j] : s[j];
       }
       *reinterpret_cast<f32x4*>(qs + i) = v;
       if (i >= G * D && pos < a.n_ctx) {

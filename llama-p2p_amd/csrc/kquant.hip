@@ -909,6 +909,14 @@ __device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Ws
     kq_load_x<T, 1, NB>(fr, Xq, Xd, Xb, kb + f % NKW);
   };
   constexpr int LU = (EPI == EPI_SWIGLU) ? 32 : 64;
+  // one token's q|k|v: pos / slot once, each tile's RoPE pairs when the tile starts (mm_pers_kernel's
+  // prefetch: in the epilogue they were a chain of dependent round trips)
+  int qpos = 0, qslot = 0;
+  f32x4 qcs[TPW];
+  if constexpr (EPI == EPI_QKV && NB == 1) {
+    const int c0 = colr[0] < a.M ? colr[0] : a.M - 1;
+    qpos = a.pos[c0], qslot = a.slot[c0];
+  }
   auto finish = [&](int i) {
     const int tile = tile_of(i);
     if (w != 0 || tile >= ntiles) return;
@@ -923,7 +931,8 @@ __device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Ws
         s += rb[ww][n][lane];
         if constexpr (EPI == EPI_SWIGLU) up += rb[ww][n][lane + 32];
       }
-      epi_store<EPI>(a, tile, lane, colr[n], s, up);
+      if constexpr (EPI == EPI_QKV && NB == 1) qkv_store_pre(a, tile * 16 + (lane >> 4) * 4, colr[0], s, qpos, qslot, qcs[i]);
+      else epi_store<EPI>(a, tile, lane, colr[n], s, up);
     }
   };
 
@@ -949,6 +958,7 @@ __device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Ws
     f32x4 acc[1][NB];
 #pragma unroll
     for (int n = 0; n < NB; ++n) acc[0][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI == EPI_QKV && NB == 1) qcs[i] = qkv_cs(a, min(tile_of(i), ntiles - 1) * 16 + (lane >> 4) * 4, qpos);
 #pragma unroll
     for (int k = 0; k < NKW; ++k) {
       const int f = i * NKW + k;
