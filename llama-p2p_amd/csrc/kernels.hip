@@ -1089,7 +1089,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
         sv[k] = *reinterpret_cast<const f32x4*>(a.slabs + min(k, a.nslab - 1) * a.slab_stride + (size_t)c * N + row);
       const int dd = i % D;
       const f32x4 csv =
-          *reinterpret_cast<const f32x4*>(a.rope_cs + ((size_t)min(pos, a.n_ctx - 1) * (D / 2) + dd / 2) * 2);
+          *reinterpret_cast<const f32x4*>(a.rope_cs + ((size_t)max(0, min(pos, a.n_ctx - 1)) * (D / 2) + dd / 2) * 2);
       // slab order, as qkv_finish_kernel; the slabs past nslab add exact zeros (a branch per slab
       // would pull its load into the branch again)
       f32x4 v = sv[0];
@@ -2435,7 +2435,7 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
     const float* gsrc = a.norm_w ? a.norm_w : a.xf;
 #pragma unroll
     for (int p = 0; p < QP; ++p) {
-      const int i = min(lane * 4 + 256 * p, nk - 4);
+      const int i = max(0, min(lane * 4 + 256 * p, nk - 4));  // nk = 0: a wave with no K tiles
       gv[p] = *reinterpret_cast<const f32x4*>(gsrc + kbase + i);
 #pragma unroll
       for (int c = 0; c < QM; ++c)
@@ -2510,7 +2510,7 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
   int kt = kb;
   const int nfull = (ke - kb) / U;
 #pragma unroll
-  for (int u = 0; u < U; ++u) load_w(ring[u], min(kt + u, ke - 1));  // unconditional (see xs_load); unused when nfull == 0
+  for (int u = 0; u < U; ++u) load_w(ring[u], max(0, min(kt + u, ke - 1)));  // unconditional (see xs_load); unused when nfull == 0
   if constexpr (QP > 0) {  // build the image while the ring is in flight
 #pragma unroll
     for (int c = 0; c < QM; ++c) {

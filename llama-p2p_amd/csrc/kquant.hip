@@ -533,7 +533,7 @@ __device__ __forceinline__ void ql_load(QlRegs& r, const MMArgs& a, int kb, int 
   const float* wsrc = a.norm_w ? a.norm_w : a.xf;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    const int it = min(rr + 4 * q, nsb - 1);
+    const int it = max(0, min(rr + 4 * q, nsb - 1));  // a wave may own no super-block (K < 256 * waves)
     const size_t k0 = (size_t)(kb + it) * 256 + 16 * t;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
