@@ -32,10 +32,11 @@ namespace mx {
 //               8*(e&3) + (u&7) of dword u>>3, u = 2j + (e>>2)
 //   Q6_K  [2048, 3072): lane l's 4 dwords at 2048 + 16l: bits 4-5 of value (j, e) at bits
 //               8*(e&3) + 2*(u&3) of dword u>>2
-//   Q4_K / Q5_K scales at SC = 2048 / 2560:  SC + 8r + j: 6-bit scale of row r, sub-block j;
-//               SC + 128 + 8r + j: 6-bit min of row r, sub-block j;  SC + 256 + 4r: f16 d, f16 dmin
-//   Q6_K scales at SC = 3072:  SC + 16r + g: int8 scale of row r, 16-value group g;
-//               SC + 256 + 2r: f16 d of row r
+//   scales lane-major, row r = 4q + i (q = r >> 2): byte SC + 64q + 4c + i is lane c + 16q's
+//   byte i (the rows of the MFMA C-layout lane group q), so one dword per lane holds its 4 rows:
+//   Q4_K / Q5_K at SC = 2048 / 2560:  column c < 8: 6-bit scale of sub-block c, c >= 8: 6-bit min
+//               of sub-block c - 8;  SC + 256 + 16q + 2i: f16 d of row r, SC + 264 + 16q + 2i: f16 dmin
+//   Q6_K at SC = 3072:  column c: int8 scale of 16-value group c;  SC + 256 + 2r: f16 d of row r
 // ---------------------------------------------------------------------------
 template <int T>
 struct KqTile;
@@ -105,8 +106,9 @@ __global__ void pack_kq_kernel(uint8_t* dst, const uint8_t* src, int N, int K, i
         for (int c = 0; c < 4; ++c) *reinterpret_cast<uint32_t*>(tile + 2048 + 16 * lane + 4 * c) = H[c];
     }
     constexpr int SC = KqTile<T>::SC;
+    uint8_t* scr = tile + SC + 64 * (r >> 2) + (r & 3);  // column c at scr[4c]
     if (T == 14) {
-      for (int g = 0; g < 16; ++g) tile[SC + 16 * r + g] = b[192 + g];
+      for (int g = 0; g < 16; ++g) scr[4 * g] = b[192 + g];
       tile[SC + 256 + 2 * r] = b[208];
       tile[SC + 256 + 2 * r + 1] = b[209];
     } else {
@@ -120,10 +122,14 @@ __global__ void pack_kq_kernel(uint8_t* dst, const uint8_t* src, int N, int K, i
           sc[j] = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
           mn[j] = (q[j + 4] >> 4) | ((q[j] >> 6) << 4);
         }
-        tile[SC + 8 * r + j] = sc[j];
+        scr[4 * j] = sc[j];
+        scr[4 * (8 + j)] = mn[j];
       }
-      for (int j = 0; j < 8; ++j) tile[SC + 128 + 8 * r + j] = mn[j];
-      for (int c = 0; c < 4; ++c) tile[SC + 256 + 4 * r + c] = b[c];
+      uint8_t* dr = tile + SC + 256 + 16 * (r >> 2) + 2 * (r & 3);
+      dr[0] = b[0];  // d
+      dr[1] = b[1];
+      dr[8] = b[2];  // dmin
+      dr[9] = b[3];
     }
   }
 }
@@ -411,15 +417,15 @@ __global__ __launch_bounds__(256) void dequant_kq_kernel(uint16_t* dst, const ui
     float y[8];
     if constexpr (T == 14) {
       const float d = f16b(t + SC + 256 + 2 * r);
-      const int sc = (int)(int8_t)t[SC + 16 * r + 2 * j + (g >> 1)];
+      const int sc = (int)(int8_t)t[SC + 64 * (r >> 2) + 4 * (2 * j + (g >> 1)) + (r & 3)];
       const float ds = d * (float)sc;
 #pragma unroll
       for (int e = 0; e < 8; ++e) y[e] = ds * (float)((int)(((e < 4 ? lo : hi) >> (8 * (e & 3))) & 0xFFu) - 32);
     } else {
-      const float d = f16b(t + SC + 256 + 4 * r);
-      const float dmin = f16b(t + SC + 256 + 4 * r + 2);
-      const float d1 = d * (float)t[SC + 32 * (r >> 2) + 8 * (r & 3) + j];
-      const float m1 = dmin * (float)t[SC + 128 + 8 * r + j];
+      const float d = f16b(t + SC + 256 + 16 * (r >> 2) + 2 * (r & 3));
+      const float dmin = f16b(t + SC + 264 + 16 * (r >> 2) + 2 * (r & 3));
+      const float d1 = d * (float)t[SC + 64 * (r >> 2) + 4 * j + (r & 3)];
+      const float m1 = dmin * (float)t[SC + 64 * (r >> 2) + 4 * (8 + j) + (r & 3)];
 #pragma unroll
       for (int e = 0; e < 8; ++e) y[e] = d1 * (float)((((e < 4 ? lo : hi) >> (8 * (e & 3))) & 0xFFu)) - m1;
     }
@@ -459,8 +465,8 @@ struct KqFrag {
   u32x4 qs[RT][2];
   u32x4 h[RT];      // Q5_K: dwords 0-1; Q6_K: 0-3
   u32x4 sc[RT][4];  // Q4_K / Q5_K: [0..1]; Q6_K: [0..3]
-  u32x4 dm[RT];     // Q4_K / Q5_K: f16 (d, dmin) x 4 rows; Q6_K: dwords 0-1 = f16 d x 4 rows
-  u32x2 mw[RT];     // Q4_K / Q5_K: the row's 6-bit mins (bytes 0-7 = sub-blocks), raw as loaded
+  u32x4 dm[RT];     // Q4_K / Q5_K: f16 d x 4 rows, then f16 dmin x 4 rows; Q6_K: dwords 0-1 = f16 d x 4 rows
+  u32x2 mw[RT];     // Q4_K / Q5_K: mins dwords of sub-blocks g, g+4 (byte lane&3 = this lane's A row), raw
   u32x4 x[NB][4];
   float dx[NB];
   f32x2 xb[NB];
@@ -487,9 +493,11 @@ __device__ __forceinline__ void kq_load_w(KqFrag<RT, NB>& f, const uint8_t* cons
       f.dm[r] = u32x4{dv[0], dv[1], 0u, 0u};
     } else {
 #pragma unroll
-      for (int c = 0; c < 2; ++c) f.sc[r][c] = *reinterpret_cast<const u32x4*>(t + SC + 32 * g + 16 * c);
-      // kept raw: extracting the mins here would wait for this load at once (draining the ring)
-      f.mw[r] = *reinterpret_cast<const u32x2*>(t + SC + 128 + 8 * (lane & 15));
+      for (int c = 0; c < 2; ++c) f.sc[r][c] = *reinterpret_cast<const u32x4*>(t + SC + 64 * g + 16 * c);
+      // the mins of this lane's A row (lane & 15) for sub-blocks g and g + 4 (the mins MFMA's k = g),
+      // kept raw: extracting them here would wait for this load at once (draining the ring)
+      const uint8_t* mq = t + SC + 64 * ((lane & 15) >> 2) + 32 + 4 * g;
+      f.mw[r] = u32x2{*reinterpret_cast<const uint32_t*>(mq), *reinterpret_cast<const uint32_t*>(mq + 16)};
       f.dm[r] = *reinterpret_cast<const u32x4*>(t + SC + 256 + 16 * g);
     }
   }
@@ -622,12 +630,11 @@ __device__ __forceinline__ void kq_compute(f32x4 (&acc)[RT][NB], const KqFrag<RT
         }
         const long A = (long)(((unsigned long)hi << 32) | lo);
         if constexpr (T == 14) {
-          // int8 scales of row 4g+i, groups 2j and 2j+1: bytes 16i + 2j, +1 of the row group's 64
+          // int8 scales of row 4g+i, groups 2j and 2j+1: byte i of dwords 2j, 2j+1 of the row group's 64
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const uint32_t sw = scw[4 * i + (j >> 1)];
-            sc[i] = (int)(int8_t)(sw >> (16 * (j & 1)));
-            sc1[i] = (int)(int8_t)(sw >> (16 * (j & 1) + 8));
+            sc[i] = (int)(int8_t)(scw[2 * j] >> (8 * i));
+            sc1[i] = (int)(int8_t)(scw[2 * j + 1] >> (8 * i));
           }
           const long A0 = g < 2 ? A : 0l, A1 = g < 2 ? 0l : A;
 #pragma unroll
@@ -638,9 +645,9 @@ __device__ __forceinline__ void kq_compute(f32x4 (&acc)[RT][NB], const KqFrag<RT
             Pc1[n] = __builtin_amdgcn_mfma_i32_16x16x32_i8(A1, B, i32x4{0, 0, 0, 0}, 0, 0, 0);
           }
         } else {
-          // 6-bit scales of row 4g+i, sub-block j: byte 8i + j of the row group's 32
+          // 6-bit scales of row 4g+i, sub-block j: byte i of dword j of the row group's 32
 #pragma unroll
-          for (int i = 0; i < 4; ++i) sc[i] = (int)((scw[2 * i + (j >> 2)] >> (8 * (j & 3))) & 0xFFu);
+          for (int i = 0; i < 4; ++i) sc[i] = (int)((scw[j] >> (8 * i)) & 0xFFu);
 #pragma unroll
           for (int n = 0; n < NB; ++n) {
             const u32x4& xc = f.x[n][j >> 1];
@@ -680,24 +687,247 @@ __device__ __forceinline__ void kq_compute(f32x4 (&acc)[RT][NB], const KqFrag<RT
         for (int i = 0; i < 4; ++i) acc[r][n][i] += ((float)d4[i] * dx) * (float)S[n][i];
       } else {
         // mins: sum_j m[row][j] * bsum32[j][col] on the f32 MFMA (k = sub-block g, then g + 4)
-        const float m0 = (float)((f.mw[r][0] >> (8 * g)) & 0xFFu);  // mins of sub-blocks g, g + 4
-        const float m1 = (float)((f.mw[r][1] >> (8 * g)) & 0xFFu);
+        const int rb = 8 * (threadIdx.x & 3);  // this lane's A row within its mins dwords
+        const float m0 = (float)((f.mw[r][0] >> rb) & 0xFFu);  // mins of sub-blocks g, g + 4
+        const float m1 = (float)((f.mw[r][1] >> rb) & 0xFFu);
         f32x4 Mn = __builtin_amdgcn_mfma_f32_16x16x4f32(m0, f.xb[n][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         Mn = __builtin_amdgcn_mfma_f32_16x16x4f32(m1, f.xb[n][1], Mn, 0, 0, 0);
         const f16x8 dm = __builtin_bit_cast(f16x8, f.dm[r]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          acc[r][n][i] += ((float)dm[2 * i] * dx) * (float)S[n][i];
-          acc[r][n][i] -= ((float)dm[2 * i + 1] * dx) * Mn[i];
+          acc[r][n][i] += ((float)dm[i] * dx) * (float)S[n][i];
+          acc[r][n][i] -= ((float)dm[4 + i] * dx) * Mn[i];
         }
       }
     }
   }
 }
 
-template <int T, int KS, int RT, int NB, int EPI, int U, bool QL>
+// ---------------------------------------------------------------------------
+// One token, block-diagonal form.  With one token kq_compute fills one of the 16 B columns of every
+// MFMA and spends its VALU on per-sub-block int32 scaling of the 15 empty ones too (VALU-bound at
+// ~3.3 TB/s).  Here the 16 columns carry the super-block's sub-blocks instead: for sub-block j the
+// B operand holds the token's 32 q of sub-block j in column j (Q6_K: its two 16-value groups in
+// columns 2j, 2j+1) and zeros elsewhere, so the 8 MFMAs of a super-block accumulate into ONE C
+// whose column c is the integer product sum of sub-block (group) c for the tile's 16 rows.  Then
+// per lane (column c, rows 4q..4q+3): one scale byte per row from its dword of the lane-major scale
+// layout, one int multiply, and a DPP row reduction over the columns --
+//   Q4_K / Q5_K: columns 0-7 give S = sum_j sc_j * P_j (lane 7), columns 8-15 the mins term
+//                Mn = sum_j m_j * bsum32_j (lane 15; the lane's bsum32 from the Q8_K image),
+//   Q6_K:        S = sum_g sc_g * (P_g - 32 * bsum16_g) over all 16 columns (the -32 of every
+//                6-bit value taken out of the A operand: an exact integer identity),
+// which are ggml's super-block integers exactly; the f32 scaling is kq_compute's.  The result of a
+// tile ends in lane 0 of each row group (kq_bd_finish), i.e. column 0 of the C layout: the token.
+// ---------------------------------------------------------------------------
+struct KqBdX {
+  u32x2 X;    // this lane's 8 q of its column's sub-block (group) slice, zero where it carries none
+  int bs;     // Q4_K / Q5_K lanes c >= 8: bsum32 of sub-block c - 8; Q6_K: bsum16 of group c
+  float dx;   // the super-block's d
+};
+
+// the token's super-block sb (xq / xd / xb: the Q8_K row, or a wave image indexed the same way)
+template <int T>
+__device__ __forceinline__ KqBdX kq_bd_x(const int8_t* xq, const float* xd, const float* xb, int sb, int lane) {
+  const int c = lane & 15, q = lane >> 4;
+  KqBdX r;
+  // permuted Q8_K order: k = 32j + 8q + e of the super-block at 64q + 8j + e
+  if constexpr (T == 14) {
+    const u32x2 v = *reinterpret_cast<const u32x2*>(xq + (size_t)sb * 256 + 64 * q + 8 * (c >> 1));
+    const bool on = (q >> 1) == (c & 1);  // lanes q = 0,1 hold group 2j's 16 values, q = 2,3 group 2j+1's
+    r.X = on ? v : u32x2{0u, 0u};
+    int p = __builtin_amdgcn_sdot4((int)r.X[0], 0x01010101, 0, false);
+    p = __builtin_amdgcn_sdot4((int)r.X[1], 0x01010101, p, false);
+    p += __shfl_xor(p, 16);
+    r.bs = p + __shfl_xor(p, 32);  // column c's 16 values: two lanes of the four
+  } else {
+    const int j = c & 7;
+    const u32x2 v = *reinterpret_cast<const u32x2*>(xq + (size_t)sb * 256 + 64 * q + 8 * j);
+    r.X = c < 8 ? v : u32x2{0u, 0u};
+    r.bs = (int)xb[(size_t)sb * 8 + 2 * (j & 3) + (j >> 2)];  // exact: an integer sum
+  }
+  r.dx = xd[sb];
+  return r;
+}
+
+// kq_bd_x for lane l of a wave without cross-lane operations (the LDS image builder; Q6_K's bsum16
+// summed over both halves of the group from the row itself)
+template <int T>
+__device__ __forceinline__ KqBdX kq_bd_x_lane(const int8_t* xq, const float* xd, const float* xb, int sb, int l) {
+  const int c = l & 15, q = l >> 4;
+  KqBdX r;
+  if constexpr (T == 14) {
+    const int j = c >> 1, h = c & 1;
+    const u32x2 v = *reinterpret_cast<const u32x2*>(xq + (size_t)sb * 256 + 64 * q + 8 * j);
+    r.X = (q >> 1) == h ? v : u32x2{0u, 0u};
+    int p = 0;
+#pragma unroll
+    for (int qq = 2 * h; qq < 2 * h + 2; ++qq) {  // group c = lanes q = 2h, 2h+1 of column c
+      const u32x2 g = *reinterpret_cast<const u32x2*>(xq + (size_t)sb * 256 + 64 * qq + 8 * j);
+      p = __builtin_amdgcn_sdot4((int)g[0], 0x01010101, p, false);
+      p = __builtin_amdgcn_sdot4((int)g[1], 0x01010101, p, false);
+    }
+    r.bs = p;
+  } else {
+    const int j = c & 7;
+    const u32x2 v = *reinterpret_cast<const u32x2*>(xq + (size_t)sb * 256 + 64 * q + 8 * j);
+    r.X = c < 8 ? v : u32x2{0u, 0u};
+    r.bs = (int)xb[(size_t)sb * 8 + 2 * (j & 3) + (j >> 2)];
+  }
+  r.dx = xd[sb];
+  return r;
+}
+
+// weights of one super-block of one tile: the 4-bit planes and high bits as kq_load_w, the lane's
+// scale dword (lane-major layout) and f16 d (lanes c >= 8 of Q4_K / Q5_K: dmin) of its 4 rows
+template <int T>
+__device__ __forceinline__ void kq_load_w_bd(KqFrag<1, 1>& f, const uint8_t* t, int lane) {
+  constexpr int SC = KqTile<T>::SC;
+  const int g = lane >> 4;
+  f.qs[0][0] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t) + lane);
+  f.qs[0][1] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t + 1024) + lane);
+  if constexpr (T == 13) {
+    const u32x2 hv = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(t + 2048) + lane);
+    f.h[0] = u32x4{hv[0], hv[1], 0u, 0u};
+  }
+  if constexpr (T == 14) f.h[0] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t + 2048) + lane);
+  f.sc[0][0][0] = *reinterpret_cast<const uint32_t*>(t + SC + 4 * lane);
+  const u32x2 dv = *reinterpret_cast<const u32x2*>(t + SC + 256 + (T == 14 ? 8 * g : 16 * g + (lane & 8)));
+  f.dm[0] = u32x4{dv[0], dv[1], 0u, 0u};
+}
+
+// in-row DPP sums of 4 ints: lane l adds lane (l - n) mod 16 (row_ror), steps 4, 2, 1 (8-lane sums
+// in lanes 7 and 15) or 8, 4, 2, 1 (the row sum in every lane)
+#define KQ_ROR_ADD4(op, n)                                                               \
+  op "_dpp %0, %0, %0 row_ror:" #n " row_mask:0xf bank_mask:0xf\n\t" op "_dpp %1, %1, %1 row_ror:" #n \
+     " row_mask:0xf bank_mask:0xf\n\t" op "_dpp %2, %2, %2 row_ror:" #n " row_mask:0xf bank_mask:0xf\n\t" op \
+     "_dpp %3, %3, %3 row_ror:" #n " row_mask:0xf bank_mask:0xf\n\t"
+__device__ __forceinline__ void row8_isum4(int (&v)[4]) {
+  asm volatile("s_nop 1\n\t" KQ_ROR_ADD4("v_add_u32", 4) KQ_ROR_ADD4("v_add_u32", 2) KQ_ROR_ADD4("v_add_u32", 1)
+               : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+}
+__device__ __forceinline__ void row16_isum4(int (&v)[4]) {
+  asm volatile("s_nop 1\n\t" KQ_ROR_ADD4("v_add_u32", 8) KQ_ROR_ADD4("v_add_u32", 4) KQ_ROR_ADD4("v_add_u32", 2)
+                   KQ_ROR_ADD4("v_add_u32", 1)
+               : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+}
+
+template <int T>
+__device__ __forceinline__ void kq_compute_bd(f32x4& acc, const KqFrag<1, 1>& f, const KqBdX& x, int lane) {
+  const int c = lane & 15;
+  const int jsel = T == 14 ? (c >> 1) : c;  // the sub-block whose MFMA this lane's column joins
+  uint32_t D[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    D[k] = f.qs[0][0][k];
+    D[4 + k] = f.qs[0][1][k];
+  }
+  i32x4 C0 = i32x4{0, 0, 0, 0}, C1 = i32x4{0, 0, 0, 0};  // two chains: no MFMA waits on the previous
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t lo = D[j] & 0x0F0F0F0Fu, hi = (D[j] >> 4) & 0x0F0F0F0Fu;
+    if constexpr (T == 13) {
+      const uint32_t H = f.h[0][j >> 2];
+      lo |= ((H >> ((2 * j) & 7)) & 0x01010101u) << 4;
+      hi |= ((H >> ((2 * j + 1) & 7)) & 0x01010101u) << 4;
+    }
+    if constexpr (T == 14) {  // 6-bit values 0..63 (the -32 is applied to the sums)
+      const uint32_t H = f.h[0][j >> 1];
+      lo |= ((H >> (4 * (j & 1))) & 0x03030303u) << 4;
+      hi |= ((H >> (4 * (j & 1) + 2)) & 0x03030303u) << 4;
+    }
+    const long A = (long)(((unsigned long)hi << 32) | lo);
+    const bool on = jsel == j;
+    const long B = (long)(((unsigned long)(on ? x.X[1] : 0u) << 32) | (on ? x.X[0] : 0u));
+    if (j & 1) C1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(A, B, C1, 0, 0, 0);
+    else C0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(A, B, C0, 0, 0, 0);
+  }
+  const uint32_t s = f.sc[0][0][0];
+  int t[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int P = C0[i] + C1[i];
+    if constexpr (T == 14) t[i] = __mul24((int)(int8_t)(s >> (8 * i)), P - 32 * x.bs);  // |P - 32 bs| < 2^18
+    else t[i] = __mul24((int)((s >> (8 * i)) & 0xFFu), c < 8 ? P : x.bs);                // < 2^17
+  }
+  if constexpr (T == 14) row16_isum4(t);
+  else row8_isum4(t);
+  // ggml: (f16(d) * d_x) * S, and for the mins (f16(dmin) * d_x) * Mn subtracted: lanes 8-15 carry
+  // dmin and -d_x, so lane 15 accumulates -(dmin * d_x) * Mn exactly
+  const f16x4 dd = __builtin_bit_cast(f16x4, u32x2{f.dm[0][0], f.dm[0][1]});
+  const float dxs = (T != 14 && c >= 8) ? -x.dx : x.dx;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] += ((float)dd[i] * dxs) * (float)t[i];
+}
+
+// kq_compute_bd with the block-diagonal B operands read from LDS (Bs[j][lane], mkq_bd_tile_kernel)
+template <int T>
+__device__ __forceinline__ void kq_compute_bd_lds(f32x4& acc, const KqFrag<1, 1>& f, const u32x2 (*Bs)[64], int bs,
+                                                  float dx, int lane) {
+  const int c = lane & 15;
+  uint32_t D[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    D[k] = f.qs[0][0][k];
+    D[4 + k] = f.qs[0][1][k];
+  }
+  i32x4 C0 = i32x4{0, 0, 0, 0}, C1 = i32x4{0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t lo = D[j] & 0x0F0F0F0Fu, hi = (D[j] >> 4) & 0x0F0F0F0Fu;
+    if constexpr (T == 13) {
+      const uint32_t H = f.h[0][j >> 2];
+      lo |= ((H >> ((2 * j) & 7)) & 0x01010101u) << 4;
+      hi |= ((H >> ((2 * j + 1) & 7)) & 0x01010101u) << 4;
+    }
+    if constexpr (T == 14) {
+      const uint32_t H = f.h[0][j >> 1];
+      lo |= ((H >> (4 * (j & 1))) & 0x03030303u) << 4;
+      hi |= ((H >> (4 * (j & 1) + 2)) & 0x03030303u) << 4;
+    }
+    const long A = (long)(((unsigned long)hi << 32) | lo);
+    const u32x2 bv = Bs[j][lane];
+    const long B = (long)(((unsigned long)bv[1] << 32) | bv[0]);
+    if (j & 1) C1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(A, B, C1, 0, 0, 0);
+    else C0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(A, B, C0, 0, 0, 0);
+  }
+  const uint32_t s = f.sc[0][0][0];
+  int t[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int P = C0[i] + C1[i];
+    if constexpr (T == 14) t[i] = __mul24((int)(int8_t)(s >> (8 * i)), P - 32 * bs);
+    else t[i] = __mul24((int)((s >> (8 * i)) & 0xFFu), c < 8 ? P : bs);
+  }
+  if constexpr (T == 14) row16_isum4(t);
+  else row8_isum4(t);
+  const f16x4 dd = __builtin_bit_cast(f16x4, u32x2{f.dm[0][0], f.dm[0][1]});
+  const float dxs = (T != 14 && c >= 8) ? -dx : dx;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] += ((float)dd[i] * dxs) * (float)t[i];
+}
+
+// end of a tile: Q4_K / Q5_K hold d-terms in lane 7 and mins terms in lane 15 of each row; their
+// sum goes to lane 0 (Q6_K: every lane already holds the row's total)
+template <int T>
+__device__ __forceinline__ void kq_bd_finish(f32x4& acc) {
+  if constexpr (T != 14) {
+    float v0 = acc[0], v1 = acc[1], v2 = acc[2], v3 = acc[3];
+    asm volatile("s_nop 1\n\t" KQ_ROR_ADD4("v_add_f32", 8)
+                 "s_nop 1\n\t"
+                 "v_mov_b32_dpp %0, %0 row_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_mov_b32_dpp %1, %1 row_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_mov_b32_dpp %2, %2 row_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_mov_b32_dpp %3, %3 row_ror:1 row_mask:0xf bank_mask:0xf"
+                 : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));
+    acc = f32x4{v0, v1, v2, v3};
+  }
+}
+#undef KQ_ROR_ADD4
+
+template <int T, int KS, int RT, int NB, int EPI, int U, bool QL, bool BD>
 __device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int tile_in_seg, int tile0,
                                          f32x4 (*red)[RT][NB][64]) {
+  static_assert(!BD || (RT == 1 && NB == 1), "block-diagonal form: one token, one tile");
   constexpr int TB = KqTile<T>::BYTES;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -746,10 +976,76 @@ __device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int 
   };
   auto compute = [&](const Frag& f) { kq_compute<T, RT, NB>(acc, f, g); };
 
-  Frag ring[U];
   int sb = kb;
   const int nfull = (ke - kb) / U;
   QlRegs qr;
+  if constexpr (BD) {  // one token (kq_compute_bd): weights and activation operands ring together
+    const int8_t* bq = QL ? iq - kb * 256 : a.xq;
+    const float* bd = QL ? id - kb : a.xd;
+    const float* bb = QL ? ib - kb * 8 : a.xb;
+    Frag ring[U];
+    KqBdX xr[U];
+    if (U >= (a.K / 256 + KS - 1) / KS) {  // (uniform) the whole slice in flight: U loads, no ring turns
+      const int n = ke - kb;
+      auto sbi = [&](int u) { return max(min(kb + u, ke - 1), 0); };  // clamped: loads past the slice are unused
+      if constexpr (QL) ql_load(qr, a, kb, n, lane);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        kq_load_w_bd<T>(ring[u], Wr[0] + (size_t)sbi(u) * TB, lane);
+        if constexpr (!QL) xr[u] = kq_bd_x<T>(bq, bd, bb, sbi(u), lane);
+      }
+      if constexpr (QL) {
+        ql_build(qr, a, n, lane, iq, id, ib);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int u = 0; u < U; ++u) xr[u] = kq_bd_x<T>(bq, bd, bb, n > 0 ? sbi(u) : kb, lane);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (u < n) kq_compute_bd<T>(acc[0][0], ring[u], xr[u], lane);
+      kq_bd_finish<T>(acc[0][0]);
+    } else {
+    if constexpr (QL) ql_load(qr, a, kb, ke - kb, lane);
+    if (nfull > 0) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        kq_load_w_bd<T>(ring[u], Wr[0] + (size_t)(sb + u) * TB, lane);
+        if constexpr (!QL) xr[u] = kq_bd_x<T>(bq, bd, bb, sb + u, lane);
+      }
+    }
+    if constexpr (QL) {
+      ql_build(qr, a, ke - kb, lane, iq, id, ib);
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
+      __builtin_amdgcn_wave_barrier();
+      if (nfull > 0)
+#pragma unroll
+        for (int u = 0; u < U; ++u) xr[u] = kq_bd_x<T>(bq, bd, bb, sb + u, lane);
+    }
+    if (nfull > 0) {
+      for (int ch = 1; ch < nfull; ++ch) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          kq_compute_bd<T>(acc[0][0], ring[u], xr[u], lane);
+          kq_load_w_bd<T>(ring[u], Wr[0] + (size_t)(sb + U + u) * TB, lane);
+          xr[u] = kq_bd_x<T>(bq, bd, bb, sb + U + u, lane);
+        }
+        sb += U;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) kq_compute_bd<T>(acc[0][0], ring[u], xr[u], lane);
+      sb += U;
+    }
+    for (; sb < ke; ++sb) {
+      Frag f;
+      kq_load_w_bd<T>(f, Wr[0] + (size_t)sb * TB, lane);
+      const KqBdX x = kq_bd_x<T>(bq, bd, bb, sb, lane);
+      kq_compute_bd<T>(acc[0][0], f, x, lane);
+    }
+    kq_bd_finish<T>(acc[0][0]);
+    }
+  } else {
+  Frag ring[U];
   if constexpr (QL) ql_load(qr, a, kb, ke - kb, lane);
   if (nfull > 0) {
 #pragma unroll
@@ -789,6 +1085,7 @@ __device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int 
     Frag f;
     load(f, sb);
     compute(f);
+  }
   }
 
 #pragma unroll
@@ -834,7 +1131,7 @@ __device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int 
   }
 }
 
-template <int KS, int RT, int NB, int EPI, int U, bool QL>
+template <int KS, int RT, int NB, int EPI, int U, bool QL, bool BD = false>
 __global__ __launch_bounds__(64 * KS) void mkq_kernel(MMArgs a) {
   __shared__ f32x4 red[KS][RT][NB][64];
   const int tile0 = blockIdx.x * RT;
@@ -843,9 +1140,9 @@ __global__ __launch_bounds__(64 * KS) void mkq_kernel(MMArgs a) {
   const int t_begin = seg ? a.kq_tile_end[seg - 1] : 0;
   const uint8_t* W = reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[seg];
   switch (a.kq_type[seg]) {
-    case 12: mkq_body<12, KS, RT, NB, EPI, U, QL>(a, W, tile0 - t_begin, tile0, red); break;
-    case 13: mkq_body<13, KS, RT, NB, EPI, U, QL>(a, W, tile0 - t_begin, tile0, red); break;
-    case 14: mkq_body<14, KS, RT, NB, EPI, U, QL>(a, W, tile0 - t_begin, tile0, red); break;
+    case 12: mkq_body<12, KS, RT, NB, EPI, U, QL, BD>(a, W, tile0 - t_begin, tile0, red); break;
+    case 13: mkq_body<13, KS, RT, NB, EPI, U, QL, BD>(a, W, tile0 - t_begin, tile0, red); break;
+    case 14: mkq_body<14, KS, RT, NB, EPI, U, QL, BD>(a, W, tile0 - t_begin, tile0, red); break;
   }
 }
 
@@ -859,8 +1156,11 @@ __global__ __launch_bounds__(64 * KS) void mkq_kernel(MMArgs a) {
 // of the scale arithmetic may still differ by an ulp).
 // CONTIG: the work-group's tiles are blockIdx.x*TPW + i (one segment of the matrix, starting at
 // tile tseg0, whose packed tiles start at Wseg) instead of blockIdx.x + i*G
-template <int T, int KS, int NKW, int TPW, int NB, int EPI, int U, bool QL, bool CONTIG = false>
+// BD: one token in the block-diagonal form (kq_compute_bd; NB = 1, M = 1): the ring holds weights
+// only, the wave's NKW super-blocks of activation operands stay in registers for all its tiles
+template <int T, int KS, int NKW, int TPW, int NB, int EPI, int U, bool QL, bool CONTIG = false, bool BD = false>
 __device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Wseg, int tseg0) {
+  static_assert(!BD || NB == 1, "block-diagonal form: one token");
   constexpr int TB = KqTile<T>::BYTES;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -902,11 +1202,23 @@ __device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Ws
     const int i = f / NKW, k = f % NKW;
     const int tile = min(tile_of(i), ntiles - 1) - tseg0;
     const uint8_t* Wt[1] = {W + ((size_t)tile * SB + kb + k) * TB};
-    kq_load_w<T, 1, NB>(fr, Wt, lane, g);
+    if constexpr (BD) kq_load_w_bd<T>(fr, Wt[0], lane);
+    else kq_load_w<T, 1, NB>(fr, Wt, lane, g);
   };
   auto load = [&](Frag& fr, int f) {
     load_w(fr, f);
-    kq_load_x<T, 1, NB>(fr, Xq, Xd, Xb, kb + f % NKW);
+    if constexpr (!BD) kq_load_x<T, 1, NB>(fr, Xq, Xd, Xb, kb + f % NKW);
+  };
+  // BD activation operands: the Q8_K row (QL: the wave image) indexed by absolute super-block
+  KqBdX bx[BD ? NKW : 1];
+  auto load_bx = [&]() {
+    if constexpr (BD) {
+      const int8_t* bq = QL ? iq - kb * 256 : a.xq;
+      const float* bd = QL ? id - kb : a.xd;
+      const float* bb = QL ? ib - kb * 8 : a.xb;
+#pragma unroll
+      for (int k = 0; k < NKW; ++k) bx[k] = kq_bd_x<T>(bq, bd, bb, kb + k, lane);
+    }
   };
   constexpr int LU = (EPI == EPI_SWIGLU) ? 32 : 64;
   // one token's q|k|v: pos / slot once, each tile's RoPE pairs when the tile starts (mm_pers_kernel's
@@ -939,6 +1251,7 @@ __device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Ws
   Frag ring[U];
   QlRegs qr;
   if constexpr (QL) ql_load(qr, a, kb, NKW, lane);  // once per work-group: the slice is the same for every tile
+  if constexpr (BD && !QL) load_bx();
 #pragma unroll
   for (int f = 0; f < U; ++f) {
     if constexpr (QL) load_w(ring[f], f);
@@ -948,8 +1261,10 @@ __device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Ws
     ql_build(qr, a, NKW, lane, iq, id, ib);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
     __builtin_amdgcn_wave_barrier();
+    if constexpr (BD) load_bx();
+    else
 #pragma unroll
-    for (int f = 0; f < U; ++f) kq_load_x<T, 1, NB>(ring[f], Xq, Xd, Xb, kb + f % NKW);
+      for (int f = 0; f < U; ++f) kq_load_x<T, 1, NB>(ring[f], Xq, Xd, Xb, kb + f % NKW);
   }
   // fully unrolled over the TPW tiles (a loop back-edge renames the ring with moves that wait for
   // the loads, draining it)
@@ -962,12 +1277,14 @@ __device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Ws
 #pragma unroll
     for (int k = 0; k < NKW; ++k) {
       const int f = i * NKW + k;
-      kq_compute<T, 1, NB>(acc, ring[f % U], g);
+      if constexpr (BD) kq_compute_bd<T>(acc[0][0], ring[f % U], bx[k], lane);
+      else kq_compute<T, 1, NB>(acc, ring[f % U], g);
       if (f + U < TPW * NKW) load(ring[f % U], f + U);
       // issue the refill here: left to itself the scheduler sinks a tile's refills below its last
       // compute, which then waits for vmcnt(0) (the ring empty once per tile)
       __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (BD) kq_bd_finish<T>(acc[0][0]);
 #pragma unroll
     for (int n = 0; n < NB; ++n) red[i & 1][w][n][lane] = acc[0][n];
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only: the ring stays in flight
@@ -977,9 +1294,9 @@ __device__ __forceinline__ void mkq_pers_body(const MMArgs& a, const uint8_t* Ws
   }
 }
 
-template <int T, int KS, int NKW, int TPW, int NB, int EPI, int U, bool QL>
+template <int T, int KS, int NKW, int TPW, int NB, int EPI, int U, bool QL, bool BD>
 __global__ __launch_bounds__(64 * KS) void mkq_pers_kernel(MMArgs a) {
-  mkq_pers_body<T, KS, NKW, TPW, NB, EPI, U, QL>(a, reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[0], 0);
+  mkq_pers_body<T, KS, NKW, TPW, NB, EPI, U, QL, false, BD>(a, reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[0], 0);
 }
 
 // One token of a matrix with row segments of different types (q|k Q4_K + v Q6_K): TPW contiguous
@@ -992,9 +1309,89 @@ __global__ __launch_bounds__(64 * KS) void mkq_pers_seg_kernel(MMArgs a) {
   const int tb = seg ? a.kq_tile_end[seg - 1] : 0;
   const uint8_t* Ws = reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[seg];
   switch (a.kq_type[seg]) {
-    case 12: mkq_pers_body<12, KS, NKW, TPW, 1, EPI, U, true, true>(a, Ws, tb); break;
-    case 13: mkq_pers_body<13, KS, NKW, TPW, 1, EPI, U, true, true>(a, Ws, tb); break;
-    case 14: mkq_pers_body<14, KS, NKW, TPW, 1, EPI, U, true, true>(a, Ws, tb); break;
+    case 12: mkq_pers_body<12, KS, NKW, TPW, 1, EPI, U, true, true, true>(a, Ws, tb); break;
+    case 13: mkq_pers_body<13, KS, NKW, TPW, 1, EPI, U, true, true, true>(a, Ws, tb); break;
+    case 14: mkq_pers_body<14, KS, NKW, TPW, 1, EPI, U, true, true, true>(a, Ws, tb); break;
+  }
+}
+
+// One token, every wave owning whole tiles (the whole K): the tile-persistent kernels above split
+// each tile's K over 8 waves, so every tile ends in an LDS reduction behind a work-group barrier,
+// where the slowest wave and wave 0's epilogue hold up the rest.  Here wave w of work-group b walks
+// tiles (b * W + w) + i * gridDim.x * W, i < TPW, its U-deep weight ring running across them, and
+// finishes each tile from registers.  The token's activation operands are built once per
+// work-group in LDS, already in block-diagonal form: the Q8_K row (RMS_NORM + quantise on load by
+// the first SB/8 waves, ql_build), then per super-block s and sub-block j the B operand of every
+// lane (its 8 q or zeros) and per lane its bsum -- so a super-block's B operands are 8 conflict-free
+// ds_read_b64 and no VALU.  Two barriers per launch.  K = 256 * SB, SB 8 or 16.
+template <int SB>
+struct KqBdImg {
+  int8_t q[SB * 256];  // Q8_K row (permuted), d, sub-block sums: ql_build's image
+  float d[SB];
+  float b[SB * 8];
+  u32x2 B[SB][8][64];  // block-diagonal B operand of lane l for (super-block, sub-block)
+  int bs[SB][64];      // kq_bd_x's bs of lane l
+};
+
+template <int T, int W, int SB, int TPW, int EPI, int U>
+__global__ __launch_bounds__(64 * W) void mkq_bd_tile_kernel(MMArgs a) {
+  static_assert(SB % 8 == 0 && SB / 8 <= W, "the first SB/8 waves quantise 8 super-blocks each");
+  constexpr int TB = KqTile<T>::BYTES;
+  constexpr int NF = TPW * SB;  // flat ring positions (tile i, super-block k)
+  __shared__ KqBdImg<SB> im;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ntiles = a.N / TILE_N;
+  const int G = gridDim.x * W;
+  const uint8_t* W0 = reinterpret_cast<const uint8_t*>(a.W) + a.kq_off[0];
+  auto tile_of = [&](int i) { return (int)blockIdx.x * W + w + i * G; };
+  using Frag = KqFrag<1, 1>;
+  Frag ring[U];
+  auto load_w = [&](Frag& f, int fl) {
+    const int tile = min(tile_of(fl / SB), ntiles - 1);  // phantom tiles re-read the last (dropped)
+    kq_load_w_bd<T>(f, W0 + ((size_t)tile * SB + fl % SB) * TB, lane);
+  };
+
+  // prologue: the quantising waves load their norm operands first, every wave issues its ring
+  QlRegs qr;
+  const bool quant = w < SB / 8;
+  if (quant) ql_load(qr, a, 8 * w, 8, lane);
+#pragma unroll
+  for (int f = 0; f < U; ++f) load_w(ring[f], f);
+  if (quant) ql_build(qr, a, 8, lane, im.q + 8 * w * 256, im.d + 8 * w, im.b + 8 * w * 8);
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the image is written (the weight ring stays in flight)
+  __builtin_amdgcn_s_barrier();
+  // block-diagonal operands: thread t handles (super-block, lane) pairs t, t + 64W, ...
+  for (int u = threadIdx.x; u < SB * 64; u += 64 * W) {
+    const int sb = u >> 6, l = u & 63;
+    const KqBdX x = kq_bd_x_lane<T>(im.q, im.d, im.b, sb, l);
+    const int jsel = T == 14 ? ((l & 15) >> 1) : (l & 15);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) im.B[sb][j][l] = jsel == j ? x.X : u32x2{0u, 0u};
+    im.bs[sb][l] = x.bs;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_s_barrier();
+
+  // tiles in a run-time loop, super-blocks unrolled: U divides SB, so every tile uses the ring
+  // slots in the same order and the loop carries the ring without renaming it
+  static_assert(SB % U == 0, "ring slots line up across tiles");
+  for (int i = 0; i < TPW; ++i) {
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < SB; ++k) {
+      kq_compute_bd_lds<T>(acc, ring[k % U], im.B[k], im.bs[k][lane], im.d[k], lane);
+      const int fl = i * SB + k + U;
+      if (fl < NF) load_w(ring[k % U], fl);
+      __builtin_amdgcn_sched_barrier(0);  // the refill issues here, not sunk below the next compute
+    }
+    kq_bd_finish<T>(acc);
+    const int tile = tile_of(i);
+    f32x4 up = acc;
+    if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) up[r] = __shfl_xor(acc[r], 32);
+    }
+    if (tile < ntiles && (lane & 15) == 0 && (EPI != EPI_SWIGLU || lane < 32)) epi_store<EPI>(a, tile, lane, 0, acc, up);
   }
 }
 
@@ -1005,17 +1402,22 @@ static int launch_kq_qkv_pers(const MMArgs& a, hipStream_t s) {
   if (off || a.M != 1 || a.xq != nullptr || a.K != 4096 || (a.N / TILE_N) % 2) return -1;
   for (int i = 0; i < a.kq_n; ++i)
     if (a.kq_tile_end[i] % 2) return -1;
-  mkq_pers_seg_kernel<8, 2, 2, EPI_QKV, 2><<<a.N / TILE_N / 2, 512, 8 * QL_WAVE_BYTES, s>>>(a);
+  mkq_pers_seg_kernel<8, 2, 2, EPI_QKV, 4><<<a.N / TILE_N / 2, 512, 8 * QL_WAVE_BYTES, s>>>(a);
   return 0;
 }
 
-template <int T, int NKW, int TPW, int NB, int EPI, int U>
+// U: ring depth for 2..16 tokens; UB: one token (block-diagonal, weights only in the ring)
+// (one token: KSB waves per work-group, each NKW * 8 / KSB super-blocks of every tile)
+template <int T, int NKW, int TPW, int NB, int EPI, int U, int UB, int KSB = 8>
 static void launch_kq_pers_t(const MMArgs& a, int ntiles, hipStream_t s) {
   const int grid = (ntiles + TPW - 1) / TPW;
-  if (a.xq == nullptr)
-    mkq_pers_kernel<T, 8, NKW, TPW, NB, EPI, U, true><<<grid, 512, 8 * QL_WAVE_BYTES, s>>>(a);
+  constexpr int NKB = NKW * 8 / KSB;
+  if (a.xq == nullptr)  // one token, quantised on load
+    mkq_pers_kernel<T, KSB, NKB, TPW, NB, EPI, UB, true, true><<<grid, 64 * KSB, KSB * QL_WAVE_BYTES, s>>>(a);
+  else if (a.M == 1)
+    mkq_pers_kernel<T, KSB, NKB, TPW, NB, EPI, UB, false, true><<<grid, 64 * KSB, 0, s>>>(a);
   else
-    mkq_pers_kernel<T, 8, NKW, TPW, NB, EPI, U, false><<<grid, 512, 0, s>>>(a);
+    mkq_pers_kernel<T, 8, NKW, TPW, NB, EPI, U, false, false><<<grid, 512, 0, s>>>(a);
 }
 
 // single-type matrices of the Llama shapes: gate/up (K 4096, 1792 tiles / TinyLlama K 2048, 704),
@@ -1025,12 +1427,49 @@ template <int T, int NB, int EPI>
 static int launch_kq_pers_ty(const MMArgs& a, int ntiles, hipStream_t s) {
   const int SB = a.K / 256;
   if constexpr (EPI == EPI_SWIGLU) {
-    if (SB == 16 && ntiles == 1792) return launch_kq_pers_t<T, 2, 7, NB, EPI, 2>(a, ntiles, s), 0;
-    if (SB == 8 && ntiles == 704) return launch_kq_pers_t<T, 1, 3, NB, EPI, 2>(a, ntiles, s), 0;
+    if (SB == 16 && ntiles == 1792) return launch_kq_pers_t<T, 2, 7, NB, EPI, 2, 4>(a, ntiles, s), 0;
+    if (SB == 8 && ntiles == 704) return launch_kq_pers_t<T, 1, 3, NB, EPI, 2, 3>(a, ntiles, s), 0;
   } else {
-    if (SB == 16 && ntiles > 256 * 8) return launch_kq_pers_t<T, 2, 8, NB, EPI, 2>(a, ntiles, s), 0;  // 16: spills
-    if (SB == 8 && ntiles > 256 * 4) return launch_kq_pers_t<T, 1, 8, NB, EPI, 2>(a, ntiles, s), 0;
+    if (SB == 16 && ntiles > 256 * 8) return launch_kq_pers_t<T, 2, 8, NB, EPI, 2, 4>(a, ntiles, s), 0;  // 16: spills
+    if (SB == 8 && ntiles > 256 * 4) return launch_kq_pers_t<T, 1, 8, NB, EPI, 2, 4>(a, ntiles, s), 0;
   }
+  return -1;
+}
+
+// one token quantised on load, single-type gate/up or lm_head: mkq_bd_tile_kernel when the shape has
+// an instantiation (K 4096 / 2048: Llama-3-8B, TinyLlama; K 8192 spills), else -1
+template <int T, int EPI>
+static int launch_kq_bd_tile_t(const MMArgs& a, int ntiles, hipStream_t s) {
+  const int SB = a.K / 256;
+  auto go = [&](auto wc, auto sbc, auto tc) {
+    constexpr int W = decltype(wc)::value, S = decltype(sbc)::value, TP = decltype(tc)::value;
+    const int grid = (ntiles + W * TP - 1) / (W * TP);
+    mkq_bd_tile_kernel<T, W, S, TP, EPI, 8><<<grid, 64 * W, 0, s>>>(a);
+    return 0;
+  };
+  using std::integral_constant;
+  if constexpr (EPI == EPI_SWIGLU) {
+    if (SB == 16 && ntiles <= 1792) return go(integral_constant<int, 7>{}, integral_constant<int, 16>{}, integral_constant<int, 1>{});
+    if (SB == 8 && ntiles <= 768) return go(integral_constant<int, 3>{}, integral_constant<int, 8>{}, integral_constant<int, 1>{});
+  } else {
+    if (SB == 16 && ntiles <= 8192) return go(integral_constant<int, 8>{}, integral_constant<int, 16>{}, integral_constant<int, 4>{});
+    if (SB == 8 && ntiles <= 2048) return go(integral_constant<int, 8>{}, integral_constant<int, 8>{}, integral_constant<int, 1>{});
+  }
+  return -1;
+}
+static int launch_kq_bd_tile(int epi, const MMArgs& a, int ntiles, hipStream_t s) {
+  static const bool off = getenv("MX_NO_KQ_BD_TILE") != nullptr;  // tests: the K-split persistent kernel's path
+  if (off || a.M != 1 || a.xq != nullptr || a.kq_n != 1 || !a.xf || (a.norm_w && (!a.ssq || a.np * 16 != a.K)))
+    return -1;
+  const int t = a.kq_type[0];
+  if (epi == EPI_SWIGLU)
+    return t == 12 ? launch_kq_bd_tile_t<12, EPI_SWIGLU>(a, ntiles, s)
+         : t == 13 ? launch_kq_bd_tile_t<13, EPI_SWIGLU>(a, ntiles, s)
+                   : launch_kq_bd_tile_t<14, EPI_SWIGLU>(a, ntiles, s);
+  if (epi == EPI_F32)
+    return t == 12 ? launch_kq_bd_tile_t<12, EPI_F32>(a, ntiles, s)
+         : t == 13 ? launch_kq_bd_tile_t<13, EPI_F32>(a, ntiles, s)
+                   : launch_kq_bd_tile_t<14, EPI_F32>(a, ntiles, s);
   return -1;
 }
 
@@ -1038,6 +1477,7 @@ static int launch_kq_pers(int epi, const MMArgs& a, int ntiles, hipStream_t s) {
   // MX_NO_KQ_PERS: the one-tile-per-work-group kernel (read per launch: tests compare the two)
   static const bool off = getenv("MX_NO_KQ_PERS") != nullptr;  // tests: the grouped kernel's path
   if (off || a.kq_n != 1 || a.M > 16) return -1;  // 17-32 rows (two column tiles): spills
+  if (launch_kq_bd_tile(epi, a, ntiles, s) == 0) return 0;
   const int t = a.kq_type[0];
   auto by_nb = [&](auto nb) -> int {
     constexpr int NB = decltype(nb)::value;
@@ -1056,10 +1496,27 @@ static int launch_kq_pers(int epi, const MMArgs& a, int ntiles, hipStream_t s) {
   return by_nb(std::integral_constant<int, 1>{});
 }
 
+// one token, one tile per work-group: 8 waves split K, each with its whole slice of super-blocks in
+// flight (U >= slice: 1, 2, 4, 7, 8); longer slices ring 2 deep
+template <int EPI, bool QL>
+static void launch_mkq_bd(const MMArgs& a, int ntiles, hipStream_t s) {
+  const int per = (a.K / 256 + 7) / 8;
+  const dim3 grid(ntiles, 1);
+  const size_t lds = QL ? 8 * QL_WAVE_BYTES : 0;
+  if (per <= 1) mkq_kernel<8, 1, 1, EPI, 1, QL, true><<<grid, 512, lds, s>>>(a);
+  else if (per <= 2) mkq_kernel<8, 1, 1, EPI, 2, QL, true><<<grid, 512, lds, s>>>(a);
+  else if (per <= 4) mkq_kernel<8, 1, 1, EPI, 4, QL, true><<<grid, 512, lds, s>>>(a);
+  else if (QL && per <= 7) mkq_kernel<8, 1, 1, EPI, QL ? 7 : 2, QL, true><<<grid, 512, lds, s>>>(a);
+  else if (QL && per <= 8) mkq_kernel<8, 1, 1, EPI, QL ? 8 : 2, QL, true><<<grid, 512, lds, s>>>(a);
+  else mkq_kernel<8, 1, 1, EPI, 2, QL, true><<<grid, 512, lds, s>>>(a);  // (quantise-on-load slices are <= 8)
+}
+
 template <int EPI>
 static void launch_mkq_epi(const MMArgs& a, int ntiles, hipStream_t s) {
   if (a.xq == nullptr) {  // one token, quantised on load (launch_mkq checked the slice fits)
-    mkq_kernel<8, 1, 1, EPI, 2, true><<<dim3(ntiles, 1), 512, 8 * QL_WAVE_BYTES, s>>>(a);
+    launch_mkq_bd<EPI, true>(a, ntiles, s);
+  } else if (a.M == 1) {
+    launch_mkq_bd<EPI, false>(a, ntiles, s);
   } else if (a.M <= 16) {
     mkq_kernel<8, 1, 1, EPI, 2, false><<<dim3(ntiles, 1), 512, 0, s>>>(a);
   } else if (a.M <= 32) {  // (a 2-deep ring spills ~460 B/lane at two column tiles: U = 1)
