@@ -2383,8 +2383,16 @@ void launch_quantize_q8(int8_t* xq, float* xd, const float* src, int ld, int M, 
 // the scale from the residual writers' ssq partials, as mm_kernel's XS path -- into registers
 // BEFORE issuing its weight ring (QP float4 per lane and row: slice <= 256*QP), then quantises
 // them to Q8_0 (8 lanes per block) into a wave-private LDS image its B fragments are read from.
-template <int KS, int RT, int NB, int EPI, int U, int QP, int QM, bool Q4>
+//
+// BD (one token): the block-diagonal form of kquant.hip's kq_compute_bd -- 16 consecutive 32-weight
+// blocks (8 tiles) of the wave's K-slice share one MFMA accumulator, block j's B operand carrying the
+// token's 32 q in column j only, so C column c is block c's exact int32 product for the tile's 16 rows;
+// each lane scales its column once per 16 blocks by d_w * d_x of that block (ggml's per-block f32
+// product), and one DPP row sum per tile adds the columns.  Same block integers and per-block f32
+// products as the per-tile form; only the f32 summation order of the blocks differs.
+template <int KS, int RT, int NB, int EPI, int U, int QP, int QM, bool Q4, bool BD = false>
 __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
+  static_assert(!BD || (RT == 1 && NB == 1 && 8 % U == 0), "block-diagonal form: one token, one tile, U | 8");
   constexpr int TB = Q4 ? Q4_TILE_BYTES : Q8_TILE_BYTES, SO = Q4 ? 512 : 1024;  // tile bytes, scale offset
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -2506,12 +2514,8 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
     }
   };
 
-  Frag ring[U];
-  int kt = kb;
-  const int nfull = (ke - kb) / U;
-#pragma unroll
-  for (int u = 0; u < U; ++u) load_w(ring[u], max(0, min(kt + u, ke - 1)));  // unconditional (see xs_load); unused when nfull == 0
-  if constexpr (QP > 0) {  // build the image while the ring is in flight
+  auto build_image = [&]() {  // QP: quantise the wave's K-slice into its LDS image
+  if constexpr (QP > 0) {
 #pragma unroll
     for (int c = 0; c < QM; ++c) {
       if (c >= a.M) break;
@@ -2542,6 +2546,77 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
     __builtin_amdgcn_wave_barrier();
   }
+  };
+
+  if constexpr (BD) {
+    // ring = the weight int8 / nibble parts of the slice's tiles; per group of 8 tiles each lane's
+    // own operands: the token's 8 q of block c (c = lane & 15: tile c >> 1, half c & 1), that block's
+    // d_x, and the 4 rows' f16 d_w of that block -- loaded one group ahead
+    const int c = lane & 15, q = lane >> 4;
+    const int8_t* xq0 = QP > 0 ? reinterpret_cast<const int8_t*>(qimg) - kb * Q8_TILE_K : a.xq;
+    const float* xd0 = QP > 0 ? dimg - 2 * kb : a.xd;
+    u32x4 rq[U];
+    auto load_q = [&](int u, int kt) {
+      const uint8_t* t = Wr[0] + (size_t)max(0, min(kt, ke - 1)) * TB;
+      if constexpr (Q4) {
+        const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(t) + lane);
+        rq[u] = u32x4{v[0], v[1], 0u, 0u};
+      } else {
+        rq[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t) + lane);
+      }
+    };
+    struct GrpOps { u32x2 x, dw; float dx; };
+    auto load_grp_w = [&](GrpOps& o, int g) {
+      const int t = max(0, min(kb + 8 * g + (c >> 1), ke - 1));
+      o.dw = *reinterpret_cast<const u32x2*>(Wr[0] + (size_t)t * TB + SO + 16 * q + 8 * (c & 1));
+    };
+    auto load_grp_x = [&](GrpOps& o, int g) {
+      const int tt = kb + 8 * g + (c >> 1), t = max(0, min(tt, ke - 1));
+      const u32x2 v = *reinterpret_cast<const u32x2*>(xq0 + (size_t)t * Q8_TILE_K + 16 * q + 8 * (c & 1));
+      o.x = tt < ke ? v : u32x2{0u, 0u};  // blocks past the slice add nothing
+      o.dx = xd0[2 * t + (c & 1)];
+    };
+    const int ng = (ke - kb + 7) / 8;
+    GrpOps cur, nxt;
+#pragma unroll
+    for (int u = 0; u < U; ++u) load_q(u, kb + u);
+    load_grp_w(cur, 0);
+    if constexpr (QP == 0) load_grp_x(cur, 0);
+    build_image();
+    if constexpr (QP > 0) load_grp_x(cur, 0);
+    f32x4 ab = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < ng; ++g) {
+      load_grp_w(nxt, g + 1);
+      load_grp_x(nxt, g + 1);
+      i32x4 C0 = i32x4{0, 0, 0, 0}, C1 = i32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int kt = kb + 8 * g + u;
+        if (kt < ke) {  // (wave-uniform)
+          const u32x4& f = rq[u % U];
+          const long a0 = Q4 ? q4_operand(f[0]) : (long)(((unsigned long)f[1] << 32) | f[0]);
+          const long a1 = Q4 ? q4_operand(f[1]) : (long)(((unsigned long)f[3] << 32) | f[2]);
+          const bool on0 = c == 2 * u, on1 = c == 2 * u + 1;
+          const long b0 = (long)(((unsigned long)(on0 ? cur.x[1] : 0u) << 32) | (on0 ? cur.x[0] : 0u));
+          const long b1 = (long)(((unsigned long)(on1 ? cur.x[1] : 0u) << 32) | (on1 ? cur.x[0] : 0u));
+          C0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, b0, C0, 0, 0, 0);
+          C1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, b1, C1, 0, 0, 0);
+        }
+        load_q(u % U, kt + U);  // unconditional, clamped (the refill past the slice is unused)
+      }
+      const f16x4 dw = __builtin_bit_cast(f16x4, cur.dw);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ab[i] = fmaf((float)dw[i] * cur.dx, (float)(C0[i] + C1[i]), ab[i]);
+      cur = nxt;
+    }
+    acc[0][0] = f32x4{row16_sum(ab[0]), row16_sum(ab[1]), row16_sum(ab[2]), row16_sum(ab[3])};
+  } else {
+  Frag ring[U];
+  int kt = kb;
+  const int nfull = (ke - kb) / U;
+#pragma unroll
+  for (int u = 0; u < U; ++u) load_w(ring[u], max(0, min(kt + u, ke - 1)));  // unconditional (see xs_load); unused when nfull == 0
+  build_image();  // while the ring is in flight
   if (nfull > 0) {
     for (int ch = 1; ch < nfull; ++ch) {
 #pragma unroll
@@ -2559,6 +2634,7 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
     Frag f;
     load_w(f, kt);
     mma(f, kt);
+  }
   }
 
 #pragma unroll
@@ -2610,7 +2686,8 @@ static void launch_mq8_ql(const MMArgs& a, hipStream_t s) {
   const int KT = a.K / Q8_TILE_K;
   const int QB = (KT + 7) / 8 * Q8_TILE_K + 16, QS = (KT + 7) / 8 * 2;
   const size_t lds = (size_t)8 * QM * (QB + 4 * QS);
-  mq8_kernel<8, 1, 1, EPI, 4, QP, QM, Q4><<<dim3(a.N / TILE_N, 1), 512, lds, s>>>(a);
+  if constexpr (QM == 1) mq8_kernel<8, 1, 1, EPI, 4, QP, QM, Q4, true><<<dim3(a.N / TILE_N, 1), 512, lds, s>>>(a);
+  else mq8_kernel<8, 1, 1, EPI, 4, QP, QM, Q4><<<dim3(a.N / TILE_N, 1), 512, lds, s>>>(a);
 }
 
 template <int EPI, int QP, bool Q4>
@@ -2631,7 +2708,9 @@ bool mq8_can_quantize_on_load(int M, int K, bool norm) {
 template <int EPI, bool Q4>
 static int launch_mq8_epi(const MMArgs& a, hipStream_t s) {
   const int ntiles = a.N / TILE_N;
-  if (a.M <= 16) {
+  if (a.M == 1) {
+    mq8_kernel<8, 1, 1, EPI, 4, 0, 1, Q4, true><<<dim3(ntiles, 1), 512, 0, s>>>(a);
+  } else if (a.M <= 16) {
     mq8_kernel<8, 1, 1, EPI, 4, 0, 1, Q4><<<dim3(ntiles, 1), 512, 0, s>>>(a);
   } else if (a.M <= 32) {
     const int cfg = ntiles % 4 ? 0 : EPI == EPI_QKV ? 1 : (EPI == EPI_SWIGLU || EPI == EPI_F32) ? 3 : 0;
