@@ -1540,6 +1540,77 @@ static void launch_mkq_epi(const MMArgs& a, int ntiles, hipStream_t s) {
 // f32 scaling), and the whole K stays in one wave, so the epilogue runs from registers.
 // Single-type matrices (one segment): gate/up and the lm_head of a K-quant file.
 // ---------------------------------------------------------------------------
+// 17-32 rows, Q4_K: the 6-bit sub-block scales folded into the int8 A operand.  kq_compute scales
+// every sub-block's int32 products per output (NB column tiles x 4 values x 8 sub-blocks of VALU
+// per super-block: VALU-bound at ~2.9 TB/s).  Here each 6-bit scale is split sc = 8h + l (l, h < 8),
+// so q * l and q * h (q < 16) are int8 values <= 105: every lane multiplies its 4-bit row values by
+// l and by h (v_pk_mul_lo_u16 on byte pairs: no product reaches a carry), and two accumulators take
+// sum_j (q_j * l_j) . x_j and sum_j (q_j * h_j) . x_j over the whole super-block -- on
+// v_mfma_i32_16x16x64_i8, two sub-blocks per MFMA (the K order inside one MFMA is the lanes' own, the
+// same for A and B).  S = C_l + 8 C_h is ggml's integer sum_j sc_j (q_j . x_j) exactly; the mins and
+// the f32 scaling are kq_compute's.
+template <int NB>
+__device__ __forceinline__ void kq_load_w_fold(KqFrag<1, NB>& f, const uint8_t* t, int lane) {
+  constexpr int SC = KqTile<12>::SC;
+  const int g = lane >> 4, rq = (lane & 15) >> 2;
+  f.qs[0][0] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t) + lane);
+  f.qs[0][1] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t + 1024) + lane);
+  // the scales of this lane's A row (lane & 15): byte lane & 3 of dwords 0..7 of its row group
+  f.sc[0][0] = *reinterpret_cast<const u32x4*>(t + SC + 64 * rq);
+  f.sc[0][1] = *reinterpret_cast<const u32x4*>(t + SC + 64 * rq + 16);
+  const uint8_t* mq = t + SC + 64 * rq + 32 + 4 * g;
+  f.mw[0] = u32x2{*reinterpret_cast<const uint32_t*>(mq), *reinterpret_cast<const uint32_t*>(mq + 16)};
+  f.dm[0] = *reinterpret_cast<const u32x4*>(t + SC + 256 + 16 * g);
+}
+
+template <int NB>
+__device__ __forceinline__ void kq_compute_fold(f32x4 (&acc)[1][NB], const KqFrag<1, NB>& f, int lane) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const int g = lane >> 4;
+  const uint32_t sel = 0x0C000C00u | (uint32_t)(lane & 3) * 0x00010001u;  // byte lane&3 -> bytes 0 and 2
+  i32x4 Cl[NB], Ch[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) Cl[n] = Ch[n] = i32x4{0, 0, 0, 0};
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {  // sub-blocks 2m, 2m+1
+    u32x4 Al, Ah;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int j = 2 * m + hh;
+      const uint32_t D = f.qs[0][j >> 2][j & 3];
+      const uint32_t lo = D & 0x0F0F0F0Fu, hi = (D >> 4) & 0x0F0F0F0Fu;
+      const uint32_t s2 = __builtin_amdgcn_perm(0u, f.sc[0][j >> 2][j & 3], sel);  // (sc, sc) as u16 pair
+      const u16x2 l2 = __builtin_bit_cast(u16x2, s2 & 0x00070007u), h2 = __builtin_bit_cast(u16x2, (s2 >> 3) & 0x00070007u);
+      Al[2 * hh] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, lo) * l2);
+      Al[2 * hh + 1] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, hi) * l2);
+      Ah[2 * hh] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, lo) * h2);
+      Ah[2 * hh + 1] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, hi) * h2);
+    }
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const i32x4 B = __builtin_bit_cast(i32x4, f.x[n][m]);
+      Cl[n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, Al), B, Cl[n], 0, 0, 0);
+      Ch[n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, Ah), B, Ch[n], 0, 0, 0);
+    }
+  }
+  const int rb = 8 * (lane & 3);
+  const float m0 = (float)((f.mw[0][0] >> rb) & 0xFFu), m1 = (float)((f.mw[0][1] >> rb) & 0xFFu);
+  const f16x8 dm = __builtin_bit_cast(f16x8, f.dm[0]);
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    const float dx = f.dx[n];
+    f32x4 Mn = __builtin_amdgcn_mfma_f32_16x16x4f32(m0, f.xb[n][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    Mn = __builtin_amdgcn_mfma_f32_16x16x4f32(m1, f.xb[n][1], Mn, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int S = Cl[n][i] + 8 * Ch[n][i];
+      acc[0][n][i] += ((float)dm[i] * dx) * (float)S;
+      acc[0][n][i] -= ((float)dm[4 + i] * dx) * Mn[i];
+    }
+  }
+  (void)g;
+}
+
 template <int T, int W, int NB, int EPI, int U>
 __device__ __forceinline__ void mkq_wide_body(const MMArgs& a, int tile, const uint8_t* Wseg, int tile_in_seg) {
   constexpr int TB = KqTile<T>::BYTES;
@@ -1604,9 +1675,11 @@ __device__ __forceinline__ void mkq_wide_body(const MMArgs& a, int tile, const u
 
   using Frag = KqFrag<1, NB>;
   Frag ring[U];
+  constexpr bool FOLD = T == 12;  // Q4_K: scales folded into the A operand (kq_compute_fold)
   auto load_w = [&](Frag& f, int sb) {
     const uint8_t* Wt[1] = {Wr + (size_t)sb * TB};
-    kq_load_w<T, 1, NB>(f, Wt, lane, g);
+    if constexpr (FOLD) kq_load_w_fold<NB>(f, Wt[0], lane);
+    else kq_load_w<T, 1, NB>(f, Wt, lane, g);
   };
   f32x4 acc[1][NB];
 #pragma unroll
@@ -1635,7 +1708,8 @@ __device__ __forceinline__ void mkq_wide_body(const MMArgs& a, int tile, const u
       f.dx[n] = sdx[buf][row];
       if constexpr (T != 14) f.xb[n] = *reinterpret_cast<const f32x2*>(&ssb[buf][row][2 * g]);
     }
-    kq_compute<T, 1, NB>(acc, f, g);
+    if constexpr (FOLD) kq_compute_fold<NB>(acc, f, lane);
+    else kq_compute<T, 1, NB>(acc, f, g);
     load_w(f, min(sb + U, nsb - 1));  // past the end: re-read the last super-block (no branch)
     store_x(1 - H, buf ^ 1);
     __syncthreads();
