@@ -1607,8 +1607,12 @@ __global__ __launch_bounds__(256) void swiglu_finish_kernel(MMArgs a, const floa
   }
 }
 
-template <int EPI, int NBUF>
+// RW: row tiles per wave -- 4 (256-row blocks) or 3 (192-row blocks, for N whose 256-row grid leaves
+// the last round of work-groups part-empty: Llama-3-8B q|k|v, N 6144 = 24 x 256 -> 384 blocks = 1.5
+// rounds on 256 CUs, = 32 x 192 -> 512 = 2 full rounds)
+template <int EPI, int NBUF, int RW = 4>
 __global__ __launch_bounds__(512, 1) void gemm_kernel(MMArgs a) {
+  constexpr int BN = 64 * RW, AT = 4 * RW;  // rows per block, A (row) tiles per block
   __shared__ __attribute__((aligned(1024))) uint8_t lds[NBUF * 32768];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1622,10 +1626,13 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(MMArgs a) {
   const int m0 = mb * GB_M;
   const int r16 = lane & 15;
 
-  // wave w copies A tiles 2w, 2w+1 and B (token) tiles 2w, 2w+1 of every k-tile.  Sources as a
-  // wave-uniform base + a 32-bit per-lane offset (3 VGPRs instead of 8: the loop runs at the cap)
-  const uint8_t* abase = reinterpret_cast<const uint8_t*>(a.W) + (size_t)(nb * 16 + w * 2) * KT * 1024;
-  const size_t astep = (size_t)KT * 1024;  // next row tile
+  // wave w copies A tiles 2w, 2w+1 (RW = 3: the last two waves repeat tile AT-1 -- the same bytes to
+  // the same LDS slot, so every wave still issues 4 loads per k-tile for the counted waits) and B
+  // (token) tiles 2w, 2w+1 of every k-tile.  Sources as a wave-uniform base + a 32-bit per-lane
+  // offset (3 VGPRs instead of 8: the loop runs at the cap)
+  const int at0 = min(w * 2, AT - 1), at1 = min(w * 2 + 1, AT - 1);
+  const uint8_t* abase = reinterpret_cast<const uint8_t*>(a.W) + (size_t)(nb * AT + at0) * KT * 1024;
+  const size_t astep = (size_t)(at1 - at0) * KT * 1024;  // the second row tile
   const uint32_t aoff = lane * 16;
   uint32_t boff[2];
 #pragma unroll
@@ -1637,28 +1644,28 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(MMArgs a) {
     uint8_t* base = lds + (kt % NBUF) * 32768;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int t = w * 2 + i;
-      __builtin_amdgcn_global_load_lds((gvoid*)(abase + i * astep + (size_t)kt * 1024 + aoff), (lvoid*)(base + t * 1024),
+      const int t = w * 2 + i, ta = i ? at1 : at0;
+      __builtin_amdgcn_global_load_lds((gvoid*)(abase + i * astep + (size_t)kt * 1024 + aoff), (lvoid*)(base + ta * 1024),
                                        16, 0, 0);
       __builtin_amdgcn_global_load_lds((gvoid*)(a.X + boff[i] + (size_t)kt * TILE_K), (lvoid*)(base + 16384 + t * 1024),
                                        16, 0, 0);
     }
   };
 
-  f32x4 acc[4][8];
+  f32x4 acc[RW][8];
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < RW; ++r)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   struct Frags {
-    u32x4 a[4], b[8];
+    u32x4 a[RW], b[8];
   };
   auto read = [&](Frags& f, int kt) {
     const uint8_t* Ab = lds + (kt % NBUF) * 32768;
     const uint8_t* Bb = Ab + 16384;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) f.a[r] = *reinterpret_cast<const u32x4*>(Ab + (wn * 4 + r) * 1024 + lane * 16);
+    for (int r = 0; r < RW; ++r) f.a[r] = *reinterpret_cast<const u32x4*>(Ab + (wn * RW + r) * 1024 + lane * 16);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f.b[j] = *reinterpret_cast<const u32x4*>(Bb + (wm * 8 + j) * 1024 + lane * 16);
   };
@@ -1666,7 +1673,7 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(MMArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < RW; ++r)
         acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.a[r]),
                                                             __builtin_bit_cast(bf16x8, f.b[j]), acc[r][j], 0, 0, 0);
   };
@@ -1703,8 +1710,8 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(MMArgs a) {
     read(nxt, min(kt + 1, t1 - 1));
     mfma(cur);
     // the 12 reads first, then the 32 MFMAs (the default schedule issued the reads behind 24 MFMAs)
-    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, RW + 8, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, RW * 8, 0);
   };
   int kt = t0;
   for (; kt + 1 < t1; kt += 2) {
@@ -1713,9 +1720,9 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(MMArgs a) {
   }
   if (kt < t1) step(F0, F1, kt);
 
-  const int tile0 = nb * (GB_N / 16) + wn * 4;
+  const int tile0 = nb * AT + wn * RW;
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < RW; ++r)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const f32x4 sv = acc[r][j];
@@ -1772,9 +1779,23 @@ int launch_gemm_split(int epi, const MMArgs& a, float* slabs, size_t slab_floats
   return epi == EPI_RESID ? S : 0;
 }
 
+// fraction of the work-group slots of the last round (256 CUs, one block each) that is used
+static double gemm_round_fill(int blocks) { return (double)blocks / (256.0 * ((blocks + 255) / 256)); }
+
 int launch_gemm(int epi, const MMArgs& a, hipStream_t s) {
   if (a.M < 1 || !a.X || !gemm_supported(a.N, a.K)) return -1;
-  const int grid = (a.N / GB_N) * ((a.M + GB_M - 1) / GB_M);
+  const int nm = (a.M + GB_M - 1) / GB_M;
+  const int grid = (a.N / GB_N) * nm;
+  if (a.N % 192 == 0 && gemm_round_fill((a.N / 192) * nm) > gemm_round_fill(grid) + 0.05) {
+    const int g3 = (a.N / 192) * nm;
+    switch (epi) {
+      case EPI_F32: gemm_kernel<EPI_F32, GEMM_NBUF, 3><<<g3, 512, 0, s>>>(a); return 0;
+      case EPI_RESID: gemm_kernel<EPI_RESID, GEMM_NBUF, 3><<<g3, 512, 0, s>>>(a); return 0;
+      case EPI_QKV: gemm_kernel<EPI_QKV, GEMM_NBUF, 3><<<g3, 512, 0, s>>>(a); return 0;
+      case EPI_SWIGLU: gemm_kernel<EPI_SWIGLU, GEMM_NBUF, 3><<<g3, 512, 0, s>>>(a); return 0;
+    }
+    return -1;
+  }
   switch (epi) {
     case EPI_F32: launch_gemm_v<EPI_F32>(a, grid, s); return 0;
     case EPI_RESID: launch_gemm_v<EPI_RESID>(a, grid, s); return 0;
