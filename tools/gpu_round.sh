@@ -24,13 +24,13 @@ for s in $STEPS; do
       tail -1 $OUT/bench.log ;;
     prof)
       MX_NO_GRAPHS=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- \
-        python3 bench.py --steps 16 --warmup 2 --batch1-steps 8 --tiny-tokens 16 --prefill-prompts 0 --q8-steps 0 --kq-steps 0 --big-steps 0 --no-cpu-baseline > $OUT/prof.log 2>&1 \
+        python3 bench.py --steps 16 --warmup 2 --batch1-steps 8 --tiny-tokens 16 --prefill-prompts 0 --q8-steps 0 --kq-steps 0 --q40-steps 0 --big-steps 0 --geometry-steps 0 --serve-requests 0 --no-cpu-baseline > $OUT/prof.log 2>&1 \
         || { tail -30 $OUT/prof.log; exit 1; }
       tail -1 $OUT/prof.log ;;
     pmc)
       for grp in FETCH_SIZE WRITE_SIZE; do
         MX_NO_GRAPHS=1 timeout -s KILL 240 rocprofv3 --pmc $grp -d $OUT/pmc_$grp -o pmc -- \
-          python3 bench.py --steps 4 --warmup 1 --batch1-steps 0 --tiny-tokens 0 --prefill-prompts 0 --q8-steps 0 --kq-steps 0 --big-steps 0 --no-cpu-baseline > $OUT/pmc_$grp.log 2>&1 \
+          python3 bench.py --steps 4 --warmup 1 --batch1-steps 0 --tiny-tokens 0 --prefill-prompts 0 --q8-steps 0 --kq-steps 0 --q40-steps 0 --big-steps 0 --geometry-steps 0 --serve-requests 0 --no-cpu-baseline > $OUT/pmc_$grp.log 2>&1 \
           || { tail -30 $OUT/pmc_$grp.log; exit 1; }
       done ;;
   esac
