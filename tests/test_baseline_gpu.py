@@ -157,6 +157,54 @@ def test_8b_full_depth_32_sequences(mx, oracle_mod):
     assert exact >= 0.85 * M * (G + 1)
 
 
+def test_8b_full_depth_batch1(mx, oracle_mod):
+    """The bench's batch-1 shape at full depth: all 32 Llama-3-8B layers and the 128256-token head, one
+    sequence -- its prompt through the 17-64-row path, then one-token steps: a teacher-forced logits
+    step (the persistent GEMVs with RMS_NORM on load, the one-row attention) and 8 device greedy-loop
+    steps (the graph the bench replays), against the oracle with test_8b_full_depth_32_sequences' bar
+    (2x the oracle's self-deviation under 1e-6 activation noise)."""
+    from llama_p2p_amd import synth
+
+    name = "llama3-8b"
+    shape = synth.SHAPES[name]
+    G = 8
+    rng = np.random.default_rng(21)
+    prompt = np.concatenate([[1], rng.integers(3, shape.n_vocab, 23)]).astype(np.int32)
+    eng = mx.Engine(f"synthetic:{name}:seed=0", n_ctx=64, n_seq_max=2)
+    n = len(prompt)
+    eng.forward_rows([1] * (n - 1), list(range(n - 1)), [int(t) for t in prompt[:-1]], want_logits=False)
+    got = eng.forward_logits(prompt[-1:], n - 1, slot=1)[0]  # one-token step
+    first = int(np.argmax(got))
+    b = eng.batch(slots=[1], pos=[n], ids=[first], max_steps=G)
+    for _ in range(G):
+        b.step()
+    toks = b.tokens()[0].tolist()
+    b.close()
+    eng.close()
+    chain = [first] + toks
+    om = oracle_mod.OracleModel(shape, seed=0)
+    seq = np.concatenate([prompt, np.asarray(chain[:-1], np.int32)])
+    lg = om.context(64).eval(seq, 0, all_logits=True)
+    oracle_mod.q8_jitter(1e-6)
+    try:
+        self_dev = float(np.abs(om.context(64).eval(seq, 0, all_logits=True) - lg).max())
+    finally:
+        oracle_mod.q8_jitter(0.0)
+    om.close()
+    ref = lg[n - 1]
+    err = float(np.abs(got - ref).max())
+    exact = 0
+    for k, t in enumerate(chain):
+        row = lg[n - 1 + k]
+        bar = 2 * max(2 * self_dev, float(logit_tol(row).max()))
+        assert float(row.max() - row[t]) <= bar, f"step {k}: picked {t}, oracle max at {int(row.argmax())}"
+        exact += int(t == int(row.argmax()))
+    print(f"llama3-8b full depth, batch 1: step max|d| {err:.4g}, oracle self-deviation {self_dev:.4g} "
+          f"(max|ref| {np.abs(lg).max():.3g}); {exact}/{G + 1} greedy picks exact")
+    assert err <= 2 * self_dev + 1e-4 * float(np.abs(lg).max()), (err, self_dev)
+    assert exact >= G  # at most one near tie
+
+
 def test_8b_full_vocab_32_rows(mx, oracle_mod):
     """Config 3's step shape: Llama-3-8B layers with the 128256-token lm_head, exactly 32 rows (the
     17-64-row wide path).  Teacher-forced 32-row logits, the device top-k candidates of the sampler
