@@ -199,6 +199,9 @@ struct mx_engine {
   // gate/up as a row-tile-persistent GEMV with RMS_NORM on load (<= 4 rows); MX_NO_PERS=1 for A/B
   bool use_pers = getenv("MX_NO_PERS") == nullptr;
   bool q8_gemm_prefill = getenv("MX_Q8_GEMM_PREFILL") != nullptr;  // see enqueue_forward
+  // K-quant prefill chunks with ggml's arithmetic (Q8_K activations, the int8 K-quant GEMVs at every
+  // row count) instead of bf16 GEMMs over dequantised weights; see enqueue_forward
+  bool kq_ggml_prefill = getenv("MX_KQ_GGML_PREFILL") != nullptr;
   float* ssq = nullptr;  // [MAX_ROWS][n_embd/16] per-tile sums of squares of x
   // rows of the next forward belong to distinct sequences (decode): no row attends to another row's
   // new K/V, so the wide path lets the attention kernel finish q/k/v from the split-K slabs
@@ -987,7 +990,7 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
       launch_embed(x, tok_embd, ids, M, h, (nol || qql) ? ssq : nullptr, s);
     }
   }
-  if (wkq && M > MAX_ROWS && kqd_qkv && !argmax && !(head && n_out > MAX_ROWS))
+  if (wkq && !kq_ggml_prefill && M > MAX_ROWS && kqd_qkv && !argmax && !(head && n_out > MAX_ROWS))
     return enqueue_forward_gemm(M, pos, slot, x_out, head, rowmap, n_out, s);  // dequantised bf16 GEMMs
   // Q8_0 prefill chunks as dequantised bf16 GEMMs (llama.cpp's GPU-backend route for large batches):
   // ~5x the default's rate, but bf16 activations instead of ggml's Q8_0 rows, so opt-in

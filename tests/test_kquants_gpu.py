@@ -11,6 +11,8 @@ Other block types (F16 files, mixes without a native path): the engine dequantis
 (dequant_bf16_kernel) and runs the bf16 path -- bit-identical to a BF16 file holding numpy's
 dequantisation of the same blocks, and close to the CPU oracle built from those bf16 weights.  (Q4_0
 files run natively: tests/test_q4_0_gpu.py.)"""
+import os
+
 import numpy as np
 import pytest
 
@@ -339,3 +341,40 @@ def test_kq_prefill_gemm_vs_oracle(mx, oracle_mod, name, ftype, n_prompt):
     assert_logits_close(got, ref, f"{name} {ftype} after K-quant GEMM prefill")
     assert_tokens_match(got, ref, f"{name} {ftype} after K-quant GEMM prefill")
     eng.close()
+
+
+@pytest.mark.parametrize("name,ftype,n_prompt", [("test-8b-ffn", "q4_k_m", 150), ("test-d128", "q5_k_m", 120)])
+def test_kq_prefill_ggml_arithmetic_vs_oracle(mx, oracle_mod, name, ftype, n_prompt):
+    """MX_KQ_GGML_PREFILL=1: prompt chunks of > 64 rows run with ggml's arithmetic (every row quantised
+    to Q8_K, the int8 K-quant GEMVs, no dequantised bf16 GEMM): the prompt's logits of every row and the
+    next decode step against the oracle under the Q8 jitter bound (2x the oracle's own deviation under
+    1e-6 relative activation noise), as test_kq_prefill_and_decode_vs_oracle."""
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES[name]
+    ids = _seq(shape, n_prompt + 1, seed=37)
+    os.environ["MX_KQ_GGML_PREFILL"] = "1"
+    try:
+        eng = mx.Engine(f"synthetic:{name}:seed=0:{ftype}", n_ctx=512, n_seq_max=2)
+    finally:
+        del os.environ["MX_KQ_GGML_PREFILL"]
+    # rows 64.. of the prompt: one chunk of > 64 rows without logits (the path under test), then the
+    # next token attends to the K/V it stored
+    got = eng.forward_logits(ids[:64], 0, slot=0)
+    assert eng.forward_rows([0] * (n_prompt - 64), list(range(64, n_prompt)), ids[64:n_prompt], want_logits=False) is None
+    nxt = eng.forward_logits(ids[n_prompt:], n_prompt, slot=0)
+    eng.close()
+    rows = list(range(64)) + [n_prompt]
+    ref = _oracle_kq(oracle_mod, shape, 0, ftype).context(512).eval(ids, 0, all_logits=True)[rows]
+    oracle_mod.q8_jitter(1e-6)
+    try:
+        jit = _oracle_kq(oracle_mod, shape, 0, ftype).context(512).eval(ids, 0, all_logits=True)[rows]
+    finally:
+        oracle_mod.q8_jitter(0.0)
+    self_dev = float(np.abs(jit - ref).max())
+    allg = np.concatenate([got, nxt])
+    err = float(np.abs(allg - ref).max())
+    print(f"{name} {ftype} ggml-arithmetic prefill: max|d| {err:.4g}, oracle self-deviation {self_dev:.4g}, "
+          f"max|ref| {np.abs(ref).max():.4g}")
+    assert err <= 2 * self_dev + 1e-4 * np.abs(ref).max(), (err, self_dev)
+    assert_tokens_match(allg, ref, f"{name} {ftype} ggml-arithmetic prefill")
