@@ -1640,8 +1640,10 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(MMArgs a) {
     const int tok = min(m0 + (w * 2 + i) * 16 + r16, a.M - 1);
     boff[i] = (uint32_t)tok * (uint32_t)a.ldx + 8 * (lane >> 4);
   }
-  auto issue = [&](int kt) {
-    uint8_t* base = lds + (kt % NBUF) * 32768;
+  // k-tile min(kt, t1-1) into buffer kt % NBUF
+  auto issue = [&](int kt_buf) {
+    uint8_t* base = lds + (kt_buf % NBUF) * 32768;
+    const int kt = min(kt_buf, t1 - 1);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int t = w * 2 + i, ta = i ? at1 : at0;
@@ -1677,48 +1679,59 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(MMArgs a) {
         acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.a[r]),
                                                             __builtin_bit_cast(bf16x8, f.b[j]), acc[r][j], 0, 0, 0);
   };
-  // wait until this thread's copies of k-tile `kt` landed, given that k-tiles up to `issued` were issued
-  auto wait_tile = [&](int kt, int issued) {
-    const int later = min(issued, t1 - 1) - kt;
-    if (later >= 4) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else if (later == 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else if (later == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
+  // Every k-tile step issues one k-tile's copies (the source clamped to the last k-tile past the
+  // end: a few redundant copies into buffers nobody reads again), so the count of copies in flight
+  // behind k-tile kt+1 is always NBUF-2 k-tiles and the waits are constants
+  static_assert(NBUF == 4, "vmcnt counts below assume a 4-buffer ring");
 
   // the fragments of k-tile kt+1 are read from LDS while k-tile kt's MFMAs run; every buffer holds
   // one k-tile: kt+1 (being read) and kt+2 .. kt+NBUF (in flight)
 #pragma unroll
-  for (int i = 0; i < NBUF; ++i)
-    if (t0 + i < t1) issue(t0 + i);
+  for (int i = 0; i < NBUF; ++i) issue(t0 + i);
   Frags F0, F1;
-  wait_tile(t0, t0 + NBUF - 1);
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // t0 landed, NBUF-1 k-tiles behind it
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   read(F0, t0);
+  // a step that is not the last: kt+1 < t1
   auto step = [&](Frags& cur, Frags& nxt, int kt) {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of kt landed (the compiler sees it)
-    if (kt + 1 < t1) {
-      wait_tile(kt + 1, kt + NBUF - 1);
-      __builtin_amdgcn_s_barrier();  // kt+1 landed for every wave; nobody reads buffer kt any more
-      asm volatile("" ::: "memory");
-      if (kt + NBUF < t1) issue(kt + NBUF);  // into buffer kt
-    }
-    // unconditional (the last k-tile re-reads its own buffer, unused): a branch here would join
-    // the paths between these reads and the MFMAs, and the join waits for the reads
-    read(nxt, min(kt + 1, t1 - 1));
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // kt+1 landed (kt+2, kt+3 in flight)
+    __builtin_amdgcn_s_barrier();  // kt+1 landed for every wave; nobody reads buffer kt any more
+    asm volatile("" ::: "memory");
+    issue(kt + NBUF);  // into buffer kt
+    read(nxt, kt + 1);
     mfma(cur);
-    // the 12 reads first, then the 32 MFMAs (the default schedule issued the reads behind 24 MFMAs)
-    __builtin_amdgcn_sched_group_barrier(0x100, RW + 8, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, RW * 8, 0);
+    // copies and reads each behind one MFMA, so the MFMA pipe runs while this wave issues them (all
+    // reads then all MFMAs left it idle while both waves of a SIMD issued their copies and reads)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < RW + 8; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, RW * 8 - 4 - (RW + 8), 0);
   };
+  auto last = [&](Frags& cur) {
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    mfma(cur);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the redundant tail copies land before exit
+  };
+  // (the last step shares one body for both parities -- two copies of it spilled 128 VGPRs)
   int kt = t0;
-  for (; kt + 1 < t1; kt += 2) {
+  for (; kt + 2 < t1; kt += 2) {
     step(F0, F1, kt);
     step(F1, F0, kt + 1);
   }
-  if (kt < t1) step(F0, F1, kt);
+  if (kt + 1 < t1) {
+    step(F0, F1, kt);
+    F0 = F1;
+  }
+  last(F0);
 
   const int tile0 = nb * AT + wn * RW;
 #pragma unroll
