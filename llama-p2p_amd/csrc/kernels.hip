@@ -1682,21 +1682,23 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(MMArgs a) {
   // Every k-tile step issues one k-tile's copies (the source clamped to the last k-tile past the
   // end: a few redundant copies into buffers nobody reads again), so the count of copies in flight
   // behind k-tile kt+1 is always NBUF-2 k-tiles and the waits are constants
-  static_assert(NBUF == 4, "vmcnt counts below assume a 4-buffer ring");
+  static_assert(NBUF == 4 || NBUF == 5, "vmcnt counts below assume a 4- or 5-buffer ring");
 
   // the fragments of k-tile kt+1 are read from LDS while k-tile kt's MFMAs run; every buffer holds
   // one k-tile: kt+1 (being read) and kt+2 .. kt+NBUF (in flight)
 #pragma unroll
   for (int i = 0; i < NBUF; ++i) issue(t0 + i);
   Frags F0, F1;
-  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // t0 landed, NBUF-1 k-tiles behind it
+  if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // t0 landed, NBUF-1 k-tiles behind it
+  else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   read(F0, t0);
   // a step that is not the last: kt+1 < t1
   auto step = [&](Frags& cur, Frags& nxt, int kt) {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of kt landed (the compiler sees it)
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // kt+1 landed (kt+2, kt+3 in flight)
+    if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // kt+1 landed (NBUF-2 k-tiles in flight)
+    else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // kt+1 landed for every wave; nobody reads buffer kt any more
     asm volatile("" ::: "memory");
     issue(kt + NBUF);  // into buffer kt
@@ -2957,6 +2959,174 @@ static int launch_mq8_wide(int epi, const MMArgs& a, hipStream_t s) {
   return -1;
 }
 
+// ---------------------------------------------------------------------------
+// Q8_0 x Q8_0 prompt GEMM (>= Q8_GEMM_MIN_M rows): ggml's ggml_vec_dot_q8_0_q8_0 arithmetic -- per
+// 32-weight block the exact int32 product of the two int8 vectors (v_mfma_i32_16x16x32_i8: K = one
+// block), times d_w * d_x, summed in f32 -- as a blocked GEMM instead of the GEMV kernels above
+// (which re-stream every weight tile once per 64 tokens).  Block = 8 waves, 256 weight rows (16 Q8
+// tiles) x 128 tokens; wave (wn, wm) = 4 row tiles x 4 token tiles, 32 MFMAs per 64-deep k-step.
+// Staged global -> LDS by LDS-DMA, one k-step (one Q8 tile column) per ring buffer: the 16 tiles'
+// int8 parts (lane-linear 1 KiB A images, copied verbatim), the 128 tokens' q (gathered into the same
+// lane-linear B images), the tiles' f16 d_w (64 B each) and the tokens' d_x (two floats each); the
+// k-loop is gemm_kernel's (constant counted waits, copies and reads behind MFMAs).  The f32 scaling
+// (per block and output: d_w * d_x, convert, fma) is VALU work of the same count as the MFMAs' MACs
+// / 32 -- it, not the MFMA, bounds this kernel.
+// ---------------------------------------------------------------------------
+constexpr int Q8_GEMM_MIN_M = 256;
+constexpr int QG_M = 128, QG_NBUF = 4;
+constexpr int QG_A = 0, QG_B = 16384, QG_DW = QG_B + 8192, QG_DX = QG_DW + 1024, QG_BUF = QG_DX + 1024;
+
+template <int EPI, bool Q4>
+__global__ __launch_bounds__(512, 1) void q8gemm_kernel(MMArgs a) {
+  constexpr int NBUF = QG_NBUF;
+  // Q4 (Q4_0 tiles, ggml_vec_dot_q4_0_q8_0): 512-byte nibble parts (two tiles per copy, 8 bytes per
+  // lane, expanded to the int8 q - 8 by q4_operand), scales at byte 512
+  constexpr int TB = Q4 ? Q4_TILE_BYTES : Q8_TILE_BYTES, SO = Q4 ? 512 : 1024, AB = Q4 ? 512 : 1024;
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[NBUF * QG_BUF];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wn = w & 3, wm = w >> 2;
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int nmb = (a.M + QG_M - 1) / QG_M;
+  const int mb = wgid % nmb, nb = wgid / nmb;
+  const int KT = a.K / Q8_TILE_K, KB = a.K / 32;
+  const int t0 = 0, t1 = KT;
+  const int m0 = mb * QG_M;
+
+  // copies: wave w moves A tiles 2w, 2w+1 (int8 parts), token tile w, the d_w of tiles 2w, 2w+1
+  // (lanes 0..7, 16 B each) and the d_x of tokens 16w..16w+15 (lanes 0..31, one float each)
+  const uint8_t* abase = reinterpret_cast<const uint8_t*>(a.W) + (size_t)(nb * 16 + 2 * w) * KT * TB;
+  const size_t astep = (size_t)KT * TB;
+  const int tokb = min(m0 + w * 16 + (lane & 15), a.M - 1);
+  const int8_t* bsrc = a.xq + (size_t)tokb * a.K + (lane >> 4) * 16;
+  const uint8_t* dwsrc = abase + (size_t)(lane >> 2) * astep + SO + 16 * (lane & 3);
+  const int tokd = min(m0 + w * 16 + (lane >> 1), a.M - 1);
+  const float* dxsrc = a.xd + (size_t)tokd * KB + (lane & 1);
+  auto issue = [&](int kt_buf) {  // k-step min(kt_buf, t1-1) into buffer kt_buf % NBUF
+    uint8_t* base = lds + (kt_buf % NBUF) * QG_BUF;
+    const int kt = min(kt_buf, t1 - 1);
+    if constexpr (Q4) {
+      __builtin_amdgcn_global_load_lds((gvoid*)(abase + (lane >> 5) * astep + (size_t)kt * TB + (lane & 31) * 16),
+                                       (lvoid*)(base + QG_A + w * 1024), 16, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_global_load_lds((gvoid*)(abase + i * astep + (size_t)kt * TB + lane * 16),
+                                         (lvoid*)(base + QG_A + (2 * w + i) * 1024), 16, 0, 0);
+    }
+    __builtin_amdgcn_global_load_lds((gvoid*)(bsrc + (size_t)kt * Q8_TILE_K), (lvoid*)(base + QG_B + w * 1024), 16, 0, 0);
+    if (lane < 8)
+      __builtin_amdgcn_global_load_lds((gvoid*)(dwsrc + (size_t)kt * TB), (lvoid*)(base + QG_DW + w * 128),
+                                       16, 0, 0);
+    if (lane < 32)
+      __builtin_amdgcn_global_load_lds((gvoid*)(dxsrc + 2 * kt), (lvoid*)(base + QG_DX + w * 128), 4, 0, 0);
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  struct Frags {
+    u32x4 a[4], b[4], dw[4];
+    f32x2 dx[4];
+  };
+  auto read = [&](Frags& f, int kt) {
+    const uint8_t* B0 = lds + (kt % NBUF) * QG_BUF;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if constexpr (Q4) {
+        const u32x2 v = *reinterpret_cast<const u32x2*>(B0 + QG_A + (wn * 4 + r) * AB + lane * 8);
+        f.a[r] = u32x4{v[0], v[1], 0u, 0u};
+      } else {
+        f.a[r] = *reinterpret_cast<const u32x4*>(B0 + QG_A + (wn * 4 + r) * AB + lane * 16);
+      }
+      f.dw[r] = *reinterpret_cast<const u32x4*>(B0 + QG_DW + (wn * 4 + r) * 64 + 16 * (lane >> 4));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f.b[j] = *reinterpret_cast<const u32x4*>(B0 + QG_B + (wm * 4 + j) * 1024 + lane * 16);
+      f.dx[j] = *reinterpret_cast<const f32x2*>(B0 + QG_DX + ((wm * 4 + j) * 16 + (lane & 15)) * 8);
+    }
+  };
+  auto mfma = [&](const Frags& f) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long a0 = Q4 ? q4_operand(f.a[r][0]) : (long)(((unsigned long)f.a[r][1] << 32) | f.a[r][0]);
+      const long a1 = Q4 ? q4_operand(f.a[r][1]) : (long)(((unsigned long)f.a[r][3] << 32) | f.a[r][2]);
+      const f16x8 dw = __builtin_bit_cast(f16x8, f.dw[r]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const long b0 = (long)(((unsigned long)f.b[j][1] << 32) | f.b[j][0]);
+        const long b1 = (long)(((unsigned long)f.b[j][3] << 32) | f.b[j][2]);
+        const i32x4 p0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, b0, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        const i32x4 p1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, b1, i32x4{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // mq8_kernel's per-block f32 step
+          acc[r][j][i] = fmaf((float)dw[i] * f.dx[j][0], (float)p0[i], acc[r][j][i]);
+          acc[r][j][i] = fmaf((float)dw[4 + i] * f.dx[j][1], (float)p1[i], acc[r][j][i]);
+        }
+      }
+    }
+  };
+
+  // 5 copies (Q4: 4) per wave and k-step; waits: k-step kt landed with NBUF-2 k-steps behind it.  The
+  // fragments are read at the top of each step (single-buffered: the per-block scaling needs the
+  // registers double-buffering would take); the other wave of the SIMD covers the read latency
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; ++i) issue(t0 + i);
+  for (int kt = t0; kt < t1; ++kt) {
+    if constexpr (Q4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // kt landed for every wave; buffer kt-1 is free
+    asm volatile("" ::: "memory");
+    issue(kt + NBUF - 1);  // into buffer kt-1
+    Frags f;
+    read(f, kt);
+    mfma(f);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  const int tile0 = nb * 16 + wn * 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 sv = acc[r][j];
+      f32x4 up = sv;
+      if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(sv[i], 32);
+      }
+      const int col = m0 + wm * 64 + j * 16 + (lane & 15);
+      if (col >= a.M || (EPI == EPI_SWIGLU && lane >= 32)) continue;
+      epi_store<EPI>(a, tile0 + r, lane, col, sv, up);
+    }
+}
+
+// A blocked grid of fewer than QG_MIN_GRID work-groups leaves most CUs idle for a whole K sweep;
+// the GEMVs (one weight pass per 64 tokens, every CU busy) are then faster (Llama-3-8B attn_output /
+// ffn_down at 256 rows: 32 blocks)
+constexpr int QG_MIN_GRID = 64;
+static int launch_q8gemm(int epi, const MMArgs& a, hipStream_t s) {
+  if (a.M < Q8_GEMM_MIN_M || a.N % 256 || a.K % Q8_TILE_K || !a.xq || !a.xd) return -1;
+  const int grid = (a.N / 256) * ((a.M + QG_M - 1) / QG_M);
+  if (grid < QG_MIN_GRID) return -1;
+  auto go = [&](auto q4c) {
+    constexpr bool Q4 = decltype(q4c)::value;
+    switch (epi) {
+      case EPI_F32: q8gemm_kernel<EPI_F32, Q4><<<grid, 512, 0, s>>>(a); return 0;
+      case EPI_RESID: q8gemm_kernel<EPI_RESID, Q4><<<grid, 512, 0, s>>>(a); return 0;
+      case EPI_QKV: q8gemm_kernel<EPI_QKV, Q4><<<grid, 512, 0, s>>>(a); return 0;
+      case EPI_SWIGLU: q8gemm_kernel<EPI_SWIGLU, Q4><<<grid, 512, 0, s>>>(a); return 0;
+    }
+    return -1;
+  };
+  return a.wq4 ? go(std::true_type{}) : go(std::false_type{});
+}
+
 int launch_mq8(int epi, const MMArgs& a, hipStream_t s) {
   if (a.M < 1 || a.K % Q8_TILE_K || a.N % TILE_N) return -1;
   if (epi == EPI_SWIGLU && !a.actf && !a.act) return -1;
@@ -2977,6 +3147,7 @@ int launch_mq8(int epi, const MMArgs& a, hipStream_t s) {
     return a.wq4 ? ql(std::true_type{}) : ql(std::false_type{});
   }
   if (!a.xd) return -1;
+  if (launch_q8gemm(epi, a, s) == 0) return 0;
   if (launch_mq8_wide(epi, a, s) == 0) return 0;
   auto go = [&](auto q4c) {
     constexpr bool Q4 = decltype(q4c)::value;

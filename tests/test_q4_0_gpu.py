@@ -81,6 +81,31 @@ def test_q4_0_prefill_and_decode_vs_oracle(mx, oracle_mod, name):
     eng.close()
 
 
+@pytest.mark.parametrize("P", [300, 520])
+def test_q4_0_gemm_prefill_vs_oracle(mx, oracle_mod, P):
+    """A >= 256-row Q4_0 prompt chunk on q8gemm_kernel's Q4 form (ggml_vec_dot_q4_0_q8_0: nibbles
+    expanded to q - 8 in registers, per-block int32 products on the int8 MFMA): at 300 rows q|k|v
+    only, at 520 all four matrices; the next 8 rows against the oracle under the jitter bound."""
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES["test-h4096"]
+    ids = _seq(shape, P + 8, seed=11)
+    eng = mx.Engine("synthetic:test-h4096:seed=0:q4_0", n_ctx=544, n_seq_max=2)
+    assert eng.forward_rows([0] * P, list(range(P)), ids[:P], want_logits=False) is None
+    got = eng.forward_logits(ids[P:], P, slot=0)
+    ref = _oracle_q4(oracle_mod, shape, 0).context(544).eval(ids, 0, all_logits=True)[P:]
+    err = np.abs(got - ref).max()
+    oracle_mod.q8_jitter(1e-6)
+    try:
+        jit = _oracle_q4(oracle_mod, shape, 0).context(544).eval(ids, 0, all_logits=True)[P:]
+    finally:
+        oracle_mod.q8_jitter(0.0)
+    dev = np.abs(jit - ref).max()
+    assert err <= 2 * dev + 1e-4 * np.abs(ref).max(), (err, dev)
+    _tokens_decided(got, ref, dev, f"q4_0 gemm prefill P={P}")
+    eng.close()
+
+
 def test_q4_0_gguf_equals_synthetic(mx, tmp_path):
     """The synthetic q4_0 model written as a GGUF by numpy (gguf.quantize_q4_0 == the oracle's quantiser,
     tests/test_q4_0.py) and synthesised on the device (synth_q4_packed_kernel) give bit-identical logits:

@@ -112,6 +112,34 @@ def test_q8_large_prefill_then_wide_rows(mx, oracle_mod):
     eng.close()
 
 
+@pytest.mark.parametrize("name,P", [("test-h4096", 300), ("test-h4096", 520)])
+def test_q8_gemm_prefill_vs_oracle(mx, oracle_mod, name, P):
+    """A >= 256-row Q8_0 prompt chunk runs q8gemm_kernel (ggml_vec_dot_q8_0_q8_0's per-block int32
+    products on the int8 MFMA, times d_w * d_x, in 256-row x 128-token blocks) wherever its grid has
+    >= 64 blocks: at 300 rows q|k|v only (attn_output / gate-up / ffn_down stay on the GEMVs), at 520
+    all four, with a ragged last token block; the next 8 rows' logits, which attend to the K/V it
+    stored and read the residual it wrote, against the oracle's Q8_0 forward, within twice the
+    oracle's own deviation under 1e-6 noise."""
+    from llama_p2p_amd import synth
+
+    shape = synth.SHAPES[name]
+    ids = _seq(shape, P + 8, seed=11)
+    eng = mx.Engine(f"synthetic:{name}:seed=0:q8_0", n_ctx=544, n_seq_max=2)
+    assert eng.forward_rows([0] * P, list(range(P)), ids[:P], want_logits=False) is None
+    got = eng.forward_logits(ids[P:], P, slot=0)
+    ref = _oracle_q8(oracle_mod, shape, 0).context(544).eval(ids, 0, all_logits=True)[P:]
+    assert_logits_close(got, ref, f"{name} q8 gemm prefill")
+    assert_tokens_match(got, ref, f"{name} q8 gemm prefill")
+    oracle_mod.q8_jitter(1e-6)
+    try:
+        jit = _oracle_q8(oracle_mod, shape, 0).context(544).eval(ids, 0, all_logits=True)[P:]
+    finally:
+        oracle_mod.q8_jitter(0.0)
+    err, self_dev = np.abs(got - ref).max(), np.abs(jit - ref).max()
+    assert err <= 2 * self_dev + 1e-4 * np.abs(ref).max(), (err, self_dev)
+    eng.close()
+
+
 def test_q8_batch_greedy_loop_vs_oracle(mx, oracle_mod):
     """device-resident greedy loop (graph replay + on-device argmax) on a Q8_0 model."""
     from llama_p2p_amd import synth
