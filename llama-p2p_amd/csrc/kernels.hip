@@ -3051,30 +3051,47 @@ __global__ __launch_bounds__(512, 1) void q8gemm_kernel(MMArgs a) {
       f.dx[j] = *reinterpret_cast<const f32x2*>(B0 + QG_DX + ((wm * 4 + j) * 16 + (lane & 15)) * 8);
     }
   };
+  // The per-block f32 step is mq8_kernel's -- acc = fma(d_w * d_x, (float)sumi, acc), block 0 then
+  // block 1 -- on packed f32 pairs.  (float)sumi without v_cvt_f32_i32 (not packable): the MFMA
+  // starts from C = 0x4B400000, the bits of 1.5 * 2^23, so it returns the bits of 12582912 + sumi
+  // exactly (|sumi| <= 32 * 127 * 127 < 2^22 keeps the exponent), and one packed subtract of
+  // 12582912 leaves sumi exactly
+  constexpr int QG_MAGIC = 0x4B400000;
   auto mfma = [&](const Frags& f) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const long a0 = Q4 ? q4_operand(f.a[r][0]) : (long)(((unsigned long)f.a[r][1] << 32) | f.a[r][0]);
       const long a1 = Q4 ? q4_operand(f.a[r][1]) : (long)(((unsigned long)f.a[r][3] << 32) | f.a[r][2]);
       const f16x8 dw = __builtin_bit_cast(f16x8, f.dw[r]);
+      f32x2 dwp[2][2];  // [block][row pair]
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) dwp[b][pp] = f32x2{(float)dw[4 * b + 2 * pp], (float)dw[4 * b + 2 * pp + 1]};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const long b0 = (long)(((unsigned long)f.b[j][1] << 32) | f.b[j][0]);
         const long b1 = (long)(((unsigned long)f.b[j][3] << 32) | f.b[j][2]);
-        const i32x4 p0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, b0, i32x4{0, 0, 0, 0}, 0, 0, 0);
-        const i32x4 p1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, b1, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        const i32x4 mg = i32x4{QG_MAGIC, QG_MAGIC, QG_MAGIC, QG_MAGIC};
+        const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, b0, mg, 0, 0, 0));
+        const f32x4 x1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, b1, mg, 0, 0, 0));
+        const f32x2 dx0 = f32x2{f.dx[j][0], f.dx[j][0]}, dx1 = f32x2{f.dx[j][1], f.dx[j][1]};
+        const f32x2 off = f32x2{12582912.0f, 12582912.0f};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {  // mq8_kernel's per-block f32 step
-          acc[r][j][i] = fmaf((float)dw[i] * f.dx[j][0], (float)p0[i], acc[r][j][i]);
-          acc[r][j][i] = fmaf((float)dw[4 + i] * f.dx[j][1], (float)p1[i], acc[r][j][i]);
+        for (int pp = 0; pp < 2; ++pp) {
+          f32x2 c = f32x2{acc[r][j][2 * pp], acc[r][j][2 * pp + 1]};
+          c = __builtin_elementwise_fma(dwp[0][pp] * dx0, f32x2{x0[2 * pp], x0[2 * pp + 1]} - off, c);
+          c = __builtin_elementwise_fma(dwp[1][pp] * dx1, f32x2{x1[2 * pp], x1[2 * pp + 1]} - off, c);
+          acc[r][j][2 * pp] = c[0];
+          acc[r][j][2 * pp + 1] = c[1];
         }
       }
     }
   };
 
   // 5 copies (Q4: 4) per wave and k-step; waits: k-step kt landed with NBUF-2 k-steps behind it.  The
-  // fragments are read at the top of each step (single-buffered: the per-block scaling needs the
-  // registers double-buffering would take); the other wave of the SIMD covers the read latency
+  // fragments are read at the top of each step: double-buffering them (gemm_kernel's loop) spills
+  // 66-86 VGPRs here
 #pragma unroll
   for (int i = 0; i < NBUF - 1; ++i) issue(t0 + i);
   for (int kt = t0; kt < t1; ++kt) {
