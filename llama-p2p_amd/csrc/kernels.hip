@@ -3058,10 +3058,24 @@ __global__ __launch_bounds__(512, 1) void q8gemm_kernel(MMArgs a) {
   // 12582912 leaves sumi exactly
   constexpr int QG_MAGIC = 0x4B400000;
   auto mfma = [&](const Frags& f) {
+    // the MFMAs of row tile r+1 are issued before the scaling of row tile r (an MFMA's result is read
+    // 8 passes after its issue: scaling right behind its own MFMA stalled the wave on every pair)
+    f32x4 x[4][4][2];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const long a0 = Q4 ? q4_operand(f.a[r][0]) : (long)(((unsigned long)f.a[r][1] << 32) | f.a[r][0]);
       const long a1 = Q4 ? q4_operand(f.a[r][1]) : (long)(((unsigned long)f.a[r][3] << 32) | f.a[r][2]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const long b0 = (long)(((unsigned long)f.b[j][1] << 32) | f.b[j][0]);
+        const long b1 = (long)(((unsigned long)f.b[j][3] << 32) | f.b[j][2]);
+        const i32x4 mg = i32x4{QG_MAGIC, QG_MAGIC, QG_MAGIC, QG_MAGIC};
+        x[r][j][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, b0, mg, 0, 0, 0));
+        x[r][j][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, b1, mg, 0, 0, 0));
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
       const f16x8 dw = __builtin_bit_cast(f16x8, f.dw[r]);
       f32x2 dwp[2][2];  // [block][row pair]
 #pragma unroll
@@ -3070,23 +3084,26 @@ __global__ __launch_bounds__(512, 1) void q8gemm_kernel(MMArgs a) {
         for (int pp = 0; pp < 2; ++pp) dwp[b][pp] = f32x2{(float)dw[4 * b + 2 * pp], (float)dw[4 * b + 2 * pp + 1]};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const long b0 = (long)(((unsigned long)f.b[j][1] << 32) | f.b[j][0]);
-        const long b1 = (long)(((unsigned long)f.b[j][3] << 32) | f.b[j][2]);
-        const i32x4 mg = i32x4{QG_MAGIC, QG_MAGIC, QG_MAGIC, QG_MAGIC};
-        const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, b0, mg, 0, 0, 0));
-        const f32x4 x1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, b1, mg, 0, 0, 0));
         const f32x2 dx0 = f32x2{f.dx[j][0], f.dx[j][0]}, dx1 = f32x2{f.dx[j][1], f.dx[j][1]};
         const f32x2 off = f32x2{12582912.0f, 12582912.0f};
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) {
           f32x2 c = f32x2{acc[r][j][2 * pp], acc[r][j][2 * pp + 1]};
-          c = __builtin_elementwise_fma(dwp[0][pp] * dx0, f32x2{x0[2 * pp], x0[2 * pp + 1]} - off, c);
-          c = __builtin_elementwise_fma(dwp[1][pp] * dx1, f32x2{x1[2 * pp], x1[2 * pp + 1]} - off, c);
+          c = __builtin_elementwise_fma(dwp[0][pp] * dx0, f32x2{x[r][j][0][2 * pp], x[r][j][0][2 * pp + 1]} - off, c);
+          c = __builtin_elementwise_fma(dwp[1][pp] * dx1, f32x2{x[r][j][1][2 * pp], x[r][j][1][2 * pp + 1]} - off, c);
           acc[r][j][2 * pp] = c[0];
           acc[r][j][2 * pp + 1] = c[1];
         }
       }
     }
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);
   };
 
   // 5 copies (Q4: 4) per wave and k-step; waits: k-step kt landed with NBUF-2 k-steps behind it.  The
