@@ -2769,6 +2769,11 @@ static int launch_mq8_ql_epi(const MMArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
+// int32 -> f32 without v_cvt_f32_i32: an int8 MFMA started from these bits (1.5 * 2^23) returns the
+// bits of 12582912 + sumi, exact for |sumi| < 2^22 (a Q8_0 block: <= 32 * 127 * 127); subtracting
+// 12582912 in f32 (packed, two values per instruction) leaves sumi exactly
+constexpr int QG_MAGIC = 0x4B400000;
+
 // Q8_0 GEMV for 17..32 tokens with the activations shared through LDS (mkq_wide_kernel's scheme in
 // kquant.hip): each wave owns one 16-row tile over the whole K; the W waves of a work-group share
 // each staged 256-k chunk of Q8_0 activation rows (32 tokens x 256 q, k permuted within 64-k groups
@@ -2778,7 +2783,7 @@ static int launch_mq8_ql_epi(const MMArgs& a, hipStream_t s) {
 // scaled by d_w * d_x in f32); the whole K stays in one wave, so the epilogue runs from registers.
 // ---------------------------------------------------------------------------
 template <int W, int EPI, int U, bool Q4>
-__global__ __launch_bounds__(64 * W) void mq8_wide_kernel(MMArgs a) {
+__global__ __launch_bounds__(64 * W, 2) void mq8_wide_kernel(MMArgs a) {
   constexpr int TB = Q4 ? Q4_TILE_BYTES : Q8_TILE_BYTES, SO = Q4 ? 512 : 1024;  // tile bytes, scale offset
   constexpr int NB = 2, ROWS = 32;
   constexpr int QP = 256 + 16;     // int8 per LDS row (+16 B: conflict-free fragment reads)
@@ -2869,6 +2874,13 @@ __global__ __launch_bounds__(64 * W) void mq8_wide_kernel(MMArgs a) {
       const long a0 = Q4 ? q4_operand(f.q[k][0]) : (long)(((unsigned long)f.q[k][1] << 32) | f.q[k][0]);
       const long a1 = Q4 ? q4_operand(f.q[k][1]) : (long)(((unsigned long)f.q[k][3] << 32) | f.q[k][2]);
       const f16x8 dw = __builtin_bit_cast(f16x8, f.d[k]);
+      // scaling on packed f32 pairs, int32 -> f32 by the magic accumulator start (QG_MAGIC)
+      f32x2 w0[2], w1[2];
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        w0[pp] = f32x2{(float)dw[2 * pp], (float)dw[2 * pp + 1]};
+        w1[pp] = f32x2{(float)dw[4 + 2 * pp], (float)dw[4 + 2 * pp + 1]};
+      }
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
         const int row = n * 16 + (lane & 15);
@@ -2876,12 +2888,18 @@ __global__ __launch_bounds__(64 * W) void mq8_wide_kernel(MMArgs a) {
         const f32x2 dx = *reinterpret_cast<const f32x2*>(&sd[buf][row][2 * k]);
         const long b0 = (long)(((unsigned long)xb[1] << 32) | xb[0]);
         const long b1 = (long)(((unsigned long)xb[3] << 32) | xb[2]);
-        const i32x4 p0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, b0, i32x4{0, 0, 0, 0}, 0, 0, 0);
-        const i32x4 p1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, b1, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        const i32x4 mg = i32x4{QG_MAGIC, QG_MAGIC, QG_MAGIC, QG_MAGIC};
+        const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, b0, mg, 0, 0, 0));
+        const f32x4 x1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, b1, mg, 0, 0, 0));
+        const f32x2 dx0 = f32x2{dx[0], dx[0]}, dx1 = f32x2{dx[1], dx[1]};
+        const f32x2 off = f32x2{12582912.0f, 12582912.0f};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          acc[n][i] = fmaf((float)dw[i] * dx[0], (float)p0[i], acc[n][i]);
-          acc[n][i] = fmaf((float)dw[4 + i] * dx[1], (float)p1[i], acc[n][i]);
+        for (int pp = 0; pp < 2; ++pp) {
+          f32x2 c = f32x2{acc[n][2 * pp], acc[n][2 * pp + 1]};
+          c = __builtin_elementwise_fma(w0[pp] * dx0, f32x2{x0[2 * pp], x0[2 * pp + 1]} - off, c);
+          c = __builtin_elementwise_fma(w1[pp] * dx1, f32x2{x1[2 * pp], x1[2 * pp + 1]} - off, c);
+          acc[n][2 * pp] = c[0];
+          acc[n][2 * pp + 1] = c[1];
         }
       }
     }
@@ -3056,7 +3074,6 @@ __global__ __launch_bounds__(512, 1) void q8gemm_kernel(MMArgs a) {
   // starts from C = 0x4B400000, the bits of 1.5 * 2^23, so it returns the bits of 12582912 + sumi
   // exactly (|sumi| <= 32 * 127 * 127 < 2^22 keeps the exponent), and one packed subtract of
   // 12582912 leaves sumi exactly
-  constexpr int QG_MAGIC = 0x4B400000;
   auto mfma = [&](const Frags& f) {
     // the MFMAs of row tile r+1 are issued before the scaling of row tile r (an MFMA's result is read
     // 8 passes after its issue: scaling right behind its own MFMA stalled the wave on every pair)

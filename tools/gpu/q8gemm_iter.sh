@@ -10,7 +10,7 @@ timeout -k 10 400 python -u -m pytest tests/test_q8_gpu.py tests/test_q4_0_gpu.p
 tail -2 $OUT/pytest_q8.log
 ARGS="--steps 2 --warmup 1 --batch1-steps 0 --tiny-tokens 0 --q8-steps 4 --kq-steps 0 --q40-steps 4 --big-steps 0 --geometry-steps 0 --serve-requests 0 --no-cpu-baseline"
 timeout -k 10 300 python -u bench.py $ARGS > $OUT/bench.log 2>&1 || { tail -30 $OUT/bench.log; exit 1; }
-tail -1 $OUT/bench.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps([d.get("q8_0", {}).get("prefill"), d.get("q4_0", {}).get("prefill")]))'
+tail -1 $OUT/bench.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); [print(k, d[k]["prefill"]["tok_s"], d[k]["decode_M32"]["tok_s"], d[k]["gate_up_M32"]["us_per_launch"], d[k]["gate_up_M32"]["frac"], d[k]["batch1"]["tok_s"]) for k in ("q8_0", "q4_0")]'
 MX_NO_GRAPHS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o q8 -- python3 bench.py $ARGS \
   > $OUT/prof.log 2>&1 || { tail -30 $OUT/prof.log; exit 1; }
 db=$(find $OUT/prof -name '*.db' | head -1)
