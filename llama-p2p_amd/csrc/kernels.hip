@@ -2992,7 +2992,9 @@ static int launch_mq8_wide(int epi, const MMArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------------------
 constexpr int Q8_GEMM_MIN_M = 256;
 constexpr int QG_M = 128, QG_NBUF = 4;
-constexpr int QG_A = 0, QG_B = 16384, QG_DW = QG_B + 8192, QG_DX = QG_DW + 1024, QG_BUF = QG_DX + 1024;
+// per buffer: A images [16][1 KiB], B images [8][1 KiB], then per wave w 256 B of scales: the d_x of
+// tokens 16w..16w+15 ([token][2] floats, 128 B) and the d_w of tiles 2w, 2w+1 (64 B each)
+constexpr int QG_A = 0, QG_B = 16384, QG_SC = QG_B + 8192, QG_BUF = QG_SC + 2048;
 
 template <int EPI, bool Q4>
 __global__ __launch_bounds__(512, 1) void q8gemm_kernel(MMArgs a) {
@@ -3012,15 +3014,17 @@ __global__ __launch_bounds__(512, 1) void q8gemm_kernel(MMArgs a) {
   const int t0 = 0, t1 = KT;
   const int m0 = mb * QG_M;
 
-  // copies: wave w moves A tiles 2w, 2w+1 (int8 parts), token tile w, the d_w of tiles 2w, 2w+1
-  // (lanes 0..7, 16 B each) and the d_x of tokens 16w..16w+15 (lanes 0..31, one float each)
+  // copies: wave w moves A tiles 2w, 2w+1 (int8 parts), token tile w, and in ONE 4-byte copy its
+  // scales: lanes 0..31 the d_x of tokens 16w..16w+15 (one float each), lanes 32..63 the d_w of
+  // tiles 2w, 2w+1 (one f16 pair each)
   const uint8_t* abase = reinterpret_cast<const uint8_t*>(a.W) + (size_t)(nb * 16 + 2 * w) * KT * TB;
   const size_t astep = (size_t)KT * TB;
   const int tokb = min(m0 + w * 16 + (lane & 15), a.M - 1);
   const int8_t* bsrc = a.xq + (size_t)tokb * a.K + (lane >> 4) * 16;
-  const uint8_t* dwsrc = abase + (size_t)(lane >> 2) * astep + SO + 16 * (lane & 3);
-  const int tokd = min(m0 + w * 16 + (lane >> 1), a.M - 1);
-  const float* dxsrc = a.xd + (size_t)tokd * KB + (lane & 1);
+  const int tokd = min(m0 + w * 16 + ((lane & 31) >> 1), a.M - 1);
+  const uint8_t* scsrc = lane < 32 ? reinterpret_cast<const uint8_t*>(a.xd + (size_t)tokd * KB + (lane & 1))
+                                   : abase + (size_t)((lane >> 4) & 1) * astep + SO + 4 * (lane & 15);
+  const int scstep = lane < 32 ? 8 : TB;  // bytes per k-step
   auto issue = [&](int kt_buf) {  // k-step min(kt_buf, t1-1) into buffer kt_buf % NBUF
     uint8_t* base = lds + (kt_buf % NBUF) * QG_BUF;
     const int kt = min(kt_buf, t1 - 1);
@@ -3034,11 +3038,7 @@ __global__ __launch_bounds__(512, 1) void q8gemm_kernel(MMArgs a) {
                                          (lvoid*)(base + QG_A + (2 * w + i) * 1024), 16, 0, 0);
     }
     __builtin_amdgcn_global_load_lds((gvoid*)(bsrc + (size_t)kt * Q8_TILE_K), (lvoid*)(base + QG_B + w * 1024), 16, 0, 0);
-    if (lane < 8)
-      __builtin_amdgcn_global_load_lds((gvoid*)(dwsrc + (size_t)kt * TB), (lvoid*)(base + QG_DW + w * 128),
-                                       16, 0, 0);
-    if (lane < 32)
-      __builtin_amdgcn_global_load_lds((gvoid*)(dxsrc + 2 * kt), (lvoid*)(base + QG_DX + w * 128), 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((gvoid*)(scsrc + (size_t)kt * scstep), (lvoid*)(base + QG_SC + w * 256), 4, 0, 0);
   };
 
   f32x4 acc[4][4];
@@ -3061,12 +3061,13 @@ __global__ __launch_bounds__(512, 1) void q8gemm_kernel(MMArgs a) {
       } else {
         f.a[r] = *reinterpret_cast<const u32x4*>(B0 + QG_A + (wn * 4 + r) * AB + lane * 16);
       }
-      f.dw[r] = *reinterpret_cast<const u32x4*>(B0 + QG_DW + (wn * 4 + r) * 64 + 16 * (lane >> 4));
+      const int T = wn * 4 + r;
+      f.dw[r] = *reinterpret_cast<const u32x4*>(B0 + QG_SC + (T >> 1) * 256 + 128 + (T & 1) * 64 + 16 * (lane >> 4));
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       f.b[j] = *reinterpret_cast<const u32x4*>(B0 + QG_B + (wm * 4 + j) * 1024 + lane * 16);
-      f.dx[j] = *reinterpret_cast<const f32x2*>(B0 + QG_DX + ((wm * 4 + j) * 16 + (lane & 15)) * 8);
+      f.dx[j] = *reinterpret_cast<const f32x2*>(B0 + QG_SC + (wm * 4 + j) * 256 + (lane & 15) * 8);
     }
   };
   // The per-block f32 step is mq8_kernel's -- acc = fma(d_w * d_x, (float)sumi, acc), block 0 then
@@ -3123,14 +3124,14 @@ __global__ __launch_bounds__(512, 1) void q8gemm_kernel(MMArgs a) {
     __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);
   };
 
-  // 5 copies (Q4: 4) per wave and k-step; waits: k-step kt landed with NBUF-2 k-steps behind it.  The
+  // 4 copies (Q4: 3) per wave and k-step; waits: k-step kt landed with NBUF-2 k-steps behind it.  The
   // fragments are read at the top of each step: double-buffering them (gemm_kernel's loop) spills
   // 66-86 VGPRs here
 #pragma unroll
   for (int i = 0; i < NBUF - 1; ++i) issue(t0 + i);
   for (int kt = t0; kt < t1; ++kt) {
-    if constexpr (Q4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    if constexpr (Q4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // kt landed for every wave; buffer kt-1 is free
     asm volatile("" ::: "memory");
     issue(kt + NBUF - 1);  // into buffer kt-1
