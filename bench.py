@@ -10,7 +10,8 @@ untimed), then K greedy decode steps timed.  A "step" = one decode token for
 every sequence of every micro-batch.
 
 N = 1: one GPU runs the whole model, one micro-batch of 32 sequences.
-N > 1: launched by torch.distributed.run, one rank per GPU; rank r holds a
+N > 1: one rank per GPU (started by torch.distributed.run, or -- for the plain
+`python3 bench.py --gpus N` -- by this script itself, llama-p2p_amd/launch.py); rank r holds a
 contiguous, byte-balanced layer shard (pipeline stage r); N micro-batches of 32
 sequences are in flight; hidden states go stage->stage with RCCL send/recv
 over xGMI and the sampled token ids go back from the last stage to stage 0
@@ -588,8 +589,17 @@ def main():
     ap.add_argument("--budget", type=float, default=360.0,
                     help="seconds after which optional sections are skipped")
     ap.add_argument("--force-pipeline", action="store_true", help="run the torch.distributed pipeline path even at N=1")
+    ap.add_argument("--micro-batches", type=int, default=0, help="pipeline micro-batches in flight (0: one per stage)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="pipeline path on CPU over gloo with a toy executor (launcher / schedule check, no GPU)")
     ap.add_argument("--probe-only", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    from llama_p2p_amd import launch
+
+    if launch.needs_launch(args.gpus):
+        # plain `python3 bench.py --gpus N`: start the N ranks here (before anything touches the GPU)
+        os.environ["MX_LAUNCHER"] = "bench.py (launch.spawn_ranks)"
+        sys.exit(launch.spawn_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
     if args.probe_only:
         print(json.dumps(hbm_probe()), flush=True)
         return
@@ -602,7 +612,7 @@ def main():
     sys.stdout = os.fdopen(real_stdout, "w", buffering=1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1 or args.gpus > 1 or args.force_pipeline:
+    if world > 1 or args.gpus > 1 or args.force_pipeline or args.dry_run:
         from llama_p2p_amd import pipeline
 
         return pipeline.bench_main(args, METRIC, make_prompts)

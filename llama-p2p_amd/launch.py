@@ -1,0 +1,90 @@
+"""Start one process per GPU for ``bench.py --gpus N`` when no launcher did.
+
+The driver may start the bench as ``torch.distributed.run --nproc-per-node N bench.py --gpus N``
+(RANK / WORLD_SIZE set: nothing to do here) or as the plain ``python3 bench.py --gpus N``.  In the
+second case the parent becomes a launcher: it starts N children of the same command with the
+torch.distributed env:// variables set (MASTER_ADDR 127.0.0.1, a free port, RANK = LOCAL_RANK = i),
+forwards rank 0's stdout (the one JSON line) and sends every other rank's stdout to stderr, then
+exits with the first failing child's status.
+
+The parent never imports torch or touches the GPU: the children are started as new processes
+(no fork of a GPU-initialised process, no exec), which is the only safe shape on this pool.  This
+replaces the reference's peer forwarding (``/root/reference/llama_p2p_network.py:135-154``): the
+peers are the node's GPUs, one pipeline stage each.
+"""
+from __future__ import annotations
+
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+from typing import List, Optional, Sequence
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def needs_launch(n: int, env=None) -> bool:
+    """True when ``--gpus n`` asks for ranks that no launcher has started."""
+    env = os.environ if env is None else env
+    return n > 1 and "WORLD_SIZE" not in env
+
+
+def rank_env(rank: int, world: int, port: int, base=None) -> dict:
+    env = dict(os.environ if base is None else base)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                "LOCAL_WORLD_SIZE": str(world), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0", "PYTHONUNBUFFERED": "1"})
+    return env
+
+
+def spawn_ranks(n: int, argv: Sequence[str], timeout: Optional[float] = None, stdout=None) -> int:
+    """Run ``[python] + argv`` as ranks 0..n-1; returns the exit status (0, or the first failure's).
+
+    A rank that fails ends the others (by their exact PIDs: SIGTERM, then SIGKILL after 10 s), so a
+    stuck RCCL rendezvous cannot outlive a crashed peer."""
+    port = free_port()
+    out = sys.stdout if stdout is None else stdout
+    out.flush()
+    procs: List[subprocess.Popen] = []
+    for r in range(n):
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=rank_env(r, n, port),
+                                      stdout=out if r == 0 else sys.stderr, stderr=sys.stderr))
+    t0 = time.time()
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print(f"[launch] rank {procs.index(p)} exited with {rc}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                _stop(live)
+        if timeout is not None and time.time() - t0 > timeout and live:
+            print(f"[launch] ranks still running after {timeout:.0f}s; stopping them", file=sys.stderr, flush=True)
+            _stop(live)
+            status = status or 124
+        time.sleep(0.05)
+    return status
+
+
+def _stop(procs):
+    for p in procs:
+        if p.poll() is None:
+            p.send_signal(signal.SIGTERM)
+    t = time.time()
+    while any(p.poll() is None for p in procs) and time.time() - t < 10:
+        time.sleep(0.05)
+    for p in procs:
+        if p.poll() is None:
+            p.kill()
+            p.wait()

@@ -247,34 +247,60 @@ class Stage:
 
 
 def bench_main(args, metric: str, make_prompts):
-    """bench.py --gpus N under torch.distributed.run: one pipeline stage per rank."""
+    """bench.py --gpus N, one pipeline stage per rank (started by torch.distributed.run or by
+    launch.spawn_ranks).  ``args.dry_run``: the same schedule, timing and report on CPU over gloo
+    with ``DryEngine`` standing in for the HIP engine (tests/test_bench_launch.py)."""
+    import zlib
+
     import numpy as np
     import torch
     import torch.distributed as dist
 
     from . import synth
-    from .engine import Engine
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    dry = bool(getattr(args, "dry_run", False))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if world == 1:
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    torch.cuda.set_device(local)
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    if dry:
+        device = torch.device("cpu")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:
+        device = torch.device("cuda", local)
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+    world_rd, backend = dist.get_world_size(), str(dist.get_backend())
+    if world_rd != world:
+        raise RuntimeError(f"torch.distributed world size {world_rd} != WORLD_SIZE {world}")
     shape = synth.SHAPES[args.model]
     layer_bytes = 2 * (2 * shape.n_embd ** 2 + 2 * shape.n_embd * shape.n_embd_kv + 3 * shape.n_embd * shape.n_ff)
     head_bytes = 2 * shape.n_vocab * shape.n_embd
     parts = partition_layers(shape.n_layer, layer_bytes, head_bytes, world, embed_cost=0)
     lb, le = parts[rank]
-    S, M = world, args.seqs
-    eng = Engine(f"synthetic:{args.model}:seed=0", n_ctx=args.n_ctx, n_seq_max=S * M, layer_begin=lb,
-                 layer_end=le, device=local, handoff_bf16=True)
-    comm = TorchComm(rank, world)
-    work_stream = torch.cuda.Stream(device=local)  # engine kernels and RCCL hand-offs are ordered on it
-    torch.cuda.set_stream(work_stream)
-    stage = Stage(EngineAdapter(eng), comm, rank, world, shape.n_embd, torch.device("cuda", local), S,
-                  dtype=torch.bfloat16)  # hidden states cross stage boundaries in bf16
-    prompts = make_prompts(shape.n_vocab, S * M)
+    S = int(getattr(args, "micro_batches", 0) or world)
+    M = args.seqs
+    comm = TorchComm(rank, world) if world > 1 else None
+    if dry:
+        eng = DryEngine(lb, le, S * M, shape.n_layer)
+        vocab = eng.V
+        stage = Stage(eng, comm, rank, world, eng.H, device, S)
+        sync = lambda: None  # noqa: E731
+    else:
+        from .engine import Engine
+
+        eng = Engine(f"synthetic:{args.model}:seed=0", n_ctx=args.n_ctx, n_seq_max=S * M, layer_begin=lb,
+                     layer_end=le, device=local, handoff_bf16=True)
+        vocab = shape.n_vocab
+        work_stream = torch.cuda.Stream(device=local)  # engine kernels and RCCL hand-offs are ordered on it
+        torch.cuda.set_stream(work_stream)
+        stage = Stage(EngineAdapter(eng), comm, rank, world, shape.n_embd, device, S,
+                      dtype=torch.bfloat16)  # hidden states cross stage boundaries in bf16
+        sync = torch.cuda.synchronize
+    prompts = make_prompts(vocab, S * M)
     mb_rows, mb_state = [], []
     for mb in range(S):
         slots, pos, ids, st = [], [], [], ([], [], [])
@@ -291,24 +317,37 @@ def bench_main(args, metric: str, make_prompts):
         mb_state.append(st)
     stage.prefill(mb_rows)
     stage.setup_decode(mb_state, max_steps=args.warmup + args.steps)
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
     stage.decode_steps(args.warmup, 0)
     stage.finish()
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
     t0 = time.perf_counter()
     stage.decode_steps(args.steps, args.warmup)
     stage.finish()
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
-    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=torch.device("cuda", local))
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = float(dt.item())
-    us, wbytes = eng.profile_kernel(2, M, iters=2)
-    kbytes = wbytes + M * shape.n_embd * 2 + M * shape.n_ff * 2
-    info = eng.info
-    wb = torch.tensor([float(info.weight_bytes)], dtype=torch.float64, device=torch.device("cuda", local))
+    # the generated tokens live on the last stage: their CRC goes to rank 0 for the line
+    toks = stage.tokens()
+    crc = zlib.crc32(np.ascontiguousarray(np.stack(toks).astype(np.int32)).tobytes()) if toks is not None else None
+    if world > 1 and stage.last:
+        comm.send_obj(crc, 0)
+    elif world > 1 and rank == 0:
+        crc = comm.recv_obj(world - 1)
+    roof = None
+    if not dry:
+        us, wbytes = eng.profile_kernel(2, M, iters=2)
+        kbytes = wbytes + M * shape.n_embd * 2 + M * shape.n_ff * 2
+        roof = {"bound": "hbm", "achieved": round(kbytes / us / 1e3, 1), "peak": 8000.0, "unit": "GB/s",
+                "frac": round(kbytes / us / 1e3 / 8000.0, 4), "traffic": traffic_bytes(args.model, M),
+                "kernel": ("mm_wide_kernel" if M > 16 else "mm_kernel") +
+                          "<EPI_SWIGLU> (ffn_gate+ffn_up+SiLU*up), rank 0",
+                "us_per_launch": round(us, 2), "bytes_per_launch": int(kbytes)}
+    wb = torch.tensor([float(eng.info.weight_bytes)], dtype=torch.float64, device=device)
     dist.all_reduce(wb)
     total_tokens = args.steps * S * M
     if rank == 0:
@@ -318,25 +357,114 @@ def bench_main(args, metric: str, make_prompts):
             "metric": metric, "value": round(total_tokens / dt, 2), "unit": "tokens/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic (seeded random bf16 weights of the exact shape; random prompt ids)",
+            "data": ("dry run: toy CPU executor over gloo (schedule and launch check, not a measurement)" if dry else
+                     "synthetic (seeded random bf16 weights of the exact shape; random prompt ids)"),
             "config": {"workload": f"{args.model} greedy decode, {world}-stage pipeline, {S} micro-batches x {M} "
                                    f"sequences in flight, prompts U[16,256] (seed 2), n_ctx {args.n_ctx}",
                        "model": args.model, "stages": world, "micro_batches": S, "seqs_per_micro_batch": M,
                        "layer_ranges": parts, "parallelism": f"pp{world}", "handoff": "bf16"},
+            "dist": {"backend": backend, "world_size": world_rd,
+                     "launcher": os.environ.get("MX_LAUNCHER", "torch.distributed.run or external")},
+            "tokens_crc32": crc,
             "step_hbm_gbs": round(step_bytes / dt * args.steps / 1e9, 1),
             "step_hbm_frac": round(step_bytes / (dt / args.steps) / 1e9 / 8000.0 / world, 4),
-            "roofline": {"bound": "hbm", "achieved": round(kbytes / us / 1e3, 1), "peak": 8000.0, "unit": "GB/s",
-                         "frac": round(kbytes / us / 1e3 / 8000.0, 4), "traffic": traffic_bytes(args.model, M),
-                         "kernel": ("mm_wide_kernel" if M > 16 else "mm_kernel") +
-                                   "<EPI_SWIGLU> (ffn_gate+ffn_up+SiLU*up), rank 0",
-                         "us_per_launch": round(us, 2), "bytes_per_launch": int(kbytes)},
+            "roofline": roof,
         }
+        if dry:
+            line["dry_run"] = True
         print(json.dumps(line), flush=True)
     for b in stage.batches:
         b.close()
-    eng.close()
+    if not dry:
+        eng.close()
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class DryEngine:
+    """CPU stand-in for the HIP engine behind ``Stage`` (``bench.py --dry-run``): an embedding,
+    ``n_layer`` layers whose output depends on a per-(slot, layer) running state (so a mis-routed
+    micro-batch or slot changes the tokens, as a wrong KV cache would), and a greedy head; the stage
+    holds layers [lb, le).  Same tensor interface as ``EngineAdapter`` / ``engine.Batch``."""
+
+    H, V = 32, 512
+
+    class _Info:
+        def __init__(self, nbytes):
+            self.weight_bytes = nbytes
+
+    def __init__(self, lb: int, le: int, n_slots: int, n_layer: int):
+        import torch
+
+        self.torch = torch
+        g = torch.Generator().manual_seed(0)
+        self.E = torch.randn(self.V, self.H, generator=g)
+        self.A = [torch.randn(self.H, self.H, generator=g) * 0.3 for _ in range(n_layer)]
+        self.W = torch.randn(self.H, self.V, generator=g)
+        self.lb, self.le = lb, le
+        self.state = torch.zeros(n_layer, n_slots, self.H)
+        self.info = DryEngine._Info(4 * self.H * self.H * (le - lb))
+
+    def layers(self, x, slots):
+        torch = self.torch
+        idx = torch.tensor(slots)
+        for l in range(self.lb, self.le):
+            s = self.state[l, idx] * 0.5 + x
+            self.state[l, idx] = s
+            x = x + torch.tanh(s @ self.A[l]) * 0.5
+        return x
+
+    def stage_rows_tensors(self, slots, pos, ids, x_in, x_out):
+        torch = self.torch
+        x = self.E[torch.tensor(ids).long()] if x_in is None else x_in.clone()
+        # one sequence's rows are consumed in order, as prompt prefill does
+        for i in range(len(slots)):
+            x[i:i + 1] = self.layers(x[i:i + 1], [slots[i]])
+        if x_out is not None:
+            x_out.copy_(x)
+
+    def batch(self, slots, pos, ids, max_steps):
+        return _DryBatch(self, slots, ids)
+
+
+class _DryBatch:
+    def __init__(self, eng, slots, ids):
+        torch = eng.torch
+        self.eng, self.slots = eng, list(slots)
+        self.ids = torch.tensor(ids if ids is not None else [0] * len(slots), dtype=torch.int32)
+        self.hist = []
+
+    def bind_ids_tensor(self, t):
+        t.copy_(self.ids)
+        self.ids = t
+
+    def step_tensors(self, x_in=None, x_out=None):
+        torch = self.eng.torch
+        x = self.eng.E[self.ids.long()] if x_in is None else x_in.clone()
+        x = self.eng.layers(x, self.slots)
+        if x_out is not None:
+            x_out.copy_(x)
+        else:
+            tok = (x @ self.eng.W).argmax(-1).to(torch.int32)
+            self.ids.copy_(tok)
+            self.hist.append(tok.clone())
+
+    def tokens(self):
+        import numpy as np
+
+        torch = self.eng.torch
+        return torch.stack(self.hist, 1).numpy() if self.hist else np.zeros((len(self.slots), 0), np.int32)
+
+    def close(self):
+        pass
 
 
 def traffic_bytes(model: str, M: int):
