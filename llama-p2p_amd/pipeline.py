@@ -144,6 +144,15 @@ class TorchComm:
             w.wait()
         self._pending.clear()
 
+    def abort(self, err: str = ""):
+        """Tear the communicators down so that peers blocked in a receive fail instead of waiting
+        forever (gloo: "connection closed by peer"; RCCL: the communicator abort)."""
+        for g in ([self.obj_group] if self.obj_group is not None else []) + [None]:
+            try:
+                self.dist.distributed_c10d._abort_process_group(g)
+            except Exception:  # noqa: BLE001 -- best effort on an already failing rank
+                pass
+
 
 class Stage:
     """One pipeline stage: S micro-batches of M sequences, greedy decode."""

@@ -20,7 +20,11 @@ shards (pipeline.py), and this module puts the same request API on top of that s
     top-p, min-p, temperature, counter-based draws), so sampling requests run K steps per round too.
   * Hidden states cross stage boundaries in bf16 (``handoff_bf16``: half the bytes of f32).
   * Per-stage busy time is reported to rank 0 every few rounds into a second scoreboard whose mean
-    times give ``proposed_partition`` (stage placement from measured scores).
+    times give ``proposed_partition`` (stage placement from measured scores); when the proposed
+    split predicts a markedly lower slowest-stage time, ``StagePlanner`` has the scheduler drain the
+    lanes and every rank rebuilds its stage on the new layer range (``serve_loop``'s ``rebuild``).
+  * A failure on any rank fails every outstanding request and aborts the peers' transport, so no
+    caller or peer stays blocked.
 
 Transport- and executor-agnostic like pipeline.Stage: tests drive it on CPU over gloo (and an
 in-process rendezvous) with a toy executor, and on one GPU with in-process stage engines.
@@ -80,6 +84,8 @@ class Scheduler:
         self.ids = itertools.count(1)
         self.board = PeerScoreboard(list(range(lanes)), policy=policy, seed=seed)
         self.stop = False
+        self.failed: Optional[str] = None
+        self.drain_to = None  # new stage ranges: admit nothing until the lanes are empty, then re-split
         self.rounds = 0
         # placement decisions: (request id, lane, candidate lanes, scoreboard snapshot before the pick)
         self.placements = collections.deque(maxlen=100000)
@@ -87,6 +93,8 @@ class Scheduler:
     # ---- request side (any thread)
     def submit(self, prompt, max_tokens, samp, seed):
         with self.cv:
+            if self.failed is not None:
+                raise RuntimeError(f"pipeline server failed: {self.failed}")
             if self.stop:
                 raise RuntimeError("pipeline server shutting down")
             r = PRequest(next(self.ids), prompt, samp, seed, max_tokens)
@@ -119,6 +127,28 @@ class Scheduler:
             self.stop = True
             self.cv.notify_all()
 
+    def fail_all(self, err: str):
+        """A round (or a peer) failed: every queued and admitted request returns the error, and the
+        scheduler refuses new ones."""
+        with self.cv:
+            self.failed = err
+            self.stop = True
+            for r in list(self.pending) + [x for ln in self.table for x in ln if x is not None]:
+                r.error, r.done = err, True
+            self.pending.clear()
+            self.table = [[None] * self.M for _ in range(self.S)]
+            self.cv.notify_all()
+
+    def begin_drain(self, parts):
+        with self.cv:
+            self.drain_to = [tuple(p) for p in parts]
+            self.cv.notify_all()
+
+    def end_drain(self):
+        with self.cv:
+            self.drain_to = None
+            self.cv.notify_all()
+
     # ---- server side (the round loop)
     def _free_lanes(self):
         return [l for l in range(self.S) if any(x is None for x in self.table[l])]
@@ -136,8 +166,10 @@ class Scheduler:
                     r.error, r.done = "pipeline server shutting down", True
                 self.cv.notify_all()
                 return {"stop": True}
+            if self.drain_to is not None and not self._active():
+                return {"repartition": list(self.drain_to)}
             admit = []
-            while self.pending:
+            while self.pending and self.drain_to is None:
                 r = self.pending[0]
                 if r.cancel:  # cancelled before admission: no tokens
                     self.pending.popleft()
@@ -168,8 +200,12 @@ class Scheduler:
                         room = min(room, self.n_ctx - r.pos)
                         need = max(need, r.max_tokens - 1)
             K = max(1, min(room, need))
-            if self.pending and self._free_lanes():
-                K = 1
+            if self.pending:
+                # requests wait for a row: end the round when the first row runs out of tokens, so
+                # its row is free for the next round's admissions (EOS cannot be foreseen)
+                soon = min(r.max_tokens - len(r.out) if r not in admit else r.max_tokens - 1
+                           for l in active for r in self.table[l] if r is not None)
+                K = max(1, min(K, soon))
             lanes = []
             for l in active:
                 pos, ids, new = [], [], []
@@ -304,7 +340,9 @@ class StageRunner:
     def _step(self, b, x_in=None, x_out=None):
         """One lane step, bracketed by events on the work stream (after the hand-off waits were
         enqueued, so the pair times this stage's kernels only): the stage's busy time."""
-        if self.device.type == "cuda":
+        if self.world == 1:  # one stage: no placement to inform
+            b.step_tensors(x_in, x_out)
+        elif self.device.type == "cuda":
             e0, e1 = self.torch.cuda.Event(enable_timing=True), self.torch.cuda.Event(enable_timing=True)
             e0.record()
             b.step_tensors(x_in, x_out)
@@ -404,44 +442,83 @@ class StageRunner:
             b.close()
 
 
-def serve_loop(runner: StageRunner, comm, sched: Optional[Scheduler], n_ctx: int, stage_board=None):
-    """The round loop of every rank: rank 0 plans (sched) and broadcasts, every rank runs the plan.
-    Per-stage busy time is gathered every runner.stage_time_every rounds into stage_board (rank 0)."""
-    while True:
-        plan = sched.next_plan() if runner.first else None
-        if runner.world > 1:
-            plan = comm.bcast_obj(plan, 0)
-        if plan.get("stop"):
-            return
-        if plan.get("idle"):
-            continue
+def _abort_peers(comm, err: str):
+    """Best effort: make the peers' blocked receives fail instead of waiting forever."""
+    abort = getattr(comm, "abort", None)
+    if abort is not None:
         try:
+            abort(err)
+        except Exception:  # noqa: BLE001 -- already failing
+            pass
+
+
+def serve_loop(runner: StageRunner, comm, sched: Optional[Scheduler], n_ctx: int, stage_board=None,
+               rebuild=None, planner: Optional["StagePlanner"] = None):
+    """The round loop of every rank: rank 0 plans (sched) and broadcasts, every rank runs the plan.
+    Per-stage busy time is gathered every runner.stage_time_every rounds into the planner's board
+    (or stage_board) on rank 0.  A ``repartition`` plan (the planner's drained re-split) makes every
+    rank replace its stage: ``rebuild(new_parts) -> StageRunner``.  Returns the last runner."""
+    if planner is not None:
+        stage_board = planner.board
+    while True:
+        try:
+            plan = sched.next_plan() if runner.first else None
+            if runner.world > 1:
+                plan = comm.bcast_obj(plan, 0)
+            if plan.get("stop"):
+                return runner
+            if plan.get("idle"):
+                continue
+            if "repartition" in plan:
+                parts = [tuple(p) for p in plan["repartition"]]
+                if rebuild is None:
+                    raise RuntimeError("repartition plan on a stage without a rebuild callback")
+                runner = rebuild(parts)
+                if runner.first:
+                    if planner is not None:
+                        planner.applied(parts)
+                        stage_board = planner.board
+                    sched.end_drain()
+                continue
             runner.run_round(plan, sched, n_ctx)
-        except Exception as e:  # a failed round fails its requests (rank 0) and ends the loop
+            if runner.world > 1 and runner.rounds % runner.stage_time_every == 0:
+                busy = runner.take_busy()
+                if runner.first:
+                    times = [busy] + [comm.recv_obj(r) for r in range(1, runner.world)]
+                    if planner is not None:
+                        new = planner.observe(times, runner.stage_time_every)
+                        if new is not None:
+                            sched.begin_drain(new)
+                    elif stage_board is not None:
+                        for st, t in enumerate(times):
+                            stage_board.update(st, True, t / runner.stage_time_every)
+                else:
+                    comm.send_obj(busy, 0)
+        except Exception as e:  # a failed round (or peer) fails every request and the peers' transport
             if sched is not None:
-                with sched.cv:
-                    for ln in sched.table:
-                        for r in ln:
-                            if r is not None:
-                                r.error, r.done = repr(e), True
-                    sched.table = [[None] * sched.M for _ in range(sched.S)]
-                    sched.cv.notify_all()
+                sched.fail_all(repr(e))
+            _abort_peers(comm, repr(e))
             raise
-        if runner.world > 1 and runner.rounds % runner.stage_time_every == 0:
-            busy = runner.take_busy()
-            if runner.first:
-                times = [busy] + [comm.recv_obj(r) for r in range(1, runner.world)]
-                if stage_board is not None:
-                    for s, t in enumerate(times):
-                        stage_board.update(s, True, t / runner.stage_time_every)
-            else:
-                comm.send_obj(busy, 0)
 
 
 def proposed_partition(stage_board: PeerScoreboard, parts, head_layers: float = 0.0):
-    """Stage placement from measured scores: each stage's mean round time / its layer count gives a
-    per-layer cost on that GPU; layers are re-split (pipeline.partition_layers' DP, per-stage cost
-    weights) so that the slowest stage's predicted time is minimal.  Returns the new ranges."""
+    """Stage placement from measured scores: each stage's mean round time / its layer count (the
+    last stage's counting the head as ``head_layers`` layers) gives a per-layer cost on that GPU;
+    the min-max DP over (stage, first layer) -- O(S * L^2) -- re-splits the layers so that the
+    slowest stage's predicted time is minimal (ties: smaller sum of squares).  Returns the current
+    ranges unless the new split is strictly better."""
+    w = stage_weights(stage_board, parts, head_layers)
+    if w is None:
+        return list(parts)
+    S, n_layer = len(parts), parts[-1][1]
+    new = _minmax_split(w, n_layer, head_layers)
+    if predicted_max(w, new, head_layers) < predicted_max(w, parts, head_layers) * (1 - 1e-9):
+        return new
+    return list(parts)
+
+
+def stage_weights(stage_board: PeerScoreboard, parts, head_layers: float = 0.0):
+    """Relative per-layer cost of each stage's GPU (mean 1) from the measured stage times, or None."""
     st = stage_board.stats()
     S = len(parts)
     speeds = []
@@ -451,33 +528,78 @@ def proposed_partition(stage_board: PeerScoreboard, parts, head_layers: float = 
         speeds.append(t / n if t > 0 else None)
     known = [v for v in speeds if v]
     if not known:
-        return list(parts)
+        return None
     mean = sum(known) / len(known)
-    w = [v / mean if v else 1.0 for v in speeds]
-    n_layer = parts[-1][1]
-    best = None
+    return [v / mean if v else 1.0 for v in speeds]
 
-    def rec(s, lb, acc):
-        nonlocal best
-        if s == S - 1:
-            c = w[s] * (n_layer - lb + head_layers)
-            cand = (max(acc + [c]), acc + [c])
-            bounds.append((lb, n_layer))
-            if best is None or cand[0] < best[0] - 1e-12:
-                best = (cand[0], list(bounds))
-            bounds.pop()
-            return
-        for le in range(lb + 1, n_layer - (S - 1 - s) + 1):
-            c = w[s] * (le - lb)
-            if best is not None and c >= best[0]:
-                break
-            bounds.append((lb, le))
-            rec(s + 1, le, acc + [c])
-            bounds.pop()
 
-    bounds: List = []
-    rec(0, 0, [])
-    return best[1]
+def predicted_max(w, parts, head_layers: float = 0.0) -> float:
+    S = len(parts)
+    return max(w[s] * (le - lb + (head_layers if s == S - 1 else 0.0)) for s, (lb, le) in enumerate(parts))
+
+
+def _minmax_split(w, n_layer: int, head_layers: float):
+    S = len(w)
+    INF = float("inf")
+    # best[s][lb] = (max, sumsq, next boundary) for layers [lb, n_layer) over stages s..S-1
+    best = [[(INF, INF, -1)] * (n_layer + 1) for _ in range(S)]
+    for lb in range(n_layer):
+        c = w[S - 1] * (n_layer - lb + head_layers)
+        best[S - 1][lb] = (c, c * c, n_layer)
+    for s in range(S - 2, -1, -1):
+        for lb in range(s, n_layer - (S - 1 - s)):
+            cur = (INF, INF, -1)
+            for le in range(lb + 1, n_layer - (S - 2 - s)):
+                c = w[s] * (le - lb)
+                m, q, _ = best[s + 1][le]
+                cand = (max(c, m), c * c + q, le)
+                if (round(cand[0], 9), cand[1]) < (round(cur[0], 9), cur[1]):
+                    cur = cand
+            best[s][lb] = cur
+    out, lb = [], 0
+    for s in range(S):
+        le = best[s][lb][2]
+        out.append((lb, le))
+        lb = le
+    return out
+
+
+class StagePlanner:
+    """Rank 0's stage placement (the reference's select_peer / update_peer_performance,
+    p2p:156-168, applied to stages): per-stage busy times go into a PeerScoreboard; once every
+    stage has ``min_samples`` samples, a proposed split whose predicted slowest-stage time is at
+    least ``min_gain`` lower than the current one is returned (the scheduler then drains the lanes
+    and every rank rebuilds its stage).  After a re-split the board starts afresh."""
+
+    def __init__(self, parts, head_layers: float = 0.0, min_gain: float = 0.10, min_samples: int = 2,
+                 enabled: bool = True):
+        self.parts = [tuple(p) for p in parts]
+        self.head_layers, self.min_gain, self.min_samples, self.enabled = head_layers, min_gain, min_samples, enabled
+        self.board = PeerScoreboard(list(range(len(parts))), policy="score_aware")
+        self.history = []  # (parts before, parts after, predicted max before, after, stage weights)
+
+    def observe(self, times, rounds_per_sample: int = 1):
+        for s, t in enumerate(times):
+            self.board.update(s, True, t / rounds_per_sample)
+        if not self.enabled:
+            return None
+        st = self.board.stats()
+        if any(st.get(s, {}).get("success", 0) < self.min_samples for s in range(len(self.parts))):
+            return None
+        w = stage_weights(self.board, self.parts, self.head_layers)
+        if w is None:
+            return None
+        new = proposed_partition(self.board, self.parts, self.head_layers)
+        cur_t, new_t = predicted_max(w, self.parts, self.head_layers), predicted_max(w, new, self.head_layers)
+        if new != self.parts and new_t <= cur_t * (1.0 - self.min_gain):
+            self.history.append({"from": list(self.parts), "to": list(new), "predicted_max_from": cur_t,
+                                 "predicted_max_to": new_t, "weights": w, "t": time.time()})
+            return new
+        return None
+
+    def applied(self, parts):
+        self.parts = [tuple(p) for p in parts]
+        self.board = PeerScoreboard(list(range(len(parts))), policy="score_aware")
 
 
 # ------------------------------------------------------------------------------ engine executor
@@ -543,10 +665,12 @@ class PipelineFront:
     llama.Llama.create_completion drives the pipeline unchanged.  The round loop runs on a thread."""
 
     def __init__(self, runner: StageRunner, comm, sched: Scheduler, n_ctx: int, n_vocab: int, n_embd: int,
-                 stage_board: Optional[PeerScoreboard] = None):
+                 stage_board: Optional[PeerScoreboard] = None, rebuild=None, planner: Optional[StagePlanner] = None):
         self.runner, self.comm, self.sched, self.n_ctx = runner, comm, sched, n_ctx
         self.n_vocab, self.n_embd = n_vocab, n_embd
         self.stage_board = stage_board
+        self.planner = planner
+        self._rebuild = rebuild
         self.engine = None  # this stage's engine, closed with the front
         self.stage_threads = []  # in-process stages (local_pipeline_llama): joined on close
         self.error = None
@@ -561,9 +685,16 @@ class PipelineFront:
 
                 torch.cuda.set_device(dev)
                 torch.cuda.set_stream(torch.cuda.Stream(device=dev))
-            serve_loop(self.runner, self.comm, self.sched, self.n_ctx, self.stage_board)
+            rebuild = None
+            if self._rebuild is not None:
+                def rebuild(parts):
+                    self.runner = self._rebuild(self, parts)
+                    return self.runner
+            self.runner = serve_loop(self.runner, self.comm, self.sched, self.n_ctx, self.stage_board,
+                                     rebuild=rebuild, planner=self.planner)
         except Exception as e:  # noqa: BLE001 -- surfaced to callers through their requests
             self.error = e
+            self.sched.fail_all(repr(e))
 
     def submit(self, ids, max_tokens, seed=None, **kw):
         import random
@@ -575,10 +706,9 @@ class PipelineFront:
             samp.get("frequency_penalty", 0.0) != 0.0 or samp.get("presence_penalty", 0.0) != 0.0
         if sampling and not (1 <= tk <= 64 and 0 <= rl <= 64):
             raise ValueError("pipeline serving samples on the device: top_k must be 1..64 and repeat_last_n 0..64")
-        if self.error is not None:
-            raise RuntimeError(f"pipeline server failed: {self.error!r}")
         s = seed if seed is not None and seed >= 0 else random.getrandbits(63)
         mt = max_tokens if max_tokens and max_tokens > 0 else self.n_ctx - len(ids)
+        # Scheduler.submit refuses under its lock once the round loop has failed (fail_all)
         return self.sched.submit(list(map(int, ids)), min(mt, self.n_ctx - len(ids)), samp, s)
 
     def poll(self, rid, n_have=0):
@@ -607,20 +737,30 @@ class PipelineFront:
         self.stage_threads = []
 
 
+def _layer_costs(model_path):
+    """(bytes per layer, head bytes) of a synthetic model path, or None for a GGUF."""
+    from . import synth
+
+    syn = synth.parse_synthetic_path(model_path)
+    if syn is None:
+        return None
+    sh = syn[0]
+    return 2 * (2 * sh.n_embd ** 2 + 2 * sh.n_embd * sh.n_embd_kv + 3 * sh.n_embd * sh.n_ff), 2 * sh.n_vocab * sh.n_embd
+
+
 def _stage_setup(model_path, rank, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts=None):
     """Engine holding this rank's byte-balanced layer range, its executor and runner pieces."""
     from . import engine as E
     from .pipeline import partition_layers
 
     if parts is None:
+        costs = _layer_costs(model_path)
+        if costs is None:
+            raise ValueError("pipeline serving of a GGUF needs explicit stage ranges (parts=...)")
         from . import synth
 
-        syn = synth.parse_synthetic_path(model_path)
-        if syn is None:
-            raise ValueError("pipeline serving of a GGUF needs explicit stage ranges (parts=...)")
-        sh = syn[0]
-        layer = 2 * (2 * sh.n_embd ** 2 + 2 * sh.n_embd * sh.n_embd_kv + 3 * sh.n_embd * sh.n_ff)
-        parts = partition_layers(sh.n_layer, layer, 2 * sh.n_vocab * sh.n_embd, world)
+        sh = synth.parse_synthetic_path(model_path)[0]
+        parts = partition_layers(sh.n_layer, costs[0], costs[1], world)
     lb, le = parts[rank]
     eng = E.Engine(model_path, n_ctx=n_ctx, n_seq_max=lanes * rows, layer_begin=lb, layer_end=le,
                    device=device.index if device.type == "cuda" else -1, handoff_bf16=handoff_bf16)
@@ -629,24 +769,40 @@ def _stage_setup(model_path, rank, world, lanes, rows, n_ctx, kmax, device, hand
 
 def serve_stage(model_path: str, comm, rank: int, world: int, lanes: int, rows: int = 32, n_ctx: int = 512,
                 kmax: int = 8, device=None, handoff_bf16: bool = True, parts=None):
-    """Ranks 1..S-1: hold a stage and execute rank 0's round plans until it stops."""
+    """Ranks 1..S-1: hold a stage and execute rank 0's round plans until it stops (a repartition
+    plan replaces the stage engine by one holding the new layer range)."""
     import torch
 
     device = device or torch.device("cuda", torch.cuda.current_device())
     eng, parts = _stage_setup(model_path, rank, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts)
-    runner = StageRunner(EngineExecutor(eng, device), comm, rank, world, lanes, rows, kmax, device)
+    held = {"eng": eng, "runner": StageRunner(EngineExecutor(eng, device), comm, rank, world, lanes, rows, kmax,
+                                              device)}
+
+    def rebuild(new_parts):
+        held["runner"].close()
+        held["eng"].close()
+        held["runner"] = held["eng"] = None
+        e2, _ = _stage_setup(model_path, rank, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, new_parts)
+        held["eng"] = e2
+        held["runner"] = StageRunner(EngineExecutor(e2, device), comm, rank, world, lanes, rows, kmax, device)
+        return held["runner"]
+
     try:
-        serve_loop(runner, comm, None, n_ctx)
+        serve_loop(held["runner"], comm, None, n_ctx, rebuild=rebuild)
     finally:
-        runner.close()
-        eng.close()
+        if held["runner"] is not None:
+            held["runner"].close()
+        if held["eng"] is not None:
+            held["eng"].close()
 
 
 def pipeline_llama(model_path: str, comm, world: int, lanes: Optional[int] = None, rows: int = 32,
                    n_ctx: int = 512, kmax: int = 8, device=None, handoff_bf16: bool = True, parts=None,
-                   policy: str = "score_aware", seed: Optional[int] = None, verbose: bool = False):
+                   policy: str = "score_aware", seed: Optional[int] = None, verbose: bool = False,
+                   repartition: bool = True, min_gain: float = 0.10):
     """Rank 0: a Llama-compatible object whose completions run on the S-stage pipeline (ranks 1..S-1
-    run serve_stage with the same arguments)."""
+    run serve_stage with the same arguments).  ``repartition``: apply the stage planner's re-splits
+    (drain, rebuild every stage, resume) when they predict >= ``min_gain`` lower slowest-stage time."""
     import torch
 
     from .llama import Llama
@@ -656,12 +812,25 @@ def pipeline_llama(model_path: str, comm, world: int, lanes: Optional[int] = Non
     eng, parts = _stage_setup(model_path, 0, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts)
     runner = StageRunner(EngineExecutor(eng, device), comm, 0, world, lanes, rows, kmax, device)
     sched = Scheduler(lanes, rows, n_ctx, eng.info.eos_id, kmax, policy=policy, seed=seed)
-    stage_board = PeerScoreboard(list(range(world)), policy="score_aware")
+    costs = _layer_costs(model_path)
+    head_layers = costs[1] / costs[0] if costs else 1.0
+    planner = StagePlanner(parts, head_layers=head_layers, min_gain=min_gain, enabled=repartition)
+
+    def rebuild(front, new_parts):
+        front.runner.close()
+        front.engine.close()
+        front.engine = None
+        e2, _ = _stage_setup(model_path, 0, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, new_parts)
+        front.engine = e2
+        llm.parts = list(new_parts)
+        return StageRunner(EngineExecutor(e2, device), comm, 0, world, lanes, rows, kmax, device)
+
     # vocabulary size from the model (stage 0 has no head: n_vocab comes from the model info)
-    front = PipelineFront(runner, comm, sched, n_ctx, eng.info.n_vocab, eng.info.n_embd, stage_board)
+    front = PipelineFront(runner, comm, sched, n_ctx, eng.info.n_vocab, eng.info.n_embd, planner.board,
+                          rebuild=rebuild, planner=planner)
     llm = Llama.from_engine(model_path, front, n_ctx=n_ctx, verbose=verbose)
     front.engine = eng
-    llm.parts, llm.stage_board, llm.scheduler = parts, stage_board, sched
+    llm.parts, llm.stage_board, llm.scheduler, llm.planner = parts, planner.board, sched, planner
     return llm
 
 
@@ -674,6 +843,7 @@ class LocalHub:
 
         self._q = collections.defaultdict(queue.Queue)
         self.lock = threading.Lock()
+        self.aborted: Optional[str] = None
 
     def q(self, src, dst):
         with self.lock:
@@ -690,6 +860,24 @@ class LocalComm:
     def __init__(self, hub: LocalHub, rank: int, world: int, timeout: float = 120.0):
         self.hub, self.rank, self.world, self.timeout = hub, rank, world, timeout
 
+    def _get(self, src):
+        """Next message from src; raises once any stage has aborted (or after the timeout)."""
+        import queue
+
+        q = self.hub.q(src, self.rank)
+        t0 = time.time()
+        while True:
+            if self.hub.aborted is not None:
+                raise RuntimeError(f"pipeline peer aborted: {self.hub.aborted}")
+            try:
+                return q.get(timeout=0.1)
+            except queue.Empty:
+                if time.time() - t0 > self.timeout:
+                    raise TimeoutError(f"stage {self.rank}: nothing from stage {src} in {self.timeout:.0f}s")
+
+    def abort(self, err: str):
+        self.hub.aborted = self.hub.aborted or f"stage {self.rank}: {err}"
+
     def send(self, t, dst):
         import torch
 
@@ -699,7 +887,7 @@ class LocalComm:
         self.hub.q(self.rank, dst).put(("t", c))
 
     def recv(self, t, src):
-        kind, c = self.hub.q(src, self.rank).get(timeout=self.timeout)
+        kind, c = self._get(src)
         assert kind == "t", "hand-off order mismatch: expected a tensor"
         t.copy_(c)
 
@@ -716,7 +904,7 @@ class LocalComm:
         self.hub.q(self.rank, dst).put(("o", obj))
 
     def recv_obj(self, src):
-        kind, obj = self.hub.q(src, self.rank).get(timeout=self.timeout)
+        kind, obj = self._get(src)
         assert kind == "o", "hand-off order mismatch: expected an object"
         return obj
 
@@ -731,7 +919,7 @@ class LocalComm:
 
 def local_pipeline_llama(model_path: str, parts, lanes: int = 2, rows: int = 8, n_ctx: int = 512, kmax: int = 8,
                          device=None, handoff_bf16: bool = True, policy: str = "score_aware",
-                         seed: Optional[int] = None):
+                         seed: Optional[int] = None, repartition: bool = True, min_gain: float = 0.10):
     """S = len(parts) stage engines of one model in THIS process (one GPU), each served by its own
     thread and stream, behind one Llama-compatible front: the pipeline server end to end without a
     multi-GPU launch (tests; a 1-GPU rehearsal of the S-GPU layout)."""
@@ -759,7 +947,7 @@ def local_pipeline_llama(model_path: str, parts, lanes: int = 2, rows: int = 8, 
     torch.cuda.set_stream(torch.cuda.Stream(device=device))
     ready.wait()
     llm = pipeline_llama(model_path, comms[0], world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts,
-                         policy=policy, seed=seed)
+                         policy=policy, seed=seed, repartition=repartition, min_gain=min_gain)
     llm._engine.stage_threads = threads
     llm._stage_threads, llm._stage_errors = threads, errors
     return llm

@@ -67,6 +67,9 @@ def main():
     ap.add_argument("--replicas", action="store_true")
     ap.add_argument("--policy", default="score_aware", choices=["score_aware", "reference"])
     ap.add_argument("--time-scale", type=float, default=1.0, help="<1 compresses the arrival clock")
+    ap.add_argument("--min-gain", type=float, default=0.10,
+                    help="apply a stage re-split when it predicts this much lower slowest-stage time")
+    ap.add_argument("--no-repartition", action="store_true")
     args = ap.parse_args()
     from llama_p2p_amd import synth
     from llama_p2p_amd.placement import PeerScoreboard, poisson_schedule, serve
@@ -112,7 +115,8 @@ def main():
             dist.destroy_process_group()
             return
         llm = pipeserve.pipeline_llama(path, comm, world, world, args.rows, args.n_ctx, device=dev,
-                                       policy=args.policy, seed=0)
+                                       policy=args.policy, seed=0, repartition=not args.no_repartition,
+                                       min_gain=args.min_gain)
         mode = f"{world} stages, one GPU each (RCCL)"
     else:
         from llama_p2p_amd.pipeline import partition_layers
@@ -121,7 +125,8 @@ def main():
         parts = partition_layers(shape.n_layer, 2 * (2 * h * h + 2 * h * kv + 3 * h * ff), 2 * shape.n_vocab * h,
                                  args.stages)
         llm = pipeserve.local_pipeline_llama(path, parts, lanes=args.lanes or args.stages, rows=args.rows, n_ctx=args.n_ctx,
-                                             policy=args.policy, seed=0)
+                                             policy=args.policy, seed=0, repartition=not args.no_repartition,
+                                             min_gain=args.min_gain)
         mode = f"{args.stages} stages in one process on one GPU, {args.lanes or args.stages} lanes"
     front = llm._engine
     res = drive(lambda p, g: front.generate(p, g, temperature=0.0, ignore_eos=True), sched, args.gen,
@@ -132,8 +137,10 @@ def main():
     res.update({"model": args.model, "mode": mode, "policy": args.policy, "rate": args.rate,
                 "time_scale": args.time_scale, "prompt_len": [args.prompt_lo, args.prompt_hi], "gen": args.gen,
                 "layer_ranges": llm.parts, "requests_per_lane": lanes, "lane_scores": llm.scheduler.board.stats(),
-                "stage_scores": llm.stage_board.stats(),
-                "proposed_partition": pipeserve.proposed_partition(llm.stage_board, llm.parts),
+                "stage_scores": llm.planner.board.stats(),
+                "proposed_partition": pipeserve.proposed_partition(llm.planner.board, llm.parts,
+                                                                   llm.planner.head_layers),
+                "repartitions": llm.planner.history,
                 "rounds": llm.scheduler.rounds})
     llm.close()
     print(json.dumps(res), flush=True)
