@@ -35,6 +35,7 @@ sys.path.insert(0, ROOT)
 METRIC = "decode tokens/sec (node) + % HBM roofline, Llama-3-8B at 1/2/4/8-stage"
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
 MFMA_PEAK_BF16 = 2.5e15  # dense bf16 MFMA, MI355X spec (MI355X_MICROARCH.md; no sparsity)
+MFMA_PEAK_I8 = 5.0e15  # dense int8 MFMA: the K=64 / 32x32x32 forms at 2x the bf16 rate (MI355X_MICROARCH.md)
 MB_SEQS = 32
 
 
@@ -257,7 +258,9 @@ def quant_bench(args, wtype: str, steps: int):
     if args.prefill_prompts > 0:
         # > 64-row chunks: K-quant as dequantised bf16 GEMMs; Q8_0 as grouped Q8_0 GEMVs (ggml's
         # arithmetic), or dequantised bf16 GEMMs with MX_Q8_GEMM_PREFILL=1
-        out["prefill"] = prefill_bench(eng, shape, args.prefill_prompts, args.prefill_len)
+        # Q8_0 / Q4_0 chunks run the int8-MFMA GEMM (q8gemm_kernel): utilisation against the int8 peak
+        out["prefill"] = prefill_bench(eng, shape, args.prefill_prompts, args.prefill_len,
+                                       int8=wtype in ("q8_0", "q4_0"))
     eng.close()
     return out
 
@@ -406,10 +409,12 @@ def hbm_probe(gib: int = 4, iters: int = 8):
                       "(read + write) or read bytes / HIP-event time"}
 
 
-def prefill_bench(eng, shape, n_prompts: int, plen: int):
+def prefill_bench(eng, shape, n_prompts: int, plen: int, int8: bool = False):
     """Batched prefill: n_prompts prompts of plen tokens (seed 3) pushed through the
     engine's GEMM path (chunks of up to PREFILL_ROWS = 4096 rows) with no lm_head (logits of prompt tokens are not needed), timed on the
-    host around the whole pass.  MFMA utilisation = achieved dense bf16 FLOP/s / 2.5 PFLOP/s."""
+    host around the whole pass.  MFMA utilisation = achieved dense FLOP/s (OP/s) / the dense peak of
+    the arithmetic the GEMMs run in: bf16 2.5 PFLOP/s, or for the Q8_0 / Q4_0 int8 GEMM (int8=True)
+    the int8 dense peak of 5 POPS."""
     import numpy as np
 
     rng = np.random.default_rng(3)
@@ -430,8 +435,10 @@ def prefill_bench(eng, shape, n_prompts: int, plen: int):
     linear = L * (h * (h + 2 * kv) + h * h + 3 * h * ff)
     attn = 4 * L * h * n_prompts * plen * (plen + 1) // 2  # QK^T + PV, causal
     flops = 2 * n_tok * linear + attn
+    peak = MFMA_PEAK_I8 if int8 else MFMA_PEAK_BF16
     return {"tok_s": round(n_tok / dt, 1), "ms": round(dt * 1e3, 2), "tokens": n_tok,
-            "tflops": round(flops / dt / 1e12, 1), "mfma_frac": round(flops / dt / MFMA_PEAK_BF16, 4),
+            "tflops": round(flops / dt / 1e12, 1), "mfma_frac": round(flops / dt / peak, 4),
+            "mfma_peak": {"dtype": "int8" if int8 else "bf16", "tflops": peak / 1e12},
             "sample": f"{n_prompts} prompts x {plen} tokens, 4096-row GEMM chunks, no lm_head"}
 
 
@@ -454,23 +461,25 @@ def make_text_prompts(n, tokenize, seed=2, lo=16, hi=256):
 
 
 class _CountingModel:
-    """The node's ``self.model``: forwards to Llama (greedy, the parity setting) and counts completion
-    tokens (cached_inference itself returns text only)."""
+    """The node's ``self.model``: forwards to Llama and counts completion tokens (cached_inference
+    itself returns text only).  greedy: temperature 0 (the parity setting); otherwise the reference's
+    literal call, llama-cpp-python's defaults (temperature 0.8, top_k 40, top_p 0.95, min_p 0.05)."""
 
-    def __init__(self, llm):
+    def __init__(self, llm, greedy: bool = True):
         import threading
 
         self.llm, self.tokens, self.calls, self.lock = llm, 0, 0, threading.Lock()
+        self.kw = {"temperature": 0.0} if greedy else {}
 
     def __call__(self, prompt, **kw):
-        out = self.llm(prompt, temperature=0.0, **kw)
+        out = self.llm(prompt, **self.kw, **kw)
         with self.lock:
             self.tokens += out["usage"]["completion_tokens"]
             self.calls += 1
         return out
 
 
-def serving_bench(args, n: int = 32):
+def serving_bench(args, n: int = 32, greedy: bool = True):
     """BASELINE config 3 as worded -- Llama-3-8B bf16 serving 32 concurrent synthetic requests with the
     result cache on -- through the drop-in node: n client threads send JSON inference requests at once
     over an in-process REP transport with concurrent contexts (node.LocalTransport) ->
@@ -487,7 +496,7 @@ def serving_bench(args, n: int = 32):
 
     path = f"synthetic:{args.model}"
     llm = Llama(model_path=path, verbose=False, n_seq_max=max(n, 1), n_ctx=args.n_ctx)
-    model = _CountingModel(llm)
+    model = _CountingModel(llm, greedy)
     tr = LocalTransport()
     node = LlamaP2PNode(path, 5000, cache_size=100, secret_key="k", model=model, transport=tr, n_contexts=n)
     threading.Thread(target=node.handle_requests, daemon=True).start()
@@ -527,8 +536,9 @@ def serving_bench(args, n: int = 32):
     node.active = False
     llm.close()
     lat1.sort()
+    how = "greedy" if greedy else "llama-cpp-python default sampling (temperature 0.8, top_k 40, top_p 0.95, min_p 0.05)"
     return {"workload": f"config 3: {path} bf16, {n} concurrent requests through handle_requests (REP contexts) "
-                        f"-> cached_inference -> Llama(prompt, max_tokens=100), greedy; then the same {n} again",
+                        f"-> cached_inference -> Llama(prompt, max_tokens=100), {how}; then the same {n} again",
             "wave1": {"requests": n, "calls": calls1 - calls0, "prompt_tokens": n_prompt_tok,
                       "generated_tokens": gen1, "wall_s": round(dt1, 4), "tok_s": round(gen1 / dt1, 1),
                       "p50_latency_s": round(lat1[len(lat1) // 2], 4), "max_latency_s": round(lat1[-1], 4)},
@@ -638,6 +648,13 @@ def main():
         if "wave1" in sv:
             sv["ratio_to_value"] = round(sv["wave1"]["tok_s"] / line["value"], 4)
         line["serving"] = sv
+        # the reference's literal call (p2p:125): Llama(prompt, max_tokens=100) with its default sampling
+        sd = sec.run("serving_default_sampling", lambda: serving_bench(args, args.serve_requests, greedy=False))
+        if "wave1" in sd:
+            sd["ratio_to_value"] = round(sd["wave1"]["tok_s"] / line["value"], 4)
+            if "wave1" in sv:
+                sd["ratio_to_greedy_serving"] = round(sd["wave1"]["tok_s"] / sv["wave1"]["tok_s"], 4)
+        line["serving_default_sampling"] = sd
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = sec.run("cpu_baseline", lambda: cpu_baseline(args.model))
     if args.tiny_tokens > 0:

@@ -1603,7 +1603,8 @@ void mx_engine::samp_row(const Request* r, SampRow* o) const {
 // when that stays inside n_ctx (so the rows form 16-position blocks of one sequence and the flash
 // prefill attention runs; the pad K/V is overwritten by the first decode steps before anything
 // reads it), lm_head only on each request's last prompt row, and the first token by the device
-// argmax (ties -> lowest id) or, for sampling requests, the host sampler chain.
+// argmax (ties -> lowest id) or, for sampling requests, the device sampling chain (the host sampler
+// when a request's settings are outside the device chain's range).
 int mx_engine::prefill_batch(std::vector<Request*>& reqs) {
   static const bool trace = getenv("MX_SCHED_TRACE") != nullptr;
   const auto t0 = std::chrono::steady_clock::now();
@@ -1639,9 +1640,17 @@ int mx_engine::prefill_batch(std::vector<Request*>& reqs) {
   const int chunk = gemm_ok() ? PREFILL_ROWS : MAX_ROWS;
   const int total = (int)slots.size();
   std::vector<int32_t> tok(reqs.size());
-  bool any_sampling = false;
-  for (Request* r : reqs) any_sampling |= r->samp.temperature > 0.f || has_penalties(r->samp);
+  bool any_sampling = false, dev_pick = use_dev_topk;
+  for (Request* r : reqs)
+    if (r->samp.temperature > 0.f || has_penalties(r->samp)) {
+      any_sampling = true;
+      dev_pick &= device_sampleable(r->samp);
+    }
+  // every sampling request fits the device chain: first tokens are drawn on the device (the same
+  // samp_pick and counter-based draw 0 as the host sampler), no logits rows cross PCIe
+  dev_pick &= any_sampling;
   std::vector<float> lg;
+  std::vector<SampRow> sr;
   size_t q0 = 0;  // first request whose last row is not yet evaluated
   for (int i = 0; i < total;) {
     // chunk [i, e): at most `chunk` rows and at most MAX_ROWS request ends (logits rows)
@@ -1666,10 +1675,27 @@ int mx_engine::prefill_batch(std::vector<Request*>& reqs) {
                                     n_out, false, nullptr, nullptr, nullptr, 0, nullptr, 0, st);
     rows_blocked = false;
     if (frc) return frc;
-    if (n_out) {
+    int ktop = 0;
+    if (n_out && dev_pick) {
+      sr.resize(n_out);
+      for (int k = 0; k < n_out; k++) {
+        samp_row(reqs[q0 + k], &sr[k]);
+        const mx_sampling& sp = reqs[q0 + k]->samp;
+        if (sp.temperature > 0.f || has_penalties(sp)) ktop = std::max(ktop, std::min(sp.top_k, n_vocab));
+      }
+    }
+    if (n_out && ktop > 0) {
+      HIPC(hipMemcpyAsync(d_samp, sr.data(), n_out * sizeof(SampRow), hipMemcpyHostToDevice, st));
+      pick_samp = d_samp;
+      pick_k = ktop;
+      pick(n_out, nullptr, nullptr, nullptr, 0, nullptr, 0, st);
+      pick_samp = nullptr;
+      pick_k = 0;
+      HIPC(hipMemcpyAsync(tok.data() + q0, d_tok, n_out * 4, hipMemcpyDeviceToHost, st));
+    } else if (n_out) {
       launch_argmax(logits, n_vocab, n_out, n_vocab, am_val, am_idx, d_tok, nullptr, nullptr, nullptr, 0, nullptr, 0, st);
       HIPC(hipMemcpyAsync(tok.data() + q0, d_tok, n_out * 4, hipMemcpyDeviceToHost, st));
-      if (any_sampling) {
+      if (any_sampling && !dev_pick) {
         lg.resize((size_t)n_out * n_vocab);
         HIPC(hipMemcpyAsync(lg.data(), logits, lg.size() * 4, hipMemcpyDeviceToHost, st));
       }
@@ -1679,7 +1705,8 @@ int mx_engine::prefill_batch(std::vector<Request*>& reqs) {
     for (int k = 0; k < n_out; k++) {
       Request* r = reqs[q0 + k];
       int32_t t = tok[q0 + k];
-      if (r->samp.temperature > 0.f || has_penalties(r->samp)) t = sample_host(r, lg.data() + (size_t)k * n_vocab);
+      if (!dev_pick && (r->samp.temperature > 0.f || has_penalties(r->samp)))
+        t = sample_host(r, lg.data() + (size_t)k * n_vocab);
       r->out.push_back(t);
       r->next_tok = t;
     }

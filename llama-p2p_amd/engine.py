@@ -274,16 +274,22 @@ class Engine:
         _check(lib().mx_submit(self._h, ids.ctypes.data, len(ids), ctypes.byref(s), max_tokens, ctypes.byref(req)))
         return req.value
 
-    def submit_many(self, prompts, max_tokens: int, seeds=None, **kw):
+    def submit_many(self, prompts, max_tokens: int, seeds=None, per_request=None, **kw):
         """Several requests queued atomically (one scheduler round admits them all); same sampling
-        keywords as submit(), one seed per prompt.  Returns the request ids."""
+        keywords as submit() (or ``per_request``: one keyword dict per prompt), one seed per prompt.
+        Returns the request ids."""
         n = len(prompts)
         arrs = [_i32(p) for p in prompts]
         ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
         lens = _i32([len(a) for a in arrs])
         mts = _i32([max_tokens] * n)
         samp = (MxSampling * n)()
+        base = kw
         for i in range(n):
+            kw = dict(base, **per_request[i]) if per_request is not None else base
+            if per_request is not None and "seed" in kw:
+                seeds = list(seeds) if seeds is not None else [None] * n
+                seeds[i] = kw["seed"]
             lib().mx_sampling_default(ctypes.byref(samp[i]))
             s = samp[i]
             s.temperature, s.top_k = kw.get("temperature", 0.0), kw.get("top_k", 40)

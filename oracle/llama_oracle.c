@@ -942,34 +942,9 @@ static void rope_rows(float *v, int n_heads, int d, const float *cs /* [d/2][2] 
     }
 }
 
-/*
- * Evaluate n tokens at positions pos0..pos0+n-1 of this context (one llama_decode
- * of a ubatch).  logits: if all_logits, [n][V]; else [V] for the last token.
- * Returns 0 on success.
- */
-int orc_eval(orc_ctx *c, const int32_t *ids, int n, int pos0, float *logits, int all_logits) {
-    orc_model *m = c->m;
-    const orc_hparams *hp = &m->hp;
-    int exact = m->flags & ORC_EXACT;
-    int h = hp->n_embd, kvd = m->n_embd_kv, ff = hp->n_ff, V = hp->n_vocab;
-    int nh = hp->n_head, nkv = hp->n_head_kv, d = m->head_dim, gq = nh / nkv;
-    if (n <= 0 || pos0 < 0 || pos0 + n > c->n_ctx) return -1;
-    for (int t = 0; t < n; t++)
-        if (ids[t] < 0 || ids[t] >= V) return -2;
-    int T = n;
-    int mx = ff > h ? ff : h;
-    float *x = (float *)malloc(sizeof(float) * T * h);
-    float *cur = (float *)malloc(sizeof(float) * T * mx);
-    float *q = (float *)malloc(sizeof(float) * T * h);
-    float *k = (float *)malloc(sizeof(float) * T * kvd);
-    float *v = (float *)malloc(sizeof(float) * T * kvd);
-    float *att = (float *)malloc(sizeof(float) * T * h);
-    float *g = (float *)malloc(sizeof(float) * T * ff);
-    float *u = (float *)malloc(sizeof(float) * T * ff);
-    float *tmp = (float *)malloc(sizeof(float) * T * h);
-    uint16_t *scratch = (uint16_t *)malloc(sizeof(uint16_t) * T * mx);
-    const float kq_scale = 1.0f / sqrtf((float)d);
-
+/* GET_ROWS of the token embedding (bf16, Q8_0 or K-quant rows) into x[T][h] (f32). */
+static void embed_rows(const orc_model *m, const int32_t *ids, int T, float *x) {
+    const int h = m->hp.n_embd;
     for (int t = 0; t < T; t++) {
         if (m->tok_embd_kq) { /* GET_ROWS of a K-quant: dequantize_row_q{4,5,6}_K */
             const size_t rb = (size_t)(h / QK_K) * orc_kq_block_bytes(m->tok_embd_kq_type);
@@ -985,8 +960,30 @@ int orc_eval(orc_ctx *c, const int32_t *ids, int n, int pos0, float *logits, int
             for (int i = 0; i < h; i++) x[(size_t)t * h + i] = bf16_to_f32(m->tok_embd[(size_t)ids[t] * h + i]);
         }
     }
+}
 
-    for (int l = 0; l < hp->n_layer; l++) {
+/*
+ * Layers [lb, le) of llm_build_llama on the residual stream x[T][h] (in place) for T tokens of this
+ * context at positions pos0..pos0+T-1 (their K/V go into the context's cache of those layers).
+ */
+static void layers_fwd(orc_ctx *c, float *x, int T, int pos0, int lb, int le) {
+    orc_model *m = c->m;
+    const orc_hparams *hp = &m->hp;
+    int exact = m->flags & ORC_EXACT;
+    int h = hp->n_embd, kvd = m->n_embd_kv, ff = hp->n_ff;
+    int nh = hp->n_head, nkv = hp->n_head_kv, d = m->head_dim, gq = nh / nkv;
+    int mx = ff > h ? ff : h;
+    float *cur = (float *)malloc(sizeof(float) * T * mx);
+    float *q = (float *)malloc(sizeof(float) * T * h);
+    float *k = (float *)malloc(sizeof(float) * T * kvd);
+    float *v = (float *)malloc(sizeof(float) * T * kvd);
+    float *att = (float *)malloc(sizeof(float) * T * h);
+    float *g = (float *)malloc(sizeof(float) * T * ff);
+    float *u = (float *)malloc(sizeof(float) * T * ff);
+    float *tmp = (float *)malloc(sizeof(float) * T * h);
+    uint16_t *scratch = (uint16_t *)malloc(sizeof(uint16_t) * T * mx);
+    const float kq_scale = 1.0f / sqrtf((float)d);
+    for (int l = lb; l < le; l++) {
         orc_layer *L = &m->layers[l];
         for (int t = 0; t < T; t++) rmsnorm(cur + (size_t)t * h, x + (size_t)t * h, L->attn_norm, h, hp->eps);
         matmul(q, L->wq, L->q8[L_Q], L->kq[L_Q], L->kq_type[L_Q], cur, T, h, h, exact, scratch, L->q4[L_Q]);
@@ -1074,12 +1071,65 @@ int orc_eval(orc_ctx *c, const int32_t *ids, int n, int pos0, float *logits, int
         matmul(tmp, L->wd, L->q8[L_DOWN], L->kq[L_DOWN], L->kq_type[L_DOWN], g, T, ff, h, exact, scratch, L->q4[L_DOWN]);
         for (size_t i = 0; i < (size_t)T * h; i++) x[i] += tmp[i];
     }
-    int t0 = all_logits ? 0 : T - 1;
-    int nt = T - t0;
-    for (int t = 0; t < nt; t++) rmsnorm(cur + (size_t)t * h, x + (size_t)(t0 + t) * h, m->out_norm, h, hp->eps);
-    matmul(logits, m->output, m->output_q8, m->output_kq, m->output_kq_type, cur, nt, h, V, exact, scratch, m->output_q4);
+    free(cur); free(q); free(k); free(v); free(att); free(g); free(u); free(tmp); free(scratch);
+}
 
-    free(x); free(cur); free(q); free(k); free(v); free(att); free(g); free(u); free(tmp); free(scratch);
+/* Final RMS_NORM + lm_head of nt rows of x[.][h] -> logits[nt][V]. */
+static void head_rows(const orc_model *m, const float *x, int nt, float *logits) {
+    const orc_hparams *hp = &m->hp;
+    int h = hp->n_embd, V = hp->n_vocab;
+    float *cur = (float *)malloc(sizeof(float) * (size_t)nt * h);
+    uint16_t *scratch = (uint16_t *)malloc(sizeof(uint16_t) * (size_t)nt * h);
+    for (int t = 0; t < nt; t++) rmsnorm(cur + (size_t)t * h, x + (size_t)t * h, m->out_norm, h, hp->eps);
+    matmul(logits, m->output, m->output_q8, m->output_kq, m->output_kq_type, cur, nt, h, V, m->flags & ORC_EXACT,
+           scratch, m->output_q4);
+    free(cur); free(scratch);
+}
+
+/*
+ * Evaluate n tokens at positions pos0..pos0+n-1 of this context (one llama_decode
+ * of a ubatch).  logits: if all_logits, [n][V]; else [V] for the last token.
+ * Returns 0 on success.
+ */
+int orc_eval(orc_ctx *c, const int32_t *ids, int n, int pos0, float *logits, int all_logits) {
+    orc_model *m = c->m;
+    const orc_hparams *hp = &m->hp;
+    int h = hp->n_embd, V = hp->n_vocab;
+    if (n <= 0 || pos0 < 0 || pos0 + n > c->n_ctx) return -1;
+    for (int t = 0; t < n; t++)
+        if (ids[t] < 0 || ids[t] >= V) return -2;
+    float *x = (float *)malloc(sizeof(float) * (size_t)n * h);
+    embed_rows(m, ids, n, x);
+    layers_fwd(c, x, n, pos0, 0, hp->n_layer);
+    int t0 = all_logits ? 0 : n - 1;
+    head_rows(m, x + (size_t)t0 * h, n - t0, logits);
+    free(x);
+    return 0;
+}
+
+/*
+ * Per-layer parity hook (a pipeline stage of the oracle): x_out[n][h] = layers [lb, le) applied to
+ * the residual stream x_in[n][h] of n tokens at positions pos0.. (K/V of those layers are written).
+ * With ids != NULL the stream starts from their embedding (x_in ignored), with logits != NULL the
+ * final norm + lm_head of every row follow (x_out may then be NULL).  0 on success.
+ */
+int orc_layers(orc_ctx *c, const int32_t *ids, const float *x_in, int n, int pos0, int lb, int le, float *x_out,
+               float *logits) {
+    orc_model *m = c->m;
+    int h = m->hp.n_embd;
+    if (n <= 0 || pos0 < 0 || pos0 + n > c->n_ctx || lb < 0 || le > m->hp.n_layer || lb > le) return -1;
+    float *x = (float *)malloc(sizeof(float) * (size_t)n * h);
+    if (ids) {
+        for (int t = 0; t < n; t++)
+            if (ids[t] < 0 || ids[t] >= m->hp.n_vocab) { free(x); return -2; }
+        embed_rows(m, ids, n, x);
+    } else {
+        memcpy(x, x_in, sizeof(float) * (size_t)n * h);
+    }
+    layers_fwd(c, x, n, pos0, lb, le);
+    if (x_out) memcpy(x_out, x, sizeof(float) * (size_t)n * h);
+    if (logits) head_rows(m, x, n, logits);
+    free(x);
     return 0;
 }
 

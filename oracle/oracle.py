@@ -79,6 +79,8 @@ def lib():
         L.orc_ctx_free.argtypes = [vp]
         L.orc_eval.argtypes = [vp, vp, i32, i32, vp, i32]
         L.orc_eval.restype = i32
+        L.orc_layers.argtypes = [vp, vp, vp, i32, i32, i32, i32, vp, vp]
+        L.orc_layers.restype = i32
         L.orc_generate_greedy.argtypes = [vp, vp, i32, i32, i32, vp]
         L.orc_generate_greedy.restype = i32
         L.orc_num_threads.restype = i32
@@ -193,6 +195,23 @@ class OracleContext:
         if rc:
             raise ValueError(f"orc_eval rc={rc}")
         return out
+
+    def layers(self, x_in, pos0: int, layer_begin: int, layer_end: int, ids=None, logits: bool = False):
+        """Per-layer hook (orc_layers): the residual stream after layers [layer_begin, layer_end) of
+        x_in [n][n_embd] f32 (or of the embedding of ``ids``) for n tokens at positions pos0..; their
+        K/V enter this context's cache.  Returns x_out [n][n_embd], or (x_out, logits [n][V])."""
+        h = self.model.shape.n_embd
+        ids_a = None if ids is None else np.ascontiguousarray(ids, dtype=np.int32)
+        xin = None if ids_a is not None else np.ascontiguousarray(x_in, dtype=np.float32).reshape(-1, h)
+        n = len(ids_a) if ids_a is not None else xin.shape[0]
+        out = np.zeros((n, h), dtype=np.float32)
+        lg = np.zeros((n, self.model.shape.n_vocab), dtype=np.float32) if logits else None
+        rc = lib().orc_layers(self._c, ids_a.ctypes.data if ids_a is not None else None,
+                              xin.ctypes.data if xin is not None else None, n, pos0, layer_begin, layer_end,
+                              out.ctypes.data, lg.ctypes.data if lg is not None else None)
+        if rc:
+            raise ValueError(f"orc_layers rc={rc}")
+        return (out, lg) if logits else out
 
     def generate_greedy(self, prompt, n_gen: int, n_batch: int = 512) -> np.ndarray:
         prompt = np.ascontiguousarray(prompt, dtype=np.int32)

@@ -125,3 +125,25 @@ def test_oracle_rope_scaling_matches_transformers(oracle_mod, case):
     # unit factors and scale 1 are the identity, bit for bit
     m.set_rope(np.ones(sh.head_dim // 2, np.float32), 1.0)
     assert np.array_equal(m.context(64).eval(g["ids"], 0, all_logits=True), plain)
+
+
+@pytest.mark.parametrize("name", ["test-gqa8", "test-d128"])
+def test_per_layer_hook_equals_eval(oracle_mod, name):
+    """orc_layers (the per-layer parity hook) composes to orc_eval bit for bit: the embedding, every
+    layer as its own call on the previous call's residual stream, then the head -- for a prompt and
+    for a decode token that reads the K/V the per-layer calls wrote."""
+    from llama_p2p_amd import synth
+
+    sh = synth.SHAPES[name]
+    m = oracle_mod.OracleModel(sh, seed=0)
+    ids = np.random.default_rng(4).integers(3, sh.n_vocab, 11).astype(np.int32)
+    ref = m.context(32).eval(ids, 0, all_logits=True)
+    c = m.context(32)
+    for a, b in ((0, 10), (10, 11)):
+        x = c.layers(None, a, 0, 0, ids=ids[a:b])
+        for l in range(sh.n_layer):
+            x = c.layers(x, a, l, l + 1)
+        _, lg = c.layers(x, a, sh.n_layer, sh.n_layer, logits=True)
+        assert np.array_equal(lg, ref[a:b])
+    with pytest.raises(ValueError):
+        c.layers(x, 0, 0, sh.n_layer + 1)

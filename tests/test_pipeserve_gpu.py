@@ -87,3 +87,45 @@ def test_node_over_pipeline():
     assert len(node.cache) == len(prompts)
     node.active = False
     llm.close()
+
+
+def test_pipeline_sampling_chain_equals_single_engine():
+    """Seeded sampled requests (penalties, top_k <= 64) through the pipeline's device chain
+    (mx_stage_rows_pick's first draw, the window / draw-count hand-over of newly admitted rows in
+    run_round) give the tokens of the same requests through one engine's scheduler (Engine.submit),
+    with greedy and sampled rows mixed in one lane.  f32 hand-off (stage splits are bitwise equal to
+    one engine), the same admission round on both sides, and counter-based draws that do not depend
+    on the schedule (K steps per round): the tokens must be identical."""
+    from llama_p2p_amd import pipeserve, synth
+    from llama_p2p_amd.engine import Engine
+
+    name = "test-gqa8"
+    sh = synth.SHAPES[name]
+    path = f"synthetic:{name}:seed=0"
+    rng = np.random.default_rng(17)
+    prompts = [[1] + rng.integers(3, sh.n_vocab, int(rng.integers(6, 40))).tolist() for _ in range(6)]
+    kws = [dict(temperature=0.8, top_k=40, top_p=0.95, min_p=0.05, seed=101),
+           dict(temperature=0.0),
+           dict(temperature=1.1, top_k=12, top_p=0.9, min_p=0.02, repeat_penalty=1.3, repeat_last_n=16, seed=7),
+           dict(temperature=0.7, top_k=64, top_p=1.0, min_p=0.0, frequency_penalty=0.4, presence_penalty=0.3,
+                seed=99),
+           dict(temperature=0.0, repeat_penalty=1.2, repeat_last_n=32, seed=5),
+           dict(temperature=0.9, top_k=5, seed=12345)]
+    # both sides admit the six requests in ONE round (one batched prefill of the same rows, then one
+    # decode batch), so every logit is computed by the same kernels at the same row counts
+    eng = Engine(path, n_ctx=256, n_seq_max=8)
+    rids = eng.submit_many(prompts, 20, per_request=[dict(kw, ignore_eos=True) for kw in kws])
+    ref = [eng.wait(r)[0] for r in rids]
+    eng.close()
+    # one lane of 8 rows: every request shares it (greedy and sampled rows mixed)
+    llm = pipeserve.local_pipeline_llama(path, [(0, 1), (1, 3)], lanes=1, rows=8, n_ctx=256, handoff_bf16=False)
+    front = llm._engine
+    with llm.scheduler.cv:  # queued atomically: the next round admits all of them
+        rids = [front.submit(p, 20, ignore_eos=True, **kw) for p, kw in zip(prompts, kws)]
+    outs = [front.wait(r)[0] for r in rids]
+    placements = list(llm.scheduler.placements)
+    llm.close()
+    assert not llm._stage_errors, llm._stage_errors
+    assert {lane for _, lane, _, _ in placements} == {0}
+    for i, (a, b) in enumerate(zip(outs, ref)):
+        assert a == b, f"request {i} ({kws[i]}): pipeline {a} vs engine {b}"

@@ -1,13 +1,10 @@
 #!/bin/bash
-# new-test pass: the named tests (no -x), then the whole -m gpu suite with -x
-set -o pipefail
-OUT=gpurun_out/$1; shift
+# Run selected GPU tests (one pytest process), log under gpurun_out/<tag>/.
+#   tools/gpu/new_tests.sh <tag> <pytest args...>
+TAG=$1; shift
+OUT=gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest "$@" -v -s --timeout 240 --timeout-method thread > $OUT/new.log 2>&1
+timeout -k 10 1000 python -u -m pytest -x -v -s --timeout 900 --timeout-method thread "$@" > $OUT/pytest.log 2>&1
 rc=$?
-tail -25 $OUT/new.log
-if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
-rc2=$?
-tail -15 $OUT/pytest_gpu.log
-exit $(( rc > rc2 ? rc : rc2 ))
+tail -40 $OUT/pytest.log
+exit $rc
