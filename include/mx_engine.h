@@ -70,7 +70,7 @@ typedef struct {
   int32_t n_ctx, n_seq_max;
   int32_t layer_begin, layer_end, has_embed, has_head;
   uint64_t weight_bytes; /* device bytes of the weights this stage streams per decode step */
-  int32_t weight_type;       /* ggml type of the layer matrices: 30 BF16, 8 Q8_0, 12 Q4_K (Q4_K_M), 13 Q5_K (Q5_K_M) */
+  int32_t weight_type;       /* ggml type of the layer matrices: 30 BF16, 8 Q8_0, 2 Q4_0, 12 Q4_K (Q4_K_M), 13 Q5_K (Q5_K_M) */
 } mx_model_info;
 
 typedef struct {
@@ -103,8 +103,9 @@ void mx_opts_default(mx_opts* o);
 void mx_sampling_default(mx_sampling* s);
 const char* mx_last_error(void);
 
-/* model_path: a GGUF file (LLaMA; BF16, Q8_0 or Q4_K_M / Q5_K_M matrices natively, other block types
- * dequantised to bf16 at load) or "synthetic:<shape>[:seed=N][:q8_0|:q4_k_m|:q5_k_m]" */
+/* model_path: a GGUF file (LLaMA; all-BF16, all-Q8_0, all-Q4_0 and Q4_K_M / Q5_K_M files natively -- the
+ * quantised ones on the int8 MFMA with ggml's arithmetic; any other mix of F32 / F16 / BF16 / Q4_0 / Q8_0
+ * / K-quant matrices dequantised to bf16 at load) or "synthetic:<shape>[:seed=N][:q8_0|:q4_0|:q4_k_m|:q5_k_m]" */
 int mx_engine_create(const char* model_path, const mx_opts* opts, mx_engine** out);
 void mx_engine_destroy(mx_engine* e);
 /* Parse a GGUF container without touching a GPU (header, metadata, tensor table, bounds of every
