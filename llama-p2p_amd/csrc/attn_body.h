@@ -15,6 +15,7 @@ constexpr float LOG2E = 1.4426950408889634f;
 // chunk holding `pos` (FIN) or the partial last chunk needs sits behind a wave-uniform branch, so
 // the full chunks run the bare MFMA + softmax stream.
 constexpr int ATTN_FIN_MAXSLAB = 8;  // split-K slabs the FIN path can sum (the wide launchers split K at most 8 ways)
+constexpr int ATTN_MEGA_MAXSLAB = 4;  // ... and the persistent decode's q|k|v (decode1.hip caps its split at 4)
 
 struct BlockSync {
   __device__ void operator()() const { __syncthreads(); }
@@ -89,12 +90,13 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
                                                                    : nq + nkv + kvh * D + (i - G * D - D);
       // all slab and RoPE loads issued together (clamped: extra reads repeat the last slab): a run-time
       // slab loop or a load behind the RoPE branch made each load wait for itself
-      f32x4 sv[ATTN_FIN_MAXSLAB];
+      constexpr int MS = MEGA ? ATTN_MEGA_MAXSLAB : ATTN_FIN_MAXSLAB;
+      f32x4 sv[MS];
       if constexpr (MEGA) {  // 4 granules per slab (two 16-byte sc1 loads), until every tag is this op's
         for (int spin = 0;; ++spin) {
           bool ok = true;
 #pragma unroll
-          for (int k = 0; k < ATTN_FIN_MAXSLAB; ++k) {
+          for (int k = 0; k < MS; ++k) {
             const unsigned off = (unsigned)((min(k, a.nslab - 1) * a.slab_stride + (size_t)c * N + row) * 8);
             const u32x4 g0 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srs, off, 0, 16));
             const u32x4 g1 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srs, off + 16, 0, 16));
@@ -106,7 +108,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
         }
       } else {
 #pragma unroll
-        for (int k = 0; k < ATTN_FIN_MAXSLAB; ++k)
+        for (int k = 0; k < MS; ++k)
           sv[k] = *reinterpret_cast<const f32x4*>(a.slabs + min(k, a.nslab - 1) * a.slab_stride + (size_t)c * N + row);
       }
       const int dd = i % D;
@@ -116,7 +118,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
       // would pull its load into the branch again)
       f32x4 v = sv[0];
 #pragma unroll
-      for (int k = 1; k < ATTN_FIN_MAXSLAB; ++k) v += sv[k] * (k < a.nslab ? 1.0f : 0.0f);
+      for (int k = 1; k < MS; ++k) v += sv[k] * (k < a.nslab ? 1.0f : 0.0f);
       {  // RoPE (mode NORM: adjacent pairs) on q and k, as selects (a branch would pull csv's load into it)
         const bool rope = i < G * D + D && pos < a.n_ctx;
         const f32x4 s = v;

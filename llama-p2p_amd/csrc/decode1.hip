@@ -3,7 +3,7 @@
 // Batch-1 decode streams every weight byte once per token; as one kernel per op (qkv, attention,
 // attn_output, gate/up, down) each launch pays its ramp (first loads in flight) and drain, and the
 // next op's weights start only after the previous op's last work-group: ~16 us of an 82 us Llama-3-8B
-// layer.  Here every layer of the token runs in one launch of one 320-thread work-group
+// layer.  Here every layer of the token runs in one launch of one 256-thread work-group
 // per CU, and the weight stream never stops:
 //
 //   wave 0 (loader)      streams this CU's share of every matrix, layer after layer, through an LDS
@@ -12,10 +12,10 @@
 //                        layout makes it 16 KiB contiguous).  It never waits for a hand-off: only for
 //                        a free slot.  So while the consumers wait for the previous op's outputs, the
 //                        ring fills with the next op's weights (what a kernel boundary cannot do).
-//   waves 1-4 (consumers) per op: gather the op's input vector written by other CUs (write-through
+//   waves 1-3 (consumers) per op: gather the op's input vector written by other CUs (write-through
 //                        loads), RMS_NORM it where ggml does, then for each of this CU's items (row
 //                        tile x k-range) multiply the ring's slots on the MFMA (v_mfma_f32_16x16x32_bf16,
-//                        the token in B column 0; the four waves split each slot's 16 k-tiles and
+//                        the token in B column 0; the three waves split each slot's 16 k-tiles and
 //                        their partial tiles meet in LDS), and publish the op's outputs write-through.
 //
 // Hand-offs between CUs (every op needs all of the previous op's outputs) are 8-byte granules
@@ -27,7 +27,7 @@
 // engine reports it and falls back to the per-op kernels).
 //
 // Per layer: QKV (q|k|v tiles, split-K ks ways, partials) -> ATT (work-groups 0..n_head_kv-1: the
-// decode attention body of kernels.hip on the four consumer waves, finishing q/k/v from the
+// decode attention body of kernels.hip on the three consumer waves, finishing q/k/v from the
 // partials: sum, RoPE, K/V store) -> WO (x += attn.Wo) -> GU (SwiGLU of the ffn-normed x) -> DOWN
 // (x += h.Wd).  The last layer also writes x and its per-16 sums of squares for the head kernels.
 // Arithmetic = the per-op kernels': bf16 weights and activations, f32 accumulation, RMS_NORM with a
@@ -43,8 +43,11 @@ namespace {
 typedef __attribute__((address_space(1))) const void d1_gvoid;
 typedef __attribute__((address_space(3))) void d1_lvoid;
 
-constexpr int D1_CONS = 4;          // consumer waves (1..4): 4 k-tiles of each 16-k-tile slot each
-constexpr int D1_THREADS = 64 * (1 + D1_CONS);
+// consumer waves (1..3): k-tiles c, c+3, ... of each 16-k-tile slot.  Four waves per work-group =
+// one per SIMD, so a wave may hold 512 VGPRs (the attention body needs ~250); a fifth wave halves that
+// budget and spilled 120 B per lane
+constexpr int D1_CONS = 3;
+constexpr int D1_KPW = (16 + D1_CONS - 1) / D1_CONS;  // k-tiles per consumer wave and slot (6, 5, 5)
 constexpr int SLOT_BYTES = 16384;   // 16 k-tiles of one 16-row tile
 constexpr int SLOT_KT = 16;
 constexpr int MAX_INFLIGHT = 3;     // slots issued and not yet landed (vmcnt <= 48 < 63)
@@ -63,9 +66,9 @@ __device__ __forceinline__ PhaseDesc phase_desc(const D1Args& a, const uint64_t*
   const uint8_t* W = reinterpret_cast<const uint8_t*>(wtab[4 * l + p]);
   switch (p) {
     case 0: return {W, (a.h + 2 * a.kv) / 16, a.h / 32, a.ks_qkv};
-    case 1: return {W, a.h / 16, a.h / 32, 1};
+    case 1: return {W, a.h / 16, a.h / 32, a.ks_o};
     case 2: return {W, 2 * a.ff / 16, a.h / 32, 1};
-    default: return {W, a.h / 16, a.ff / 32, 1};
+    default: return {W, a.h / 16, a.ff / 32, a.ks_d};
   }
 }
 
@@ -73,6 +76,12 @@ __device__ __forceinline__ PhaseDesc phase_desc(const D1Args& a, const uint64_t*
 __device__ __forceinline__ void item_range(int n_items, int g, int G, int& i0, int& i1) {
   i0 = (int)((long long)n_items * g / G);
   i1 = (int)((long long)n_items * (g + 1) / G);
+}
+// the slots [s0, s1) of a whole row's KT/16 that k-part kp of ks covers (parts differ by <= 1 slot)
+__device__ __forceinline__ void part_slots(const PhaseDesc& d, int kp, int& s0, int& s1) {
+  const int ns = d.KT / SLOT_KT;
+  s0 = kp * ns / d.ks;
+  s1 = (kp + 1) * ns / d.ks;
 }
 
 struct Ctl {  // LDS control words
@@ -107,9 +116,12 @@ __device__ __forceinline__ void vm_wait_slots(int n) {  // vmcnt <= 16 n (n slot
 }
 
 // ---------------------------------------------------------------------------------------- loader
-template <int NS>
+// NL loader waves; wave k streams the slots k, k + NL, k + 2 NL, ... of the work-group's stream, up to
+// MAX_INFLIGHT of them in flight (vmcnt counts at most 63 loads per wave: NL waves put NL x 48 KiB in
+// flight per CU)
+template <int NS, int NL>
 __device__ void d1_loader(const D1Args& a, const uint64_t* wtab, uint8_t* ring, Ctl* ctl, unsigned long long deadline) {
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, k = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int g = blockIdx.x, G = gridDim.x;
   // slots of one layer for this work-group (the same every layer)
   int per_layer = 0;
@@ -117,62 +129,78 @@ __device__ void d1_loader(const D1Args& a, const uint64_t* wtab, uint8_t* ring, 
     const PhaseDesc d = phase_desc(a, wtab, 0, p);
     int i0, i1;
     item_range(d.T * d.ks, g, G, i0, i1);
-    per_layer += (i1 - i0) * (d.KT / d.ks / SLOT_KT);
+    for (int it = i0; it < i1; ++it) {
+      int s0, s1;
+      part_slots(d, it % d.ks, s0, s1);
+      per_layer += s1 - s0;
+    }
   }
   const int total = per_layer * a.n_layer;
-  // stream cursor
-  int l = 0, p = 0, it = 0, it1 = 0, j = 0, nsl = 1;
+  // stream cursor (at slot `cur`)
+  int l = 0, p = 0, it = 0, it1 = 0, j = 0, s0 = 0, s1 = 1, cur = 0;
   PhaseDesc d{};
   auto open_phase = [&]() {
     for (;;) {
       d = phase_desc(a, wtab, l, p);
       item_range(d.T * d.ks, g, G, it, it1);
-      nsl = d.KT / d.ks / SLOT_KT;
       j = 0;
-      if (it < it1) return;
+      if (it < it1) {
+        part_slots(d, it % d.ks, s0, s1);
+        return;
+      }
       if (++p == 4) {
         p = 0;
         if (++l == a.n_layer) return;
       }
     }
   };
+  auto advance = [&]() {  // cursor to the next slot of the stream
+    ++cur;
+    if (++j == s1 - s0) {  // next item / phase / layer
+      j = 0;
+      if (++it == it1) {
+        if (++p == 4) {
+          p = 0;
+          ++l;
+        }
+        if (l < a.n_layer) open_phase();
+      } else {
+        part_slots(d, it % d.ks, s0, s1);
+      }
+    }
+  };
   if (total > 0) open_phase();
-  int issued = 0, published = 0;
+  for (int i = 0; i < k && cur < total; ++i) advance();
+  int issued = k, published = k, inflight = 0;  // this wave's next slot to issue / to publish
   unsigned long long t_vm = 0, t_idle = 0;
-  unsigned long long* tr = a.trace ? a.trace + (size_t)g * (a.n_layer * 10 + 8) + a.n_layer * 10 : nullptr;
+  unsigned long long* tr =
+      a.trace && k == 0 ? a.trace + (size_t)g * (a.n_layer * 10 + 8) + a.n_layer * 10 : nullptr;
   while (published < total) {
-    if (issued < total && issued - published < MAX_INFLIGHT) {
+    if (issued < total && inflight < MAX_INFLIGHT) {
       const int s = issued % NS;
       const unsigned need = (unsigned)(D1_CONS * (issued / NS));
       if (__hip_atomic_load(&ctl->freed[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= need) {
-        const int tile = it / d.ks, kt0 = (it % d.ks) * (d.KT / d.ks) + j * SLOT_KT;
+        const int tile = it / d.ks, kt0 = (s0 + j) * SLOT_KT;
         const uint8_t* src = d.W + ((size_t)tile * d.KT + kt0) * 1024 + lane * 16;
         const unsigned dst = __builtin_amdgcn_readfirstlane(
             (unsigned)reinterpret_cast<uintptr_t>(ring) + (unsigned)(s * SLOT_BYTES));
 #pragma unroll
         for (int c = 0; c < SLOT_KT; ++c) glds16_nt(src + c * 1024, dst + c * 1024);
-        ++issued;
-        if (++j == nsl) {  // next item / phase / layer
-          j = 0;
-          if (++it == it1) {
-            if (++p == 4) {
-              p = 0;
-              ++l;
-            }
-            if (l < a.n_layer) open_phase();
-          }
-        }
+        issued += NL;
+        ++inflight;
+        for (int i = 0; i < NL && cur < total; ++i) advance();
         continue;
       }
     }
-    if (issued > published) {  // the oldest slot in flight: wait for it, publish it
+    if (inflight > 0) {  // this wave's oldest slot in flight: wait for it, publish it
       const unsigned long long t0 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
-      vm_wait_slots(issued - published - 1);
+      vm_wait_slots(inflight - 1);
       if (tr) t_vm += __builtin_amdgcn_s_memrealtime() - t0;
       asm volatile("" ::: "memory");
       __hip_atomic_store(&ctl->full[published % NS], (unsigned)(published + 1), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_WORKGROUP);
-      ++published;
+      published += NL;
+      --inflight;
       continue;
     }
     // nothing in flight and the next slot still in use: the consumers wait for a hand-off
@@ -198,7 +226,7 @@ struct Cons {
   const D1Args& a;
   Ctl* ctl;
   unsigned long long deadline;
-  int cw, lane, tid;  // consumer wave 0..3, lane, thread 0..255
+  int cw, lane, tid;  // consumer wave 0..2, lane, thread 0..191
   unsigned long long* tr = nullptr;  // this work-group's trace row (consumer wave 0, lane 0 writes)
   unsigned long long t_full = 0;
   __device__ void stamp(int k) {
@@ -207,9 +235,9 @@ struct Cons {
   unsigned gen = 0;   // consumer-barrier generation
   bool dead = false;
 
-  __device__ Cons(const D1Args& a_, Ctl* c, unsigned long long dl)
+  __device__ Cons(const D1Args& a_, Ctl* c, unsigned long long dl, int nl)
       : a(a_), ctl(c), deadline(dl) {
-    tid = (int)threadIdx.x - 64;
+    tid = (int)threadIdx.x - 64 * nl;
     cw = __builtin_amdgcn_readfirstlane(tid >> 6);
     lane = tid & 63;
   }
@@ -300,14 +328,28 @@ __device__ __forceinline__ void sweep(Cons& C, const unsigned long long* gran, i
     }
   }
 }
-// xf = the residual stream (f32 granules); returns this thread's share of sum(x^2) in double
-__device__ __forceinline__ double gather_x(Cons& C, float* xf, const unsigned long long* gran, int n, unsigned tag) {
+// xf = the residual stream (f32 granules, `parts` K-parts summed in part order); returns this
+// thread's share of sum(x^2) in double
+__device__ __forceinline__ double gather_x(Cons& C, float* xf, const unsigned long long* gran, int n, unsigned tag,
+                                           int parts = 1) {
   double q = 0.0;
-  sweep(C, gran, n, tag, [&](int i, unsigned a0, unsigned a1) {
-    const float x0 = __uint_as_float(a0), x1 = __uint_as_float(a1);
-    *reinterpret_cast<float2*>(xf + 2 * i) = float2{x0, x1};
-    q += (double)(x0 * x0) + (double)(x1 * x1);
-  });
+  if (parts == 1) {
+    sweep(C, gran, n, tag, [&](int i, unsigned a0, unsigned a1) {
+      const float x0 = __uint_as_float(a0), x1 = __uint_as_float(a1);
+      *reinterpret_cast<float2*>(xf + 2 * i) = float2{x0, x1};
+      q += (double)(x0 * x0) + (double)(x1 * x1);
+    });
+  } else {  // a thread sweeps the same indices in both parts: no barrier between them
+    sweep(C, gran, n, tag, [&](int i, unsigned a0, unsigned a1) {
+      *reinterpret_cast<float2*>(xf + 2 * i) = float2{__uint_as_float(a0), __uint_as_float(a1)};
+    });
+    sweep(C, gran + n, n, tag, [&](int i, unsigned a0, unsigned a1) {
+      const float2 p0 = *reinterpret_cast<const float2*>(xf + 2 * i);
+      const float x0 = p0.x + __uint_as_float(a0), x1 = p0.y + __uint_as_float(a1);
+      *reinterpret_cast<float2*>(xf + 2 * i) = float2{x0, x1};
+      q += (double)(x0 * x0) + (double)(x1 * x1);
+    });
+  }
   return q;
 }
 // dst[0..2n) = bf16 pairs from n granules
@@ -324,8 +366,19 @@ __device__ __forceinline__ void put_gran(unsigned long long* g, unsigned tag, un
 // act = bf16((x * 1/sqrt(mean(x^2) + eps)) * w) -- ggml's RMS_NORM + MUL, then the bf16 rounding
 // of src1 for the bf16 MUL_MAT; q = this thread's share of sum(x^2) (double), reduced here in a fixed
 // order (waves, then consumer waves 0, 1, 2)
+// this thread's norm weights (issued before the hand-off sweep, so their round trip overlaps it)
+struct NormW {
+  f32x4 v[GU_];
+};
+__device__ __forceinline__ NormW norm_w_load(Cons& C, const float* w, int n) {
+  NormW r;
+  const int nv = n / 4;
+#pragma unroll
+  for (int u = 0; u < GU_; ++u) r.v[u] = *reinterpret_cast<const f32x4*>(w + 4 * min(C.tid + u * 64 * D1_CONS, nv - 1));
+  return r;
+}
 __device__ __forceinline__ void rms_norm_act(Cons& C, double q, const float* xf, const float* w, uint16_t* act,
-                                             int n, float eps) {
+                                             int n, float eps, const NormW* pre = nullptr) {
   for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
   if (C.lane == 0) C.ctl->dpart[C.cw] = q;
   C.sync();
@@ -336,8 +389,13 @@ __device__ __forceinline__ void rms_norm_act(Cons& C, double q, const float* xf,
   const int nv = n / 4;
   for (int b = C.tid; b < nv; b += 64 * D1_CONS * GU_) {
     f32x4 wv[GU_];
+    if (pre && b == C.tid) {
 #pragma unroll
-    for (int u = 0; u < GU_; ++u) wv[u] = *reinterpret_cast<const f32x4*>(w + 4 * min(b + u * 64 * D1_CONS, nv - 1));
+      for (int u = 0; u < GU_; ++u) wv[u] = pre->v[u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < GU_; ++u) wv[u] = *reinterpret_cast<const f32x4*>(w + 4 * min(b + u * 64 * D1_CONS, nv - 1));
+    }
 #pragma unroll
     for (int u = 0; u < GU_; ++u) {
       const int i = b + u * 64 * D1_CONS;
@@ -359,11 +417,12 @@ __device__ __forceinline__ void run_items(Cons& C, const PhaseDesc& d, const uin
                                           float (*red)[D1_CONS][16], int& seq, int& item_par, Epi epi) {
   int i0, i1;
   item_range(d.T * d.ks, blockIdx.x, gridDim.x, i0, i1);
-  const int nsl = d.KT / d.ks / SLOT_KT;
   const int lane = C.lane;
   for (int it = i0; it < i1; ++it) {
     const int tile = it / d.ks, kp = it % d.ks;
-    const int ktb = kp * (d.KT / d.ks);
+    int s0, s1;
+    part_slots(d, kp, s0, s1);
+    const int nsl = s1 - s0, ktb = s0 * SLOT_KT;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f}, acc2 = acc;
     for (int j = 0; j < nsl; ++j) {
       const int s = seq % NS;
@@ -377,16 +436,17 @@ __device__ __forceinline__ void run_items(Cons& C, const PhaseDesc& d, const uin
       const uint8_t* base = ring + s * SLOT_BYTES;
       // this wave's k-tiles cw, cw+4, cw+8, cw+12 of the slot: all LDS reads first, then the MFMAs
       // into two accumulators (no MFMA waits for the one before it)
-      u32x4 av[SLOT_KT / D1_CONS], bv[SLOT_KT / D1_CONS];
+      u32x4 av[D1_KPW], bv[D1_KPW];
 #pragma unroll
-      for (int k = 0; k < SLOT_KT / D1_CONS; ++k) {
-        const int c = C.cw + k * D1_CONS;
+      for (int k = 0; k < D1_KPW; ++k) {
+        const int c = min(C.cw + k * D1_CONS, SLOT_KT - 1);  // the last one of waves 1, 2 is a repeat
         av[k] = *reinterpret_cast<const u32x4*>(base + c * 1024 + lane * 16);
         bv[k] = *reinterpret_cast<const u32x4*>(act + (ktb + j * SLOT_KT + c) * 32 + 8 * (lane >> 4));
       }
 #pragma unroll
-      for (int k = 0; k < SLOT_KT / D1_CONS; ++k) {
-        const u32x4 b = (lane & 15) ? u32x4{0u, 0u, 0u, 0u} : bv[k];  // the token is B column 0
+      for (int k = 0; k < D1_KPW; ++k) {
+        const bool live = C.cw + k * D1_CONS < SLOT_KT && (lane & 15) == 0;
+        const u32x4 b = live ? bv[k] : u32x4{0u, 0u, 0u, 0u};  // the token is B column 0
         if (k & 1)
           acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av[k]), __builtin_bit_cast(bf16x8, b),
                                                          acc2, 0, 0, 0);
@@ -417,8 +477,8 @@ __device__ __forceinline__ void run_items(Cons& C, const PhaseDesc& d, const uin
   }
 }
 
-template <int D, int G, int NS>
-__global__ __launch_bounds__(D1_THREADS, 1) void decode1_kernel(D1Args a) {
+template <int D, int G, int NS, int NL>
+__global__ __launch_bounds__(64 * (NL + D1_CONS), 1) void decode1_kernel(D1Args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t d1_lds[];
   uint8_t* ring = d1_lds;
   float* xf = reinterpret_cast<float*>(d1_lds + NS * SLOT_BYTES);
@@ -427,7 +487,7 @@ __global__ __launch_bounds__(D1_THREADS, 1) void decode1_kernel(D1Args a) {
   float (*red)[D1_CONS][16] = reinterpret_cast<float (*)[D1_CONS][16]>(act + amax);
   Ctl* ctl = reinterpret_cast<Ctl*>(reinterpret_cast<uint8_t*>(red) + 2 * D1_CONS * 16 * 4);
   uint64_t* wtab = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(ctl) + sizeof(Ctl));
-  for (int i = threadIdx.x; i < 4 * a.n_layer; i += D1_THREADS) {
+  for (int i = threadIdx.x; i < 4 * a.n_layer; i += 64 * (NL + D1_CONS)) {
     const D1Layer& L = a.layers[i >> 2];
     const uint16_t* w = (i & 3) == 0 ? L.qkv : (i & 3) == 1 ? L.o : (i & 3) == 2 ? L.gu : L.down;
     wtab[i] = reinterpret_cast<uint64_t>(w);
@@ -437,11 +497,11 @@ __global__ __launch_bounds__(D1_THREADS, 1) void decode1_kernel(D1Args a) {
   if (threadIdx.x < 18) reinterpret_cast<unsigned*>(ctl)[threadIdx.x] = 0u;  // full, freed, cbar, abort
   __syncthreads();  // the only full-work-group barrier: before the roles split
 
-  if (threadIdx.x < 64) {
-    d1_loader<NS>(a, wtab, ring, ctl, deadline);
+  if (threadIdx.x < 64 * NL) {
+    d1_loader<NS, NL>(a, wtab, ring, ctl, deadline);
     return;
   }
-  Cons C(a, ctl, deadline);
+  Cons C(a, ctl, deadline, NL);
   const int g = blockIdx.x, Gn = gridDim.x;
   if (a.trace) C.tr = a.trace + (size_t)g * (a.n_layer * 10 + 8);
   C.stamp(a.n_layer * 10 + 0);
@@ -473,10 +533,12 @@ __global__ __launch_bounds__(D1_THREADS, 1) void decode1_kernel(D1Args a) {
           for (int j = 0; j < 4; ++j) q += (double)(v[j] * v[j]);
         }
       }
+      rms_norm_act(C, q, xf, L.attn_norm, act, h, a.eps);
     } else {
-      q = gather_x(C, xf, a.xs, h, tag(l - 1, PH_DOWN));
+      const NormW nw = norm_w_load(C, L.attn_norm, h);
+      q = gather_x(C, xf, a.xs, h, tag(l - 1, PH_DOWN), a.ks_d);
+      rms_norm_act(C, q, xf, L.attn_norm, act, h, a.eps, &nw);
     }
-    rms_norm_act(C, q, xf, L.attn_norm, act, h, a.eps);
     C.sync();
     if (C.dead) break;
     C.stamp(l * 10 + 0);
@@ -514,17 +576,18 @@ __global__ __launch_bounds__(D1_THREADS, 1) void decode1_kernel(D1Args a) {
     C.stamp(l * 10 + 4);
     const unsigned t_wo = tag(l, PH_WO);
     run_items<NS>(C, phase_desc(a, wtab, l, 1), ring, act, red, seq, item_par,
-                  [&](int tile, int, int qd, f32x4 s, float (*)[16]) {
+                  [&](int tile, int kp, int qd, f32x4 s, float (*)[16]) {
                     const int row = tile * 16 + 4 * qd;
-                    const f32x4 xn = *reinterpret_cast<const f32x4*>(xf + row) + s;
+                    const f32x4 xn = kp ? s : *reinterpret_cast<const f32x4*>(xf + row) + s;  // part 0 + residual
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) put_gran(a.xs + row + i, t_wo, __float_as_uint(xn[i]));
+                    for (int i = 0; i < 4; ++i) put_gran(a.xs + kp * h + row + i, t_wo, __float_as_uint(xn[i]));
                   });
     C.sync();
     C.stamp(l * 10 + 5);
     // ---------------- GU: h = silu(x_n . Wg) * (x_n . Wu)
-    q = gather_x(C, xf, a.xs, h, t_wo);
-    rms_norm_act(C, q, xf, L.ffn_norm, act, h, a.eps);
+    const NormW nw2 = norm_w_load(C, L.ffn_norm, h);
+    q = gather_x(C, xf, a.xs, h, t_wo, a.ks_o);
+    rms_norm_act(C, q, xf, L.ffn_norm, act, h, a.eps, &nw2);
     C.sync();
     if (C.dead) break;
     C.stamp(l * 10 + 6);
@@ -552,12 +615,12 @@ __global__ __launch_bounds__(D1_THREADS, 1) void decode1_kernel(D1Args a) {
     const unsigned t_dn = tag(l, PH_DOWN);
     const bool last = l == a.n_layer - 1;
     run_items<NS>(C, phase_desc(a, wtab, l, 3), ring, act, red, seq, item_par,
-                  [&](int tile, int, int qd, f32x4 s, float (*)[16]) {
+                  [&](int tile, int kp, int qd, f32x4 s, float (*)[16]) {
                     const int row = tile * 16 + 4 * qd;
-                    const f32x4 xn = *reinterpret_cast<const f32x4*>(xf + row) + s;
+                    const f32x4 xn = kp ? s : *reinterpret_cast<const f32x4*>(xf + row) + s;  // part 0 + residual
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) put_gran(a.xs + row + i, t_dn, __float_as_uint(xn[i]));
-                    if (last) {  // the head's inputs: x and the per-16 sums of squares
+                    for (int i = 0; i < 4; ++i) put_gran(a.xs + kp * h + row + i, t_dn, __float_as_uint(xn[i]));
+                    if (last && a.ks_d == 1) {  // the head's inputs: x and the per-16 sums of squares
                       *reinterpret_cast<f32x4*>(a.x_out + row) = xn;
                       double qq = 0.0;
 #pragma unroll
@@ -569,6 +632,28 @@ __global__ __launch_bounds__(D1_THREADS, 1) void decode1_kernel(D1Args a) {
                   });
     C.sync();
     C.stamp(l * 10 + 9);
+  }
+  if (!C.dead && a.ks_d > 1 && g < h / 16 && C.cw == 0 && C.lane < 16) {
+    // the last layer's x in two K-parts: tile g's 16 rows summed (part order, as the gathers do) for
+    // the head kernels, with their sum of squares
+    const int row = g * 16 + C.lane;
+    const unsigned t_last = tag(a.n_layer - 1, PH_DOWN);
+    unsigned long long v0, v1;
+    for (int spin = 0;; ++spin) {
+      v0 = __hip_atomic_load(a.xs + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v1 = __hip_atomic_load(a.xs + h + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((unsigned)(v0 >> 32) == t_last && (unsigned)(v1 >> 32) == t_last) break;
+      __builtin_amdgcn_s_sleep(1);
+      if ((spin & 63) == 63 && timed_out(deadline)) {
+        atomicOr(a.err, 4u);
+        break;
+      }
+    }
+    const float x = __uint_as_float((unsigned)v0) + __uint_as_float((unsigned)v1);
+    a.x_out[row] = x;
+    double qq = (double)(x * x);
+    for (int o = 8; o > 0; o >>= 1) qq += __shfl_xor(qq, o);
+    if (C.lane == 0 && a.ssq) a.ssq[g] = (float)qq;
   }
   C.stamp(a.n_layer * 10 + 1);
   if (C.tr && C.cw == 0 && C.lane == 0) C.tr[a.n_layer * 10 + 5] = C.t_full;
@@ -596,14 +681,21 @@ size_t dyn_lds(int ns, int h, int ff, int n_layer) {
          (size_t)n_layer * 4 * 8;
 }
 
-template <int D, int G, int NS>
-int launch_ns(const D1Args& a, int n_cu, hipStream_t s, bool prepare) {
+template <int D, int G, int NS, int NL>
+int launch_nsl(const D1Args& a, int n_cu, hipStream_t s, bool prepare) {
   const size_t lds = dyn_lds(NS, a.h, a.ff, a.n_layer);
   if (prepare)  // once, outside any stream capture: the dynamic LDS above 64 KiB
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&decode1_kernel<D, G, NS>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&decode1_kernel<D, G, NS, NL>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess ? 0 : -1;
-  decode1_kernel<D, G, NS><<<n_cu, D1_THREADS, lds, s>>>(a);
+  decode1_kernel<D, G, NS, NL><<<n_cu, 64 * (NL + D1_CONS), lds, s>>>(a);
   return 0;
+}
+template <int D, int G, int NS>
+int launch_ns(const D1Args& a, int n_cu, hipStream_t s, bool prepare) {
+  // loader waves: 2 put 96 KiB in flight per CU (MX_D1_LOADERS=1: one, 48 KiB)
+  static const int nl = getenv("MX_D1_LOADERS") ? atoi(getenv("MX_D1_LOADERS")) : 2;
+  if (nl == 1 || NS < 6) return launch_nsl<D, G, NS, 1>(a, n_cu, s, prepare);
+  return launch_nsl<D, G, NS, 2>(a, n_cu, s, prepare);
 }
 
 template <int D, int G>
@@ -613,14 +705,9 @@ int launch_dg(const D1Args& a, int n_cu, hipStream_t s, bool prepare) {
   int ns = 8;
   while (ns > 3 && dyn_lds(ns, a.h, a.ff, a.n_layer) > budget) --ns;
   if (dyn_lds(ns, a.h, a.ff, a.n_layer) > budget) return -1;
-  switch (ns) {
-    case 8: return launch_ns<D, G, 8>(a, n_cu, s, prepare);
-    case 7: return launch_ns<D, G, 7>(a, n_cu, s, prepare);
-    case 6: return launch_ns<D, G, 6>(a, n_cu, s, prepare);
-    case 5: return launch_ns<D, G, 5>(a, n_cu, s, prepare);
-    case 4: return launch_ns<D, G, 4>(a, n_cu, s, prepare);
-    default: return launch_ns<D, G, 3>(a, n_cu, s, prepare);
-  }
+  if (ns >= 8) return launch_ns<D, G, 8>(a, n_cu, s, prepare);
+  if (ns >= 6) return launch_ns<D, G, 6>(a, n_cu, s, prepare);
+  return launch_ns<D, G, 3>(a, n_cu, s, prepare);
 }
 
 }  // namespace
@@ -636,7 +723,7 @@ bool decode1_supported(int h, int kv, int ff, int n_head, int n_head_kv, int hea
 
 int launch_decode1(const D1Args& a, int n_cu, hipStream_t s, bool prepare) {
   if (!decode1_supported(a.h, a.kv, a.ff, a.n_head, a.n_head_kv, a.head_dim) || a.ks_qkv < 1 ||
-      a.ks_qkv > ATTN_FIN_MAXSLAB || (a.h / 32 / a.ks_qkv) % SLOT_KT || n_cu < a.n_head_kv)
+      a.ks_qkv > ATTN_MEGA_MAXSLAB || (a.h / 32 / a.ks_qkv) % SLOT_KT || n_cu < a.n_head_kv)
     return -1;
   const int G = a.n_head / a.n_head_kv;
   if (a.head_dim == 128 && G == 4) return launch_dg<128, 4>(a, n_cu, s, prepare);

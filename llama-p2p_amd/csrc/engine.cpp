@@ -1007,7 +1007,7 @@ int mx_engine::setup_decode1() {
   const int h = n_embd, Nq = n_embd + 2 * n_embd_kv, T = Nq / 16, KT = h / 32;
   int ks = 1;
   long best = -1;
-  for (int k = 1; k <= 8; k *= 2) {  // max items per CU x slots per item, fewest ways on ties
+  for (int k = 1; k <= 4; k *= 2) {  // max items per CU x slots per item, fewest ways on ties
     if ((KT / k) % 16) break;
     const long cost = (long)((T * k + n_cu - 1) / n_cu) * (KT / k / 16);
     if (best < 0 || cost < best) best = cost, ks = k;
@@ -1032,13 +1032,17 @@ int mx_engine::setup_decode1() {
   a.rope_cs = rope_cs;
   a.x_out = x; a.ssq = ssq;
   a.ks_qkv = ks;
+  // attn_output / ffn_down: two K-parts when their h/16 row tiles leave CUs idle (TinyLlama: 128 tiles
+  // on 256 CUs), so every CU streams half a tile instead of half the CUs a whole one
+  a.ks_o = (h / 16 < n_cu && KT >= 2 * 16) ? 2 : 1;
+  a.ks_d = (h / 16 < n_cu && n_ff / 32 >= 2 * 16) ? 2 : 1;
   if (int rc = alloc((void**)&a.qkvp, (size_t)ks * Nq * 8)) return rc;  // 8-byte granules
   if (int rc = alloc((void**)&a.attn, (size_t)h / 2 * 8)) return rc;
-  if (int rc = alloc((void**)&a.xs, (size_t)h * 8)) return rc;
+  if (int rc = alloc((void**)&a.xs, (size_t)2 * h * 8)) return rc;
   if (int rc = alloc((void**)&a.hb, (size_t)n_ff / 2 * 8)) return rc;
   HIPC(hipMemset(a.qkvp, 0, (size_t)ks * Nq * 8));  // tag 0: never a live tag
   HIPC(hipMemset(a.attn, 0, (size_t)h / 2 * 8));
-  HIPC(hipMemset(a.xs, 0, (size_t)h * 8));
+  HIPC(hipMemset(a.xs, 0, (size_t)2 * h * 8));
   HIPC(hipMemset(a.hb, 0, (size_t)n_ff / 2 * 8));
   const size_t words = decode1_ctr_words(nl);
   if (int rc = alloc((void**)&a.ctr, words * 4)) return rc;

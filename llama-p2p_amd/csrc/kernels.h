@@ -108,8 +108,8 @@ struct MMArgs {
 
 
 // ---- persistent one-token decode engine (decode1.hip) -------------------------------------------
-// Every layer of a one-token step in ONE launch: one 320-thread work-group per CU (wave 0 streams the
-// CU's share of every weight matrix through an LDS ring by LDS-DMA, waves 1-4 compute from it); the
+// Every layer of a one-token step in ONE launch: one 256-thread work-group per CU (wave 0 streams the
+// CU's share of every weight matrix through an LDS ring by LDS-DMA, waves 1-3 compute from it); the
 // layers' dependent hand-offs (q|k|v partials, attention output, residual stream, SwiGLU product)
 // are write-through stores + per-(layer, phase) arrival counters, never kernel boundaries.
 struct D1Layer {
@@ -132,11 +132,12 @@ struct D1Args {
   // 8-byte store; the tag = (calls << 9) + 5 layer + op + 1 says which call, layer and op wrote it
   unsigned long long* qkvp;     // [ks_qkv][h + 2 kv] q|k|v split-K partials (f32)
   unsigned long long* attn;     // [h / 2] attention output (bf16 pairs)
-  unsigned long long* xs;       // [h] residual stream (f32)
+  unsigned long long* xs;       // [2][h] residual stream (f32; part 0 carries the residual, part 1 a K half)
   unsigned long long* hb;       // [ff / 2] SwiGLU product (bf16 pairs)
   unsigned* ctr;                // [n_layer * 5 + 2]: ticket, calls at the end (never reset)
   unsigned* err;                // timeout word (0 = fine)
-  int ks_qkv;                   // q|k|v split-K ways
+  int ks_qkv;                   // q|k|v split-K ways (<= 4)
+  int ks_o, ks_d;               // attn_output / ffn_down split-K ways (1 or 2: xs holds ks parts of x)
   // diagnosis (MX_D1_TRACE): per work-group [n_layer][5 ops][start, arrive] s_memrealtime stamps,
   // then 8 words of loader / consumer stall totals; nullptr normally
   unsigned long long* trace;

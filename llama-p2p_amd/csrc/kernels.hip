@@ -548,14 +548,20 @@ __global__ __launch_bounds__(64 * KS) void mm_pers_kernel(MMArgs a) {
   u32x4 ra[U];
 #pragma unroll
   for (int f = 0; f < U; ++f) ra[f] = wld(f / NKW, f % NKW);
-  u32x4 xb[NKW];
+  // B fragments: registers, or -- a 16-deep K-slice (Llama-3-70B q|k|v, 16 waves: 128 VGPRs per lane)
+  // with RMS_NORM on load -- read from the wave's LDS image at each MFMA (in registers they spilled
+  // 11 VGPRs to scratch)
+  constexpr bool BLDS = XS && NKW > 8;
+  u32x4 xb[BLDS ? 1 : NKW];
+  const u32x4* xp_lds = reinterpret_cast<const u32x4*>(xsw + col * xs_pitch + (lane >> 4) * 8);
   if constexpr (XS) {
     xs_build(xr, a, xsw, xs_pitch, NKW * TILE_K, lane);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
     __builtin_amdgcn_wave_barrier();
-    const u32x4* xp = reinterpret_cast<const u32x4*>(xsw + col * xs_pitch + (lane >> 4) * 8);
+    if constexpr (!BLDS) {
 #pragma unroll
-    for (int k = 0; k < NKW; ++k) xb[k] = xp[k * 4];
+      for (int k = 0; k < NKW; ++k) xb[k] = xp_lds[k * 4];
+    }
   } else {
     const u32x4* xp = reinterpret_cast<const u32x4*>(a.X + (size_t)col * a.ldx + (lane >> 4) * 8);
 #pragma unroll
@@ -629,8 +635,9 @@ __global__ __launch_bounds__(64 * KS) void mm_pers_kernel(MMArgs a) {
 #pragma unroll
     for (int k = 0; k < NKW; ++k) {
       const int f = i * NKW + k;  // flat ring position (compile-time after unrolling)
+      const u32x4 bk = BLDS ? xp_lds[k * 4] : xb[BLDS ? 0 : k];
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ra[f % U]),
-                                                    __builtin_bit_cast(bf16x8, xb[k]), acc, 0, 0, 0);
+                                                    __builtin_bit_cast(bf16x8, bk), acc, 0, 0, 0);
       if ((f + U) / NKW < TPW) ra[f % U] = wld((f + U) / NKW, (f + U) % NKW);
     }
     publish(i, acc);
