@@ -171,6 +171,9 @@ class Stage:
         self.x_in, self.x_out, self.tok = [], [], []
         self.pending_tokens = False  # stage 0 has not yet received the last step's tokens
         self.deferred = []  # sends of the previous micro-step, posted with the next receive
+        # host seconds spent issuing hand-offs / lane steps, and micro-steps issued (the hand-off's
+        # host cost per micro-step against the stage's device time, bench line "host_per_micro_step")
+        self.host_exchange_s, self.host_step_s, self.micro_steps = 0.0, 0.0, 0
 
     # -- prefill (untimed): prompt rows through every stage, 64 rows per hand-off
     def prefill(self, mb_rows: Sequence[Tuple[List[int], List[int], List[int]]], chunk: int = 64):
@@ -227,7 +230,9 @@ class Stage:
                     recvs = [(self.tok[mb], self.world - 1)] if self.pending_tokens else []
                 else:
                     recvs = [(self.x_in[mb], self.rank - 1)]
+                t0 = time.perf_counter()
                 self.comm.exchange(self.deferred, recvs)
+                t1 = time.perf_counter()
                 if self.first:
                     b.step_tensors(None, self.x_out[mb])
                     self.deferred = [(self.x_out[mb], 1)]
@@ -237,6 +242,9 @@ class Stage:
                 else:
                     b.step_tensors(self.x_in[mb], self.x_out[mb])
                     self.deferred = [(self.x_out[mb], self.rank + 1)]
+                self.host_exchange_s += t1 - t0
+                self.host_step_s += time.perf_counter() - t1
+                self.micro_steps += 1
             self.pending_tokens = True
 
     def finish(self):
@@ -332,6 +340,8 @@ def bench_main(args, metric: str, make_prompts):
     stage.finish()
     sync()
     dist.barrier()
+    stage.host_exchange_s = stage.host_step_s = 0.0
+    stage.micro_steps = 0
     t0 = time.perf_counter()
     stage.decode_steps(args.steps, args.warmup)
     stage.finish()
@@ -340,6 +350,11 @@ def bench_main(args, metric: str, make_prompts):
     dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = float(dt.item())
+    # host cost of a micro-step (max over ranks): with RCCL both the grouped send/recv and the graph
+    # replay only enqueue, so the stage's GPU stays fed while this stays below its device time
+    hs = torch.tensor([stage.host_exchange_s, stage.host_step_s], dtype=torch.float64, device=device)
+    dist.all_reduce(hs, op=dist.ReduceOp.MAX)
+    n_micro = max(1, stage.micro_steps)
     # the generated tokens live on the last stage: their CRC goes to rank 0 for the line
     toks = stage.tokens()
     crc = zlib.crc32(np.ascontiguousarray(np.stack(toks).astype(np.int32)).tobytes()) if toks is not None else None
@@ -379,6 +394,13 @@ def bench_main(args, metric: str, make_prompts):
             "step_hbm_frac": round(step_bytes / (dt / args.steps) / 1e9 / 8000.0 / world, 4),
             "roofline": roof,
         }
+        if world > 1:
+            line["host_per_micro_step"] = {
+                "exchange_us": round(float(hs[0].item()) / n_micro * 1e6, 1),
+                "step_launch_us": round(float(hs[1].item()) / n_micro * 1e6, 1),
+                "wall_us": round(dt / (args.steps * S) * 1e6, 1),
+                "note": "host seconds per micro-step, max over ranks (exchange = grouped send/recv issue; "
+                        "gloo waits inside it, RCCL only enqueues) vs wall time per micro-step"}
         if dry:
             line["dry_run"] = True
         print(json.dumps(line), flush=True)

@@ -283,6 +283,7 @@ class StageRunner:
         self.stage_time_every = stage_time_every
         self.busy_s, self.rounds = 0.0, 0
         self._events = []  # (start, end) CUDA events around this stage's lane steps
+        self.host_exchange_s, self.host_step_s, self.micro_steps = 0.0, 0.0, 0  # host issue cost of the ring
         self.lanes, self.x_in, self.x_out, self.tok = [], [], [], []
         for l in range(lanes):
             b = executor.make_lane([l * rows + i for i in range(rows)], kmax)
@@ -378,7 +379,9 @@ class StageRunner:
                     recvs = [(self.tok[l], self.world - 1)] if pending_tokens else []
                 else:
                     recvs = [(self.x_in[l], self.rank - 1)]
+                t0 = time.perf_counter()
                 self.comm.exchange(deferred, recvs)
+                t1 = time.perf_counter()
                 if self.first:
                     self._step(b, None, self.x_out[l])
                     deferred = [(self.x_out[l], 1)]
@@ -388,6 +391,9 @@ class StageRunner:
                 else:
                     self._step(b, self.x_in[l], self.x_out[l])
                     deferred = [(self.x_out[l], self.rank + 1)]
+                self.host_exchange_s += t1 - t0
+                self.host_step_s += time.perf_counter() - t1
+                self.micro_steps += 1
             pending_tokens = True
         recvs = [(self.tok[l], self.world - 1) for l in active] if self.first else []
         self.comm.exchange(deferred, recvs)
@@ -436,6 +442,13 @@ class StageRunner:
             sched.apply_round(plan, tokens)
         self.rounds += 1
         return tokens
+
+    def host_stats(self):
+        """Host microseconds per decode micro-step: issuing the grouped hand-off (a blocking transport
+        waits for its peer inside it) and the lane step (graph replay + events)."""
+        n = max(1, self.micro_steps)
+        return {"micro_steps": self.micro_steps, "exchange_us": round(self.host_exchange_s / n * 1e6, 1),
+                "step_launch_us": round(self.host_step_s / n * 1e6, 1)}
 
     def close(self):
         for b in self.lanes:

@@ -141,7 +141,8 @@ def main():
                 "proposed_partition": pipeserve.proposed_partition(llm.planner.board, llm.parts,
                                                                    llm.planner.head_layers),
                 "repartitions": llm.planner.history,
-                "rounds": llm.scheduler.rounds})
+                "rounds": llm.scheduler.rounds,
+                "stage0_host_per_micro_step": front.runner.host_stats()})
     llm.close()
     print(json.dumps(res), flush=True)
     if world > 1:
