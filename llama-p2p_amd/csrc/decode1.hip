@@ -47,6 +47,7 @@ typedef __attribute__((address_space(3))) void d1_lvoid;
 // one per SIMD, so a wave may hold 512 VGPRs (the attention body needs ~250); a fifth wave halves that
 // budget and spilled 120 B per lane
 constexpr int D1_CONS = 3;
+static_assert(D1_CONS == D1_TRACE_CONS, "trace rows hold the attention stamps of D1_CONS waves");
 constexpr int D1_KPW = (16 + D1_CONS - 1) / D1_CONS;  // k-tiles per consumer wave and slot (6, 5, 5)
 constexpr int SLOT_BYTES = 16384;   // 16 k-tiles of one 16-row tile
 constexpr int SLOT_KT = 16;
@@ -174,7 +175,7 @@ __device__ void d1_loader(const D1Args& a, const uint64_t* wtab, uint8_t* ring, 
   int issued = k, published = k, inflight = 0;  // this wave's next slot to issue / to publish
   unsigned long long t_vm = 0, t_idle = 0;
   unsigned long long* tr =
-      a.trace && k == 0 ? a.trace + (size_t)g * (a.n_layer * 10 + 8) + a.n_layer * 10 : nullptr;
+      a.trace && k == 0 ? a.trace + (size_t)g * d1_trace_stride(a.n_layer) + a.n_layer * 10 : nullptr;
   while (published < total) {
     if (issued < total && inflight < MAX_INFLIGHT) {
       const int s = issued % NS;
@@ -300,52 +301,80 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, size_t 
 
 // Gathers: granule sweeps.  Each thread issues all its 16-byte sc1 loads (2 granules each) before it
 // looks at any (a load-use loop waits one round trip per iteration), and re-reads a batch until every
-// tag is the expected one.  GU_ 16-byte loads in flight per thread.
-constexpr int GU_ = 8;
-template <class Put>
+// tag is the expected one.  GS 16-byte loads per thread and batch: 192 threads x GS x 16 B, so a
+// Llama-3-8B x hand-off (32 KiB, GS 12) is ONE batch -- one round trip after the last producer's
+// stores land -- and its SwiGLU product (56 KiB, GS 18) two, where batches of 8 loads took 2-3
+// (profiles/round4_decode1_trace.txt).  Loads past the end are not issued (their tags count as
+// matching).
+constexpr int GU_ = 8;   // norm-weight prefetch per thread (f32x4)
+template <int GS, bool TWO, class Put>
 __device__ __forceinline__ void sweep(Cons& C, const unsigned long long* gran, int n, unsigned tag, Put put) {
-  const __amdgpu_buffer_rsrc_t rs = rsrc_of(gran, (size_t)n * 8);
-  const int nv = n / 2;  // 16-byte pairs
-  for (int b = C.tid; b < nv && !C.dead; b += 64 * D1_CONS * GU_) {
-    u32x4 v[GU_];
+  // two arrays (of ceil and floor GS/2; more than ~18 u32x4 in all were demoted to scratch).  TWO: the
+  // granules of two K-parts of n each, the same indices of both in one thread (v0: part 0, v1: part 1)
+  constexpr int H0 = TWO ? GS / 2 : (GS + 1) / 2, H1 = GS / 2;
+  static_assert(GS <= 18, "gather batch");
+  const __amdgpu_buffer_rsrc_t rs = rsrc_of(gran, (size_t)n * (TWO ? 16 : 8));
+  const int nv = n / 2;  // 16-byte pairs (of one part)
+  constexpr int ST = 64 * D1_CONS, STEP = TWO ? ST * H0 : ST * GS;
+  for (int b = C.tid; b < nv && !C.dead; b += STEP) {
+    u32x4 v0[H0], v1[H1];
     for (int spin = 0;; ++spin) {
 #pragma unroll
-      for (int u = 0; u < GU_; ++u) {
-        const int i = min(b + u * 64 * D1_CONS, nv - 1);
-        v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(i * 16), 0, 16 /* sc1 */));
+      for (int u = 0; u < H0; ++u) {
+        const int i = b + u * ST;
+        v0[u] = i < nv ? __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(i * 16), 0, 16 /* sc1 */))
+                       : u32x4{0u, tag, 0u, tag};
+      }
+#pragma unroll
+      for (int u = 0; u < H1; ++u) {
+        const int j = TWO ? b + u * ST : b + (H0 + u) * ST;
+        const unsigned off = (unsigned)((TWO ? j + nv : j) * 16);
+        v1[u] = j < nv ? __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16 /* sc1 */))
+                       : u32x4{0u, tag, 0u, tag};
       }
       bool ok = true;
 #pragma unroll
-      for (int u = 0; u < GU_; ++u) ok &= v[u][1] == tag && v[u][3] == tag;
+      for (int u = 0; u < H0; ++u) ok &= v0[u][1] == tag && v0[u][3] == tag;
+#pragma unroll
+      for (int u = 0; u < H1; ++u) ok &= v1[u][1] == tag && v1[u][3] == tag;
       if (ok) break;
       __builtin_amdgcn_s_sleep(1);
       if ((spin & 63) == 63 && C.check()) return;
     }
+    if constexpr (TWO) {
 #pragma unroll
-    for (int u = 0; u < GU_; ++u) {
-      const int i = b + u * 64 * D1_CONS;
-      if (i < nv) put(i, v[u][0], v[u][2]);
+      for (int u = 0; u < H0; ++u) {
+        const int i = b + u * ST;
+        if (i < nv) put(i, v0[u][0], v0[u][2], v1[u][0], v1[u][2]);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < H0; ++u) {
+        const int i = b + u * ST;
+        if (i < nv) put(i, v0[u][0], v0[u][2], 0u, 0u);
+      }
+#pragma unroll
+      for (int u = 0; u < H1; ++u) {
+        const int j = b + (H0 + u) * ST;
+        if (j < nv) put(j, v1[u][0], v1[u][2], 0u, 0u);
+      }
     }
   }
 }
-// xf = the residual stream (f32 granules, `parts` K-parts summed in part order); returns this
-// thread's share of sum(x^2) in double
+// xf = the residual stream (f32 granules; `parts` = 2: the two K-parts summed, part 0 + part 1, in
+// one sweep); returns this thread's share of sum(x^2) in double
 __device__ __forceinline__ double gather_x(Cons& C, float* xf, const unsigned long long* gran, int n, unsigned tag,
                                            int parts = 1) {
   double q = 0.0;
   if (parts == 1) {
-    sweep(C, gran, n, tag, [&](int i, unsigned a0, unsigned a1) {
+    sweep<12, false>(C, gran, n, tag, [&](int i, unsigned a0, unsigned a1, unsigned, unsigned) {
       const float x0 = __uint_as_float(a0), x1 = __uint_as_float(a1);
       *reinterpret_cast<float2*>(xf + 2 * i) = float2{x0, x1};
       q += (double)(x0 * x0) + (double)(x1 * x1);
     });
-  } else {  // a thread sweeps the same indices in both parts: no barrier between them
-    sweep(C, gran, n, tag, [&](int i, unsigned a0, unsigned a1) {
-      *reinterpret_cast<float2*>(xf + 2 * i) = float2{__uint_as_float(a0), __uint_as_float(a1)};
-    });
-    sweep(C, gran + n, n, tag, [&](int i, unsigned a0, unsigned a1) {
-      const float2 p0 = *reinterpret_cast<const float2*>(xf + 2 * i);
-      const float x0 = p0.x + __uint_as_float(a0), x1 = p0.y + __uint_as_float(a1);
+  } else {
+    sweep<12, true>(C, gran, n, tag, [&](int i, unsigned a0, unsigned a1, unsigned b0, unsigned b1) {
+      const float x0 = __uint_as_float(a0) + __uint_as_float(b0), x1 = __uint_as_float(a1) + __uint_as_float(b1);
       *reinterpret_cast<float2*>(xf + 2 * i) = float2{x0, x1};
       q += (double)(x0 * x0) + (double)(x1 * x1);
     });
@@ -355,7 +384,7 @@ __device__ __forceinline__ double gather_x(Cons& C, float* xf, const unsigned lo
 // dst[0..2n) = bf16 pairs from n granules
 __device__ __forceinline__ void gather_pairs(Cons& C, uint16_t* dst, const unsigned long long* gran, int n,
                                              unsigned tag) {
-  sweep(C, gran, n, tag, [&](int i, unsigned a0, unsigned a1) {
+  sweep<18, false>(C, gran, n, tag, [&](int i, unsigned a0, unsigned a1, unsigned, unsigned) {
     *reinterpret_cast<u32x2*>(dst + 4 * i) = u32x2{a0, a1};
   });
 }
@@ -503,7 +532,7 @@ __global__ __launch_bounds__(64 * (NL + D1_CONS), 1) void decode1_kernel(D1Args 
   }
   Cons C(a, ctl, deadline, NL);
   const int g = blockIdx.x, Gn = gridDim.x;
-  if (a.trace) C.tr = a.trace + (size_t)g * (a.n_layer * 10 + 8);
+  if (a.trace) C.tr = a.trace + (size_t)g * d1_trace_stride(a.n_layer);
   C.stamp(a.n_layer * 10 + 0);
   const unsigned calls = __hip_atomic_load(a.ctr + a.n_layer * NPH + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   auto tag = [&](int l, int p) { return (calls << 9) + (unsigned)(l * NPH + p + 1); };
@@ -564,6 +593,8 @@ __global__ __launch_bounds__(64 * (NL + D1_CONS), 1) void decode1_kernel(D1Args 
       at.nslab = a.ks_qkv; at.slab_stride = (size_t)Nq; at.rope_cs = a.rope_cs;
       at.gslab = a.qkvp; at.gtag_in = t_qkv; at.gout = a.attn; at.gtag_out = tag(l, PH_ATT);
       at.slabs = reinterpret_cast<const float*>(a.qkvp);  // FIN path marker (granules are read)
+      if (C.tr)  // the body's stamps of wave w land in this row's words n_layer * 10 + 8 + 8 w
+        at.trace = C.tr + a.n_layer * 10 + 8 - (size_t)g * D1_CONS * 8;
       attn_decode_body<D, G, D1_CONS, true, true>(at, g, 0, C.tid, AttnSync<D, G>{&C}, AttnGive{&C});
       C.sync();
       if (C.dead) break;
@@ -692,9 +723,11 @@ int launch_nsl(const D1Args& a, int n_cu, hipStream_t s, bool prepare) {
 }
 template <int D, int G, int NS>
 int launch_ns(const D1Args& a, int n_cu, hipStream_t s, bool prepare) {
-  // loader waves: 2 put 96 KiB in flight per CU (MX_D1_LOADERS=1: one, 48 KiB)
-  static const int nl = getenv("MX_D1_LOADERS") ? atoi(getenv("MX_D1_LOADERS")) : 2;
-  if (nl == 1 || NS < 6) return launch_nsl<D, G, NS, 1>(a, n_cu, s, prepare);
+  // loader waves: one puts 48 KiB in flight per CU; MX_D1_LOADERS=2 puts 96 KiB, but its fifth wave
+  // halves the VGPR budget (20 B/lane spilled at G 4) and measured slower in the steady state (8B 2.93
+  // vs 2.88 ms per launch, TinyLlama 0.810 vs 0.804: profiles/round4_decode1_trace.txt)
+  static const int nl = getenv("MX_D1_LOADERS") ? atoi(getenv("MX_D1_LOADERS")) : 1;
+  if (nl != 2 || NS < 6) return launch_nsl<D, G, NS, 1>(a, n_cu, s, prepare);
   return launch_nsl<D, G, NS, 2>(a, n_cu, s, prepare);
 }
 

@@ -1051,7 +1051,7 @@ int mx_engine::setup_decode1() {
   HIPC(hipMemset(a.err, 0, 64));
   a.trace = nullptr;
   if (getenv("MX_D1_TRACE")) {
-    const size_t n = (size_t)n_cu * (nl * 10 + 8);
+    const size_t n = (size_t)n_cu * d1_trace_stride(nl);
     if (int rc = alloc((void**)&a.trace, n * 8)) return rc;
     HIPC(hipMemset(a.trace, 0, n * 8));
   }
@@ -2586,7 +2586,7 @@ int mx_device_count(int32_t* n) {
 int mx_decode1_trace(mx_engine* e, uint64_t* out, size_t cap, int* n_groups, int* stride) {
   if (!e) return fail(MX_ERR_ARG, "null engine");
   if (!e->use_d1 || !e->d1.trace) return fail(MX_ERR_STATE, "decode1 trace not enabled (MX_D1_TRACE=1 at engine creation)");
-  const size_t st = (size_t)e->d1.n_layer * 10 + 8, n = (size_t)e->n_cu * st;
+  const size_t st = d1_trace_stride(e->d1.n_layer), n = (size_t)e->n_cu * st;
   if (n_groups) *n_groups = e->n_cu;
   if (stride) *stride = (int)st;
   if (out && cap) {

@@ -139,9 +139,12 @@ struct D1Args {
   int ks_qkv;                   // q|k|v split-K ways (<= 4)
   int ks_o, ks_d;               // attn_output / ffn_down split-K ways (1 or 2: xs holds ks parts of x)
   // diagnosis (MX_D1_TRACE): per work-group [n_layer][5 ops][start, arrive] s_memrealtime stamps,
-  // then 8 words of loader / consumer stall totals; nullptr normally
+  // then 8 words of loader / consumer stall totals, then (attention work-groups) the attention body's
+  // 8 stamps per consumer wave of the last layer; rows of d1_trace_stride words; nullptr normally
   unsigned long long* trace;
 };
+constexpr int D1_TRACE_CONS = 3;  // consumer waves (decode1.hip D1_CONS)
+__host__ __device__ constexpr size_t d1_trace_stride(int n_layer) { return (size_t)n_layer * 10 + 8 + 8 * D1_TRACE_CONS; }
 // 0: launched (prepare: only the kernel attributes set, once, outside stream capture); -1: shape not
 // supported (callers use the per-op kernels)
 int launch_decode1(const D1Args& a, int n_cu, hipStream_t s, bool prepare = false);

@@ -32,8 +32,13 @@ def main():
     rng = np.random.default_rng(1)
     ids = rng.integers(3, sh.n_vocab, args.pos + 1).astype(np.int32)
     eng.forward_rows([0] * args.pos, list(range(args.pos)), ids[:args.pos].tolist(), want_logits=False)
-    for k in range(3):
-        eng.forward_logits(ids[args.pos:args.pos + 1], args.pos, slot=0)
+    # steady state: the batch-1 decode graph replayed (as the bench times it); the trace keeps the
+    # stamps of the last launch
+    b = eng.batch(slots=[0], pos=[args.pos], ids=[int(ids[args.pos])], max_steps=16)
+    for _ in range(16):
+        b.step()
+    eng.sync()
+    b.close()
     tr = eng.decode1_trace().astype(np.int64)
     eng.close()
     L = sh.n_layer
@@ -87,6 +92,21 @@ def main():
                 prev = st[:, l - 1, 4, 1].max()
             w.append(np.median(st[:, l, p, 0]) - prev)
         out[f"{n}_handoff_to_compute_us_median"] = round(float(np.mean(w)), 2)
+    # the last layer's attention body, per consumer wave of the attention work-groups: entry, q in
+    # registers (q|k|v granules summed, RoPE, K/V stored, barrier), first chunk landed, chunk loop
+    # done, partials merged in LDS; then the op's arrival -- us after the q|k|v op's last arrival
+    nkv = sh.n_head_kv
+    base = L * 10 + 8
+    qkv_last = st[:, L - 1, 0, 1].max()
+    att = {}
+    for k, n in enumerate(["entry", "q_ready", "first_kv", "chunks_done", "merged"]):
+        v = tr[:nkv, base + k:base + 24:8]
+        v = v[v > 0]
+        if v.size:
+            att[n] = round(float(((v - t0) / 100.0 - qkv_last).mean()), 2)
+    att["arrive"] = round(float((st[:nkv, L - 1, 1, 1] - qkv_last).mean()), 2)
+    att["wo_compute_start_median"] = round(float(np.median(st[:, L - 1, 2, 0]) - qkv_last), 2)
+    out["last_layer_attention_us_after_qkv"] = att
     print(json.dumps(out), flush=True)
 
 
