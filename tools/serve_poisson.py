@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--min-gain", type=float, default=0.10,
                     help="apply a stage re-split when it predicts this much lower slowest-stage time")
     ap.add_argument("--no-repartition", action="store_true")
+    ap.add_argument("--parts", default="", help="initial stage ranges 'lb:le,lb:le,...' (in-process stages; "
+                    "default partition_layers by bytes) -- e.g. a skewed split for the planner to repair")
     args = ap.parse_args()
     from llama_p2p_amd import synth
     from llama_p2p_amd.placement import PeerScoreboard, poisson_schedule, serve
@@ -124,6 +126,12 @@ def main():
         h, kv, ff = shape.n_embd, shape.n_embd_kv, shape.n_ff
         parts = partition_layers(shape.n_layer, 2 * (2 * h * h + 2 * h * kv + 3 * h * ff), 2 * shape.n_vocab * h,
                                  args.stages)
+        if args.parts:
+            parts = [tuple(int(v) for v in r.split(":")) for r in args.parts.split(",")]
+            if parts[0][0] != 0 or parts[-1][1] != shape.n_layer or any(a[1] != b[0] for a, b in zip(parts, parts[1:])):
+                raise SystemExit(f"--parts must tile 0..{shape.n_layer}")
+            args.stages = len(parts)
+        initial_parts = list(parts)
         llm = pipeserve.local_pipeline_llama(path, parts, lanes=args.lanes or args.stages, rows=args.rows, n_ctx=args.n_ctx,
                                              policy=args.policy, seed=0, repartition=not args.no_repartition,
                                              min_gain=args.min_gain)
@@ -136,7 +144,8 @@ def main():
         lanes[lane] = lanes.get(lane, 0) + 1
     res.update({"model": args.model, "mode": mode, "policy": args.policy, "rate": args.rate,
                 "time_scale": args.time_scale, "prompt_len": [args.prompt_lo, args.prompt_hi], "gen": args.gen,
-                "layer_ranges": llm.parts, "requests_per_lane": lanes, "lane_scores": llm.scheduler.board.stats(),
+                "initial_layer_ranges": initial_parts if world == 1 else None, "layer_ranges": llm.parts,
+                "requests_per_lane": lanes, "lane_scores": llm.scheduler.board.stats(),
                 "stage_scores": llm.planner.board.stats(),
                 "proposed_partition": pipeserve.proposed_partition(llm.planner.board, llm.parts,
                                                                    llm.planner.head_layers),
