@@ -2,7 +2,7 @@
 scores, failure propagation, the round-length rule and the partition DP's cost.
 
 * Re-partition (the reference's select_peer / update_peer_performance, p2p:156-168, applied to
-  stages): over gloo at world 3 one rank's toy stage is slowed per layer; the planner's proposed
+  stages): over gloo at world 3 and 4 one rank's toy stage is slowed per layer; the planner's proposed
   split is applied (drain the lanes, every rank rebuilds its stage on the new layer range) while
   requests keep arriving, and every request's tokens still equal the one-stage run.
 * Failure: a stage that raises in the middle of a round fails every outstanding request (admitted
@@ -97,13 +97,14 @@ def _worker(rank, world, port, parts, slow_rank, q):
         dist.destroy_process_group()
 
 
-def test_repartition_applied_and_tokens_unchanged():
-    world, slow = 3, 1
+@pytest.mark.parametrize("world,slow,expect", [(3, 1, [(0, 2), (2, 4), (4, 6)]),
+                                               (4, 2, [(0, 1), (1, 2), (2, 4), (4, 6)])])
+def test_repartition_applied_and_tokens_unchanged(world, slow, expect):
     q1 = queue.Queue()
     _serve_waves(0, 1, [(0, L)], None, q1)
     ref = q1.get()
     parts = partition_layers(L, 1.0, 0.0, world)
-    assert parts == [(0, 2), (2, 4), (4, 6)]
+    assert parts == expect
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
