@@ -602,6 +602,10 @@ def main():
     ap.add_argument("--micro-batches", type=int, default=0, help="pipeline micro-batches in flight (0: one per stage)")
     ap.add_argument("--dry-run", action="store_true",
                     help="pipeline path on CPU over gloo with a toy executor (launcher / schedule check, no GPU)")
+    ap.add_argument("--handoff", default="bf16", choices=["bf16", "f32"],
+                    help="stage hand-off dtype (f32: stage splits bitwise equal to one engine)")
+    ap.add_argument("--host-handoff", action="store_true",
+                    help="pipeline rehearsal: gloo with host-staged hand-offs, ranks may share a GPU (not RCCL)")
     ap.add_argument("--probe-only", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     from llama_p2p_amd import launch

@@ -97,11 +97,14 @@ class TorchComm:
     together have to share a group (see ``Stage.decode_steps``).
     """
 
-    def __init__(self, rank: int, world: int, obj_group=None):
+    def __init__(self, rank: int, world: int, obj_group=None, host_staged: bool = False):
         import torch.distributed as dist
 
         self.dist, self.rank, self.world = dist, rank, world
         self._pending = []
+        # host_staged (gloo over device tensors: the multi-process rehearsal on ONE GPU, where RCCL
+        # cannot run two ranks): each hand-off is copied to host memory, sent over gloo, copied back
+        self.host_staged = host_staged
         # control-plane objects (round plans, token lists) go over a gloo group: host data, no device
         # round trip; on a gloo default group that group is reused
         if obj_group is None and world > 1 and dist.get_backend() != "gloo":
@@ -121,26 +124,38 @@ class TorchComm:
         self.dist.recv_object_list(box, src=src, group=self.obj_group)
         return box[0]
 
+    def _host(self, t):
+        return t.cpu() if self.host_staged and t.is_cuda else t  # .cpu() waits for the stream's writes
+
     def send(self, t, dst: int):
-        w = self.dist.isend(t, dst)
-        self._pending.append(w)
+        c = self._host(t)
+        w = self.dist.isend(c, dst)
+        self._pending.append((w, c))
         return w
 
     def recv(self, t, src: int):
-        self.dist.recv(t, src)
+        c = self._host(t) if t.is_cuda and self.host_staged else t
+        self.dist.recv(c, src)
+        if c is not t:
+            t.copy_(c)
 
     def exchange(self, sends, recvs):
         """sends = [(tensor, dst)], recvs = [(tensor, src)]; returns when all completed
         (on nccl: the current stream waits for them)."""
         P = self.dist.P2POp
-        ops = [P(self.dist.isend, t, d) for t, d in sends] + [P(self.dist.irecv, t, s) for t, s in recvs]
+        sends = [(self._host(t), d) for t, d in sends]
+        rbufs = [(self._host(t) if self.host_staged else t, t, s) for t, s in recvs]
+        ops = [P(self.dist.isend, t, d) for t, d in sends] + [P(self.dist.irecv, c, s) for c, _, s in rbufs]
         if not ops:
             return
         for w in self.dist.batch_isend_irecv(ops):
             w.wait()
+        for c, t, _ in rbufs:
+            if c is not t:
+                t.copy_(c)
 
     def drain(self):
-        for w in self._pending:
+        for w, _ in self._pending:
             w.wait()
         self._pending.clear()
 
@@ -279,12 +294,19 @@ def bench_main(args, metric: str, make_prompts):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     dry = bool(getattr(args, "dry_run", False))
+    host = bool(getattr(args, "host_handoff", False)) and not dry
+    f32 = getattr(args, "handoff", "bf16") == "f32"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if world == 1:
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     if dry:
         device = torch.device("cpu")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    elif host:  # rehearsal: real engines, ranks may share GPUs, hand-offs through host memory over gloo
+        local = local % max(1, torch.cuda.device_count())
+        device = torch.device("cuda", local)
+        torch.cuda.set_device(local)
         dist.init_process_group("gloo", rank=rank, world_size=world)
     else:
         device = torch.device("cuda", local)
@@ -300,7 +322,7 @@ def bench_main(args, metric: str, make_prompts):
     lb, le = parts[rank]
     S = int(getattr(args, "micro_batches", 0) or world)
     M = args.seqs
-    comm = TorchComm(rank, world) if world > 1 else None
+    comm = TorchComm(rank, world, host_staged=host) if world > 1 else None
     if dry:
         eng = DryEngine(lb, le, S * M, shape.n_layer)
         vocab = eng.V
@@ -310,12 +332,12 @@ def bench_main(args, metric: str, make_prompts):
         from .engine import Engine
 
         eng = Engine(f"synthetic:{args.model}:seed=0", n_ctx=args.n_ctx, n_seq_max=S * M, layer_begin=lb,
-                     layer_end=le, device=local, handoff_bf16=True)
+                     layer_end=le, device=local, handoff_bf16=not f32)
         vocab = shape.n_vocab
         work_stream = torch.cuda.Stream(device=local)  # engine kernels and RCCL hand-offs are ordered on it
         torch.cuda.set_stream(work_stream)
         stage = Stage(EngineAdapter(eng), comm, rank, world, shape.n_embd, device, S,
-                      dtype=torch.bfloat16)  # hidden states cross stage boundaries in bf16
+                      dtype=torch.float32 if f32 else torch.bfloat16)  # hidden states cross stages in bf16
         sync = torch.cuda.synchronize
     prompts = make_prompts(vocab, S * M)
     mb_rows, mb_state = [], []
@@ -347,12 +369,13 @@ def bench_main(args, metric: str, make_prompts):
     stage.finish()
     sync()
     dist.barrier()
-    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    rdev = torch.device("cpu") if host else device  # gloo reduces host tensors
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=rdev)
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = float(dt.item())
     # host cost of a micro-step (max over ranks): with RCCL both the grouped send/recv and the graph
     # replay only enqueue, so the stage's GPU stays fed while this stays below its device time
-    hs = torch.tensor([stage.host_exchange_s, stage.host_step_s], dtype=torch.float64, device=device)
+    hs = torch.tensor([stage.host_exchange_s, stage.host_step_s], dtype=torch.float64, device=rdev)
     dist.all_reduce(hs, op=dist.ReduceOp.MAX)
     n_micro = max(1, stage.micro_steps)
     # the generated tokens live on the last stage: their CRC goes to rank 0 for the line
@@ -371,7 +394,7 @@ def bench_main(args, metric: str, make_prompts):
                 "kernel": ("mm_wide_kernel" if M > 16 else "mm_kernel") +
                           "<EPI_SWIGLU> (ffn_gate+ffn_up+SiLU*up), rank 0",
                 "us_per_launch": round(us, 2), "bytes_per_launch": int(kbytes)}
-    wb = torch.tensor([float(eng.info.weight_bytes)], dtype=torch.float64, device=device)
+    wb = torch.tensor([float(eng.info.weight_bytes)], dtype=torch.float64, device=rdev)
     dist.all_reduce(wb)
     total_tokens = args.steps * S * M
     if rank == 0:
@@ -386,7 +409,7 @@ def bench_main(args, metric: str, make_prompts):
             "config": {"workload": f"{args.model} greedy decode, {world}-stage pipeline, {S} micro-batches x {M} "
                                    f"sequences in flight, prompts U[16,256] (seed 2), n_ctx {args.n_ctx}",
                        "model": args.model, "stages": world, "micro_batches": S, "seqs_per_micro_batch": M,
-                       "layer_ranges": parts, "parallelism": f"pp{world}", "handoff": "bf16"},
+                       "layer_ranges": parts, "parallelism": f"pp{world}", "handoff": "f32" if f32 else "bf16"},
             "dist": {"backend": backend, "world_size": world_rd,
                      "launcher": os.environ.get("MX_LAUNCHER", "torch.distributed.run or external")},
             "tokens_crc32": crc,
@@ -403,6 +426,10 @@ def bench_main(args, metric: str, make_prompts):
                         "gloo waits inside it, RCCL only enqueues) vs wall time per micro-step"}
         if dry:
             line["dry_run"] = True
+        if host:
+            line["rehearsal"] = ("hand-offs staged through host memory over gloo, ranks sharing "
+                                 f"{torch.cuda.device_count()} visible GPU(s): a schedule and parity check, "
+                                 "not the RCCL measurement")
         print(json.dumps(line), flush=True)
     for b in stage.batches:
         b.close()
