@@ -604,6 +604,7 @@ def main():
                     help="pipeline path on CPU over gloo with a toy executor (launcher / schedule check, no GPU)")
     ap.add_argument("--handoff", default="bf16", choices=["bf16", "f32"],
                     help="stage hand-off dtype (f32: stage splits bitwise equal to one engine)")
+    ap.add_argument("--prefill-chunk", type=int, default=64, help="pipeline prefill rows per hand-off (<= 64)")
     ap.add_argument("--host-handoff", action="store_true",
                     help="pipeline rehearsal: gloo with host-staged hand-offs, ranks may share a GPU (not RCCL)")
     ap.add_argument("--probe-only", action="store_true", help=argparse.SUPPRESS)

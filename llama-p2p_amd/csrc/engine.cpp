@@ -216,7 +216,7 @@ struct mx_engine {
   // rows of the next forward come in blocks of 16 consecutive positions of one sequence (prefill):
   // attention runs as attn_prefill_kernel, 16 queries per K/V pass
   bool rows_blocked = false;
-  static constexpr bool use_wide = true;  // 17..64-row forward through mm_wide (LDS-shared activations)
+  bool use_wide = getenv("MX_NO_WIDE") == nullptr;  // 17..64-row forward through mm_wide (LDS-shared activations)
   float* slabs = nullptr;                           // split-K partials [8][MAX_ROWS][n_embd + 2 n_embd_kv]
   size_t slab_stride = 0;
   float* gslabs = nullptr;  // split-K partials of small-M prefill GEMMs, [S][M][N] (launch_gemm_split)
@@ -265,6 +265,9 @@ struct mx_engine {
   int *tk_ws_idx = nullptr, *tk_idx = nullptr;
   int *am_idx = nullptr, *d_tok = nullptr;
   int *d_ids = nullptr, *d_pos = nullptr, *d_slot = nullptr, *d_rowmap = nullptr;
+  // pinned host staging of forward_rows_chunk's index arrays [4][R]: its async copies read from here
+  // (engine-owned), not through the runtime's staging of pageable memory
+  int32_t* h_idx = nullptr;
   std::vector<void*> allocations;
 
   // graphs for the scheduler's decode steps, by (M, top-k of the device sampling chain or 0 = argmax)
@@ -287,7 +290,7 @@ struct mx_engine {
   }
   int copy_out(void* x_out, int M, hipStream_t s) {  // the residual stream to the next stage
     if (handoff_bf16) launch_f32_to_bf16((uint16_t*)x_out, x, (size_t)M * n_embd, s);
-    else HIPC(hipMemcpyAsync(x_out, x, (size_t)M * n_embd * 4, hipMemcpyDeviceToDevice, s));
+    else launch_copy_f32((float*)x_out, x, (size_t)M * n_embd, s);
     return 0;
   }
   // SampRow of a request for a run that starts now (draw index and penalty window at this point)
@@ -392,6 +395,7 @@ mx_engine::~mx_engine() {
   d1_release(this);
 
   for (void* p : allocations) hipFree(p);
+  if (h_idx) hipHostFree(h_idx);
   if (stream) hipStreamDestroy(stream);
 }
 
@@ -477,6 +481,7 @@ int mx_engine::init_common() {
   if (int rc = alloc((void**)&d_pos, (size_t)R * 4)) return rc;
   if (int rc = alloc((void**)&d_slot, (size_t)R * 4)) return rc;
   if (int rc = alloc((void**)&d_rowmap, (size_t)R * 4)) return rc;
+  HIPC(hipHostMalloc((void**)&h_idx, (size_t)4 * R * 4, hipHostMallocDefault));
   if (int rc = alloc((void**)&sched_hist, (size_t)MAX_ROWS * SCHED_KMAX * 4)) return rc;
   if (int rc = alloc((void**)&sched_hist_count, (size_t)MAX_ROWS * 4)) return rc;
   if (int rc = alloc((void**)&d_samp, (size_t)MAX_ROWS * sizeof(SampRow))) return rc;
@@ -1100,8 +1105,7 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     if (handoff_bf16) {  // bf16 hand-off from the previous stage: widen, with the Σx² partials on the way
       launch_bf16_to_f32(x, (const uint16_t*)x_in, M, h, (nol || qql) ? ssq : nullptr, s);
     } else {
-      HIPC(hipMemcpyAsync(x, x_in, (size_t)M * h * 4, hipMemcpyDeviceToDevice, s));
-      if (nol || qql) launch_ssq(x, M, h, ssq, s);
+      launch_f32_in(x, (const float*)x_in, M, h, (nol || qql) ? ssq : nullptr, s);
     }
   } else {
     if (!has_embed) return fail(MX_ERR_STATE, "this stage has no token embedding: x_in required");
@@ -1597,14 +1601,23 @@ __global__ void advance_pos_kernel(int* pos, int M) {
 int mx_engine::forward_rows_chunk(int n, const int32_t* slots, const int32_t* pos, const int32_t* ids,
                                   const void* x_in, void* x_out, float* logits_host, hipStream_t s,
                                   bool last_row_only) {
+  if (n < 1 || n > PREFILL_ROWS) return fail(MX_ERR_ARG, "forward chunk of 1..PREFILL_ROWS rows");
   for (int i = 0; i < n; i++) {
     if (slots[i] < 0 || slots[i] >= n_seq_max) return fail(MX_ERR_ARG, "slot out of range");
     if (pos[i] < 0 || pos[i] >= n_ctx) return fail(MX_ERR_CTX, "position outside n_ctx");
     if (ids && has_embed && !x_in && (ids[i] < 0 || ids[i] >= n_vocab)) return fail(MX_ERR_ARG, "token id out of range");
   }
-  if (ids) HIPC(hipMemcpyAsync(d_ids, ids, n * 4, hipMemcpyHostToDevice, s));
-  HIPC(hipMemcpyAsync(d_pos, pos, n * 4, hipMemcpyHostToDevice, s));
-  HIPC(hipMemcpyAsync(d_slot, slots, n * 4, hipMemcpyHostToDevice, s));
+  // every call ends with a stream sync below, so the staging rows are free again at entry
+  const size_t R = PREFILL_ROWS;
+  auto h2d = [&](int* dst, const int32_t* src, int k, int row) -> int {
+    memcpy(h_idx + row * R, src, (size_t)k * 4);
+    HIPC(hipMemcpyAsync(dst, h_idx + row * R, (size_t)k * 4, hipMemcpyHostToDevice, s));
+    return 0;
+  };
+  if (ids)
+    if (int rc = h2d(d_ids, ids, n, 0)) return rc;
+  if (int rc = h2d(d_pos, pos, n, 1)) return rc;
+  if (int rc = h2d(d_slot, slots, n, 2)) return rc;
   const bool head = has_head && !x_out && logits_host;
   const int n_out = last_row_only ? 1 : n;
   {
@@ -1618,8 +1631,8 @@ int mx_engine::forward_rows_chunk(int n, const int32_t* slots, const int32_t* po
   for (int i = 0; i < n && rows_blocked; i++)
     if (i % 16 && (slots[i] != slots[i - i % 16] || pos[i] != pos[i - i % 16] + i % 16)) rows_blocked = false;
   if (head && last_row_only) {
-    const int last = n - 1;
-    HIPC(hipMemcpyAsync(d_rowmap, &last, 4, hipMemcpyHostToDevice, s));
+    const int32_t last = n - 1;
+    if (int rc = h2d(d_rowmap, &last, 1, 3)) return rc;
   }
   const int frc = enqueue_forward(n, d_ids, d_pos, d_slot, x_in, x_out, head, head && last_row_only ? d_rowmap : nullptr,
                                   n_out, false, nullptr, nullptr, nullptr, 0, nullptr, 0, s);

@@ -345,6 +345,8 @@ int launch_sample_chain(float* logits, int ldl, int M, int V, const SampRow* sam
 // hand-off conversions of the residual stream (pipeline stages): f32 <-> bf16 rows (RNE), and the
 // per-16-element sums of squares of the f32 rows made from bf16 (RMS_NORM-on-load consumers)
 void launch_f32_to_bf16(uint16_t* dst, const float* src, size_t n, hipStream_t s);
+void launch_copy_f32(float* dst, const float* src, size_t n, hipStream_t s);
+void launch_f32_in(float* x, const float* src, int M, int n, float* ssq, hipStream_t s);  // + Σx² partials
 void launch_bf16_to_f32(float* dst, const uint16_t* src, int M, int n, float* ssq, hipStream_t s);
 
 // HBM streaming probes: variant v of probe_variants() (loads in flight, grid, non-temporal) of a

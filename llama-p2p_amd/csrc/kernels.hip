@@ -1314,6 +1314,41 @@ __global__ __launch_bounds__(256) void bf16_to_f32_kernel(float* x, const uint16
   }
 }
 
+// f32 hand-off: a copy kernel, not hipMemcpyAsync -- a device-to-device memcpy may run on a copy
+// engine, and the stage split must see exactly what the previous kernels wrote (the kernels' own
+// ordering and cache rules, as the bf16 hand-off has); the receiving side writes the Σx² partials
+// in the same pass (as ssq_kernel)
+__global__ __launch_bounds__(256) void f32_copy_kernel(float* dst, const float* src, size_t n4) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x)
+    reinterpret_cast<f32x4*>(dst)[i] = reinterpret_cast<const f32x4*>(src)[i];
+}
+__global__ __launch_bounds__(256) void f32_in_kernel(float* x, const float* src, int n, float* ssq) {
+  const int c = blockIdx.x;
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(src + (size_t)c * n);
+  f32x4* d4 = reinterpret_cast<f32x4*>(x + (size_t)c * n);
+  for (int t = threadIdx.x; t < n / 16; t += blockDim.x) {
+    double q = 0.0;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const f32x4 v = s4[4 * t + h];
+      d4[4 * t + h] = v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) q += (double)(v[i] * v[i]);
+    }
+    if (ssq) ssq[(size_t)c * (n / 16) + t] = (float)q;
+  }
+}
+
+void launch_copy_f32(float* dst, const float* src, size_t n, hipStream_t s) {
+  const size_t n4 = n / 4;
+  const int grid = (int)std::min<size_t>(1024, (n4 + 255) / 256);
+  f32_copy_kernel<<<std::max(grid, 1), 256, 0, s>>>(dst, src, n4);
+}
+
+void launch_f32_in(float* x, const float* src, int M, int n, float* ssq, hipStream_t s) {
+  f32_in_kernel<<<M, 256, 0, s>>>(x, src, n, ssq);
+}
+
 void launch_f32_to_bf16(uint16_t* dst, const float* src, size_t n, hipStream_t s) {
   const size_t n4 = n / 4;
   const int grid = (int)std::min<size_t>(1024, (n4 + 255) / 256);

@@ -189,6 +189,7 @@ class Stage:
         # host seconds spent issuing hand-offs / lane steps, and micro-steps issued (the hand-off's
         # host cost per micro-step against the stage's device time, bench line "host_per_micro_step")
         self.host_exchange_s, self.host_step_s, self.micro_steps = 0.0, 0.0, 0
+        self._sync_steps = bool(os.environ.get("MX_STAGE_SYNC"))  # diagnosis: device sync after every step
 
     # -- prefill (untimed): prompt rows through every stage, 64 rows per hand-off
     def prefill(self, mb_rows: Sequence[Tuple[List[int], List[int], List[int]]], chunk: int = 64):
@@ -257,6 +258,8 @@ class Stage:
                 else:
                     b.step_tensors(self.x_in[mb], self.x_out[mb])
                     self.deferred = [(self.x_out[mb], self.rank + 1)]
+                if self._sync_steps:
+                    self.torch.cuda.synchronize()
                 self.host_exchange_s += t1 - t0
                 self.host_step_s += time.perf_counter() - t1
                 self.micro_steps += 1
@@ -354,7 +357,7 @@ def bench_main(args, metric: str, make_prompts):
             st[2].append(int(p[-1]))
         mb_rows.append((slots, pos, ids))
         mb_state.append(st)
-    stage.prefill(mb_rows)
+    stage.prefill(mb_rows, chunk=max(1, min(64, int(getattr(args, "prefill_chunk", 64) or 64))))
     stage.setup_decode(mb_state, max_steps=args.warmup + args.steps)
     sync()
     dist.barrier()
@@ -381,6 +384,8 @@ def bench_main(args, metric: str, make_prompts):
     # the generated tokens live on the last stage: their CRC goes to rank 0 for the line
     toks = stage.tokens()
     crc = zlib.crc32(np.ascontiguousarray(np.stack(toks).astype(np.int32)).tobytes()) if toks is not None else None
+    if toks is not None and os.environ.get("MX_TOKENS_DUMP"):  # diagnosis: [S][M][steps] token ids
+        np.save(os.environ["MX_TOKENS_DUMP"], np.stack(toks).astype(np.int32))
     if world > 1 and stage.last:
         comm.send_obj(crc, 0)
     elif world > 1 and rank == 0:

@@ -903,6 +903,10 @@ class LocalComm:
         kind, c = self._get(src)
         assert kind == "t", "hand-off order mismatch: expected a tensor"
         t.copy_(c)
+        if c.is_cuda:  # the snapshot came from the sender stream's pool: it must not return there (and be
+            import torch  # reused by the sender) before this stream's copy has run
+
+            torch.cuda.current_stream().synchronize()
 
     def exchange(self, sends, recvs):
         for t, d in sends:
