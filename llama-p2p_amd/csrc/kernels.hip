@@ -913,13 +913,23 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
     }
 }
 
-// q/k/v split-K partials -> sum in slab order -> RoPE + q / KV-cache stores
+// q/k/v split-K partials -> sum in slab order -> RoPE + q / KV-cache stores.  A work-group finishes
+// 32 feature quads (128 features) of 64 token rows, each thread one quad of 8 rows: a 128-byte line of
+// the tile-ordered K / V cache holds 8 positions x 8 dims (device_common.h kv_k_off / kv_v_off), so
+// for the positions of a prompt chunk every line is written by ONE work-group instead of by up to 8 of
+// the launch -- lines written in parts by several work-groups at once were what differed run to run
+// when another process shared the GPU (profiles/round4_gpu_sharing.txt)
 __global__ __launch_bounds__(256) void qkv_finish_kernel(MMArgs a, const float* slabs, int nslab, size_t stride) {
   const int N = a.n_q + 2 * a.n_kv;
-  const int quads = N / 4;
-  const int total = a.M * quads;
-  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < total; u += gridDim.x * blockDim.x) {
-    const int col = u / quads, row = (u % quads) * 4;
+  const int quads = N / 4, qblocks = (quads + 31) / 32;
+  const int cb = blockIdx.x / qblocks, qb = blockIdx.x % qblocks;
+  const int q = qb * 32 + (threadIdx.x & 31);
+  if (q >= quads) return;
+  const int row = q * 4;
+  const int c0 = cb * 64 + (threadIdx.x >> 5) * 8;
+  for (int c = 0; c < 8; ++c) {
+    const int col = c0 + c;
+    if (col >= a.M) break;
     f32x4 s = *reinterpret_cast<const f32x4*>(slabs + (size_t)col * N + row);
     for (int k = 1; k < nslab; ++k) s += *reinterpret_cast<const f32x4*>(slabs + k * stride + (size_t)col * N + row);
     qkv_store(a, row, col, s);
@@ -927,8 +937,9 @@ __global__ __launch_bounds__(256) void qkv_finish_kernel(MMArgs a, const float* 
 }
 
 void launch_qkv_finish(const MMArgs& a, const float* slabs, int nslab, size_t stride, hipStream_t s) {
-  const int total = a.M * (a.n_q + 2 * a.n_kv) / 4;
-  qkv_finish_kernel<<<(total + 255) / 256, 256, 0, s>>>(a, slabs, nslab, stride);
+  const int quads = (a.n_q + 2 * a.n_kv) / 4;
+  const int grid = (a.M + 63) / 64 * ((quads + 31) / 32);
+  qkv_finish_kernel<<<grid, 256, 0, s>>>(a, slabs, nslab, stride);
 }
 
 void launch_resid_norm(uint16_t* y, int ldy, float* x, const float* slabs, int nslab, size_t stride, const float* w,
@@ -997,10 +1008,7 @@ int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, h
                    : cfg == 3 ? launch_wide_cfg<3, 1, EPI_SLAB>(p, ksplit, s)
                               : launch_wide_cfg<4, 1, EPI_SLAB>(p, ksplit, s);
       if (rc) return -1;
-      if (epi == EPI_QKV && qkv_finish) {
-        const int total = a.M * a.N / 4;
-        qkv_finish_kernel<<<(total + 255) / 256, 256, 0, s>>>(a, slabs, ksplit, slab_stride);
-      }
+      if (epi == EPI_QKV && qkv_finish) launch_qkv_finish(a, slabs, ksplit, slab_stride, s);
       return ksplit;
     }
   }
