@@ -189,7 +189,6 @@ class Stage:
         # host seconds spent issuing hand-offs / lane steps, and micro-steps issued (the hand-off's
         # host cost per micro-step against the stage's device time, bench line "host_per_micro_step")
         self.host_exchange_s, self.host_step_s, self.micro_steps = 0.0, 0.0, 0
-        self._sync_steps = bool(os.environ.get("MX_STAGE_SYNC"))  # diagnosis: device sync after every step
 
     # -- prefill (untimed): prompt rows through every stage, 64 rows per hand-off
     def prefill(self, mb_rows: Sequence[Tuple[List[int], List[int], List[int]]], chunk: int = 64):
@@ -258,8 +257,6 @@ class Stage:
                 else:
                     b.step_tensors(self.x_in[mb], self.x_out[mb])
                     self.deferred = [(self.x_out[mb], self.rank + 1)]
-                if self._sync_steps:
-                    self.torch.cuda.synchronize()
                 self.host_exchange_s += t1 - t0
                 self.host_step_s += time.perf_counter() - t1
                 self.micro_steps += 1
