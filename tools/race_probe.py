@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--load", action="store_true")
     ap.add_argument("--mem-load", action="store_true", help="the second stream streams 2 GiB copies (HBM-bound)")
+    ap.add_argument("--alloc-load", action="store_true",
+                    help="the second thread allocates and frees 1 GiB device buffers in a loop (page-table updates)")
     ap.add_argument("--engine-load", type=int, default=0,
                     help="the load is a SECOND engine (layers [0, N)) prefilling in chunks of --load-chunk rows")
     ap.add_argument("--load-chunk", type=int, default=64)
@@ -62,6 +64,14 @@ def main():
 
     def load():
         torch.cuda.set_stream(torch.cuda.Stream())
+        if args.alloc_load:
+            while not stop.is_set():
+                t = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+                t[:4096].zero_()
+                torch.cuda.current_stream().synchronize()
+                del t
+                torch.cuda.empty_cache()
+            return
         if args.engine_load or args.load_from:
             if args.load_from:
                 e2 = Engine(f"synthetic:{args.model}:seed=0", n_ctx=512, n_seq_max=M, device=0,
@@ -102,7 +112,7 @@ def main():
 
     ready = threading.Event()
     th = threading.Thread(target=load, daemon=True) if (args.load or args.mem_load or args.engine_load or
-                                                        args.load_from) else None
+                                                        args.load_from or args.alloc_load) else None
     if th:
         th.start()
         if args.engine_load or args.load_from:
@@ -140,7 +150,7 @@ def main():
         th.join()
     same = [bool(np.array_equal(outs[0], o)) for o in outs[1:]]
     diff = [float(np.abs(outs[0] - o).max()) for o in outs[1:]]
-    print({"model": args.model, "load": args.load, "mem_load": args.mem_load, "engine_load": args.engine_load,
+    print({"model": args.model, "load": args.load, "mem_load": args.mem_load, "alloc_load": args.alloc_load, "engine_load": args.engine_load,
            "load_chunk": args.load_chunk, "load_from": args.load_from, "layers": args.layers or "all", "reps_equal": same,
            "max_abs_diff": diff, "chunk": args.chunk, "decode": args.decode, "from_layer": args.from_layer, "prompts": [args.lo, args.hi]})
     eng.close()
