@@ -339,6 +339,10 @@ def bench_main(args, metric: str, make_prompts):
         stage = Stage(EngineAdapter(eng), comm, rank, world, shape.n_embd, device, S,
                       dtype=torch.float32 if f32 else torch.bfloat16)  # hidden states cross stages in bf16
         sync = torch.cuda.synchronize
+    # every rank's engine exists before any rank computes: a context or queue being created on the
+    # same GPU while another rank's kernels run is when results were seen to vary
+    sync()
+    dist.barrier()
     prompts = make_prompts(vocab, S * M)
     mb_rows, mb_state = [], []
     for mb in range(S):
