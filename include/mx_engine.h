@@ -189,6 +189,12 @@ int mx_stage_rows_pick(mx_engine* e, int n, const int32_t* slots, const int32_t*
  * HIP events on the engine stream (benchmark roofline); kind: 0 qkv, 1 attn_output,
  * 2 ffn_gate_up, 3 ffn_down, 4 lm_head, 5 qkv with fused RMSNorm, 6 ffn_gate_up with fused
  * RMSNorm (M <= 8), 7 attention (positions = env MX_PROF_POS).  Returns mean microseconds per launch. */
+/* Diagnosis: op 0 sets the number of launches after which a 17..64-row forward stops (-1: never),
+ * op 1 synchronises the stream after every such launch (arg != 0), op 2 copies internal buffer `arg`
+ * (0 x, 1 q, 2 xn, 3 attn_out, 4 act, 5 split-K slabs, 6 K cache, 7 V cache, 8 ssq partials, 9 row
+ * positions, 10 row slots, 11 RoPE table) to
+ * `host`, at most `bytes`.  MX_POISON=1 at creation fills every allocation with 0xFF bytes. */
+int mx_debug(mx_engine* e, int op, long long arg, void* host, size_t bytes);
 int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us_per_launch, double* bytes_per_launch);
 
 int mx_sync(mx_engine* e);

@@ -122,11 +122,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
       {  // RoPE (mode NORM: adjacent pairs) on q and k, as selects (a branch would pull csv's load into it)
         const bool rope = i < G * D + D && pos < a.n_ctx;
         const f32x4 s = v;
-        f32x4 rv;
-        rv[0] = s[0] * csv[0] - s[1] * csv[1];
-        rv[1] = s[0] * csv[1] + s[1] * csv[0];
-        rv[2] = s[2] * csv[2] - s[3] * csv[3];
-        rv[3] = s[2] * csv[3] + s[3] * csv[2];
+        const f32x4 rv = rope4(s, csv);
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = rope ? rv[j] : s[j];
       }

@@ -87,6 +87,26 @@ __device__ __forceinline__ f32x4 qkv_cs(const MMArgs& a, int row, int pos) {
   return *reinterpret_cast<const f32x4*>(a.rope_cs + ((size_t)p * (d / 2) + (rl % d) / 2) * 2);
 }
 
+// RoPE (mode NORM) of two adjacent pairs (s0, s1), (s2, s3) by their (cos, sin) in c: o0 = s0 c0 - s1 c1,
+// ... as four scalar fmas.  Every operand passes through an empty asm so that the SLP vectorizer
+// cannot turn them into v_pk_mul_f32 / v_pk_fma_f32 chains: compiled packed, the result's third
+// element came out wrong in lanes 32-63 of a wave, run to run, whenever another queue's waves shared
+// the CU (profiles/round5_rope_packed_hazard.txt; qkv_finish_kernel under a second process).
+__device__ __forceinline__ float opq(float v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ f32x4 rope4(f32x4 s, f32x4 c) {
+  const float s0 = opq(s[0]), s1 = opq(s[1]), s2 = opq(s[2]), s3 = opq(s[3]);
+  const float c0 = opq(c[0]), c1 = opq(c[1]), c2 = opq(c[2]), c3 = opq(c[3]);
+  f32x4 o;
+  o[0] = opq(__builtin_fmaf(s0, c0, -(s1 * c1)));
+  o[1] = opq(__builtin_fmaf(s0, c1, s1 * c0));
+  o[2] = opq(__builtin_fmaf(s2, c2, -(s3 * c3)));
+  o[3] = opq(__builtin_fmaf(s2, c3, s3 * c2));
+  return o;
+}
+
 // q/k/v rows [row, row+4) of token column `col`: RoPE (mode NORM, adjacent pairs) on q and k,
 // q -> f32 buffer, k / v -> the f16 K / V caches (layout above).
 __device__ __forceinline__ void qkv_store_pre(const MMArgs& a, int row, int col, f32x4 s, int pos, int slot,
@@ -97,11 +117,7 @@ __device__ __forceinline__ void qkv_store_pre(const MMArgs& a, int row, int col,
     const bool is_q = row < a.n_q;
     const int rl = is_q ? row : row - a.n_q;
     const int dd = rl % d;  // multiple of 4
-    f32x4 o;
-    o[0] = s[0] * csv[0] - s[1] * csv[1];
-    o[1] = s[0] * csv[1] + s[1] * csv[0];
-    o[2] = s[2] * csv[2] - s[3] * csv[3];
-    o[3] = s[2] * csv[3] + s[3] * csv[2];
+    const f32x4 o = rope4(s, csv);
     if (is_q) {
       *reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + row) = o;
     } else {

@@ -319,7 +319,18 @@ struct mx_engine {
   int alloc(void** p, size_t bytes) {
     HIPC(hipMalloc(p, bytes));
     allocations.push_back(*p);
+    if (poison) HIPC(hipMemset(*p, 0xFF, bytes));  // NaN in every f32 / f16 / bf16 lane
     return 0;
+  }
+  // diagnosis (mx_debug): MX_POISON=1 fills every allocation with 0xFF bytes and skips the zero
+  // fills of init_common, so a read of a never-written element shows up as a NaN; dbg_stop ends the
+  // 17..64-row forward after that many launches, dbg_sync synchronises the stream after each one
+  const bool poison = getenv("MX_POISON") != nullptr;
+  int dbg_stop = -1, dbg_count = 0;
+  bool dbg_sync = false;
+  bool dbg_hit(hipStream_t s) {
+    if (dbg_sync) hipStreamSynchronize(s);
+    return dbg_stop >= 0 && ++dbg_count >= dbg_stop;
   }
   int init_common();
   int load_synthetic(const Shape& s, uint64_t seed, bool q8 = false, int kq_base = 0, bool q4 = false);
@@ -426,8 +437,10 @@ int mx_engine::init_common() {
   layer_kv_stride = slot_stride * n_seq_max;
   if (int rc = alloc((void**)&kcache, layer_kv_stride * nl * sizeof(_Float16))) return rc;
   if (int rc = alloc((void**)&vcache, layer_kv_stride * nl * sizeof(_Float16))) return rc;
-  HIPC(hipMemsetAsync(kcache, 0, layer_kv_stride * nl * sizeof(_Float16), stream));
-  HIPC(hipMemsetAsync(vcache, 0, layer_kv_stride * nl * sizeof(_Float16), stream));
+  if (!poison) {
+    HIPC(hipMemsetAsync(kcache, 0, layer_kv_stride * nl * sizeof(_Float16), stream));
+    HIPC(hipMemsetAsync(vcache, 0, layer_kv_stride * nl * sizeof(_Float16), stream));
+  }
 
   // RoPE table, ggml_rope_cache_init + rope_yarn (ext_factor 0, mscale 1): theta *= powf(base, -2/d)
   // as an f32 running product, divided by the frequency factor, times the linear freq_scale
@@ -495,9 +508,11 @@ int mx_engine::init_common() {
       if (int rc = alloc((void**)&xkb, (size_t)R * (kmax / 32) * 4)) return rc;
   }
   // poison-free start: zero activations so padded MFMA columns never read uninitialised memory
-  HIPC(hipMemsetAsync(xn, 0, (size_t)R * n_embd * 2, stream));
-  HIPC(hipMemsetAsync(attn_out, 0, (size_t)R * n_embd * 2, stream));
-  HIPC(hipMemsetAsync(act, 0, (size_t)R * n_ff * 2, stream));
+  if (!poison) {
+    HIPC(hipMemsetAsync(xn, 0, (size_t)R * n_embd * 2, stream));
+    HIPC(hipMemsetAsync(attn_out, 0, (size_t)R * n_embd * 2, stream));
+    HIPC(hipMemsetAsync(act, 0, (size_t)R * n_ff * 2, stream));
+  }
   for (int i = 0; i < n_seq_max; i++) free_slots.push_back(n_seq_max - 1 - i);
   slot_tokens.assign(n_seq_max, {});
   return 0;
@@ -1224,19 +1239,26 @@ int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void
                                     int* hist_count, int max_hist, hipStream_t s) {
   const int h = n_embd, kv = n_embd_kv, ff = n_ff;
   int nslab = 0;  // partial slabs not yet folded into x
+  dbg_count = 0;
   for (int li = 0; li < (int)layers.size(); li++) {
     const Layer& L = layers[li];
     _Float16* kc = kcache + layer_kv_stride * li;
     _Float16* vc = vcache + layer_kv_stride * li;
     launch_resid_norm(xn, h, x, slabs, nslab, slab_stride, L.attn_norm, M, h, eps, s);
     nslab = 0;
+    if (dbg_hit(s)) return 0;
     MMArgs a{};
     a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M; a.X = xn; a.ldx = h;
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
     a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
     a.slot_stride = slot_stride;
-    const int qsplit = launch_mm_wide(EPI_QKV, a, slabs, slab_stride, s, !rows_distinct);
+    const int qsplit = launch_mm_wide(EPI_QKV, a, slabs, slab_stride, s, false);
     if (qsplit < 0) return fail(MX_ERR_ARG, "wide qkv launch shape");
+    if (dbg_hit(s)) return 0;
+    if (!rows_distinct) {  // rows of one sequence attend to each other's new K/V: finish them first
+      launch_qkv_finish(a, slabs, qsplit, slab_stride, s);
+      if (dbg_hit(s)) return 0;
+    }
     AttnArgs at{};
     if (rows_distinct) {  // the attention kernel finishes q/k/v from the split-K slabs
       at.slabs = slabs; at.nslab = qsplit; at.slab_stride = slab_stride; at.rope_cs = rope_cs; at.kc_w = kc;
@@ -1247,19 +1269,24 @@ int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void
     at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;
     at.scale = 1.0f / sqrtf((float)head_dim);
     launch_attention(at, s);
+    if (dbg_hit(s)) return 0;
     MMArgs b{};
     b.W = L.o; b.N = h; b.K = h; b.X = attn_out; b.ldx = h; b.M = M;
     if ((nslab = launch_mm_wide(EPI_RESID, b, slabs, slab_stride, s)) < 0)
       return fail(MX_ERR_ARG, "wide attn_output launch shape");
+    if (dbg_hit(s)) return 0;
     launch_resid_norm(xn, h, x, slabs, nslab, slab_stride, L.ffn_norm, M, h, eps, s);
     nslab = 0;
+    if (dbg_hit(s)) return 0;
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.X = xn; c.ldx = h; c.act = act; c.lda = ff;
     if (launch_mm_wide(EPI_SWIGLU, c, slabs, slab_stride, s) < 0) return fail(MX_ERR_ARG, "wide gate/up launch shape");
+    if (dbg_hit(s)) return 0;
     MMArgs d{};
     d.W = L.down; d.N = h; d.K = ff; d.X = act; d.ldx = ff; d.M = M;
     if ((nslab = launch_mm_wide(EPI_RESID, d, slabs, slab_stride, s)) < 0)
       return fail(MX_ERR_ARG, "wide ffn_down launch shape");
+    if (dbg_hit(s)) return 0;
   }
   if (x_out || (head && rowmap)) {
     launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);
@@ -1611,7 +1638,10 @@ int mx_engine::forward_rows_chunk(int n, const int32_t* slots, const int32_t* po
   const size_t R = PREFILL_ROWS;
   auto h2d = [&](int* dst, const int32_t* src, int k, int row) -> int {
     memcpy(h_idx + row * R, src, (size_t)k * 4);
-    HIPC(hipMemcpyAsync(dst, h_idx + row * R, (size_t)k * 4, hipMemcpyHostToDevice, s));
+    if (hipMemcpyAsync(dst, h_idx + row * R, (size_t)k * 4, hipMemcpyHostToDevice, s) != hipSuccess) {
+      hipStreamSynchronize(s);  // earlier copies of this call may still read h_idx
+      return fail(MX_ERR_HIP, "index upload");
+    }
     return 0;
   };
   if (ids)
@@ -1638,7 +1668,10 @@ int mx_engine::forward_rows_chunk(int n, const int32_t* slots, const int32_t* po
                                   n_out, false, nullptr, nullptr, nullptr, 0, nullptr, 0, s);
   rows_distinct = false;
   rows_blocked = false;
-  if (frc) return frc;
+  if (frc) {  // the index copies enqueued above still read h_idx: drain them before it is reused
+    hipStreamSynchronize(s);
+    return frc;
+  }
   if (head) HIPC(hipMemcpyAsync(logits_host, logits, (size_t)n_out * n_vocab * 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   return d1_check(s);
@@ -2227,6 +2260,41 @@ int mx_stage_rows(mx_engine* e, int n, const int32_t* slots, const int32_t* pos,
   return e->forward_rows_chunk(n, slots, pos, ids, x_in, x_out, logits_out, s);
 }
 
+int mx_debug(mx_engine* e, int op, long long arg, void* host, size_t bytes) {
+  if (!e) return fail(MX_ERR_ARG, "null engine");
+  std::lock_guard<std::mutex> lk(e->gpu_mu);
+  hipSetDevice(e->device);
+  switch (op) {
+    case 0: e->dbg_stop = (int)arg; return 0;
+    case 1: e->dbg_sync = arg != 0; return 0;
+    case 2: {
+      const size_t R = PREFILL_ROWS, nl = e->layers.size();
+      const void* src = nullptr;
+      size_t n = 0;
+      switch (arg) {
+        case 0: src = e->x, n = R * e->n_embd * 4; break;
+        case 1: src = e->q, n = R * e->n_embd * 4; break;
+        case 2: src = e->xn, n = R * e->n_embd * 2; break;
+        case 3: src = e->attn_out, n = R * e->n_embd * 2; break;
+        case 4: src = e->act, n = R * e->n_ff * 2; break;
+        case 5: src = e->slabs, n = e->slab_stride * 8 * 4; break;
+        case 6: src = e->kcache, n = e->layer_kv_stride * nl * 2; break;
+        case 7: src = e->vcache, n = e->layer_kv_stride * nl * 2; break;
+        case 8: src = e->ssq, n = R * (e->n_embd / 16) * 4; break;
+        case 9: src = e->d_pos, n = R * 4; break;
+        case 10: src = e->d_slot, n = R * 4; break;
+        case 11: src = e->rope_cs, n = (size_t)e->n_ctx * e->head_dim * 4; break;
+        default: return fail(MX_ERR_ARG, "mx_debug: unknown buffer");
+      }
+      if (!host) return fail(MX_ERR_ARG, "mx_debug: null host buffer");
+      HIPC(hipDeviceSynchronize());
+      HIPC(hipMemcpy(host, src, std::min(n, bytes), hipMemcpyDeviceToHost));
+      return 0;
+    }
+  }
+  return fail(MX_ERR_ARG, "mx_debug: unknown op");
+}
+
 static int make_request(mx_engine* e, const int32_t* ids, int n, const mx_sampling* s, int max_tokens,
                         std::unique_ptr<Request>* out) {
   if (!ids || n < 1) return fail(MX_ERR_ARG, "bad arguments");
@@ -2803,6 +2871,12 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
         per = (size_t)2 * ff * h * 2;
         return (e->use_pers && mm_pers_supported(EPI_SWIGLU, M, a.N, a.K)) ? launch_mm_pers(EPI_SWIGLU, a, s)
                                                                             : launch_mm(EPI_SWIGLU, a, s);
+      case 8: case 9: case 10: {  // RMS_NORM of M rows folding 4 (8) / 8 (9) / 0 (10) split-K slabs
+        const int ns = kind == 8 ? 4 : kind == 9 ? 8 : 0;
+        per = (size_t)M * h * 4 * (2 + ns) + (size_t)M * h * 2;
+        launch_resid_norm(e->xn, h, e->x, e->slabs, ns, e->slab_stride, L.ffn_norm, M, h, e->eps, s);
+        return 0;
+      }
       case 7: {  // attention at the positions set below (ctx = pos + 1)
         AttnArgs at{};
         at.q = e->q; at.kc = e->kcache + e->layer_kv_stride * li; at.vc = e->vcache + e->layer_kv_stride * li;

@@ -27,7 +27,7 @@ EXPORTS = [
     "mx_engine_info", "mx_forward_logits", "mx_forward_rows", "mx_forward_topk", "mx_submit", "mx_wait", "mx_submit_batch", "mx_poll", "mx_cancel", "mx_batch_create",
     "mx_batch_step", "mx_batch_ids_device", "mx_batch_bind_ids", "mx_batch_tokens", "mx_batch_destroy", "mx_stage_rows",
     "mx_profile_kernel", "mx_sync", "mx_device_count", "mx_engine_stats", "mx_batch_reset", "mx_stage_rows_pick",
-    "mx_probe_copy", "mx_probe_read",
+    "mx_probe_copy", "mx_probe_read", "mx_debug",
 ]
 
 
@@ -140,6 +140,7 @@ def lib() -> ctypes.CDLL:
         L.mx_engine_stats.argtypes = [vp, P(MxStats)]
         L.mx_batch_reset.argtypes = [vp, vp, vp, vp, vp, vp]
         L.mx_stage_rows_pick.argtypes = [vp, i32, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp]
+        L.mx_debug.argtypes = [vp, i32, ctypes.c_longlong, vp, ctypes.c_size_t]
         for name in EXPORTS:
             if name not in ("mx_opts_default", "mx_sampling_default", "mx_last_error", "mx_engine_destroy",
                             "mx_batch_destroy", "mx_batch_ids_device"):
@@ -358,6 +359,24 @@ class Engine:
 
     def sync(self):
         _check(lib().mx_sync(self._h))
+
+    # -- diagnosis (include/mx_engine.h mx_debug) -------------------------------
+    DEBUG_BUFFERS = {"x": 0, "q": 1, "xn": 2, "attn_out": 3, "act": 4, "slabs": 5, "kcache": 6, "vcache": 7,
+                     "ssq": 8, "pos": 9, "slot": 10, "rope_cs": 11}
+
+    def debug_stop(self, n: int):
+        """End every 17..64-row forward after n launches (-1: never)."""
+        _check(lib().mx_debug(self._h, 0, n, None, 0))
+
+    def debug_sync(self, on: bool):
+        """Synchronise the stream after every launch of a 17..64-row forward."""
+        _check(lib().mx_debug(self._h, 1, int(on), None, 0))
+
+    def debug_read(self, name: str, nbytes: int) -> np.ndarray:
+        """The first nbytes of an internal buffer (after a device synchronize), as uint8."""
+        out = np.zeros(nbytes, dtype=np.uint8)  # past the buffer's end: zeros
+        _check(lib().mx_debug(self._h, 2, self.DEBUG_BUFFERS[name], out.ctypes.data, nbytes))
+        return out
 
     def close(self):
         if getattr(self, "_h", None):

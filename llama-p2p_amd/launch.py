@@ -43,37 +43,77 @@ def rank_env(rank: int, world: int, port: int, base=None) -> dict:
     return env
 
 
-def spawn_ranks(n: int, argv: Sequence[str], timeout: Optional[float] = None, stdout=None) -> int:
+class _Terminated(Exception):
+    pass
+
+
+def _raise_terminated(signum, frame):
+    raise _Terminated(signum)
+
+
+def _child_setup():
+    """In the child, before exec: die with the launcher (PR_SET_PDEATHSIG = SIGTERM), so a killed
+    launcher cannot leave ranks holding the GPUs and the rendezvous port."""
+    try:
+        import ctypes
+
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM, 0, 0, 0)  # PR_SET_PDEATHSIG
+    except OSError:
+        pass
+
+
+def spawn_ranks(n: int, argv: Sequence[str], timeout: Optional[float] = None, stdout=None,
+                grace: float = 300.0) -> int:
     """Run ``[python] + argv`` as ranks 0..n-1; returns the exit status (0, or the first failure's).
 
     A rank that fails ends the others (by their exact PIDs: SIGTERM, then SIGKILL after 10 s), so a
-    stuck RCCL rendezvous cannot outlive a crashed peer."""
+    stuck RCCL rendezvous cannot outlive a crashed peer; once any rank has exited, the rest get
+    ``grace`` seconds.  SIGTERM / SIGINT to the launcher stop every rank before it exits, and each
+    rank also gets SIGTERM if the launcher dies without running its handlers."""
     port = free_port()
     out = sys.stdout if stdout is None else stdout
     out.flush()
     procs: List[subprocess.Popen] = []
-    for r in range(n):
-        procs.append(subprocess.Popen([sys.executable] + list(argv), env=rank_env(r, n, port),
-                                      stdout=out if r == 0 else sys.stderr, stderr=sys.stderr))
-    t0 = time.time()
+    old = {sig: signal.signal(sig, _raise_terminated) for sig in (signal.SIGTERM, signal.SIGINT)}
     status = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            rc = p.poll()
-            if rc is None:
-                continue
-            live.remove(p)
-            if rc != 0 and status == 0:
-                status = rc if rc > 0 else 128 - rc
-                print(f"[launch] rank {procs.index(p)} exited with {rc}; stopping the other ranks",
+    try:
+        for r in range(n):
+            procs.append(subprocess.Popen([sys.executable] + list(argv), env=rank_env(r, n, port),
+                                          stdout=out if r == 0 else sys.stderr, stderr=sys.stderr,
+                                          preexec_fn=_child_setup))
+        t0 = time.time()
+        first_exit = None
+        live = list(procs)
+        while live:
+            for p in list(live):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                live.remove(p)
+                if first_exit is None:
+                    first_exit = time.time()
+                if rc != 0 and status == 0:
+                    status = rc if rc > 0 else 128 - rc
+                    print(f"[launch] rank {procs.index(p)} exited with {rc}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    _stop(live)
+            if live and timeout is not None and time.time() - t0 > timeout:
+                print(f"[launch] ranks still running after {timeout:.0f}s; stopping them", file=sys.stderr, flush=True)
+                _stop(live)
+                status = status or 124
+            if live and first_exit is not None and time.time() - first_exit > grace:
+                print(f"[launch] ranks still running {grace:.0f}s after the first exit; stopping them",
                       file=sys.stderr, flush=True)
                 _stop(live)
-        if timeout is not None and time.time() - t0 > timeout and live:
-            print(f"[launch] ranks still running after {timeout:.0f}s; stopping them", file=sys.stderr, flush=True)
-            _stop(live)
-            status = status or 124
-        time.sleep(0.05)
+                status = status or 124
+            time.sleep(0.05)
+    except _Terminated as e:
+        print(f"[launch] signal {e.args[0]}: stopping every rank", file=sys.stderr, flush=True)
+        status = 128 + int(e.args[0])
+    finally:
+        _stop(procs)
+        for sig, h in old.items():
+            signal.signal(sig, h)
     return status
 
 

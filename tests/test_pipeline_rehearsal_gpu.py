@@ -8,11 +8,10 @@ send/recv schedule, prefill hand-offs, token return, timing and the one JSON lin
 8-GPU run takes.  With the f32 hand-off a stage split is bitwise equal to one engine, so
 the CRC32 of every generated token must equal the one-stage run over the same micro-batches.
 
-Prompt rows cross stages in 16-row chunks here: with two processes on ONE GPU, 17-64-row prompt chunks
-of one sequence are not run-to-run reproducible (profiles/round4_gpu_sharing.txt: the same happens with
-two independent engine processes and no hand-off at all; one process, or <= 16-row chunks, or the
-32-row decode steps are bitwise), so the bitwise check uses the reproducible chunking.  The 8-GPU
-layout (one process per GPU) does not share a GPU.
+Prompt rows cross stages in 64-row chunks (the bench's default).  Round 4 had to narrow this to 16-row
+chunks: with two processes on one GPU the 17-64-row one-sequence chunks were not run-to-run reproducible.
+The cause was the packed-FP32 RoPE in qkv_finish_kernel (profiles/round5_rope_packed_hazard.txt), now
+scalar; tests/test_gpu_sharing_gpu.py keeps the in-process two-stream form of the same check.
 """
 import json
 import os
@@ -32,7 +31,7 @@ def _bench(*extra, timeout=240):
     env.pop("RANK", None)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--model", "llama3-8b", "--steps", "4", "--warmup", "1",
-           "--handoff", "f32", "--prefill-chunk", "16", "--no-cpu-baseline"] + list(extra)
+           "--handoff", "f32", "--prefill-chunk", "64", "--no-cpu-baseline"] + list(extra)
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
