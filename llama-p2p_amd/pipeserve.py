@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import collections
 import itertools
+import logging
 import threading
 import time
 from typing import Dict, List, Optional
@@ -43,6 +44,8 @@ from .placement import PeerScoreboard
 
 FINISH_LENGTH, FINISH_STOP = 0, 1
 
+
+_log = logging.getLogger("llama_p2p_amd.pipeserve")
 
 class PRequest:
     __slots__ = ("id", "prompt", "samp", "seed", "max_tokens", "out", "done", "finish", "cancel", "lane", "row",
@@ -273,8 +276,12 @@ class StageRunner:
     decode ring, and (last stage) the token return to rank 0."""
 
     def __init__(self, executor, comm, rank: int, world: int, lanes: int, rows: int, kmax: int, device,
-                 stage_time_every: int = 8):
+                 stage_time_every: int = 8, timing_lock=None):
         import torch
+
+        # stages sharing ONE GPU (local_pipeline_llama): lane steps are timed one stage at a time under
+        # this lock, so a stage's event pair does not also count the other stages' kernels
+        self.timing_lock = timing_lock
 
         self.ex, self.comm, self.rank, self.world = executor, comm, rank, world
         self.first, self.last = rank == 0, rank == world - 1
@@ -343,6 +350,15 @@ class StageRunner:
         enqueued, so the pair times this stage's kernels only): the stage's busy time."""
         if self.world == 1:  # one stage: no placement to inform
             b.step_tensors(x_in, x_out)
+        elif self.device.type == "cuda" and self.timing_lock is not None:
+            with self.timing_lock:
+                e0, e1 = self.torch.cuda.Event(enable_timing=True), self.torch.cuda.Event(enable_timing=True)
+                self.torch.cuda.current_stream().synchronize()  # the hand-off copies before the step
+                e0.record()
+                b.step_tensors(x_in, x_out)
+                e1.record()
+                e1.synchronize()
+            self.busy_s += e0.elapsed_time(e1) / 1e3
         elif self.device.type == "cuda":
             e0, e1 = self.torch.cuda.Event(enable_timing=True), self.torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -579,40 +595,76 @@ def _minmax_split(w, n_layer: int, head_layers: float):
 
 class StagePlanner:
     """Rank 0's stage placement (the reference's select_peer / update_peer_performance,
-    p2p:156-168, applied to stages): per-stage busy times go into a PeerScoreboard; once every
-    stage has ``min_samples`` samples, a proposed split whose predicted slowest-stage time is at
-    least ``min_gain`` lower than the current one is returned (the scheduler then drains the lanes
-    and every rank rebuilds its stage).  After a re-split the board starts afresh."""
+    p2p:156-168, applied to stages): per-stage busy times go into a PeerScoreboard (and a sample list
+    per stage).  A proposed split is returned -- the scheduler then drains the lanes and every rank
+    rebuilds its stage -- only on evidence:
+      * every stage has ``min_samples`` samples since the last re-split (and ``cooldown``
+        observations have passed since it),
+      * the predicted slowest-stage time drops by at least ``min_gain`` AND by more than ``z`` times
+        the largest relative standard error of a stage's mean time (a gain inside the noise of the
+        measurement is no reason to rebuild every stage),
+      * at most ``max_resplits`` re-splits over the planner's life.
+    Every decision that returns a split is logged and kept in ``history``; ``last`` holds the most
+    recent evaluation."""
 
-    def __init__(self, parts, head_layers: float = 0.0, min_gain: float = 0.10, min_samples: int = 2,
-                 enabled: bool = True):
+    def __init__(self, parts, head_layers: float = 0.0, min_gain: float = 0.10, min_samples: int = 8,
+                 enabled: bool = True, z: float = 3.0, max_resplits: int = 2, cooldown: int = 8):
         self.parts = [tuple(p) for p in parts]
         self.head_layers, self.min_gain, self.min_samples, self.enabled = head_layers, min_gain, min_samples, enabled
+        self.z, self.max_resplits, self.cooldown = z, max_resplits, cooldown
         self.board = PeerScoreboard(list(range(len(parts))), policy="score_aware")
-        self.history = []  # (parts before, parts after, predicted max before, after, stage weights)
+        self.samples: List[List[float]] = [[] for _ in parts]
+        self.n_obs, self.obs_at_resplit, self.resplits = 0, 0, 0
+        self.history = []  # every re-split returned: parts before / after, predicted times, evidence
+        self.last: Optional[dict] = None
+
+    @staticmethod
+    def _rse(xs) -> float:
+        """Relative standard error of the mean of xs."""
+        n = len(xs)
+        m = sum(xs) / n
+        if n < 2 or m <= 0:
+            return float("inf")
+        var = sum((x - m) ** 2 for x in xs) / (n - 1)
+        return (var ** 0.5) / m / n ** 0.5
 
     def observe(self, times, rounds_per_sample: int = 1):
         for s, t in enumerate(times):
-            self.board.update(s, True, t / rounds_per_sample)
-        if not self.enabled:
+            v = t / rounds_per_sample
+            self.board.update(s, True, v)
+            self.samples[s].append(v)
+        self.n_obs += 1
+        if not self.enabled or self.resplits >= self.max_resplits:
             return None
-        st = self.board.stats()
-        if any(st.get(s, {}).get("success", 0) < self.min_samples for s in range(len(self.parts))):
+        if self.resplits and self.n_obs - self.obs_at_resplit < self.cooldown:
+            return None
+        if any(len(x) < self.min_samples for x in self.samples):
             return None
         w = stage_weights(self.board, self.parts, self.head_layers)
         if w is None:
             return None
         new = proposed_partition(self.board, self.parts, self.head_layers)
         cur_t, new_t = predicted_max(w, self.parts, self.head_layers), predicted_max(w, new, self.head_layers)
-        if new != self.parts and new_t <= cur_t * (1.0 - self.min_gain):
-            self.history.append({"from": list(self.parts), "to": list(new), "predicted_max_from": cur_t,
-                                 "predicted_max_to": new_t, "weights": w, "t": time.time()})
+        gain = 1.0 - new_t / cur_t if cur_t > 0 else 0.0
+        noise = max(self._rse(x) for x in self.samples)
+        need = max(self.min_gain, self.z * noise)
+        self.last = {"from": list(self.parts), "proposed": list(new), "predicted_max_from": cur_t,
+                     "predicted_max_to": new_t, "gain": gain, "noise_rse": noise, "needed": need,
+                     "samples": min(len(x) for x in self.samples)}
+        if new != self.parts and gain >= need:
+            self.history.append(dict(self.last, to=list(new), weights=w, t=time.time()))
+            self.resplits += 1
+            _log.warning("stage planner: re-split %s -> %s (predicted slowest stage %.3g -> %.3g, gain %.1f%% "
+                         "> needed %.1f%%, %d samples per stage)", self.parts, new, cur_t, new_t, 100 * gain,
+                         100 * need, self.last["samples"])
             return new
         return None
 
     def applied(self, parts):
         self.parts = [tuple(p) for p in parts]
         self.board = PeerScoreboard(list(range(len(parts))), policy="score_aware")
+        self.samples = [[] for _ in parts]
+        self.obs_at_resplit = self.n_obs
 
 
 # ------------------------------------------------------------------------------ engine executor
@@ -781,7 +833,8 @@ def _stage_setup(model_path, rank, world, lanes, rows, n_ctx, kmax, device, hand
 
 
 def serve_stage(model_path: str, comm, rank: int, world: int, lanes: int, rows: int = 32, n_ctx: int = 512,
-                kmax: int = 8, device=None, handoff_bf16: bool = True, parts=None):
+                kmax: int = 8, device=None, handoff_bf16: bool = True, parts=None, timing_lock=None,
+                stage_time_every: int = 8):
     """Ranks 1..S-1: hold a stage and execute rank 0's round plans until it stops (a repartition
     plan replaces the stage engine by one holding the new layer range)."""
     import torch
@@ -789,7 +842,7 @@ def serve_stage(model_path: str, comm, rank: int, world: int, lanes: int, rows: 
     device = device or torch.device("cuda", torch.cuda.current_device())
     eng, parts = _stage_setup(model_path, rank, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts)
     held = {"eng": eng, "runner": StageRunner(EngineExecutor(eng, device), comm, rank, world, lanes, rows, kmax,
-                                              device)}
+                                              device, stage_time_every, timing_lock=timing_lock)}
 
     def rebuild(new_parts):
         held["runner"].close()
@@ -797,7 +850,8 @@ def serve_stage(model_path: str, comm, rank: int, world: int, lanes: int, rows: 
         held["runner"] = held["eng"] = None
         e2, _ = _stage_setup(model_path, rank, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, new_parts)
         held["eng"] = e2
-        held["runner"] = StageRunner(EngineExecutor(e2, device), comm, rank, world, lanes, rows, kmax, device)
+        held["runner"] = StageRunner(EngineExecutor(e2, device), comm, rank, world, lanes, rows, kmax, device,
+                                     stage_time_every, timing_lock=timing_lock)
         return held["runner"]
 
     try:
@@ -812,10 +866,13 @@ def serve_stage(model_path: str, comm, rank: int, world: int, lanes: int, rows: 
 def pipeline_llama(model_path: str, comm, world: int, lanes: Optional[int] = None, rows: int = 32,
                    n_ctx: int = 512, kmax: int = 8, device=None, handoff_bf16: bool = True, parts=None,
                    policy: str = "score_aware", seed: Optional[int] = None, verbose: bool = False,
-                   repartition: bool = True, min_gain: float = 0.10):
+                   repartition: bool = False, min_gain: float = 0.10, timing_lock=None, planner_kw=None,
+                   stage_time_every: int = 8):
     """Rank 0: a Llama-compatible object whose completions run on the S-stage pipeline (ranks 1..S-1
-    run serve_stage with the same arguments).  ``repartition``: apply the stage planner's re-splits
-    (drain, rebuild every stage, resume) when they predict >= ``min_gain`` lower slowest-stage time."""
+    run serve_stage with the same arguments).  ``repartition`` (opt-in): apply the stage planner's
+    re-splits (drain, rebuild every stage -- a full weight reload -- resume) when the measured stage
+    times predict >= ``min_gain`` lower slowest-stage time beyond their noise (StagePlanner;
+    ``planner_kw`` overrides its evidence thresholds)."""
     import torch
 
     from .llama import Llama
@@ -823,11 +880,12 @@ def pipeline_llama(model_path: str, comm, world: int, lanes: Optional[int] = Non
     device = device or torch.device("cuda", torch.cuda.current_device())
     lanes = lanes or world
     eng, parts = _stage_setup(model_path, 0, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts)
-    runner = StageRunner(EngineExecutor(eng, device), comm, 0, world, lanes, rows, kmax, device)
+    runner = StageRunner(EngineExecutor(eng, device), comm, 0, world, lanes, rows, kmax, device,
+                         stage_time_every, timing_lock=timing_lock)
     sched = Scheduler(lanes, rows, n_ctx, eng.info.eos_id, kmax, policy=policy, seed=seed)
     costs = _layer_costs(model_path)
     head_layers = costs[1] / costs[0] if costs else 1.0
-    planner = StagePlanner(parts, head_layers=head_layers, min_gain=min_gain, enabled=repartition)
+    planner = StagePlanner(parts, head_layers=head_layers, min_gain=min_gain, enabled=repartition, **(planner_kw or {}))
 
     def rebuild(front, new_parts):
         front.runner.close()
@@ -836,7 +894,8 @@ def pipeline_llama(model_path: str, comm, world: int, lanes: Optional[int] = Non
         e2, _ = _stage_setup(model_path, 0, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, new_parts)
         front.engine = e2
         llm.parts = list(new_parts)
-        return StageRunner(EngineExecutor(e2, device), comm, 0, world, lanes, rows, kmax, device)
+        return StageRunner(EngineExecutor(e2, device), comm, 0, world, lanes, rows, kmax, device,
+                           stage_time_every, timing_lock=timing_lock)
 
     # vocabulary size from the model (stage 0 has no head: n_vocab comes from the model info)
     front = PipelineFront(runner, comm, sched, n_ctx, eng.info.n_vocab, eng.info.n_embd, planner.board,
@@ -936,10 +995,12 @@ class LocalComm:
 
 def local_pipeline_llama(model_path: str, parts, lanes: int = 2, rows: int = 8, n_ctx: int = 512, kmax: int = 8,
                          device=None, handoff_bf16: bool = True, policy: str = "score_aware",
-                         seed: Optional[int] = None, repartition: bool = True, min_gain: float = 0.10):
+                         seed: Optional[int] = None, repartition: bool = False, min_gain: float = 0.10,
+                         planner_kw=None, stage_time_every: int = 8):
     """S = len(parts) stage engines of one model in THIS process (one GPU), each served by its own
     thread and stream, behind one Llama-compatible front: the pipeline server end to end without a
-    multi-GPU launch (tests; a 1-GPU rehearsal of the S-GPU layout)."""
+    multi-GPU launch (tests; a 1-GPU rehearsal of the S-GPU layout).  With ``repartition`` the stages
+    time their lane steps one at a time (a shared lock), so the planner sees each stage's own cost."""
     import torch
 
     device = device or torch.device("cuda", torch.cuda.current_device())
@@ -947,13 +1008,15 @@ def local_pipeline_llama(model_path: str, parts, lanes: int = 2, rows: int = 8, 
     hub = LocalHub()
     comms = [LocalComm(hub, r, world) for r in range(world)]
     ready, errors, threads = threading.Barrier(world), [], []
+    timing_lock = threading.Lock() if repartition else None
 
     def stage(r):
         try:
             torch.cuda.set_device(device)
             torch.cuda.set_stream(torch.cuda.Stream(device=device))
             ready.wait()
-            serve_stage(model_path, comms[r], r, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts)
+            serve_stage(model_path, comms[r], r, world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts,
+                        timing_lock=timing_lock, stage_time_every=stage_time_every)
         except Exception as e:  # noqa: BLE001
             errors.append(e)
 
@@ -964,7 +1027,8 @@ def local_pipeline_llama(model_path: str, parts, lanes: int = 2, rows: int = 8, 
     torch.cuda.set_stream(torch.cuda.Stream(device=device))
     ready.wait()
     llm = pipeline_llama(model_path, comms[0], world, lanes, rows, n_ctx, kmax, device, handoff_bf16, parts,
-                         policy=policy, seed=seed, repartition=repartition, min_gain=min_gain)
+                         policy=policy, seed=seed, repartition=repartition, min_gain=min_gain,
+                         timing_lock=timing_lock, planner_kw=planner_kw, stage_time_every=stage_time_every)
     llm._engine.stage_threads = threads
     llm._stage_threads, llm._stage_errors = threads, errors
     return llm

@@ -63,7 +63,7 @@ def _serve_waves(rank, world, parts, comm, out_q, slow_rank=-1, lanes=3, rows=3)
         P.serve_loop(runner, comm, None, N_CTX, rebuild=runner_for)
         return
     sched = P.Scheduler(lanes, rows, N_CTX, -1, kmax=4, seed=11)
-    planner = P.StagePlanner(parts, head_layers=0.0, min_gain=0.10, min_samples=2, enabled=world > 1)
+    planner = P.StagePlanner(parts, head_layers=0.0, min_gain=0.10, min_samples=4, enabled=world > 1)
     front = P.PipelineFront(runner, comm, sched, N_CTX, V, H, rebuild=lambda f, ps: runner_for(ps), planner=planner)
     res = {}
 
@@ -127,14 +127,41 @@ def test_repartition_applied_and_tokens_unchanged(world, slow, expect):
 
 def test_planner_needs_gain_and_samples():
     parts = [(0, 4), (4, 8)]
-    pl = P.StagePlanner(parts, min_gain=0.10, min_samples=2)
+    pl = P.StagePlanner(parts, min_gain=0.10, min_samples=2, z=0.0)
     assert pl.observe([1.0, 1.05]) is None  # one sample each: not yet
     assert pl.observe([1.0, 1.05]) is None  # balanced within 10 %: keep
-    pl2 = P.StagePlanner(parts, min_gain=0.10, min_samples=1)
+    pl2 = P.StagePlanner(parts, min_gain=0.10, min_samples=2, z=0.0)
+    assert pl2.observe([1.0, 2.0]) is None
     new = pl2.observe([1.0, 2.0])
     assert new is not None and new[1][1] - new[1][0] < 4
+    assert pl2.history and pl2.history[0]["gain"] >= 0.10
     pl2.applied(new)
     assert pl2.parts == new and not pl2.board.stats()  # fresh scores after a re-split
+    assert all(not x for x in pl2.samples)
+
+
+def test_planner_waits_for_evidence():
+    """Default thresholds: 8 samples per stage, a gain beyond 3x the stage times' relative standard
+    error, a cooldown after a re-split and at most 2 re-splits."""
+    parts = [(0, 4), (4, 8)]
+    pl = P.StagePlanner(parts)
+    for _ in range(7):  # stage 1 twice as slow, but only 7 samples
+        assert pl.observe([1.0, 2.0]) is None
+    assert pl.observe([1.0, 2.0]) is not None
+    # the same mean imbalance inside large noise: no re-split
+    noisy = P.StagePlanner(parts)
+    rng = np.random.default_rng(0)
+    for _ in range(12):
+        assert noisy.observe([float(rng.uniform(0.2, 3.0)), float(rng.uniform(0.2, 3.0)) * 1.3]) is None
+    assert noisy.last["needed"] > noisy.min_gain
+    # re-splits are capped, and each needs a cooldown after the previous one
+    cap = P.StagePlanner(parts, max_resplits=1)
+    for _ in range(8):
+        got = cap.observe([1.0, 2.0])
+    assert got is not None
+    cap.applied(got)
+    for _ in range(20):
+        assert cap.observe([1.0, 3.0]) is None
 
 
 def test_partition_dp_80_layers_8_stages_is_fast():
