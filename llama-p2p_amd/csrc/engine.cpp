@@ -217,14 +217,6 @@ struct mx_engine {
   // attention runs as attn_prefill_kernel, 16 queries per K/V pass
   bool rows_blocked = false;
   bool use_wide = getenv("MX_NO_WIDE") == nullptr;  // 17..64-row forward through mm_wide (LDS-shared activations)
-  // 17..64 rows: the q|k|v and gate/up wide GEMVs apply RMS_NORM on load (from f32 x and the per-16
-  // Σx² partials), and the split-K partials of attn_output / ffn_down are folded by a 256-work-group
-  // fold + Σx² launch instead of a row-wide fold + norm (MX_WIDE_NOL=1; measured slower with split-K
-  // producers: 3.585 vs 3.450 ms per 32-row 8B step, gpurun_out/r5ab1)
-  bool wide_nol = getenv("MX_WIDE_NOL") && atoi(getenv("MX_WIDE_NOL")) != 0;
-  // 17..64 rows: attn_output / ffn_down as one-tile groups with K split over 8 waves (mm_ks: x += in
-  // place, Σx² partials) instead of split-K slabs (MX_WIDE_KS=1)
-  bool wide_ks = getenv("MX_WIDE_KS") && atoi(getenv("MX_WIDE_KS")) != 0;
   float* slabs = nullptr;                           // split-K partials [8][MAX_ROWS][n_embd + 2 n_embd_kv]
   size_t slab_stride = 0;
   float* gslabs = nullptr;  // split-K partials of small-M prefill GEMMs, [S][M][N] (launch_gemm_split)
@@ -370,7 +362,7 @@ struct mx_engine {
   }
   int enqueue_forward_wide(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap,
                            int n_out, bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride,
-                           int* hist_count, int max_hist, hipStream_t s, bool nl);
+                           int* hist_count, int max_hist, hipStream_t s);
   int forward_rows_chunk(int n, const int32_t* slots, const int32_t* pos, const int32_t* ids, const void* x_in,
                          void* x_out, float* logits_host, hipStream_t s, bool last_row_only = false);
   void scheduler_loop();
@@ -1114,7 +1106,6 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
                                int* hist, int hist_stride, int* hist_count, int max_hist, hipStream_t s) {
   const int h = n_embd, kv = n_embd_kv, ff = n_ff;
   const bool wide = use_wide && M > 16;
-  const bool wnl = wide && wide_nol && !wq8 && !wkq && n_embd % 512 == 0;  // x's Σx² partials wanted
   // RMS_NORM applied on load by the consuming GEMV (M <= 16); the residual-stream writers
   // (embedding, attn_output, ffn_down, or ssq_kernel for a stage's x_in) leave per-tile partials
   const bool nol = !wide && !wq8 && !wkq && norm_on_load && mm_can_norm_on_load(M, h);
@@ -1127,9 +1118,9 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     if (launch_decode1(a, n_cu, s)) return fail(MX_ERR_HIP, "decode1 launch");
   } else if (x_in) {
     if (handoff_bf16) {  // bf16 hand-off from the previous stage: widen, with the Σx² partials on the way
-      launch_bf16_to_f32(x, (const uint16_t*)x_in, M, h, (nol || qql || wnl) ? ssq : nullptr, s);
+      launch_bf16_to_f32(x, (const uint16_t*)x_in, M, h, (nol || qql) ? ssq : nullptr, s);
     } else {
-      launch_f32_in(x, (const float*)x_in, M, h, (nol || qql || wnl) ? ssq : nullptr, s);
+      launch_f32_in(x, (const float*)x_in, M, h, (nol || qql) ? ssq : nullptr, s);
     }
   } else {
     if (!has_embed) return fail(MX_ERR_STATE, "this stage has no token embedding: x_in required");
@@ -1137,9 +1128,9 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
       if (launch_embed_kq(x, tok_embd_kq, embd_kq_type, ids, M, h, qql ? ssq : nullptr, s))
         return fail(MX_ERR_ARG, "K-quant embedding");
     } else if (embd_q8) {
-      launch_embed_q8(x, tok_embd8, ids, M, h, (nol || qql || wnl) ? ssq : nullptr, s);
+      launch_embed_q8(x, tok_embd8, ids, M, h, (nol || qql) ? ssq : nullptr, s);
     } else {
-      launch_embed(x, tok_embd, ids, M, h, (nol || qql || wnl) ? ssq : nullptr, s);
+      launch_embed(x, tok_embd, ids, M, h, (nol || qql) ? ssq : nullptr, s);
     }
   }
   if (wkq && !kq_ggml_prefill && M > MAX_ROWS && kqd_qkv && !argmax && !(head && n_out > MAX_ROWS))
@@ -1159,7 +1150,7 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
     return enqueue_forward_gemm(M, pos, slot, x_out, head, rowmap, n_out, s);
   }
   if (wide) return enqueue_forward_wide(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next,
-                                        pos_next, hist, hist_stride, hist_count, max_hist, s, wnl);
+                                        pos_next, hist, hist_stride, hist_count, max_hist, s);
   if (one && x_in) {  // a later pipeline stage: x (and its Σx² partials) already widened above
     D1Args a = d1;
     a.ids = ids; a.pos = pos; a.slot = slot; a.tok_embd = nullptr; a.x_in = x;
@@ -1242,36 +1233,22 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
 }
 
 // 17..64 rows: wide GEMVs (activations shared through LDS); attn_output and ffn_down run split-K
-// into slabs.  nl (default): the slabs are folded into x by launch_fold_ssq (256 work-groups for
-// 32 rows, x + per-16 Σx² partials) and q|k|v / gate/up apply RMS_NORM on load; otherwise the next
-// resid_norm folds them and writes the normalised bf16 rows (one work-group per row).
+// into slabs that the next resid_norm folds into the residual stream in a fixed order.
 int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap,
                                     int n_out, bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride,
-                                    int* hist_count, int max_hist, hipStream_t s, bool nl) {
+                                    int* hist_count, int max_hist, hipStream_t s) {
   const int h = n_embd, kv = n_embd_kv, ff = n_ff;
   int nslab = 0;  // partial slabs not yet folded into x
   dbg_count = 0;
-  // the operand of a normed GEMV: RMS_NORM on load from x (folding pending slabs first), or a
-  // fold + norm launch into xn
-  auto normed = [&](MMArgs& m, const float* w) -> int {
-    if (nl) {
-      if (nslab && launch_fold_ssq(x, slabs, nslab, slab_stride, ssq, M, h, s)) return -1;
-      m.X = nullptr; m.xf = x; m.norm_w = w; m.eps = eps; m.ssq = ssq; m.np = h / 16;
-    } else {
-      launch_resid_norm(xn, h, x, slabs, nslab, slab_stride, w, M, h, eps, s);
-      m.X = xn; m.ldx = h;
-    }
-    nslab = 0;
-    return 0;
-  };
   for (int li = 0; li < (int)layers.size(); li++) {
     const Layer& L = layers[li];
     _Float16* kc = kcache + layer_kv_stride * li;
     _Float16* vc = vcache + layer_kv_stride * li;
-    MMArgs a{};
-    a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M;
-    if (normed(a, L.attn_norm)) return fail(MX_ERR_ARG, "wide fold shape");
+    launch_resid_norm(xn, h, x, slabs, nslab, slab_stride, L.attn_norm, M, h, eps, s);
+    nslab = 0;
     if (dbg_hit(s)) return 0;
+    MMArgs a{};
+    a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M; a.X = xn; a.ldx = h;
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
     a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
     a.slot_stride = slot_stride;
@@ -1293,50 +1270,37 @@ int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void
     at.scale = 1.0f / sqrtf((float)head_dim);
     launch_attention(at, s);
     if (dbg_hit(s)) return 0;
-    // x += W . operand: in place (mm_ks, with the Σx² partials for RMS_NORM on load) or as split-K
-    // slabs that the next normed operand folds
-    auto resid = [&](MMArgs& m) -> int {
-      if (wide_ks) {
-        MMArgs k = m;
-        k.out = x; k.ldo = h; k.ssq = nl ? ssq : nullptr; k.np = h / 16;
-        if (launch_mm_ks(EPI_RESID, k, s) == 0) return nslab = 0;
-      }
-      return nslab = launch_mm_wide(EPI_RESID, m, slabs, slab_stride, s);
-    };
     MMArgs b{};
     b.W = L.o; b.N = h; b.K = h; b.X = attn_out; b.ldx = h; b.M = M;
-    if (resid(b) < 0) return fail(MX_ERR_ARG, "wide attn_output launch shape");
+    if ((nslab = launch_mm_wide(EPI_RESID, b, slabs, slab_stride, s)) < 0)
+      return fail(MX_ERR_ARG, "wide attn_output launch shape");
+    if (dbg_hit(s)) return 0;
+    launch_resid_norm(xn, h, x, slabs, nslab, slab_stride, L.ffn_norm, M, h, eps, s);
+    nslab = 0;
     if (dbg_hit(s)) return 0;
     MMArgs c{};
-    c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M;
-    if (normed(c, L.ffn_norm)) return fail(MX_ERR_ARG, "wide fold shape");
-    if (dbg_hit(s)) return 0;
-    c.act = act; c.lda = ff;
+    c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.X = xn; c.ldx = h; c.act = act; c.lda = ff;
     if (launch_mm_wide(EPI_SWIGLU, c, slabs, slab_stride, s) < 0) return fail(MX_ERR_ARG, "wide gate/up launch shape");
     if (dbg_hit(s)) return 0;
     MMArgs d{};
     d.W = L.down; d.N = h; d.K = ff; d.X = act; d.ldx = ff; d.M = M;
-    if (resid(d) < 0) return fail(MX_ERR_ARG, "wide ffn_down launch shape");
+    if ((nslab = launch_mm_wide(EPI_RESID, d, slabs, slab_stride, s)) < 0)
+      return fail(MX_ERR_ARG, "wide ffn_down launch shape");
     if (dbg_hit(s)) return 0;
   }
-  const bool head_fold = head && !nl && !rowmap && n_out == M;  // the head's norm folds the slabs itself
-  if (nslab && (x_out || (head && !head_fold))) {  // x itself is read next
-    if (nl) {
-      if (launch_fold_ssq(x, slabs, nslab, slab_stride, ssq, M, h, s)) return fail(MX_ERR_ARG, "wide fold shape");
-    } else {
-      launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);
-    }
+  if (x_out || (head && rowmap)) {
+    launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);
     nslab = 0;
   }
   if (x_out)
     if (int rc = copy_out(x_out, M, s)) return rc;
   if (head) {
     if (!has_head) return fail(MX_ERR_STATE, "this stage has no output head");
-    if (head_fold) {
+    if (rowmap || n_out != M) {
+      launch_rmsnorm(xn, h, x, out_norm, rowmap, n_out, h, eps, s);
+    } else {
       launch_resid_norm(xn, h, x, slabs, nslab, slab_stride, out_norm, M, h, eps, s);
       nslab = 0;
-    } else {
-      launch_rmsnorm(xn, h, x, out_norm, rowmap, n_out, h, eps, s);
     }
     MMArgs g{};
     g.W = output; g.N = n_vocab; g.K = h; g.M = n_out; g.X = xn; g.ldx = h; g.out = logits; g.ldo = n_vocab;
@@ -1346,11 +1310,7 @@ int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void
       pick(n_out, ids_next, pos_next, hist, hist_stride,
                     hist_count, max_hist, s);
   } else if (nslab) {
-    if (nl) {
-      if (launch_fold_ssq(x, slabs, nslab, slab_stride, ssq, M, h, s)) return fail(MX_ERR_ARG, "wide fold shape");
-    } else {
-      launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);
-    }
+    launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);
   }
   HIPC(hipGetLastError());
   return 0;
@@ -2911,27 +2871,11 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
         per = (size_t)2 * ff * h * 2;
         return (e->use_pers && mm_pers_supported(EPI_SWIGLU, M, a.N, a.K)) ? launch_mm_pers(EPI_SWIGLU, a, s)
                                                                             : launch_mm(EPI_SWIGLU, a, s);
-      case 11: case 12: {  // 17..64 rows: q|k|v (11) / gate/up (12) with RMS_NORM on load (wide NL)
-        a.X = nullptr; a.xf = e->x; a.eps = e->eps; a.ssq = e->ssq; a.np = h / 16; a.K = h;
-        if (kind == 11) {
-          a.W = L.qkv; a.N = h + 2 * kv; a.norm_w = L.attn_norm;
-          per = (size_t)(h + 2 * kv) * h * 2;
-          return launch_mm_wide(EPI_QKV, a, e->slabs, e->slab_stride, s) < 0;
-        }
-        a.W = L.gu; a.N = 2 * ff; a.norm_w = L.ffn_norm; a.act = e->act; a.lda = ff;
-        per = (size_t)2 * ff * h * 2;
-        return launch_mm_wide(EPI_SWIGLU, a, e->slabs, e->slab_stride, s) < 0;
-      }
-      case 15: case 16: {  // 17..64 rows: attn_output (15) / ffn_down (16) as one-tile K-split groups (mm_ks)
-        a.W = kind == 15 ? L.o : L.down; a.N = h; a.K = kind == 15 ? h : ff; a.out = e->x; a.ldo = h;
-        a.X = kind == 15 ? e->attn_out : e->act; a.ldx = a.K; a.ssq = e->ssq; a.np = h / 16;
-        per = (size_t)h * a.K * 2;
-        return launch_mm_ks(EPI_RESID, a, s);
-      }
-      case 13: case 14: {  // fold 4 (13) / 8 (14) split-K slabs into x + Σx² partials (wide NL)
-        const int ns = kind == 13 ? 4 : 8;
-        per = (size_t)M * h * 4 * (2 + ns);
-        return launch_fold_ssq(e->x, e->slabs, ns, e->slab_stride, e->ssq, M, h, s);
+      case 8: case 9: case 10: {  // RMS_NORM of M rows folding 4 (8) / 8 (9) / 0 (10) split-K slabs
+        const int ns = kind == 8 ? 4 : kind == 9 ? 8 : 0;
+        per = (size_t)M * h * 4 * (2 + ns) + (size_t)M * h * 2;
+        launch_resid_norm(e->xn, h, e->x, e->slabs, ns, e->slab_stride, L.ffn_norm, M, h, e->eps, s);
+        return 0;
       }
       case 8: case 9: case 10: {  // RMS_NORM of M rows folding 4 (8) / 8 (9) / 0 (10) split-K slabs
         const int ns = kind == 8 ? 4 : kind == 9 ? 8 : 0;

@@ -175,17 +175,11 @@ int launch_mm_pers(int epi, const MMArgs& a, hipStream_t s);
 // 17..64 rows: activation chunks shared through LDS.  EPI_QKV / EPI_RESID run split-K into
 // `slabs` ([ksplit][MAX_ROWS][N] floats, slab_stride apart); returns the split used (the caller
 // folds RESID partials with launch_resid_norm; QKV partials are finished inside), or -1.
-// 17..64 rows, K split over the 8 waves of a one-tile work-group (EPI_RESID: x += in place, the
-// Σx² partials when a.ssq is set; EPI_F32).  0 or -1 (shape / epilogue not instantiated).
-int launch_mm_ks(int epi, const MMArgs& a, hipStream_t s);
 int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s,
                    bool qkv_finish = true);  // EPI_QKV: false leaves the slabs to the attention kernel
 // x[c] += sum of nslab partial slabs (fixed order); then, if y, y = bf16(rmsnorm(x) * w)
 void launch_resid_norm(uint16_t* y, int ldy, float* x, const float* slabs, int nslab, size_t slab_stride,
-                       const float* w, int M, int n, float eps, hipStream_t s);
-// 17..64 rows with RMS_NORM on load: x[r] += nslab split-K slabs (0, 1, 2, 4, 8; fixed order) and
-// ssq[r][n/16] = per-16-element Σx² of the new rows; n a multiple of 512.  0 or -1 (shape).
-int launch_fold_ssq(float* x, const float* slabs, int nslab, size_t stride, float* ssq, int M, int n, hipStream_t s);  // X == nullptr path (RMS_NORM fused into the GEMV) is legal
+                       const float* w, int M, int n, float eps, hipStream_t s);  // X == nullptr path (RMS_NORM fused into the GEMV) is legal
 void launch_attention(const AttnArgs& a, hipStream_t s);
 // rows in blocks of 16 consecutive positions of one sequence each (prefill chunks): one
 // work-group per (kv head, block), the 16 queries share every K/V chunk

@@ -757,123 +757,6 @@ int launch_mm(int epi, const MMArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// 17..64 rows, one 16-row tile per work-group and K split over its W waves (no split-K slabs):
-// every wave streams its K-slice's weight tiles AND the matching B fragments (NB column tiles of
-// the activations, from L2) through ONE ring U k-tiles deep.  (mm_body issues its B loads right
-// before their MFMAs: with two or more column tiles that waits an L2 round trip per k-tile.)  The
-// W partial tiles meet in LDS and are summed in wave order; the epilogue is mm_body's, so
-// EPI_RESID adds into x in place and writes the per-16 Σx² partials when a.ssq is set -- the
-// 17..64-row attn_output / ffn_down without slabs or a fold launch.
-// ---------------------------------------------------------------------------
-template <int W, int NB, int EPI, int U>
-__global__ __launch_bounds__(64 * W) void mm_ks_kernel(MMArgs a) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int tile = blockIdx.x;
-  const int KT = a.K / TILE_K;
-  const int kb = KT * w / W, ke = KT * (w + 1) / W;
-  const u32x4* Wp = reinterpret_cast<const u32x4*>(a.W) + (size_t)tile * KT * 64 + lane;
-  const u32x4* Xp[NB];
-#pragma unroll
-  for (int n = 0; n < NB; ++n) {
-    const int col = min(n * 16 + (lane & 15), a.M - 1);  // padded columns re-read a valid row
-    Xp[n] = reinterpret_cast<const u32x4*>(a.X + (size_t)col * a.ldx + (lane >> 4) * 8);
-  }
-  f32x4 acc[NB];
-#pragma unroll
-  for (int n = 0; n < NB; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  u32x4 ra[U], rb[U][NB];
-  auto issue = [&](int u, int kt) {
-    ra[u] = __builtin_nontemporal_load(Wp + (size_t)kt * 64);
-#pragma unroll
-    for (int n = 0; n < NB; ++n) rb[u][n] = Xp[n][kt * 4];
-  };
-  auto mma = [&](int u) {
-#pragma unroll
-    for (int n = 0; n < NB; ++n)
-      acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ra[u]),
-                                                       __builtin_bit_cast(bf16x8, rb[u][n]), acc[n], 0, 0, 0);
-  };
-  int kt = kb;
-  const int nfull = (ke - kb) / U;
-  if (nfull > 0) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) issue(u, kt + u);
-    for (int ch = 1; ch < nfull; ++ch) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        mma(u);
-        issue(u, kt + U + u);
-      }
-      kt += U;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) mma(u);
-    kt += U;
-  }
-  for (; kt < ke; ++kt) {  // the K-slice's remainder (< U tiles), one at a time
-    issue(0, kt);
-    mma(0);
-  }
-
-  __shared__ f32x4 red[W][NB][64];
-#pragma unroll
-  for (int n = 0; n < NB; ++n) red[w][n][lane] = acc[n];
-  __syncthreads();
-  // epilogue: unit = (n, l): rows 16*tile + 4*(l>>4) + i, column n*16 + (l&15); a unit block of 64
-  // (one n) is one wave, so the Σx² shuffles of EPI_RESID stay inside it
-  constexpr int LU = (EPI == EPI_SWIGLU) ? 32 : 64;
-  static_assert(NB * LU <= 64 * W, "one unit per thread");
-  const int u = threadIdx.x;
-  if (u >= NB * LU) return;
-  const int l = u % LU, n = u / LU;
-  const int col = n * 16 + (l & 15);
-  f32x4 sv = red[0][n][l];
-#pragma unroll
-  for (int ww = 1; ww < W; ++ww) sv += red[ww][n][l];
-  if constexpr (EPI == EPI_RESID) {
-    double q = 0.0;
-    if (col < a.M) {
-      f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + tile * 16 + (l >> 4) * 4);
-      const f32x4 xv = *px + sv;
-      *px = xv;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) q += (double)(xv[i] * xv[i]);
-    }
-    if (a.ssq) {
-      q += __shfl_xor(q, 16);
-      q += __shfl_xor(q, 32);
-      if (l < 16 && col < a.M) a.ssq[(size_t)col * a.np + tile] = (float)q;
-    }
-    return;
-  }
-  if (col >= a.M) return;
-  f32x4 up = sv;
-  if constexpr (EPI == EPI_SWIGLU) {
-    up = red[0][n][l + 32];
-#pragma unroll
-    for (int ww = 1; ww < W; ++ww) up += red[ww][n][l + 32];
-  }
-  epi_store<EPI>(a, tile, l, col, sv, up);
-}
-
-int launch_mm_ks(int epi, const MMArgs& a, hipStream_t s) {
-  if (a.M < 1 || a.M > MAX_ROWS || a.K % TILE_K || a.N % TILE_N || !a.X) return -1;
-  const int ntiles = a.N / TILE_N, nb = (a.M + 15) / 16;
-  if (nb <= 2) {
-    switch (epi) {
-      case EPI_RESID: mm_ks_kernel<8, 2, EPI_RESID, 8><<<ntiles, 512, 0, s>>>(a); return 0;
-      case EPI_F32: mm_ks_kernel<8, 2, EPI_F32, 8><<<ntiles, 512, 0, s>>>(a); return 0;
-    }
-  } else {
-    switch (epi) {
-      case EPI_RESID: mm_ks_kernel<8, 4, EPI_RESID, 4><<<ntiles, 512, 0, s>>>(a); return 0;
-      case EPI_F32: mm_ks_kernel<8, 4, EPI_F32, 4><<<ntiles, 512, 0, s>>>(a); return 0;
-    }
-  }
-  return -1;
-}
-
-// ---------------------------------------------------------------------------
 // Wide GEMV for 17..64 token rows (32-sequence decode, prefill chunks).
 //
 // At 32 tokens the activation fragment per K-tile (16 tokens x 64 B per column
@@ -887,7 +770,7 @@ int launch_mm_ks(int epi, const MMArgs& a, hipStream_t s) {
 // sums go to slabs [ksplit][token][N] that resid_norm / qkv_finish add in a
 // fixed order, so results stay bit-reproducible.
 // ---------------------------------------------------------------------------
-template <int W, int RTW, int NB, int EPI, bool NL = false>
+template <int W, int RTW, int NB, int EPI>
 __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
   constexpr int KCT = 4;             // K-tiles per staged activation chunk
   constexpr int KC = KCT * TILE_K;   // 128 k
@@ -912,12 +795,7 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
   for (int r = 0; r < RTW; ++r) Wp[r] = reinterpret_cast<const u32x4*>(a.W) + (size_t)(tile0 + r) * KT * 64 + lane;
 
   // activation chunk staging: piece p -> (row, 16-B segment); rows >= M re-read row M-1 (outputs dropped)
-  // NL (RMS_NORM on load, 17..64 rows): a piece is 8 f32 of the residual stream x, turned into
-  // bf16((x * scale_row) * w) at the LDS store -- ggml's RMS_NORM + MUL feeding MUL_MAT -- with the
-  // row scales from the producers' per-16-element Σx² partials and w of this K range in LDS
-  constexpr int XV = NL ? 2 : 1;  // 16-B registers per piece
-  typedef std::conditional_t<NL, f32x4, u32x4> XT;
-  const XT* xsrc[PPT];
+  const u32x4* xsrc[PPT];
   int xrow[PPT], xseg[PPT];
 #pragma unroll
   for (int i = 0; i < PPT; ++i) {
@@ -925,41 +803,20 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
     xrow[i] = p / SEGS;
     xseg[i] = p % SEGS;
     const int rr = xrow[i] < a.M ? xrow[i] : a.M - 1;
-    if constexpr (NL)
-      xsrc[i] = reinterpret_cast<const XT*>(a.xf + (size_t)rr * a.K + (size_t)kb * TILE_K + xseg[i] * 8);
-    else
-      xsrc[i] = reinterpret_cast<const XT*>(a.X + (size_t)rr * a.ldx + (size_t)kb * TILE_K + xseg[i] * 8);
+    xsrc[i] = reinterpret_cast<const u32x4*>(a.X + (size_t)rr * a.ldx + (size_t)kb * TILE_K + xseg[i] * 8);
   }
   // activation chunks are loaded TWO chunks ahead into alternating register sets: the wait for
   // chunk c+1's pieces (before its LDS store) then retires only loads issued before the weight
   // refills of chunk c+1, so 2 chunks of weight loads stay in flight across every barrier (one
   // chunk ahead, the wait drained the ring down to the current chunk's refills)
-  XT xr[2][PPT][XV];
+  u32x4 xr[2][PPT];
   auto load_x = [&](int set, int c) {
 #pragma unroll
-    for (int i = 0; i < PPT; ++i)
-#pragma unroll
-      for (int v = 0; v < XV; ++v) xr[set][i][v] = xsrc[i][c * (KC / 8) * XV + v];
+    for (int i = 0; i < PPT; ++i) xr[set][i] = xsrc[i][c * (KC / 8)];
   };
-  extern __shared__ __attribute__((aligned(16))) float nl_dyn[];  // NL: [ROWS] scales, then w[K range]
-  auto store_x = [&](int set, int buf, int c) {
+  auto store_x = [&](int set, int buf) {
 #pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      if constexpr (NL) {
-        const float sc = nl_dyn[xrow[i]];
-        const float* wk = nl_dyn + ROWS + c * KC + xseg[i] * 8;
-        const f32x4 w0 = *reinterpret_cast<const f32x4*>(wk), w1 = *reinterpret_cast<const f32x4*>(wk + 4);
-        const f32x4 x0 = xr[set][i][0], x1 = xr[set][i][1];
-        u32x4 o;
-        o[0] = f2bf((x0[0] * sc) * w0[0]) | (f2bf((x0[1] * sc) * w0[1]) << 16);
-        o[1] = f2bf((x0[2] * sc) * w0[2]) | (f2bf((x0[3] * sc) * w0[3]) << 16);
-        o[2] = f2bf((x1[0] * sc) * w1[0]) | (f2bf((x1[1] * sc) * w1[1]) << 16);
-        o[3] = f2bf((x1[2] * sc) * w1[2]) | (f2bf((x1[3] * sc) * w1[3]) << 16);
-        *reinterpret_cast<u32x4*>(&xs[buf][xrow[i]][xseg[i] * 8]) = o;
-      } else {
-        *reinterpret_cast<u32x4*>(&xs[buf][xrow[i]][xseg[i] * 8]) = xr[set][i][0];
-      }
-    }
+    for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(&xs[buf][xrow[i]][xseg[i] * 8]) = xr[set][i];
   };
 
   f32x4 acc[RTW][NB];
@@ -982,35 +839,7 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
       for (int r = 0; r < RTW; ++r)
         ra[KCT + u][r] = __builtin_nontemporal_load(Wp[r] + (size_t)(kb + KCT + u) * 64);
   }
-  if constexpr (NL) {
-    // row scales (behind the weight ring): 8 lanes per row, each a fixed-order double sum of its
-    // share of the row's np partials (clamped loads, masked adds: no load behind a branch), then a
-    // fixed xor tree; and w of this K range into LDS
-    constexpr int RPP = NT / 8;
-    const int sub = threadIdx.x & 7;
-    for (int r0 = 0; r0 < ROWS; r0 += RPP) {
-      const int r = r0 + (int)(threadIdx.x >> 3);
-      const int rr = min(min(r, ROWS - 1), a.M - 1);
-      const f32x4* sp = reinterpret_cast<const f32x4*>(a.ssq + (size_t)rr * a.np) + sub;
-      const int nq = a.np / 32;  // f32x4 per lane (np = K/16 <= 512)
-      f32x4 q[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) q[j] = sp[min(j, nq - 1) * 8];
-      double acc = 0.0;
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (j < nq) acc += ((double)q[j][0] + (double)q[j][1]) + ((double)q[j][2] + (double)q[j][3]);
-      acc += __shfl_xor(acc, 1);
-      acc += __shfl_xor(acc, 2);
-      acc += __shfl_xor(acc, 4);
-      if (sub == 0 && r < ROWS) nl_dyn[r] = 1.0f / sqrtf((float)(acc / a.K) + a.eps);
-    }
-    const int k0 = kb * TILE_K, nk = (ke - kb) * TILE_K;
-    for (int i = threadIdx.x * 4; i < nk; i += NT * 4)
-      *reinterpret_cast<f32x4*>(nl_dyn + ROWS + i) = *reinterpret_cast<const f32x4*>(a.norm_w + k0 + i);
-    __syncthreads();
-  }
-  store_x(0, 0, 0);
+  store_x(0, 0);
   __syncthreads();
 
   // one chunk: H = ring half = c & 1 (compile time), REFILL = load the chunk two ahead into that
@@ -1038,7 +867,7 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
           ra[H * KCT + kk][r] = __builtin_nontemporal_load(Wp[r] + (size_t)(kb + (c + 2) * KCT + kk) * 64);
       }
     }
-    store_x(1 - H, buf ^ 1, c + 1 < nch ? c + 1 : nch - 1);
+    store_x(1 - H, buf ^ 1);
     __syncthreads();
   };
   using I0 = std::integral_constant<int, 0>;
@@ -1118,43 +947,6 @@ void launch_resid_norm(uint16_t* y, int ldy, float* x, const float* slabs, int n
   launch_norm_impl(y, ldy, x, slabs, nslab, stride, w, nullptr, M, n, eps, s);
 }
 
-// x[r] += the NS split-K partial slabs (fixed order), written back, and the per-16-element Σx²
-// partials of the new row for the RMS_NORM-on-load consumers: the 17..64-row fold without the norm.
-// One work-group per (row, 512 columns): 8 per Llama-3-8B row, 256 for 32 rows (the row-wide norm
-// it replaces ran on M work-groups); 4 lanes per 16 elements, their double sums combined as the
-// EPI_RESID epilogue does ((q0 + q1) + (q2 + q3)).
-template <int NS>
-__global__ __launch_bounds__(128) void fold_ssq_kernel(float* x, const float* slabs, size_t stride, float* ssq, int n) {
-  const int r = blockIdx.x;
-  const int i = (blockIdx.y * 128 + threadIdx.x) * 4;
-  f32x4* px = reinterpret_cast<f32x4*>(x + (size_t)r * n + i);
-  f32x4 v = *px, sl[NS > 0 ? NS : 1];
-#pragma unroll
-  for (int k = 0; k < NS; ++k) sl[k] = *reinterpret_cast<const f32x4*>(slabs + k * stride + (size_t)r * n + i);
-#pragma unroll
-  for (int k = 0; k < NS; ++k) v += sl[k];
-  if constexpr (NS > 0) *px = v;
-  double q = 0.0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) q += (double)(v[j] * v[j]);
-  q += __shfl_xor(q, 1);
-  q += __shfl_xor(q, 2);
-  if ((threadIdx.x & 3) == 0) ssq[(size_t)r * (n / 16) + i / 16] = (float)q;
-}
-
-int launch_fold_ssq(float* x, const float* slabs, int nslab, size_t stride, float* ssq, int M, int n, hipStream_t s) {
-  if (n % 512) return -1;
-  const dim3 grid(M, n / 512);
-  switch (nslab) {
-    case 0: fold_ssq_kernel<0><<<grid, 128, 0, s>>>(x, slabs, stride, ssq, n); return 0;
-    case 1: fold_ssq_kernel<1><<<grid, 128, 0, s>>>(x, slabs, stride, ssq, n); return 0;
-    case 2: fold_ssq_kernel<2><<<grid, 128, 0, s>>>(x, slabs, stride, ssq, n); return 0;
-    case 4: fold_ssq_kernel<4><<<grid, 128, 0, s>>>(x, slabs, stride, ssq, n); return 0;
-    case 8: fold_ssq_kernel<8><<<grid, 128, 0, s>>>(x, slabs, stride, ssq, n); return 0;
-  }
-  return -1;
-}
-
 template <int W, int RTW, int EPI>
 static int launch_wide_cfg(const MMArgs& a, int ksplit, hipStream_t s) {
   const int ntiles = a.N / TILE_N;
@@ -1162,18 +954,6 @@ static int launch_wide_cfg(const MMArgs& a, int ksplit, hipStream_t s) {
   if (ntiles % (W * RTW) || KT % (ksplit * 4)) return -1;
   dim3 grid(ntiles / (W * RTW), ksplit);
   const int nb = (a.M + 15) / 16;
-  if (a.X == nullptr) {  // RMS_NORM on load: [rows] scales + w of one K range in dynamic LDS
-    if constexpr (EPI == EPI_QKV || EPI == EPI_SWIGLU || EPI == EPI_SLAB) {
-      if (!a.xf || !a.norm_w || !a.ssq || a.np * 16 != a.K || a.np % 32 || a.np > 512) return -1;
-      const size_t lds = (size_t)(64 + a.K / ksplit) * 4;
-      if (nb <= 2)
-        mm_wide_kernel<W, RTW, 2, EPI, true><<<grid, 64 * W, lds, s>>>(a);
-      else
-        mm_wide_kernel<W, RTW, 4, EPI, true><<<grid, 64 * W, lds, s>>>(a);
-      return 0;
-    }
-    return -1;
-  }
   if (nb <= 2)
     mm_wide_kernel<W, RTW, 2, EPI><<<grid, 64 * W, 0, s>>>(a);
   else
@@ -1191,8 +971,7 @@ static int pick_ksplit(int KT, int target) {
 // Geometry from tools/gemv_sweep.hip (wide) on MI355X, Llama-3-8B shapes at 32 rows
 // (profiles/round1_gemv_sweep_wide.txt): two row tiles per wave, K split until ~256 work-groups.
 int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s, bool qkv_finish) {
-  if (a.M < 1 || a.M > MAX_ROWS || a.K % TILE_K != 0 || a.N % TILE_N != 0 || (!a.X && !a.xf)) return -1;
-  if (!a.X && epi != EPI_QKV && epi != EPI_SWIGLU) return -1;  // RMS_NORM on load: the normed GEMVs only
+  if (a.M < 1 || a.M > MAX_ROWS || a.K % TILE_K != 0 || a.N % TILE_N != 0 || !a.X) return -1;
   const int ntiles = a.N / TILE_N, KT = a.K / TILE_K;
   if (KT % 4) return -1;
   // work-groups per launch are sized to the 256 CUs (tools/gemv_sweep.hip "odd" sweep,

@@ -4,7 +4,7 @@
     python tools/step_probe.py [--M 32] [--pos 200] [--iters 20]
 
 kinds: 0 q|k|v, 1 attn_output, 2 gate/up, 3 ffn_down, 4 lm_head, 7 attention, 8/9/10 RMS_NORM folding
-4/8/0 split-K slabs, 11/12 q|k|v / gate/up with RMS_NORM on load, 13/14 fold of 4/8 slabs + Σx² partials.  Environment switches of the engine (MX_NO_WIDE, ...) apply.
+4/8/0 split-K slabs.  Environment switches of the engine (MX_NO_WIDE, ...) apply.
 """
 import argparse
 import json
@@ -21,15 +21,14 @@ def main():
     ap.add_argument("--pos", type=int, default=200)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--model", default="llama3-8b")
-    ap.add_argument("--kinds", default="0,7,1,8,2,3,9,10,4,11,12,13,14,15,16")
+    ap.add_argument("--kinds", default="0,7,1,8,2,3,9,10,4")
     args = ap.parse_args()
     os.environ["MX_PROF_POS"] = str(args.pos)
     from llama_p2p_amd.engine import Engine
 
     eng = Engine(f"synthetic:{args.model}:seed=0", n_ctx=512, n_seq_max=64, device=0)
     names = {0: "qkv", 1: "attn_output", 2: "gate_up", 3: "ffn_down", 4: "lm_head", 7: "attention",
-             8: "fold4_norm", 9: "fold8_norm", 10: "norm", 11: "qkv_nl", 12: "gate_up_nl", 13: "fold4_ssq",
-             14: "fold8_ssq", 15: "attn_output_ks", 16: "ffn_down_ks"}
+             8: "fold4_norm", 9: "fold8_norm", 10: "norm"}
     out = {"M": args.M, "pos": args.pos, "env": {k: v for k, v in os.environ.items() if k.startswith("MX_")}}
     for k in [int(v) for v in args.kinds.split(",")]:
         us, nb = eng.profile_kernel(k, args.M, args.iters)
