@@ -199,13 +199,6 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us_per_l
 
 int mx_sync(mx_engine* e);
 
-/* Diagnosis of the persistent one-token decode (engine created with env MX_D1_TRACE=1): per work-group
- * (n_groups = CUs) a row of `stride` words: for every layer, 5 ops x [compute start, arrival] stamps of
- * s_memrealtime (100 MHz) from the last launch, then kernel start / end, loader idle and landing-wait
- * ticks, loader end and the consumers' ring-wait ticks, then (attention work-groups) the attention
- * body's 8 stamps per consumer wave of the last layer.  Not a reference API. */
-int mx_decode1_trace(mx_engine* e, uint64_t* out, size_t cap, int* n_groups, int* stride);
-
 /* HBM streaming probes on `device` (no engine): the best of a sweep of 16-byte-per-lane streaming
  * kernels (loads in flight per lane x grid x non-temporal) over `bytes`-sized buffers, `iters`
  * passes each timed with HIP events.  copy: *gbs = (read + write) bytes / s; read: bytes read / s.

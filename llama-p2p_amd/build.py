@@ -17,7 +17,7 @@ LIB = os.path.join(HERE, "libmxllama.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MX_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = [("kernels.hip", "hip"), ("kquant.hip", "hip"), ("decode1.hip", "hip"), ("engine.cpp", "hip"), ("gguf.cpp", "c++")]
+SOURCES = [("kernels.hip", "hip"), ("kquant.hip", "hip"), ("engine.cpp", "hip"), ("gguf.cpp", "c++")]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-Wno-unused-variable", "-Wno-unused-result", "-Wno-unused-value"]
 

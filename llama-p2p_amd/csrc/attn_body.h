@@ -1,6 +1,6 @@
-// attn_body.h -- the decode attention body (one kv head x one row), shared by the standalone
-// attention kernel (kernels.hip: attn_decode_kernel) and the persistent one-token decode engine
-// (decode1.hip), which runs it on 3 of its 4 waves with its own barrier and cross-CU hand-offs.
+// attn_body.h -- the decode attention body (one kv head x one row) of attn_decode_kernel (kernels.hip).
+// (Round 4's persistent one-token decode ran it on 3 waves of its own work-groups; that engine was
+// measured slower than the per-op kernels and is archived under tools/archive/.)
 #pragma once
 #include "device_common.h"
 
@@ -15,28 +15,13 @@ constexpr float LOG2E = 1.4426950408889634f;
 // chunk holding `pos` (FIN) or the partial last chunk needs sits behind a wave-uniform branch, so
 // the full chunks run the bare MFMA + softmax stream.
 constexpr int ATTN_FIN_MAXSLAB = 8;  // split-K slabs the FIN path can sum (the wide launchers split K at most 8 ways)
-constexpr int ATTN_MEGA_MAXSLAB = 4;  // ... and the persistent decode's q|k|v (decode1.hip caps its split at 4)
 
-struct BlockSync {
-  __device__ void operator()() const { __syncthreads(); }
-};
-struct NoHook {
-  __device__ void operator()() const {}
-  __device__ bool dead(int) const { return false; }
-};
-
-// MEGA (decode1.hip): the NW waves are waves 1..NW of a larger work-group (tid = threadIdx.x - 64),
-// `sync` is their own barrier, the q/k/v slabs come from other CUs of the same launch (sc1 loads:
-// past this CU's L1) and the output goes to them too (bf16 pairs, sc1 stores).
-// `pre` runs after the wave's first K/V chunk is issued and before q/k/v are read; MEGA polls the
-// q|k|v granules of the other CUs until their tags match and asks pre.dead(spins) whether to give up.
-template <int D, int G, int NW, bool FIN, bool MEGA = false, class Sync = BlockSync, class Pre = NoHook>
-__device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int c, int tid = 0, Sync sync = Sync(),
-                                                 Pre pre = Pre()) {
+template <int D, int G, int NW, bool FIN>
+__device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int c) {
   constexpr int CH = ATTN_CHUNK;
   constexpr int QK = D / 32;  // k-steps of QK^T
   constexpr int DT = D / 16;  // d tiles of P.V
-  const int t_ = MEGA ? tid : (int)threadIdx.x;
+  const int t_ = threadIdx.x;
   const int lane = t_ & 63, w = __builtin_amdgcn_readfirstlane(t_ >> 6);
   const int r16 = lane & 15, q4 = lane >> 4;
   unsigned long long* tr = a.trace ? a.trace + (((size_t)c * a.n_head_kv + kvh) * NW + w) * 8 : nullptr;
@@ -74,7 +59,6 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
   // holding it is patched from LDS in compute(), so a stale read of that position is harmless.
   KV A;
   if (w * CH < ctx) load(A, w);
-  pre();
 
   // wide path: q/k/v of this (kv head, token) are still split-K partial slabs -- sum them in slab
   // order (bit-identical to qkv_finish_kernel), RoPE q and k, write this position's K and V into
@@ -82,35 +66,17 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
   constexpr bool fin = FIN;
   if constexpr (FIN) {
     const int nq = a.n_head * D, nkv = a.n_head_kv * D, N = nq + 2 * nkv;
-    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<unsigned long long*>(a.gslab), (short)0, (int)((size_t)a.nslab * a.slab_stride * 8), 0x00020000);
     for (int u = t_; u < (G * D + 2 * D) / 4; u += 64 * NW) {
       const int i = u * 4;  // qs index
       const int row = i < G * D ? kvh * G * D + i : i < G * D + D ? nq + kvh * D + (i - G * D)
                                                                    : nq + nkv + kvh * D + (i - G * D - D);
       // all slab and RoPE loads issued together (clamped: extra reads repeat the last slab): a run-time
       // slab loop or a load behind the RoPE branch made each load wait for itself
-      constexpr int MS = MEGA ? ATTN_MEGA_MAXSLAB : ATTN_FIN_MAXSLAB;
+      constexpr int MS = ATTN_FIN_MAXSLAB;
       f32x4 sv[MS];
-      if constexpr (MEGA) {  // 4 granules per slab (two 16-byte sc1 loads), until every tag is this op's
-        for (int spin = 0;; ++spin) {
-          bool ok = true;
 #pragma unroll
-          for (int k = 0; k < MS; ++k) {
-            const unsigned off = (unsigned)((min(k, a.nslab - 1) * a.slab_stride + (size_t)c * N + row) * 8);
-            const u32x4 g0 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srs, off, 0, 16));
-            const u32x4 g1 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srs, off + 16, 0, 16));
-            sv[k] = f32x4{__uint_as_float(g0[0]), __uint_as_float(g0[2]), __uint_as_float(g1[0]), __uint_as_float(g1[2])};
-            ok &= g0[1] == a.gtag_in && g0[3] == a.gtag_in && g1[1] == a.gtag_in && g1[3] == a.gtag_in;
-          }
-          if (ok || pre.dead(spin)) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < MS; ++k)
-          sv[k] = *reinterpret_cast<const f32x4*>(a.slabs + min(k, a.nslab - 1) * a.slab_stride + (size_t)c * N + row);
-      }
+      for (int k = 0; k < MS; ++k)
+        sv[k] = *reinterpret_cast<const f32x4*>(a.slabs + min(k, a.nslab - 1) * a.slab_stride + (size_t)c * N + row);
       const int dd = i % D;
       const f32x4 csv =
           *reinterpret_cast<const f32x4*>(a.rope_cs + ((size_t)max(0, min(pos, a.n_ctx - 1)) * (D / 2) + dd / 2) * 2);
@@ -139,7 +105,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
         }
       }
     }
-    sync();
+    __syncthreads();
   }
 
   // A operand of QK^T: rows = heads of the group (rows >= G are zero)
@@ -257,28 +223,8 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
       }
     }
   }
-  sync();
+  __syncthreads();
   stamp(4);  // partials in LDS
-  if constexpr (MEGA) {  // bf16 pairs, write-through (sc1) for the consuming CUs
-    for (int idx = t_; idx < G * D / 2; idx += 64 * NW) {
-      const int h = (2 * idx) / D, d = (2 * idx) % D;
-      float M = -INFINITY;
-#pragma unroll
-      for (int ww = 0; ww < NW; ++ww) M = fmaxf(M, Mm[ww][h]);
-      float L = 0.f, acc0 = 0.f, acc1 = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < NW; ++ww) {
-        const float f = (Mm[ww][h] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(Mm[ww][h] - M);
-        L += f * Ll[ww][h];
-        acc0 += f * Om[ww][h][d];
-        acc1 += f * Om[ww][h][d + 1];
-      }
-      const unsigned pr = f2bf(acc0 / L) | (f2bf(acc1 / L) << 16);
-      __hip_atomic_store(a.gout + ((kvh * G + h) * D + d) / 2, ((unsigned long long)a.gtag_out << 32) | pr,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return;
-  }
   for (int idx = t_; idx < G * D; idx += 64 * NW) {
     const int h = idx / D, d = idx % D;
     float M = -INFINITY;

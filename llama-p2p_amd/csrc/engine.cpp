@@ -203,13 +203,6 @@ struct mx_engine {
   // row count) instead of bf16 GEMMs over dequantised weights; see enqueue_forward
   bool kq_ggml_prefill = getenv("MX_KQ_GGML_PREFILL") != nullptr;
   float* ssq = nullptr;  // [MAX_ROWS][n_embd/16] per-tile sums of squares of x
-  // one-token steps of bf16 models as ONE persistent launch (decode1.hip); MX_NO_DECODE1=1 for A/B.
-  // One engine per device holds it (two persistent launches on one GPU could not both be resident).
-  bool use_d1 = false;
-  D1Args d1{};
-  int n_cu = 0;
-  int setup_decode1();
-  int d1_check(hipStream_t s);
   // rows of the next forward belong to distinct sequences (decode): no row attends to another row's
   // new K/V, so the wide path lets the attention kernel finish q/k/v from the split-K slabs
   bool rows_distinct = false;
@@ -375,25 +368,6 @@ struct mx_engine {
   void finish(Request* r, int why);
 };
 
-// decode1 (persistent one-token launch): at most one engine per device uses it
-static std::mutex g_d1_mu;
-static std::map<int, const mx_engine*> g_d1_owner;
-static bool d1_claim(const mx_engine* e, int dev) {
-  std::lock_guard<std::mutex> lk(g_d1_mu);
-  auto it = g_d1_owner.find(dev);
-  if (it != g_d1_owner.end() && it->second != e) return false;
-  g_d1_owner[dev] = e;
-  return true;
-}
-static void d1_release(const mx_engine* e) {
-  std::lock_guard<std::mutex> lk(g_d1_mu);
-  for (auto it = g_d1_owner.begin(); it != g_d1_owner.end(); ++it)
-    if (it->second == e) {
-      g_d1_owner.erase(it);
-      return;
-    }
-}
-
 mx_engine::~mx_engine() {
   {
     std::lock_guard<std::mutex> lk(mu);
@@ -403,7 +377,6 @@ mx_engine::~mx_engine() {
   if (worker.joinable()) worker.join();
   for (auto& kv : sched_graphs) hipGraphExecDestroy(kv.second);
   if (stream) hipStreamSynchronize(stream);
-  d1_release(this);
 
   for (void* p : allocations) hipFree(p);
   if (h_idx) hipHostFree(h_idx);
@@ -1010,97 +983,6 @@ out:
 }
 
 // One forward of M <= MAX_ROWS rows through this stage's layers.
-// The persistent one-token launch (decode1.hip) for bf16 models whose shapes it covers: hand-off
-// buffers, the per-layer pointer table, monotonic arrival counters (zeroed once), the q|k|v split-K
-// ways that balance the q|k|v items over the CUs, and the kernel's LDS attribute (set here, outside
-// any stream capture).  Not an error when unavailable: the per-op kernels stay in use.
-int mx_engine::setup_decode1() {
-  // opt-in while it is slower than the per-op kernels: MX_DECODE1=1
-  if (!getenv("MX_DECODE1") || getenv("MX_NO_DECODE1") || wq8 || wkq || layers.empty()) return 0;
-  for (const Layer& L : layers)
-    if (!L.qkv || !L.o || !L.gu || !L.down) return 0;
-  if (!decode1_supported(n_embd, n_embd_kv, n_ff, n_head, n_head_kv, head_dim)) return 0;
-  hipDeviceProp_t prop;
-  HIPC(hipGetDeviceProperties(&prop, device));
-  n_cu = prop.multiProcessorCount;
-  if (n_cu < n_head_kv) return 0;
-  const int h = n_embd, Nq = n_embd + 2 * n_embd_kv, T = Nq / 16, KT = h / 32;
-  int ks = 1;
-  long best = -1;
-  for (int k = 1; k <= 4; k *= 2) {  // max items per CU x slots per item, fewest ways on ties
-    if ((KT / k) % 16) break;
-    const long cost = (long)((T * k + n_cu - 1) / n_cu) * (KT / k / 16);
-    if (best < 0 || cost < best) best = cost, ks = k;
-  }
-  if (!d1_claim(this, device)) return 0;
-  const int nl = (int)layers.size();
-  std::vector<D1Layer> tab(nl);
-  for (int li = 0; li < nl; li++) {
-    const Layer& L = layers[li];
-    tab[li] = D1Layer{L.qkv, L.o, L.gu, L.down, L.attn_norm, L.ffn_norm, kcache + layer_kv_stride * li,
-                      vcache + layer_kv_stride * li};
-  }
-  D1Layer* dtab = nullptr;
-  if (int rc = alloc((void**)&dtab, nl * sizeof(D1Layer))) return rc;
-  HIPC(hipMemcpy(dtab, tab.data(), nl * sizeof(D1Layer), hipMemcpyHostToDevice));
-  D1Args& a = d1;
-  a.layers = dtab;
-  a.n_layer = nl;
-  a.h = h; a.kv = n_embd_kv; a.ff = n_ff; a.n_head = n_head; a.n_head_kv = n_head_kv; a.head_dim = head_dim;
-  a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.slot_stride = slot_stride;
-  a.eps = eps; a.scale = 1.0f / sqrtf((float)head_dim);
-  a.rope_cs = rope_cs;
-  a.x_out = x; a.ssq = ssq;
-  a.ks_qkv = ks;
-  // attn_output / ffn_down: two K-parts when their h/16 row tiles leave CUs idle (TinyLlama: 128 tiles
-  // on 256 CUs), so every CU streams half a tile instead of half the CUs a whole one
-  a.ks_o = (h / 16 < n_cu && KT >= 2 * 16) ? 2 : 1;
-  a.ks_d = (h / 16 < n_cu && n_ff / 32 >= 2 * 16) ? 2 : 1;
-  if (int rc = alloc((void**)&a.qkvp, (size_t)ks * Nq * 8)) return rc;  // 8-byte granules
-  if (int rc = alloc((void**)&a.attn, (size_t)h / 2 * 8)) return rc;
-  if (int rc = alloc((void**)&a.xs, (size_t)2 * h * 8)) return rc;
-  if (int rc = alloc((void**)&a.hb, (size_t)n_ff / 2 * 8)) return rc;
-  HIPC(hipMemset(a.qkvp, 0, (size_t)ks * Nq * 8));  // tag 0: never a live tag
-  HIPC(hipMemset(a.attn, 0, (size_t)h / 2 * 8));
-  HIPC(hipMemset(a.xs, 0, (size_t)2 * h * 8));
-  HIPC(hipMemset(a.hb, 0, (size_t)n_ff / 2 * 8));
-  const size_t words = decode1_ctr_words(nl);
-  if (int rc = alloc((void**)&a.ctr, words * 4)) return rc;
-  if (int rc = alloc((void**)&a.err, 64)) return rc;
-  HIPC(hipMemset(a.ctr, 0, words * 4));
-  HIPC(hipMemset(a.err, 0, 64));
-  a.trace = nullptr;
-  if (getenv("MX_D1_TRACE")) {
-    const size_t n = (size_t)n_cu * d1_trace_stride(nl);
-    if (int rc = alloc((void**)&a.trace, n * 8)) return rc;
-    HIPC(hipMemset(a.trace, 0, n * 8));
-  }
-  if (launch_decode1(a, n_cu, stream, true) != 0) {
-    d1_release(this);
-    return 0;
-  }
-  use_d1 = true;
-  return 0;
-}
-
-// a timed-out persistent launch (its spins are bounded) is reported once and the engine falls back to
-// the per-op kernels; counters re-zeroed for consistency
-int mx_engine::d1_check(hipStream_t s) {
-  if (!use_d1) return 0;
-  unsigned v = 0;
-  HIPC(hipMemcpyAsync(&v, d1.err, 4, hipMemcpyDeviceToHost, s));
-  HIPC(hipStreamSynchronize(s));
-  if (!v) return 0;
-  use_d1 = false;
-  d1_release(this);
-  HIPC(hipMemsetAsync(d1.err, 0, 4, s));
-  HIPC(hipMemsetAsync(d1.ctr, 0, decode1_ctr_words(d1.n_layer) * 4, s));
-  for (auto& kv : sched_graphs) hipGraphExecDestroy(kv.second);
-  sched_graphs.clear();
-  return fail(MX_ERR_HIP, "persistent one-token decode timed out (code " + std::to_string(v) +
-                              "); this step's results are invalid, later steps use the per-op kernels");
-}
-
 int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int* slot, const void* x_in, void* x_out,
                                bool head, const int* rowmap, int n_out, bool argmax, int* ids_next, int* pos_next,
                                int* hist, int hist_stride, int* hist_count, int max_hist, hipStream_t s) {
@@ -1110,13 +992,7 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
   // (embedding, attn_output, ffn_down, or ssq_kernel for a stage's x_in) leave per-tile partials
   const bool nol = !wide && !wq8 && !wkq && norm_on_load && mm_can_norm_on_load(M, h);
   const bool qql = q8_on_load(M) || kq_on_load(M);  // residual-stream Σx² partials wanted
-  // one token of a bf16 model: every layer in one persistent launch (it embeds the token itself)
-  const bool one = use_d1 && M == 1 && (x_in || (!embd_kq_type && !embd_q8));
-  if (one && !x_in) {
-    D1Args a = d1;
-    a.ids = ids; a.pos = pos; a.slot = slot; a.tok_embd = tok_embd; a.x_in = nullptr;
-    if (launch_decode1(a, n_cu, s)) return fail(MX_ERR_HIP, "decode1 launch");
-  } else if (x_in) {
+  if (x_in) {
     if (handoff_bf16) {  // bf16 hand-off from the previous stage: widen, with the Σx² partials on the way
       launch_bf16_to_f32(x, (const uint16_t*)x_in, M, h, (nol || qql) ? ssq : nullptr, s);
     } else {
@@ -1151,11 +1027,6 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
   }
   if (wide) return enqueue_forward_wide(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next,
                                         pos_next, hist, hist_stride, hist_count, max_hist, s);
-  if (one && x_in) {  // a later pipeline stage: x (and its Σx² partials) already widened above
-    D1Args a = d1;
-    a.ids = ids; a.pos = pos; a.slot = slot; a.tok_embd = nullptr; a.x_in = x;
-    if (launch_decode1(a, n_cu, s)) return fail(MX_ERR_HIP, "decode1 launch");
-  }
   // on-load only for attn_norm -> qkv: qkv's 384 work-groups run 1.5 rounds, so its per-work-group
   // prologue costs less than a norm launch; gate/up (7 rounds) and lm_head (31) keep the norm kernel
   // (tools/kernel_probe.py, profiles/round1_norm_on_load.txt)
@@ -1167,7 +1038,7 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
       m.X = xn; m.ldx = h;
     }
   };
-  for (int li = 0; li < (int)layers.size() && !one; li++) {
+  for (int li = 0; li < (int)layers.size(); li++) {
     const Layer& L = layers[li];
     _Float16* kc = kcache + layer_kv_stride * li;
     _Float16* vc = vcache + layer_kv_stride * li;
@@ -1674,7 +1545,7 @@ int mx_engine::forward_rows_chunk(int n, const int32_t* slots, const int32_t* po
   }
   if (head) HIPC(hipMemcpyAsync(logits_host, logits, (size_t)n_out * n_vocab * 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
-  return d1_check(s);
+  return 0;
 }
 
 // ---------------------------------------------------------------- scheduler
@@ -1876,7 +1747,6 @@ int mx_engine::prefill_batch(std::vector<Request*>& reqs) {
       }
     }
     HIPC(hipStreamSynchronize(st));
-    if (int rc = d1_check(st)) return rc;
     std::lock_guard<std::mutex> lk(mu);
     for (int k = 0; k < n_out; k++) {
       Request* r = reqs[q0 + k];
@@ -1995,7 +1865,6 @@ int mx_engine::sched_step(std::vector<Request*>& rows) {
     HIPC(hipMemcpyAsync(lg.data(), logits, (size_t)M * n_vocab * 4, hipMemcpyDeviceToHost, s));
   }
   HIPC(hipStreamSynchronize(s));
-  if (int rc = d1_check(s)) return rc;
   if (trace) {
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     fprintf(stderr, "sched: decode M=%d K=%d %s%s%.3f ms\n", M, K, dev_chain ? "(device sampling) " : "",
@@ -2184,7 +2053,6 @@ int mx_engine_create(const char* model_path, const mx_opts* opts, mx_engine** ou
     rc = e->load_gguf(path);
   }
   if (rc) return rc;
-  if ((rc = e->setup_decode1())) return rc;
   *out = e.release();
   return 0;
 }
@@ -2497,7 +2365,6 @@ int mx_batch_tokens(mx_engine* e, mx_batch* b, int32_t* out, int cap, int* n_ste
   std::lock_guard<std::mutex> lk(e->gpu_mu);
   hipSetDevice(e->device);
   HIPC(hipDeviceSynchronize());
-  if (int rc = e->d1_check(e->stream)) return rc;
   std::vector<int32_t> cnt(b->M);
   HIPC(hipMemcpy(cnt.data(), b->d_hist_count, b->M * 4, hipMemcpyDeviceToHost));
   if (n_steps) *n_steps = cnt[0];
@@ -2640,7 +2507,6 @@ int mx_stage_rows_pick(mx_engine* e, int n, const int32_t* slots, const int32_t*
     if (frc) return frc;
     if (no) HIPC(hipMemcpyAsync(tok_out + k0, e->d_tok, no * 4, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
-    if (int rc = e->d1_check(s)) return rc;
     k0 = k1;
     i = end;
   }
@@ -2661,20 +2527,6 @@ int mx_device_count(int32_t* n) {
   int c = 0;
   if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
   *n = c;
-  return 0;
-}
-
-int mx_decode1_trace(mx_engine* e, uint64_t* out, size_t cap, int* n_groups, int* stride) {
-  if (!e) return fail(MX_ERR_ARG, "null engine");
-  if (!e->use_d1 || !e->d1.trace) return fail(MX_ERR_STATE, "decode1 trace not enabled (MX_D1_TRACE=1 at engine creation)");
-  const size_t st = d1_trace_stride(e->d1.n_layer), n = (size_t)e->n_cu * st;
-  if (n_groups) *n_groups = e->n_cu;
-  if (stride) *stride = (int)st;
-  if (out && cap) {
-    std::lock_guard<std::mutex> lk(e->gpu_mu);
-    HIPC(hipStreamSynchronize(e->stream));
-    HIPC(hipMemcpy(out, e->d1.trace, std::min(cap, n) * 8, hipMemcpyDeviceToHost));
-  }
   return 0;
 }
 
@@ -2871,12 +2723,6 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
         per = (size_t)2 * ff * h * 2;
         return (e->use_pers && mm_pers_supported(EPI_SWIGLU, M, a.N, a.K)) ? launch_mm_pers(EPI_SWIGLU, a, s)
                                                                             : launch_mm(EPI_SWIGLU, a, s);
-      case 8: case 9: case 10: {  // RMS_NORM of M rows folding 4 (8) / 8 (9) / 0 (10) split-K slabs
-        const int ns = kind == 8 ? 4 : kind == 9 ? 8 : 0;
-        per = (size_t)M * h * 4 * (2 + ns) + (size_t)M * h * 2;
-        launch_resid_norm(e->xn, h, e->x, e->slabs, ns, e->slab_stride, L.ffn_norm, M, h, e->eps, s);
-        return 0;
-      }
       case 8: case 9: case 10: {  // RMS_NORM of M rows folding 4 (8) / 8 (9) / 0 (10) split-K slabs
         const int ns = kind == 8 ? 4 : kind == 9 ? 8 : 0;
         per = (size_t)M * h * 4 * (2 + ns) + (size_t)M * h * 2;

@@ -50,10 +50,6 @@ struct AttnArgs {
   size_t slab_stride;
   const float* rope_cs;  // [n_ctx][head_dim/2][2]
   _Float16 *kc_w, *vc_w; // writable views of kc / vc
-  // persistent decode (decode1.hip): the slabs and the output as tagged 8-byte granules of other CUs
-  const unsigned long long* gslab;  // [nslab][n_q + 2 n_kv] {f32 bits, tag}
-  unsigned long long* gout;         // [n_head * head_dim / 2] {bf16 pair, tag}
-  unsigned gtag_in, gtag_out;
   // diagnosis only (mx_profile_kernel with MX_ATTN_TRACE): per (row, kv head, wave) 8 wall-clock
   // stamps (100 MHz) at the kernel's phases; nullptr normally
   unsigned long long* trace;
@@ -106,50 +102,6 @@ struct MMArgs {
 };
 
 
-
-// ---- persistent one-token decode engine (decode1.hip) -------------------------------------------
-// Every layer of a one-token step in ONE launch: one 256-thread work-group per CU (wave 0 streams the
-// CU's share of every weight matrix through an LDS ring by LDS-DMA, waves 1-3 compute from it); the
-// layers' dependent hand-offs (q|k|v partials, attention output, residual stream, SwiGLU product)
-// are write-through stores + per-(layer, phase) arrival counters, never kernel boundaries.
-struct D1Layer {
-  const uint16_t *qkv, *o, *gu, *down;  // packed bf16 tiles (the same matrices the GEMVs read)
-  const float *attn_norm, *ffn_norm;
-  _Float16 *kc, *vc;                    // this layer's K / V caches
-};
-struct D1Args {
-  const D1Layer* layers;  // device array [n_layer]
-  int n_layer, h, kv, ff, n_head, n_head_kv, head_dim, n_ctx, ctx_stride;
-  size_t slot_stride;
-  float eps, scale;
-  const float* rope_cs;
-  const int *ids, *pos, *slot;  // device scalars of the one row
-  const uint16_t* tok_embd;     // bf16 [V][h] (first stage), or nullptr: x_in
-  const float* x_in;            // f32 [h] stage input
-  float* x_out;                 // f32 [h] residual after the last layer (the head / hand-off read it)
-  float* ssq;                   // [h/16] per-16 sums of squares of x_out (the head's RMS_NORM on load)
-  // hand-off buffers of 8-byte granules {value bits, tag} (hipMalloc), each written by ONE write-through
-  // 8-byte store; the tag = (calls << 9) + 5 layer + op + 1 says which call, layer and op wrote it
-  unsigned long long* qkvp;     // [ks_qkv][h + 2 kv] q|k|v split-K partials (f32)
-  unsigned long long* attn;     // [h / 2] attention output (bf16 pairs)
-  unsigned long long* xs;       // [2][h] residual stream (f32; part 0 carries the residual, part 1 a K half)
-  unsigned long long* hb;       // [ff / 2] SwiGLU product (bf16 pairs)
-  unsigned* ctr;                // [n_layer * 5 + 2]: ticket, calls at the end (never reset)
-  unsigned* err;                // timeout word (0 = fine)
-  int ks_qkv;                   // q|k|v split-K ways (<= 4)
-  int ks_o, ks_d;               // attn_output / ffn_down split-K ways (1 or 2: xs holds ks parts of x)
-  // diagnosis (MX_D1_TRACE): per work-group [n_layer][5 ops][start, arrive] s_memrealtime stamps,
-  // then 8 words of loader / consumer stall totals, then (attention work-groups) the attention body's
-  // 8 stamps per consumer wave of the last layer; rows of d1_trace_stride words; nullptr normally
-  unsigned long long* trace;
-};
-constexpr int D1_TRACE_CONS = 3;  // consumer waves (decode1.hip D1_CONS)
-__host__ __device__ constexpr size_t d1_trace_stride(int n_layer) { return (size_t)n_layer * 10 + 8 + 8 * D1_TRACE_CONS; }
-// 0: launched (prepare: only the kernel attributes set, once, outside stream capture); -1: shape not
-// supported (callers use the per-op kernels)
-int launch_decode1(const D1Args& a, int n_cu, hipStream_t s, bool prepare = false);
-bool decode1_supported(int h, int kv, int ff, int n_head, int n_head_kv, int head_dim);
-size_t decode1_ctr_words(int n_layer);
 
 // packing / synthetic weights.  mode: PACK_ROWS (logical row r -> packed row r + offset),
 // PACK_GATE / PACK_UP (ffn_gate / ffn_up rows interleaved by 8-row halves of each tile)

@@ -133,7 +133,6 @@ def lib() -> ctypes.CDLL:
         L.mx_stage_rows.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp]
         L.mx_profile_kernel.argtypes = [vp, i32, i32, i32, P(ctypes.c_double), P(ctypes.c_double)]
         L.mx_sync.argtypes = [vp]
-        L.mx_decode1_trace.argtypes = [vp, vp, ctypes.c_size_t, P(i32), P(i32)]
         L.mx_probe_copy.argtypes = [i32, ctypes.c_size_t, i32, P(ctypes.c_double), ctypes.c_char_p, i32]
         L.mx_probe_read.argtypes = [i32, ctypes.c_size_t, i32, P(ctypes.c_double), ctypes.c_char_p, i32]
         L.mx_device_count.argtypes = [P(i32)]
@@ -337,15 +336,6 @@ class Engine:
     # -- device-resident batches (bench, pipeline) ---------------------------
     def batch(self, slots, pos, ids=None, max_steps: int = 0) -> "Batch":
         return Batch(self, slots, pos, ids, max_steps)
-
-    def decode1_trace(self) -> np.ndarray:
-        """Stamps of the last persistent one-token launch (engine created with MX_D1_TRACE=1):
-        uint64 [work-groups][stride] (see include/mx_engine.h, mx_decode1_trace)."""
-        ng, st = ctypes.c_int32(), ctypes.c_int32()
-        _check(lib().mx_decode1_trace(self._h, None, 0, ctypes.byref(ng), ctypes.byref(st)))
-        out = np.zeros((ng.value, st.value), dtype=np.uint64)
-        _check(lib().mx_decode1_trace(self._h, out.ctypes.data, out.size, None, None))
-        return out
 
     def profile_kernel(self, kind: int, M: int, iters: int = 3):
         us, nb = ctypes.c_double(), ctypes.c_double()
