@@ -16,7 +16,8 @@ constexpr float LOG2E = 1.4426950408889634f;
 // the full chunks run the bare MFMA + softmax stream.
 constexpr int ATTN_FIN_MAXSLAB = 8;  // split-K slabs the FIN path can sum (the wide launchers split K at most 8 ways)
 
-template <int D, int G, int NW, bool FIN>
+// MS: slabs the FIN path loads (>= a.nslab; the ones past a.nslab re-read the last and add zero)
+template <int D, int G, int NW, bool FIN, int MS = ATTN_FIN_MAXSLAB>
 __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int c) {
   constexpr int CH = ATTN_CHUNK;
   constexpr int QK = D / 32;  // k-steps of QK^T
@@ -72,7 +73,6 @@ __device__ __forceinline__ void attn_decode_body(const AttnArgs& a, int kvh, int
                                                                    : nq + nkv + kvh * D + (i - G * D - D);
       // all slab and RoPE loads issued together (clamped: extra reads repeat the last slab): a run-time
       // slab loop or a load behind the RoPE branch made each load wait for itself
-      constexpr int MS = ATTN_FIN_MAXSLAB;
       f32x4 sv[MS];
 #pragma unroll
       for (int k = 0; k < MS; ++k)

@@ -2610,6 +2610,7 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
   hipStream_t s = e->stream;
   const int h = e->n_embd, kv = e->n_embd_kv, ff = e->n_ff;
   const int prof_pos = std::min(e->n_ctx - 1, std::max(0, getenv("MX_PROF_POS") ? atoi(getenv("MX_PROF_POS")) : 0));
+  const bool prof_fin = getenv("MX_PROF_FIN") != nullptr;  // kind 7: the FIN form (slabs finished in the kernel)
   std::vector<int32_t> zero(M, prof_pos), slots(M);
   for (int i = 0; i < M; i++) slots[i] = i % e->n_seq_max;
   HIPC(hipMemcpyAsync(e->d_pos, zero.data(), M * 4, hipMemcpyHostToDevice, s));
@@ -2735,6 +2736,10 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
         at.pos = e->d_pos; at.slot = e->d_slot; at.out = e->attn_out; at.ldo = h; at.M = M; at.n_head = e->n_head;
         at.n_head_kv = e->n_head_kv; at.head_dim = e->head_dim; at.n_ctx = e->n_ctx; at.ctx_stride = e->ctx_stride;
         at.slot_stride = e->slot_stride; at.scale = 1.0f / sqrtf((float)e->head_dim);
+        if (prof_fin) {  // the 32-row decode's form: q/k/v still as 4 split-K slabs, finished here
+          at.slabs = e->slabs; at.nslab = 4; at.slab_stride = e->slab_stride; at.rope_cs = e->rope_cs;
+          at.kc_w = e->kcache + e->layer_kv_stride * li; at.vc_w = e->vcache + e->layer_kv_stride * li;
+        }
         per = (size_t)M * (prof_pos + 1) * kv * 2 * 2;
         launch_attention(at, s);
         return 0;
@@ -2774,6 +2779,10 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
     at.ldo = h; at.M = M; at.n_head = e->n_head; at.n_head_kv = e->n_head_kv; at.head_dim = e->head_dim;
     at.n_ctx = e->n_ctx; at.ctx_stride = e->ctx_stride; at.slot_stride = e->slot_stride;
     at.scale = 1.0f / sqrtf((float)e->head_dim); at.trace = tr;
+    if (prof_fin) {
+      at.slabs = e->slabs; at.nslab = 4; at.slab_stride = e->slab_stride; at.rope_cs = e->rope_cs;
+      at.kc_w = e->kcache; at.vc_w = e->vcache;
+    }
     launch_attention(at, s);
     HIPC(hipStreamSynchronize(s));
     std::vector<unsigned long long> t(n);

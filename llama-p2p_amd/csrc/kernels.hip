@@ -1037,19 +1037,19 @@ bool mm_can_norm_on_load(int M, int K) {
 #include "attn_body.h"
 namespace mx {
 
-template <int D, int G, int NW, bool FIN>
+template <int D, int G, int NW, bool FIN, int MS>
 __global__ __launch_bounds__(64 * NW) void attn_decode_kernel(AttnArgs a) {
-  attn_decode_body<D, G, NW, FIN>(a, blockIdx.x, blockIdx.y);
+  attn_decode_body<D, G, NW, FIN, MS>(a, blockIdx.x, blockIdx.y);
 }
 
-template <int D, bool FIN, int NW>
+template <int D, bool FIN, int NW, int MS = ATTN_FIN_MAXSLAB>
 static void launch_attn_dfw(const AttnArgs& a, hipStream_t s) {
   dim3 grid(a.n_head_kv, a.M);
   switch (a.n_head / a.n_head_kv) {
-    case 1: attn_decode_kernel<D, 1, NW, FIN><<<grid, 64 * NW, 0, s>>>(a); break;
-    case 2: attn_decode_kernel<D, 2, NW, FIN><<<grid, 64 * NW, 0, s>>>(a); break;
-    case 4: attn_decode_kernel<D, 4, NW, FIN><<<grid, 64 * NW, 0, s>>>(a); break;
-    case 8: attn_decode_kernel<D, 8, NW, FIN><<<grid, 64 * NW, 0, s>>>(a); break;
+    case 1: attn_decode_kernel<D, 1, NW, FIN, MS><<<grid, 64 * NW, 0, s>>>(a); break;
+    case 2: attn_decode_kernel<D, 2, NW, FIN, MS><<<grid, 64 * NW, 0, s>>>(a); break;
+    case 4: attn_decode_kernel<D, 4, NW, FIN, MS><<<grid, 64 * NW, 0, s>>>(a); break;
+    case 8: attn_decode_kernel<D, 8, NW, FIN, MS><<<grid, 64 * NW, 0, s>>>(a); break;
   }
 }
 
@@ -1060,7 +1060,8 @@ static void launch_attn_dfw(const AttnArgs& a, hipStream_t s) {
 // rows and 7-20% slower at 1-32 rows.
 template <int D>
 static void launch_attn_d(const AttnArgs& a, hipStream_t s) {
-  if (a.slabs) launch_attn_dfw<D, true, 8>(a, s);
+  if (a.slabs && a.nslab <= 4) launch_attn_dfw<D, true, 8, 4>(a, s);  // Llama-3-8B's q|k|v splits K 4 ways
+  else if (a.slabs) launch_attn_dfw<D, true, 8>(a, s);
   else if (a.M >= 128) launch_attn_dfw<D, false, 4>(a, s);
   else launch_attn_dfw<D, false, 8>(a, s);
 }
@@ -2644,8 +2645,10 @@ __global__ __launch_bounds__(64 * W, 2) void mq8_wide_kernel(MMArgs a) {
       *reinterpret_cast<u32x4*>(base + xdst[i]) = xr[set][i];
     }
   };
+  typedef std::conditional_t<Q4, u32x2, u32x4> QT;  // a lane's share of one tile: 8 B (Q4) / 16 B (Q8)
   struct Frag {
-    u32x4 q[4], d[4];  // the chunk's 4 Q8 tiles: int8 operands, f16 block scales of this lane's row group
+    QT q[4];
+    u32x4 d[4];  // the chunk's 4 tiles: int8 (Q4: nibble) operands, f16 block scales of this lane's row group
   };
   Frag ring[U];
   auto load_w = [&](Frag& f, int ch) {
@@ -2653,8 +2656,7 @@ __global__ __launch_bounds__(64 * W, 2) void mq8_wide_kernel(MMArgs a) {
     for (int k = 0; k < 4; ++k) {
       const uint8_t* t = Wt + (size_t)(ch * 4 + k) * TB;
       if constexpr (Q4) {
-        const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(t) + lane);
-        f.q[k] = u32x4{v[0], v[1], 0u, 0u};
+        f.q[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(t) + lane);
       } else {
         f.q[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t) + lane);
       }
@@ -2680,8 +2682,14 @@ __global__ __launch_bounds__(64 * W, 2) void mq8_wide_kernel(MMArgs a) {
     const Frag f = ring[R];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const long a0 = Q4 ? q4_operand(f.q[k][0]) : (long)(((unsigned long)f.q[k][1] << 32) | f.q[k][0]);
-      const long a1 = Q4 ? q4_operand(f.q[k][1]) : (long)(((unsigned long)f.q[k][3] << 32) | f.q[k][2]);
+      long a0, a1;
+      if constexpr (Q4) {
+        a0 = q4_operand(f.q[k][0]);
+        a1 = q4_operand(f.q[k][1]);
+      } else {
+        a0 = (long)(((unsigned long)f.q[k][1] << 32) | f.q[k][0]);
+        a1 = (long)(((unsigned long)f.q[k][3] << 32) | f.q[k][2]);
+      }
       const f16x8 dw = __builtin_bit_cast(f16x8, f.d[k]);
       // scaling on packed f32 pairs, int32 -> f32 by the magic accumulator start (QG_MAGIC)
       f32x2 w0[2], w1[2];
