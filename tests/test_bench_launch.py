@@ -70,3 +70,73 @@ def test_failing_rank_fails_the_launch():
     p = _run(["--gpus", "2", "--dry-run", "--model", "no-such-model", "--steps", "1", "--warmup", "0"], timeout=120)
     assert p.returncode != 0
     assert not [l for l in p.stdout.splitlines() if l.strip()]
+
+
+_HANG = r"""
+import os, sys, time
+sys.path.insert(0, {root!r})
+from llama_p2p_amd import launch
+if os.environ.get("RANK") is not None:          # a rank: report its pid, then hang
+    open(os.path.join({tmp!r}, "rank" + os.environ["RANK"]), "w").write(str(os.getpid()))
+    time.sleep(600)
+    sys.exit(0)
+sys.exit(launch.spawn_ranks(2, [__file__], grace={grace}))
+"""
+
+
+def _alive(pid):
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    try:  # a zombie is not a live rank
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().split()[2] != "Z"
+    except FileNotFoundError:
+        return False
+
+
+def _ranks(tmp, n=2, t_max=60):
+    import time
+
+    t0 = time.time()
+    while time.time() - t0 < t_max:
+        got = [os.path.join(tmp, f"rank{r}") for r in range(n)]
+        if all(os.path.exists(g) and open(g).read() for g in got):
+            return [int(open(g).read()) for g in got]
+        time.sleep(0.1)
+    raise AssertionError("ranks did not start")
+
+
+def test_sigterm_to_launcher_stops_every_rank(tmp_path):
+    """A launcher killed by the driver (SIGTERM) must not leave ranks holding GPUs and the port."""
+    import signal
+    import time
+
+    script = tmp_path / "hang.py"
+    script.write_text(_HANG.format(root=ROOT, tmp=str(tmp_path), grace=300))
+    p = subprocess.Popen([sys.executable, str(script)], cwd=ROOT)
+    pids = _ranks(str(tmp_path))
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=30) == 128 + signal.SIGTERM
+    t0 = time.time()
+    while any(_alive(q) for q in pids) and time.time() - t0 < 20:
+        time.sleep(0.1)
+    assert not any(_alive(q) for q in pids)
+
+
+def test_sigkill_to_launcher_still_stops_ranks(tmp_path):
+    """Even when the launcher dies without running its handlers, PR_SET_PDEATHSIG ends its ranks."""
+    import signal
+    import time
+
+    script = tmp_path / "hang.py"
+    script.write_text(_HANG.format(root=ROOT, tmp=str(tmp_path), grace=300))
+    p = subprocess.Popen([sys.executable, str(script)], cwd=ROOT)
+    pids = _ranks(str(tmp_path))
+    p.send_signal(signal.SIGKILL)
+    p.wait(timeout=30)
+    t0 = time.time()
+    while any(_alive(q) for q in pids) and time.time() - t0 < 20:
+        time.sleep(0.1)
+    assert not any(_alive(q) for q in pids)
