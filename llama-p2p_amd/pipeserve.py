@@ -92,6 +92,7 @@ class Scheduler:
         self.rounds = 0
         # placement decisions: (request id, lane, candidate lanes, scoreboard snapshot before the pick)
         self.placements = collections.deque(maxlen=100000)
+        self.placement_state = collections.deque(maxlen=100000)  # (avg_time per lane, in flight per lane)
 
     # ---- request side (any thread)
     def submit(self, prompt, max_tokens, samp, seed):
@@ -182,7 +183,11 @@ class Scheduler:
                 if not free:
                     break
                 self.pending.popleft()
-                snap = {t: (p["success"], p["failure"]) for t, p in self.board.stats().items()}
+                st = self.board.stats()
+                snap = {t: (p["success"], p["failure"]) for t, p in st.items()}
+                # the rest of what score_aware reads (running mean latency, requests in flight): a
+                # placement can be replayed from the log (tests/test_config5_gpu.py)
+                self.placement_state.append(({t: p["avg_time"] for t, p in st.items()}, dict(self.board.inflight)))
                 lane = self.board.select(candidates=free)
                 self.placements.append((r.id, lane, free, snap))
                 row = self.table[lane].index(None)

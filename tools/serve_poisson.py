@@ -70,6 +70,7 @@ def main():
     ap.add_argument("--min-gain", type=float, default=0.10,
                     help="apply a stage re-split when it predicts this much lower slowest-stage time")
     ap.add_argument("--no-repartition", action="store_true")
+    ap.add_argument("--stage-time-every", type=int, default=8, help="rounds per stage-time sample of the planner")
     ap.add_argument("--parts", default="", help="initial stage ranges 'lb:le,lb:le,...' (in-process stages; "
                     "default partition_layers by bytes) -- e.g. a skewed split for the planner to repair")
     args = ap.parse_args()
@@ -118,7 +119,7 @@ def main():
             return
         llm = pipeserve.pipeline_llama(path, comm, world, world, args.rows, args.n_ctx, device=dev,
                                        policy=args.policy, seed=0, repartition=not args.no_repartition,
-                                       min_gain=args.min_gain)
+                                       min_gain=args.min_gain, stage_time_every=args.stage_time_every)
         mode = f"{world} stages, one GPU each (RCCL)"
     else:
         from llama_p2p_amd.pipeline import partition_layers
@@ -134,8 +135,13 @@ def main():
         initial_parts = list(parts)
         llm = pipeserve.local_pipeline_llama(path, parts, lanes=args.lanes or args.stages, rows=args.rows, n_ctx=args.n_ctx,
                                              policy=args.policy, seed=0, repartition=not args.no_repartition,
-                                             min_gain=args.min_gain)
+                                             min_gain=args.min_gain, stage_time_every=args.stage_time_every)
         mode = f"{args.stages} stages in one process on one GPU, {args.lanes or args.stages} lanes"
+    from llama_p2p_amd.pipeline import partition_layers as _pl
+
+    _h, _kv, _ff = shape.n_embd, shape.n_embd_kv, shape.n_ff
+    balanced = [tuple(p) for p in _pl(shape.n_layer, 2 * (2 * _h * _h + 2 * _h * _kv + 3 * _h * _ff),
+                                      2 * shape.n_vocab * _h, len(llm.parts))]
     front = llm._engine
     res = drive(lambda p, g: front.generate(p, g, temperature=0.0, ignore_eos=True), sched, args.gen,
                 args.time_scale)
@@ -149,7 +155,9 @@ def main():
                 "stage_scores": llm.planner.board.stats(),
                 "proposed_partition": pipeserve.proposed_partition(llm.planner.board, llm.parts,
                                                                    llm.planner.head_layers),
-                "repartitions": llm.planner.history,
+                "repartitions": llm.planner.history, "planner_last": llm.planner.last,
+                "byte_balanced": balanced,
+                "max_layer_delta_vs_balanced": max(abs((b - a) - (d - c)) for (a, b), (c, d) in zip(llm.parts, balanced)),
                 "rounds": llm.scheduler.rounds,
                 "stage0_host_per_micro_step": front.runner.host_stats()})
     llm.close()
