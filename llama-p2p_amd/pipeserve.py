@@ -622,6 +622,7 @@ class StagePlanner:
         self.n_obs, self.obs_at_resplit, self.resplits = 0, 0, 0
         self.history = []  # every re-split returned: parts before / after, predicted times, evidence
         self.last: Optional[dict] = None
+        self.pending = None  # a returned re-split not yet applied (the lanes are draining)
 
     @staticmethod
     def _rse(xs) -> float:
@@ -639,8 +640,8 @@ class StagePlanner:
             self.board.update(s, True, v)
             self.samples[s].append(v)
         self.n_obs += 1
-        if not self.enabled or self.resplits >= self.max_resplits:
-            return None
+        if not self.enabled or self.resplits >= self.max_resplits or self.pending is not None:
+            return None  # (pending: a re-split is draining; it is proposed once)
         if self.resplits and self.n_obs - self.obs_at_resplit < self.cooldown:
             return None
         if any(len(x) < self.min_samples for x in self.samples):
@@ -659,6 +660,7 @@ class StagePlanner:
         if new != self.parts and gain >= need:
             self.history.append(dict(self.last, to=list(new), weights=w, t=time.time()))
             self.resplits += 1
+            self.pending = list(new)
             _log.warning("stage planner: re-split %s -> %s (predicted slowest stage %.3g -> %.3g, gain %.1f%% "
                          "> needed %.1f%%, %d samples per stage)", self.parts, new, cur_t, new_t, 100 * gain,
                          100 * need, self.last["samples"])
@@ -666,6 +668,7 @@ class StagePlanner:
         return None
 
     def applied(self, parts):
+        self.pending = None
         self.parts = [tuple(p) for p in parts]
         self.board = PeerScoreboard(list(range(len(parts))), policy="score_aware")
         self.samples = [[] for _ in parts]

@@ -154,6 +154,10 @@ def test_planner_waits_for_evidence():
     for _ in range(12):
         assert noisy.observe([float(rng.uniform(0.2, 3.0)), float(rng.uniform(0.2, 3.0)) * 1.3]) is None
     assert noisy.last["needed"] > noisy.min_gain
+    # proposed once while it drains (observations keep coming until every stage has rebuilt)
+    once = P.StagePlanner(parts)
+    got = [once.observe([1.0, 2.0]) for _ in range(12)]
+    assert sum(g is not None for g in got) == 1 and len(once.history) == 1
     # re-splits are capped, and each needs a cooldown after the previous one
     cap = P.StagePlanner(parts, max_resplits=1)
     for _ in range(8):

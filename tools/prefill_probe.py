@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--len", type=int, default=128)
     ap.add_argument("--sweep", default="")
     ap.add_argument("--targets", default="256")
+    ap.add_argument("--quant", default="", help="q8_0 | q4_0 | q4_k_m (synthetic quantised model)")
     args = ap.parse_args()
     from llama_p2p_amd import synth
     from llama_p2p_amd.engine import Engine
@@ -43,7 +44,8 @@ def main():
                 print(f"target {tgt:>4} rows {L:5d}: {best * 1e3:8.2f} ms  {L / best:9.0f} tok/s", flush=True)
             eng.close()
         return
-    eng = Engine(f"synthetic:{args.model}:seed=0", n_ctx=512, n_seq_max=args.prompts)
+    eng = Engine(f"synthetic:{args.model}:seed=0" + (f":{args.quant}" if args.quant else ""), n_ctx=512,
+                 n_seq_max=args.prompts)
     rng = np.random.default_rng(3)
     slots = np.repeat(np.arange(args.prompts), args.len)
     pos = np.tile(np.arange(args.len), args.prompts)
