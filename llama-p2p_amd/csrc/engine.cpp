@@ -2611,6 +2611,7 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
   const int h = e->n_embd, kv = e->n_embd_kv, ff = e->n_ff;
   const int prof_pos = std::min(e->n_ctx - 1, std::max(0, getenv("MX_PROF_POS") ? atoi(getenv("MX_PROF_POS")) : 0));
   const bool prof_fin = getenv("MX_PROF_FIN") != nullptr;  // kind 7: the FIN form (slabs finished in the kernel)
+  const bool prof_warm = getenv("MX_PROF_WARM") != nullptr;  // diagnosis: every launch on layer 0 (Infinity-Cache warm)
   std::vector<int32_t> zero(M, prof_pos), slots(M);
   for (int i = 0; i < M; i++) slots[i] = i % e->n_seq_max;
   HIPC(hipMemcpyAsync(e->d_pos, zero.data(), M * 4, hipMemcpyHostToDevice, s));
@@ -2758,7 +2759,7 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
       launches++;
     } else {
       for (int li = 0; li < nl; li++) {
-        one(li);
+        one(prof_warm ? 0 : li);
         launches++;
       }
     }

@@ -1839,6 +1839,16 @@ __device__ __forceinline__ long q4_operand(uint32_t d) {
   return (long)(((unsigned long)hi << 32) | lo);
 }
 
+// The same operand times 16, in 4 VALU ops instead of 10: with x = d ^ 0x88, the nibble x & 0xF read
+// as a signed 4-bit value is n - 8, so the byte (x & 0xF) << 4 read as int8 is 16 (n - 8) exactly.
+// An int8 MFMA over it returns 16 x the block's integer sum; the caller takes the 16 out of the
+// activation scale (d_x / 16: a power of two, so every rounding after it is unchanged).
+__device__ __forceinline__ long q4_operand16(uint32_t d) {
+  const uint32_t x = d ^ 0x88888888u;
+  const uint32_t lo = (x << 4) & 0xF0F0F0F0u, hi = x & 0xF0F0F0F0u;
+  return (long)(((unsigned long)hi << 32) | lo);
+}
+
 // place one Q4_0 block (row, block b; q = the 32 unsigned nibble values) into its packed tile
 __device__ __forceinline__ void q4_place(uint8_t* dst, int P, int b, int KT2, uint16_t dbits, const uint8_t (&q)[32]) {
   uint8_t* tile = dst + ((size_t)(P >> 4) * KT2 + (b >> 1)) * Q4_TILE_BYTES;
@@ -2642,7 +2652,12 @@ __global__ __launch_bounds__(64 * W, 2) void mq8_wide_kernel(MMArgs a) {
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
       uint8_t* base = xq_piece[i] ? reinterpret_cast<uint8_t*>(&sq[buf][0][0]) : reinterpret_cast<uint8_t*>(&sd[buf][0][0]);
-      *reinterpret_cast<u32x4*>(base + xdst[i]) = xr[set][i];
+      u32x4 v = xr[set][i];
+      if constexpr (Q4) {  // d_x / 16 for q4_operand16's 16 x (n - 8) operands
+        const u32x4 v16 = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, v) * 0.0625f);
+        v = xq_piece[i] ? v : v16;
+      }
+      *reinterpret_cast<u32x4*>(base + xdst[i]) = v;
     }
   };
   typedef std::conditional_t<Q4, u32x2, u32x4> QT;  // a lane's share of one tile: 8 B (Q4) / 16 B (Q8)
@@ -2684,8 +2699,8 @@ __global__ __launch_bounds__(64 * W, 2) void mq8_wide_kernel(MMArgs a) {
     for (int k = 0; k < 4; ++k) {
       long a0, a1;
       if constexpr (Q4) {
-        a0 = q4_operand(f.q[k][0]);
-        a1 = q4_operand(f.q[k][1]);
+        a0 = q4_operand16(f.q[k][0]);
+        a1 = q4_operand16(f.q[k][1]);
       } else {
         a0 = (long)(((unsigned long)f.q[k][1] << 32) | f.q[k][0]);
         a1 = (long)(((unsigned long)f.q[k][3] << 32) | f.q[k][2]);
@@ -2753,6 +2768,185 @@ __global__ __launch_bounds__(64 * W, 2) void mq8_wide_kernel(MMArgs a) {
   }
 }
 
+// The same GEMV with the MFMA operands swapped: the activations are A (token rows) and the weight tile
+// is B, so a lane's C values are 4 TOKENS of ONE weight row (lane & 15).  Its two block scales d_w are
+// then two f16 per tile (two 2-byte loads, two converts) instead of eight (4 rows x 2 blocks), and
+// the 4 d_x of its tokens one 16-byte LDS read per block from a block-major d_x image; the products
+// t = d_x * d_w, the int32 -> f32 (magic start) and the fma are unchanged, so the sums are bit-identical
+// to mq8_wide_kernel's.  The weights come through a buffer resource with the tile offset in a scalar
+// (no per-load 64-bit address arithmetic); the C layout is transposed back through LDS at the end
+// (per wave, once) for the usual epilogues.  Used for Q4_0 (Llama-3-8B gate/up at 32 rows 23.5 vs
+// 24.8 us); Q8_0 measured slower (27.5 vs 24.7 us: profiles/round5_quant_wide_variants.txt).
+template <int W, int EPI, int U, bool Q4>
+__global__ __launch_bounds__(64 * W) void mq8_wsw_kernel(MMArgs a) {
+  constexpr int TB = Q4 ? Q4_TILE_BYTES : Q8_TILE_BYTES, SO = Q4 ? 512 : 1024;
+  constexpr int NB = 2, ROWS = 32;
+  constexpr int QP = 256 + 16;   // int8 per LDS row (+16 B: conflict-free fragment reads)
+  constexpr int NQ = ROWS * 16;  // 16-B pieces of q per chunk
+  constexpr int ND = ROWS * 2;   // 16-B pieces of the block scales (8 floats per token)
+  constexpr int NT = 64 * W;
+  constexpr int PPT = (NQ + NT - 1) / NT;
+  static_assert(U == 2 || U == 4, "ring depth");
+  static_assert(ND <= 64, "the block scales are staged by wave 0");
+  __shared__ __attribute__((aligned(16))) int8_t sq[2][ROWS][QP];
+  __shared__ __attribute__((aligned(16))) float sdt[2][8][ROWS];      // d_x block-major
+  __shared__ __attribute__((aligned(16))) float tr[W][NB][16][20];    // epilogue transpose
+
+  const int lane = threadIdx.x & 63, tid = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int KT = a.K / Q8_TILE_K;
+  // grid.y > 1 (EPI_SLAB): this work-group's K range of 256-k chunks [cb, cb + NCH)
+  const int NCHT = a.K / 256, cb = NCHT * blockIdx.y / gridDim.y, NCH = NCHT * (blockIdx.y + 1) / gridDim.y - cb;
+  const int tile = blockIdx.x * W + w;
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(a.W) + ((size_t)tile * KT + cb * 4) * TB), (short)0,
+      NCH * 4 * TB, 0x00020000);
+  const int r = lane & 15;
+  const unsigned qoff = lane * (Q4 ? 8u : 16u), doff = SO + 16 * (r >> 2) + 2 * (r & 3);
+
+  const u32x4* xsrc[PPT];
+  int xdst[PPT];
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int p = min(tid + i * NT, NQ - 1);
+    const int row = p / 16, rr = row < a.M ? row : a.M - 1;
+    xsrc[i] = reinterpret_cast<const u32x4*>(a.xq + (size_t)rr * a.K + (size_t)cb * 256 + (p % 16) * 16);
+    xdst[i] = row * QP + (p % 16) * 16;
+  }
+  const int drow = min(tid >> 1, ROWS - 1), drr = drow < a.M ? drow : a.M - 1, dhalf = tid & 1;
+  const u32x4* dsrc = reinterpret_cast<const u32x4*>(a.xd + (size_t)drr * (a.K / 32) + cb * 8 + dhalf * 4);
+  u32x4 xr[2][PPT], dr[2];
+  auto load_x = [&](int set, int ch) {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) xr[set][i] = xsrc[i][ch * 16];
+    if (w == 0) dr[set] = dsrc[ch * 2];
+  };
+  auto store_x = [&](int set, int buf) {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i)
+      *reinterpret_cast<u32x4*>(reinterpret_cast<uint8_t*>(&sq[buf][0][0]) + xdst[i]) = xr[set][i];
+    if (w == 0) {
+      f32x4 d = __builtin_bit_cast(f32x4, dr[set]);
+      if constexpr (Q4) d = d * 0.0625f;  // d_x / 16 for q4_operand16's 16 x (n - 8) operands
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sdt[buf][dhalf * 4 + e][drow] = d[e];
+    }
+  };
+  typedef std::conditional_t<Q4, u32x2, u32x4> QT;
+  struct Frag {
+    QT q[4];
+    uint32_t d0[4], d1[4];  // this lane's weight row: f16 d_w of blocks 0 / 1 of each tile (low half)
+  };
+  Frag ring[U];
+  auto load_w = [&](Frag& f, int ch) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int so = (ch * 4 + k) * TB;
+      if constexpr (Q4)
+        f.q[k] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(wrs, qoff, so, 2));
+      else
+        f.q[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, qoff, so, 2));
+      f.d0[k] = __builtin_amdgcn_raw_buffer_load_b16(wrs, doff, so, 0);
+      f.d1[k] = __builtin_amdgcn_raw_buffer_load_b16(wrs, doff + 8, so, 0);
+    }
+  };
+  f32x4 acc[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_x(0, 0);
+  load_x(1, NCH > 1 ? 1 : 0);
+#pragma unroll
+  for (int u = 0; u < U; ++u) load_w(ring[u], u < NCH ? u : NCH - 1);
+  store_x(0, 0);
+  __syncthreads();
+
+  const int q4 = (lane >> 4) * 4;
+  auto step = [&](auto Hc, auto Rc, int ch) {
+    constexpr int H = decltype(Hc)::value;
+    constexpr int R = decltype(Rc)::value;
+    const int buf = ch & 1;
+    load_x(H, ch + 2 < NCH ? ch + 2 : NCH - 1);
+    const Frag f = ring[R];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      long b0, b1;
+      if constexpr (Q4) {
+        b0 = q4_operand16(f.q[k][0]);
+        b1 = q4_operand16(f.q[k][1]);
+      } else {
+        b0 = (long)(((unsigned long)f.q[k][1] << 32) | f.q[k][0]);
+        b1 = (long)(((unsigned long)f.q[k][3] << 32) | f.q[k][2]);
+      }
+      const float w0 = (float)__builtin_bit_cast(_Float16, (uint16_t)f.d0[k]);
+      const float w1 = (float)__builtin_bit_cast(_Float16, (uint16_t)f.d1[k]);
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        const int row = n * 16 + (lane & 15);
+        const u32x4 xb = *reinterpret_cast<const u32x4*>(&sq[buf][row][k * 64 + (lane >> 4) * 16]);
+        const f32x4 dx0 = *reinterpret_cast<const f32x4*>(&sdt[buf][2 * k][n * 16 + q4]);
+        const f32x4 dx1 = *reinterpret_cast<const f32x4*>(&sdt[buf][2 * k + 1][n * 16 + q4]);
+        const long a0 = (long)(((unsigned long)xb[1] << 32) | xb[0]);
+        const long a1 = (long)(((unsigned long)xb[3] << 32) | xb[2]);
+        const i32x4 mg = i32x4{QG_MAGIC, QG_MAGIC, QG_MAGIC, QG_MAGIC};
+        const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, b0, mg, 0, 0, 0));
+        const f32x4 x1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, b1, mg, 0, 0, 0));
+        const f32x2 off = f32x2{12582912.0f, 12582912.0f};
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          f32x2 c = f32x2{acc[n][2 * pp], acc[n][2 * pp + 1]};
+          c = __builtin_elementwise_fma(f32x2{dx0[2 * pp], dx0[2 * pp + 1]} * f32x2{w0, w0},
+                                        f32x2{x0[2 * pp], x0[2 * pp + 1]} - off, c);
+          c = __builtin_elementwise_fma(f32x2{dx1[2 * pp], dx1[2 * pp + 1]} * f32x2{w1, w1},
+                                        f32x2{x1[2 * pp], x1[2 * pp + 1]} - off, c);
+          acc[n][2 * pp] = c[0];
+          acc[n][2 * pp + 1] = c[1];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one tile at a time (hoisted LDS reads of all four spill)
+    }
+    load_w(ring[R], min(ch + U, NCH - 1));  // past the end: re-read the last chunk (no branch)
+    store_x(1 - H, buf ^ 1);
+    __syncthreads();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  for (int ch = 0; ch < NCH; ch += U) {
+    step(I0{}, I0{}, ch);
+    if (ch + 1 < NCH) step(I1{}, I1{}, ch + 1);
+    if constexpr (U == 4) {
+      if (ch + 2 < NCH) step(I0{}, I2{}, ch + 2);
+      if (ch + 3 < NCH) step(I1{}, I3{}, ch + 3);
+    }
+  }
+  // C^T -> the usual layout through this wave's tr
+#pragma unroll
+  for (int n = 0; n < NB; ++n)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tr[w][n][q4 + i][r] = acc[n][i];  // [token][weight row]
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's own writes, read back below
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int n = 0; n < NB; ++n) acc[n] = *reinterpret_cast<const f32x4*>(&tr[w][n][r][q4]);
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    const f32x4 sv = acc[n];
+    f32x4 up = sv;
+    if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(sv[i], 32);
+    }
+    const int col = n * 16 + (lane & 15);
+    if (col >= a.M || (EPI == EPI_SWIGLU && lane >= 32)) continue;
+    if constexpr (EPI == EPI_SLAB)
+      *reinterpret_cast<f32x4*>(a.out + blockIdx.y * a.slab_stride + (size_t)col * a.ldo + tile * 16 + (lane >> 4) * 4) = sv;
+    else
+      epi_store<EPI>(a, tile, lane, col, sv, up);
+  }
+}
+
 // 17..32 tokens, attn_output / ffn_down / q|k|v of a Q8_0 file: 4-wave groups, K split over grid.y
 // until ~256 work-groups, partial slabs [ks][token][N] (folded by launch_rmsnorm_q8's FOLD form, or
 // finished by the decode attention / launch_qkv_finish).  Returns ks, or -1 (use launch_mq8).
@@ -2779,9 +2973,9 @@ static int launch_mq8_wide(int epi, const MMArgs& a, hipStream_t s) {
   if (epi != EPI_SWIGLU && epi != EPI_F32) return -1;
   auto go = [&](auto wc) {
     constexpr int W = decltype(wc)::value;
-    if (a.wq4) {
-      if (epi == EPI_SWIGLU) mq8_wide_kernel<W, EPI_SWIGLU, 2, true><<<ntiles / W, 64 * W, 0, s>>>(a);
-      else mq8_wide_kernel<W, EPI_F32, 2, true><<<ntiles / W, 64 * W, 0, s>>>(a);
+    if (a.wq4) {  // Q4_0: the swapped-operand form
+      if (epi == EPI_SWIGLU) mq8_wsw_kernel<W, EPI_SWIGLU, 2, true><<<ntiles / W, 64 * W, 0, s>>>(a);
+      else mq8_wsw_kernel<W, EPI_F32, 2, true><<<ntiles / W, 64 * W, 0, s>>>(a);
     } else {
       if (epi == EPI_SWIGLU) mq8_wide_kernel<W, EPI_SWIGLU, 2, false><<<ntiles / W, 64 * W, 0, s>>>(a);
       else mq8_wide_kernel<W, EPI_F32, 2, false><<<ntiles / W, 64 * W, 0, s>>>(a);

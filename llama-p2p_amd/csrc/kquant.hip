@@ -1626,7 +1626,7 @@ __device__ __forceinline__ void mkq_wide_body(const MMArgs& a, int tile, const u
   __shared__ __attribute__((aligned(16))) float ssb[2][ROWS][8];
   __shared__ float sdx[2][ROWS];
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, tid = threadIdx.x;
+  const int lane = threadIdx.x & 63, g = lane >> 4, tid = threadIdx.x;
   const int SB = a.K / 256;
   // grid.y > 1 (EPI_SLAB): this work-group's K range of super-blocks [kb, kb + nsb)
   const int kb = SB * blockIdx.y / gridDim.y, nsb = SB * (blockIdx.y + 1) / gridDim.y - kb;
