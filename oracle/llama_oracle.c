@@ -228,12 +228,19 @@ void orc_set_rope(orc_model *m, const float *freq_factors, float freq_scale) {
     m->rope_freq_scale = freq_scale;
 }
 
-void orc_fill_synthetic(orc_model *m, uint64_t seed) {
+/* Synthesise layers [lb, le) and, with globals, token_embd / output / output_norm: a per-layer test of
+ * a model too large to synthesise whole on the host (Llama-3-70B) fills only the layers it runs; the
+ * other layers' buffers stay untouched (never committed). */
+void orc_fill_synthetic_layers(orc_model *m, uint64_t seed, int lb, int le, int globals) {
     size_t h = m->hp.n_embd, kv = m->n_embd_kv, ff = m->hp.n_ff, V = m->hp.n_vocab;
-    synth_bf16(m->tok_embd, seed, K_TOK_EMBD, V * h);
-    synth_bf16(m->output, seed, K_OUTPUT, V * h);
-    synth_norm(m->out_norm, seed, K_OUT_NORM, h);
-    for (int l = 0; l < m->hp.n_layer; l++) {
+    if (globals) {
+        synth_bf16(m->tok_embd, seed, K_TOK_EMBD, V * h);
+        synth_bf16(m->output, seed, K_OUTPUT, V * h);
+        synth_norm(m->out_norm, seed, K_OUT_NORM, h);
+    }
+    if (lb < 0) lb = 0;
+    if (le > m->hp.n_layer) le = m->hp.n_layer;
+    for (int l = lb; l < le; l++) {
         orc_layer *L = &m->layers[l];
         synth_norm(L->attn_norm, seed, layer_tid(l, L_ATTN_NORM), h);
         synth_bf16(L->wq, seed, layer_tid(l, L_Q), h * h);
@@ -246,6 +253,8 @@ void orc_fill_synthetic(orc_model *m, uint64_t seed) {
         synth_bf16(L->wd, seed, layer_tid(l, L_DOWN), h * ff);
     }
 }
+
+void orc_fill_synthetic(orc_model *m, uint64_t seed) { orc_fill_synthetic_layers(m, seed, 0, m->hp.n_layer, 1); }
 
 /* Set one tensor from caller memory (bf16 bits for matrices, f32 for norms).
  * layer = -1 for global tensors; kind uses the synth.py numbering. */

@@ -46,6 +46,7 @@ def lib():
         L.orc_create.argtypes = [ctypes.POINTER(_HP), i32]
         L.orc_free.argtypes = [vp]
         L.orc_fill_synthetic.argtypes = [vp, u64]
+        L.orc_fill_synthetic_layers.argtypes = [vp, u64, i32, i32, i32]
         L.orc_set_tensor.argtypes = [vp, i32, i32, vp]
         L.orc_set_tensor.restype = i32
         L.orc_set_tensor_q8.argtypes = [vp, i32, i32, vp]
@@ -105,6 +106,11 @@ class OracleModel:
         self._m = lib().orc_create(ctypes.byref(hp), ORC_EXACT if exact else 0)
         if seed is not None:
             lib().orc_fill_synthetic(self._m, seed)
+
+    def fill_synthetic_layers(self, seed: int, layer_begin: int, layer_end: int, globals_: bool = True):
+        """Synthesise only layers [layer_begin, layer_end) (+ embedding / head with globals_): for
+        per-layer checks of a model too large to synthesise whole (create with seed=None)."""
+        lib().orc_fill_synthetic_layers(self._m, seed, layer_begin, layer_end, 1 if globals_ else 0)
 
     def set_tensor(self, layer: int, kind: int, arr: np.ndarray):
         arr = np.ascontiguousarray(arr)

@@ -147,3 +147,26 @@ def test_per_layer_hook_equals_eval(oracle_mod, name):
         assert np.array_equal(lg, ref[a:b])
     with pytest.raises(ValueError):
         c.layers(x, 0, 0, sh.n_layer + 1)
+
+
+def test_layer_range_synthesis_equals_whole_model(oracle_mod):
+    """orc_fill_synthetic_layers (the 70B per-layer GPU test's oracle) fills exactly what the whole-model
+    fill does for its layers: one layer on the same input gives the same bits, and the head too."""
+    from llama_p2p_amd import synth
+
+    sh = synth.SHAPES["test-tiny"]
+    whole = oracle_mod.OracleModel(sh, seed=3)
+    part = oracle_mod.OracleModel(sh, seed=None)
+    last = sh.n_layer - 1
+    part.fill_synthetic_layers(3, 1, 2, globals_=False)
+    part.fill_synthetic_layers(3, last, last + 1, globals_=True)
+    x = np.random.default_rng(0).normal(0, 0.5, (5, sh.n_embd)).astype(np.float32)
+    for l, head in ((1, False), (last, True)):
+        a, b = whole.context(16), part.context(16)
+        ra, rb = a.layers(x, 0, l, l + 1, logits=head), b.layers(x, 0, l, l + 1, logits=head)
+        for u, v in zip(ra if head else [ra], rb if head else [rb]):
+            assert np.array_equal(u, v)
+        a.close()
+        b.close()
+    whole.close()
+    part.close()
