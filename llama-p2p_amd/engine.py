@@ -96,6 +96,20 @@ _lib = None
 _lib_lock = threading.Lock()
 
 
+def _torch_hip_first():
+    """Initialise PyTorch's HIP runtime before the engine's.  The process holds two: libmxllama.so links
+    /opt/rocm's libamdhip64.so.7 / libhsa-runtime64.so.1, PyTorch loads its bundled copies; once the
+    engine's runtime has opened the GPU, PyTorch's sees none ("No HIP GPUs are available"), while the
+    other order works (tools/hip_runtime_order_probe.py).  The pipeline, the bench and the tests use
+    both, so the engine's loader initialises PyTorch's first (nothing to do without a GPU)."""
+    try:
+        import torch
+    except ImportError:
+        return
+    if torch.cuda.is_available():
+        torch.cuda.init()
+
+
 def lib() -> ctypes.CDLL:
     """Load libmxllama.so (raises if it was not built)."""
     global _lib
@@ -105,6 +119,7 @@ def lib() -> ctypes.CDLL:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} not found: build it with `python llama-p2p_amd/build.py` "
                               "(the engine has no CPU fallback)")
+        _torch_hip_first()
         L = ctypes.CDLL(LIB_PATH)
         vp, i32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64
         P = ctypes.POINTER

@@ -1011,6 +1011,7 @@ def local_pipeline_llama(model_path: str, parts, lanes: int = 2, rows: int = 8, 
     time their lane steps one at a time (a shared lock), so the planner sees each stage's own cost."""
     import torch
 
+    torch.cuda.init()  # lazy CUDA init here, not raced by the stage threads below
     device = device or torch.device("cuda", torch.cuda.current_device())
     world = len(parts)
     hub = LocalHub()

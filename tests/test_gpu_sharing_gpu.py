@@ -45,6 +45,7 @@ def _run(world, S=2, M=32, steps=5, chunk=64):
     layer = 2 * (2 * sh.n_embd ** 2 + 2 * sh.n_embd * sh.n_embd_kv + 3 * sh.n_embd * sh.n_ff)
     parts = partition_layers(sh.n_layer, layer, 2 * sh.n_vocab * sh.n_embd, world)
     dev = torch.device("cuda", 0)
+    torch.cuda.init()  # torch's lazy CUDA init in the main thread, not raced by the two stage threads
     hub = pipeserve.LocalHub()
     out, errs = [None] * world, []
     bar, lock = threading.Barrier(world), threading.Lock()
