@@ -995,16 +995,10 @@ int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, h
       else if (epi == EPI_QKV && ntiles % 8 == 0) cfg = 0, groups = ntiles / 8;
       else if (a.K <= 8192 && ntiles % 2 == 0) cfg = 1, groups = ntiles / 2;
       else cfg = 2, groups = ntiles / 4;
-      int target = cfg == 4 ? 8 : (cfg == 3 || cfg == 1) ? 4
-                                : std::min(4, std::max(1, (256 + groups - 1) / std::max(1, groups)));
-      static int ks_env[3] = {-1, -1, -1};  // A/B: MX_WIDE_KS=q,o,d split targets (q|k|v, K <= 8192, K > 8192)
-      static const bool ks_set = [] {
-        if (const char* v = getenv("MX_WIDE_KS")) sscanf(v, "%d,%d,%d", &ks_env[0], &ks_env[1], &ks_env[2]);
-        return true;
-      }();
-      (void)ks_set;
-      const int ki = epi == EPI_QKV ? 0 : a.K > 8192 ? 2 : 1;
-      if (ks_env[ki] > 0) target = std::min(ks_env[ki], 8);  // the slab buffer holds 8
+      // split targets measured in round 5 (profiles/round5_wide_variants_rejected.txt D): q|k|v 4, attn_output 4,
+      // ffn_down 8 beat every 2 / 4 / 8 combination tried
+      const int target = cfg == 4 ? 8 : (cfg == 3 || cfg == 1) ? 4
+                                      : std::min(4, std::max(1, (256 + groups - 1) / std::max(1, groups)));
       const int ksplit = pick_ksplit(KT, target);
       if (!ksplit) return -1;
       MMArgs p = a;
