@@ -97,11 +97,12 @@ _lib_lock = threading.Lock()
 
 
 def _torch_hip_first():
-    """Initialise PyTorch's HIP runtime before the engine's.  The process holds two: libmxllama.so links
-    /opt/rocm's libamdhip64.so.7 / libhsa-runtime64.so.1, PyTorch loads its bundled copies; once the
-    engine's runtime has opened the GPU, PyTorch's sees none ("No HIP GPUs are available"), while the
-    other order works (tools/hip_runtime_order_probe.py).  The pipeline, the bench and the tests use
-    both, so the engine's loader initialises PyTorch's first (nothing to do without a GPU)."""
+    """Initialise PyTorch's HIP runtime before loading the engine, so the process has ONE runtime.
+    libmxllama.so NEEDs libamdhip64.so.7; PyTorch's libc10_hip.so NEEDs libamdhip64.so and loads its
+    bundled copy, whose SONAME is also libamdhip64.so.7 -- loaded after PyTorch, the engine binds to that
+    copy (and PyTorch stream handles passed to mx_batch_step are objects of the same runtime).  Loaded
+    first, the engine pulled in /opt/rocm's copy and PyTorch's second copy then saw no GPU ("No HIP GPUs
+    are available"; tools/hip_runtime_order_probe.py).  Nothing to do without a GPU."""
     try:
         import torch
     except ImportError:
