@@ -3087,72 +3087,93 @@ __global__ __launch_bounds__(512, 1) void q8gemm_kernel(MMArgs a) {
   // block 1 -- on packed f32 pairs.  (float)sumi without v_cvt_f32_i32 (not packable): the MFMA
   // starts from C = 0x4B400000, the bits of 1.5 * 2^23, so it returns the bits of 12582912 + sumi
   // exactly (|sumi| <= 32 * 127 * 127 < 2^22 keeps the exponent), and one packed subtract of
-  // 12582912 leaves sumi exactly
-  auto mfma = [&](const Frags& f) {
-    // the MFMAs of row tile r+1 are issued before the scaling of row tile r (an MFMA's result is read
-    // 8 passes after its issue: scaling right behind its own MFMA stalled the wave on every pair)
-    f32x4 x[4][4][2];
+  // 12582912 leaves sumi exactly.  4 copies (Q4: 3) per wave and k-step, NBUF-2 k-steps in flight
+  // behind the one being read.  Pipelined row tile by row tile: the 8 MFMAs of row tile r+1 go into
+  // one of two result sets while row tile r is scaled from the other (64 result VGPRs instead of
+  // 128), and the NEXT k-step's fragments are read from LDS while this one's MFMAs run (two fragment
+  // sets, gemm_kernel's step).  Round 5: 1555 -> 1491 us for the Llama-3-8B gate/up at 4096 rows,
+  // Q4_0 1647 -> 1530, against holding all 32 results at once and reading the k-step's fragments at
+  // its top.  Unpacking Q4 at 16x (q4_operand16, d_w / 16) measured 1530 -> 1650 us here, rejected.
+  auto mfma_r = [&](const Frags& f, auto Rc, f32x4 (&x)[4][2]) {
+    constexpr int r = decltype(Rc)::value;
+    const long a0 = Q4 ? q4_operand(f.a[r][0]) : (long)(((unsigned long)f.a[r][1] << 32) | f.a[r][0]);
+    const long a1 = Q4 ? q4_operand(f.a[r][1]) : (long)(((unsigned long)f.a[r][3] << 32) | f.a[r][2]);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const long a0 = Q4 ? q4_operand(f.a[r][0]) : (long)(((unsigned long)f.a[r][1] << 32) | f.a[r][0]);
-      const long a1 = Q4 ? q4_operand(f.a[r][1]) : (long)(((unsigned long)f.a[r][3] << 32) | f.a[r][2]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const long b0 = (long)(((unsigned long)f.b[j][1] << 32) | f.b[j][0]);
-        const long b1 = (long)(((unsigned long)f.b[j][3] << 32) | f.b[j][2]);
-        const i32x4 mg = i32x4{QG_MAGIC, QG_MAGIC, QG_MAGIC, QG_MAGIC};
-        x[r][j][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, b0, mg, 0, 0, 0));
-        x[r][j][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, b1, mg, 0, 0, 0));
-      }
+    for (int j = 0; j < 4; ++j) {
+      const long b0 = (long)(((unsigned long)f.b[j][1] << 32) | f.b[j][0]);
+      const long b1 = (long)(((unsigned long)f.b[j][3] << 32) | f.b[j][2]);
+      const i32x4 mg = i32x4{QG_MAGIC, QG_MAGIC, QG_MAGIC, QG_MAGIC};
+      x[j][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, b0, mg, 0, 0, 0));
+      x[j][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, b1, mg, 0, 0, 0));
     }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const f16x8 dw = __builtin_bit_cast(f16x8, f.dw[r]);
-      f32x2 dwp[2][2];  // [block][row pair]
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int pp = 0; pp < 2; ++pp) dwp[b][pp] = f32x2{(float)dw[4 * b + 2 * pp], (float)dw[4 * b + 2 * pp + 1]};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f32x2 dx0 = f32x2{f.dx[j][0], f.dx[j][0]}, dx1 = f32x2{f.dx[j][1], f.dx[j][1]};
-        const f32x2 off = f32x2{12582912.0f, 12582912.0f};
-#pragma unroll
-        for (int pp = 0; pp < 2; ++pp) {
-          f32x2 c = f32x2{acc[r][j][2 * pp], acc[r][j][2 * pp + 1]};
-          c = __builtin_elementwise_fma(dwp[0][pp] * dx0, f32x2{x[r][j][0][2 * pp], x[r][j][0][2 * pp + 1]} - off, c);
-          c = __builtin_elementwise_fma(dwp[1][pp] * dx1, f32x2{x[r][j][1][2 * pp], x[r][j][1][2 * pp + 1]} - off, c);
-          acc[r][j][2 * pp] = c[0];
-          acc[r][j][2 * pp + 1] = c[1];
-        }
-      }
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-    __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-    __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-    __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);
-    __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);
   };
-
-  // 4 copies (Q4: 3) per wave and k-step; waits: k-step kt landed with NBUF-2 k-steps behind it.  The
-  // fragments are read at the top of each step: double-buffering them (gemm_kernel's loop) spills
-  // 66-86 VGPRs here
+  auto scale_r = [&](const Frags& f, auto Rc, const f32x4 (&x)[4][2]) {
+    constexpr int r = decltype(Rc)::value;
+    const f16x8 dw = __builtin_bit_cast(f16x8, f.dw[r]);
+    f32x2 dwp[2][2];  // [block][row pair]
 #pragma unroll
-  for (int i = 0; i < NBUF - 1; ++i) issue(t0 + i);
-  for (int kt = t0; kt < t1; ++kt) {
-    if constexpr (Q4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) dwp[b][pp] = f32x2{(float)dw[4 * b + 2 * pp], (float)dw[4 * b + 2 * pp + 1]};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x2 dx0 = f32x2{f.dx[j][0], f.dx[j][0]}, dx1 = f32x2{f.dx[j][1], f.dx[j][1]};
+      const f32x2 off = f32x2{12582912.0f, 12582912.0f};
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        f32x2 c = f32x2{acc[r][j][2 * pp], acc[r][j][2 * pp + 1]};
+        c = __builtin_elementwise_fma(dwp[0][pp] * dx0, f32x2{x[j][0][2 * pp], x[j][0][2 * pp + 1]} - off, c);
+        c = __builtin_elementwise_fma(dwp[1][pp] * dx1, f32x2{x[j][1][2 * pp], x[j][1][2 * pp + 1]} - off, c);
+        acc[r][j][2 * pp] = c[0];
+        acc[r][j][2 * pp + 1] = c[1];
+      }
+    }
+  };
+  using R0 = std::integral_constant<int, 0>;
+  using R1 = std::integral_constant<int, 1>;
+  using R2 = std::integral_constant<int, 2>;
+  using R3 = std::integral_constant<int, 3>;
+  auto compute = [&](const Frags& f) {
+    f32x4 xa[4][2], xb[4][2];
+    mfma_r(f, R0{}, xa);
+    mfma_r(f, R1{}, xb);
+    scale_r(f, R0{}, xa);
+    mfma_r(f, R2{}, xa);
+    scale_r(f, R1{}, xb);
+    mfma_r(f, R3{}, xb);
+    scale_r(f, R2{}, xa);
+    scale_r(f, R3{}, xb);
+  };
+#pragma unroll
+  for (int i = 0; i < NBUF; ++i) issue(t0 + i);
+  if constexpr (Q4) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // t0 landed, NBUF-1 k-steps behind it
+  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  Frags F0, F1;
+  read(F0, t0);
+  auto step = [&](Frags& cur, Frags& nxt, int kt) {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of kt landed
+    if constexpr (Q4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // kt+1 landed (NBUF-2 k-steps in flight)
     else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // kt landed for every wave; buffer kt-1 is free
+    __builtin_amdgcn_s_barrier();  // kt+1 landed for every wave; nobody reads buffer kt any more
     asm volatile("" ::: "memory");
-    issue(kt + NBUF - 1);  // into buffer kt-1
-    Frags f;
-    read(f, kt);
-    mfma(f);
+    issue(kt + NBUF);  // into buffer kt
+    read(nxt, kt + 1);
+    compute(cur);
+  };
+  int kt = t0;
+  for (; kt + 2 < t1; kt += 2) {
+    step(F0, F1, kt);
+    step(F1, F0, kt + 1);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (kt + 1 < t1) {
+    step(F0, F1, kt);
+    F0 = F1;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  compute(F0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the redundant tail copies land before exit
 
   const int tile0 = nb * 16 + wn * 4;
 #pragma unroll
