@@ -2804,7 +2804,8 @@ __global__ __launch_bounds__(64 * W) void mq8_wsw_kernel(MMArgs a) {
       const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(a.W) + ((size_t)tile * KT + cb * 4) * TB), (short)0,
       NCH * 4 * TB, 0x00020000);
   const int r = lane & 15;
-  const unsigned qoff = lane * (Q4 ? 8u : 16u), doff = SO + 16 * (r >> 2) + 2 * (r & 3);
+  const unsigned qoff = lane * (Q4 ? 8u : 16u), doff = SO + 16 * (r >> 2) + 4 * ((r & 3) >> 1);
+  const unsigned dsh = 16 * (r & 1);
 
   const u32x4* xsrc[PPT];
   int xdst[PPT];
@@ -2837,7 +2838,10 @@ __global__ __launch_bounds__(64 * W) void mq8_wsw_kernel(MMArgs a) {
   typedef std::conditional_t<Q4, u32x2, u32x4> QT;
   struct Frag {
     QT q[4];
-    uint32_t d0[4], d1[4];  // this lane's weight row: f16 d_w of blocks 0 / 1 of each tile (low half)
+    // f16 d_w of blocks 0 / 1 of each tile: the dword holding this lane's row and its neighbour, the half
+    // selected at use.  16-bit loads made hipcc mask or pack the ring as it arrived -- a wait for every
+    // load, vmcnt(0), before each barrier (round 5: Llama-3-8B gate/up at 32 rows 23.35 -> 21.5 us)
+    uint32_t d0[4], d1[4];
   };
   Frag ring[U];
   auto load_w = [&](Frag& f, int ch) {
@@ -2848,8 +2852,8 @@ __global__ __launch_bounds__(64 * W) void mq8_wsw_kernel(MMArgs a) {
         f.q[k] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(wrs, qoff, so, 2));
       else
         f.q[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, qoff, so, 2));
-      f.d0[k] = __builtin_amdgcn_raw_buffer_load_b16(wrs, doff, so, 0);
-      f.d1[k] = __builtin_amdgcn_raw_buffer_load_b16(wrs, doff + 8, so, 0);
+      f.d0[k] = __builtin_amdgcn_raw_buffer_load_b32(wrs, doff, so, 0);
+      f.d1[k] = __builtin_amdgcn_raw_buffer_load_b32(wrs, doff + 8, so, 0);
     }
   };
   f32x4 acc[NB];
@@ -2880,8 +2884,8 @@ __global__ __launch_bounds__(64 * W) void mq8_wsw_kernel(MMArgs a) {
         b0 = (long)(((unsigned long)f.q[k][1] << 32) | f.q[k][0]);
         b1 = (long)(((unsigned long)f.q[k][3] << 32) | f.q[k][2]);
       }
-      const float w0 = (float)__builtin_bit_cast(_Float16, (uint16_t)f.d0[k]);
-      const float w1 = (float)__builtin_bit_cast(_Float16, (uint16_t)f.d1[k]);
+      const float w0 = (float)__builtin_bit_cast(_Float16, (uint16_t)(f.d0[k] >> dsh));
+      const float w1 = (float)__builtin_bit_cast(_Float16, (uint16_t)(f.d1[k] >> dsh));
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
         const int row = n * 16 + (lane & 15);
@@ -2915,12 +2919,18 @@ __global__ __launch_bounds__(64 * W) void mq8_wsw_kernel(MMArgs a) {
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
-  for (int ch = 0; ch < NCH; ch += U) {
+  // 4 steps per trip either way: the ring's registers are renamed at the back-edge after a vmcnt(0), so
+  // a 2-deep ring goes round twice per trip (21.5 -> 20.95 us; a 4-deep ring spills, 24.4 us; all
+  // steps unconditional, or the chunk loop fully unrolled, spill 115-1850 VGPRs)
+  for (int ch = 0; ch < NCH; ch += 4) {
     step(I0{}, I0{}, ch);
     if (ch + 1 < NCH) step(I1{}, I1{}, ch + 1);
     if constexpr (U == 4) {
       if (ch + 2 < NCH) step(I0{}, I2{}, ch + 2);
       if (ch + 3 < NCH) step(I1{}, I3{}, ch + 3);
+    } else {
+      if (ch + 2 < NCH) step(I0{}, I0{}, ch + 2);
+      if (ch + 3 < NCH) step(I1{}, I1{}, ch + 3);
     }
   }
   // C^T -> the usual layout through this wave's tr
