@@ -2967,7 +2967,8 @@ int launch_mq8_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipStream
   if (off || a.M <= 16 || a.M > 32 || !a.xq || !a.xd || a.K % 256 || a.N % 64) return -1;
   const int ntiles = a.N / TILE_N, NCH = a.K / 256;
   int ks = 1;
-  while (ks < 8 && (ntiles / 4) * ks * 2 <= 256 && NCH / (ks * 2) >= 4) ks *= 2;
+  static const int tgt = getenv("MX_SLAB_TARGET") ? atoi(getenv("MX_SLAB_TARGET")) : 256;  // A/B
+  while (ks < 8 && (ntiles / 4) * ks * 2 <= tgt && NCH / (ks * 2) >= 4) ks *= 2;
   MMArgs p = a;
   p.out = slabs;
   p.ldo = a.N;

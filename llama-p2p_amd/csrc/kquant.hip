@@ -1804,6 +1804,12 @@ static int launch_kq_wide(int epi, const MMArgs& a, int ntiles, hipStream_t s) {
   return -1;
 }
 
+// work-groups the 17..32-row split-K launches aim at (MX_SLAB_TARGET, A/B)
+static int kq_slab_target() {
+  static const int t = getenv("MX_SLAB_TARGET") ? atoi(getenv("MX_SLAB_TARGET")) : 256;
+  return t;
+}
+
 // 17..32 tokens, attn_output / ffn_down of a K-quant file (256 tiles for h 4096): 4-wave groups with K
 // split over grid.y until ~256 work-groups, partials into slabs [ksplit][token][N] that the next
 // RMS_NORM + Q8_K launch (launch_rmsnorm_q8k with slabs) folds into the residual stream in slab
@@ -1813,7 +1819,7 @@ int launch_mkq_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipStream
   if (off || a.M <= 16 || a.M > 32 || a.kq_n != 1 || !a.xq || !a.xd || !a.xb || a.K % 256 || a.N % 64) return -1;
   const int ntiles = a.N / TILE_N, SB = a.K / 256;
   int ks = 1;
-  while (ks < 8 && (ntiles / 4) * ks * 2 <= 256 && SB / (ks * 2) >= 4) ks *= 2;
+  while (ks < 8 && (ntiles / 4) * ks * 2 <= kq_slab_target() && SB / (ks * 2) >= 4) ks *= 2;
   if (ks < 2) return -1;
   MMArgs p = a;
   p.out = slabs;
@@ -1837,7 +1843,7 @@ int launch_mkq_qkv_slab(const MMArgs& a, float* slabs, size_t slab_stride, hipSt
     if (a.kq_tile_end[i] % 4) return -1;
   const int ntiles = a.N / TILE_N, SB = a.K / 256;
   int ks = 1;
-  while (ks < 8 && (ntiles / 4) * ks * 2 <= 256 && SB / (ks * 2) >= 4) ks *= 2;
+  while (ks < 8 && (ntiles / 4) * ks * 2 <= kq_slab_target() && SB / (ks * 2) >= 4) ks *= 2;
   MMArgs p = a;
   p.out = slabs;
   p.ldo = a.N;
