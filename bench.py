@@ -252,6 +252,8 @@ def quant_bench(args, wtype: str, steps: int):
         kname = {"q8_0": "mq8_kernel" if m <= 16 else "mq8_wide_kernel",
                  "q4_0": "mq8_kernel<Q4>" if m <= 16 else "mq8_wide_kernel<Q4>",
                  "q4_k_m": "mkq_pers_kernel" if m <= 16 else "mkq_wide_kernel"}[wtype]
+        if m == 1:  # one token: the form the decode runs, RMS_NORM + quantisation done on load in the GEMV
+            kname += "<quantise-on-load>"
         out[f"gate_up_M{m}"] = {"kernel": kname + "<EPI_SWIGLU>",
                                 "us_per_launch": round(us, 2), "bytes_per_launch": int(kb),
                                 "achieved_gbs": round(kb / us / 1e3, 1), "frac": round(kb / us / 1e3 / HBM_PEAK_GBS, 4)}

@@ -1256,6 +1256,7 @@ int mx_engine::enqueue_forward_q8(int M, const int* pos, const int* slot, void* 
     if (resid(b)) return fail(MX_ERR_ARG, "q8 attn_output launch shape");
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.actf = act_f; c.lda = ff; c.wq4 = wq4;
+    // (a separate RMS_NORM + quantise launch for gate/up measured slower: profiles/round5_quant_batch1_onload.txt)
     operand(c, x, h, L.ffn_norm, M, nullptr);
     if (launch_mq8(EPI_SWIGLU, c, s)) return fail(MX_ERR_ARG, "q8 gate/up launch shape");
     MMArgs d{};
@@ -2628,6 +2629,14 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
     a.M = M;
     if (e->wq8 && kind <= 4) {  // Q8_0 weights: the activations are Q8_0 rows in xq8/xqd
       a.xq = e->xq8; a.xd = e->xqd; a.wq4 = e->wq4;
+      // <= 4 rows: the form the decode runs -- the GEMV quantises its operand on load (gate/up and q|k|v
+      // with the RMS_NORM from the ssq partials)
+      const bool pql = e->q8_on_load(M) && getenv("MX_PROF_PREQUANT") == nullptr;
+      auto ql_operand = [&](const float* src, int K, const float* norm_w) {
+        if (!pql) return;
+        a.xq = nullptr; a.xd = nullptr; a.xf = src; a.norm_w = norm_w; a.eps = e->eps;
+        a.ssq = norm_w ? e->ssq : nullptr; a.np = K / 16;
+      };
       auto qb = e->wq4 ? q4_matrix_bytes : q8_matrix_bytes;
       switch (kind) {
         case 0:
@@ -2636,14 +2645,17 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
           a.kc = e->kcache + e->layer_kv_stride * li; a.vc = e->vcache + e->layer_kv_stride * li;
           a.n_ctx = e->n_ctx; a.ctx_stride = e->ctx_stride; a.n_head_kv = e->n_head_kv; a.slot_stride = e->slot_stride;
           per = qb(h + 2 * kv, h);
+          ql_operand(e->x, h, L.attn_norm);
           return launch_mq8(EPI_QKV, a, s);
         case 1: case 3:
           a.W = kind == 1 ? L.o : L.down; a.N = h; a.K = kind == 1 ? h : ff; a.out = e->x; a.ldo = h;
           per = qb(h, a.K);
+          ql_operand(kind == 1 ? e->attn_f : e->act_f, a.K, nullptr);
           return launch_mq8(EPI_RESID, a, s);
         case 2:
           a.W = L.gu; a.N = 2 * ff; a.K = h; a.actf = e->act_f; a.lda = ff;
           per = qb(2 * ff, h);
+          ql_operand(e->x, h, L.ffn_norm);
           return launch_mq8(EPI_SWIGLU, a, s);
         case 4:
           if (!e->has_head || e->out_kq_head) return -1;
@@ -2655,6 +2667,12 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
     }
     if (e->wkq && kind <= 4) {  // K-quant weights: the activations are Q8_K rows in xq8/xqd/xkb
       a.xq = e->xq8; a.xd = e->xqd; a.xb = e->xkb;
+      const bool pql = e->kq_on_load(M) && getenv("MX_PROF_PREQUANT") == nullptr;  // as the decode runs it
+      auto ql_operand = [&](const float* src, int K, const float* norm_w) {
+        if (!pql) return;
+        a.xq = nullptr; a.xd = nullptr; a.xb = nullptr; a.xf = src; a.norm_w = norm_w; a.eps = e->eps;
+        a.ssq = norm_w ? e->ssq : nullptr; a.np = K / 16;
+      };
       switch (kind) {
         case 0:
           a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.out = e->q; a.ldo = h; a.n_q = h; a.n_kv = kv;
@@ -2663,16 +2681,19 @@ int mx_profile_kernel(mx_engine* e, int kind, int M, int iters, double* us, doub
           a.n_ctx = e->n_ctx; a.ctx_stride = e->ctx_stride; a.n_head_kv = e->n_head_kv; a.slot_stride = e->slot_stride;
           L.kq_qkv.set(a);
           per = L.kq_qkv.bytes;
+          ql_operand(e->x, h, L.attn_norm);
           return launch_mkq(EPI_QKV, a, s);
         case 1: case 3:
           a.W = kind == 1 ? L.o : L.down; a.N = h; a.K = kind == 1 ? h : ff; a.out = e->x; a.ldo = h;
           (kind == 1 ? L.kq_o : L.kq_down).set(a);
           per = (kind == 1 ? L.kq_o : L.kq_down).bytes;
+          ql_operand(kind == 1 ? e->attn_f : e->act_f, a.K, nullptr);
           return launch_mkq(EPI_RESID, a, s);
         case 2:
           a.W = L.gu; a.N = 2 * ff; a.K = h; a.actf = e->act_f; a.lda = ff;
           L.kq_gu.set(a);
           per = L.kq_gu.bytes;
+          ql_operand(e->x, h, L.ffn_norm);
           return launch_mkq(EPI_SWIGLU, a, s);
         case 4:
           if (!e->has_head) return -1;
