@@ -2555,6 +2555,120 @@ static void launch_mq8_ql_m(const MMArgs& a, hipStream_t s) {
   else launch_mq8_ql<EPI, QP, 4, Q4>(a, s);
 }
 
+// One token, K 4096 (Llama-3-8B gate/up): mq8_kernel's block-diagonal quantise-on-load form, but each
+// work-group walks TPW tiles (blockIdx.x, +G, ...) with ONE quantised image -- the RMS_NORM + quantise
+// prologue once per group instead of once per tile (1792 one-tile groups paid it ~4-5 us per launch,
+// profiles/round5_quant_batch1_onload.txt) -- and its weight ring running across the tile seams (as
+// mm_pers_kernel).  Per tile the arithmetic and summation order are mq8_kernel<8,1,1,EPI,4,2,1,Q4,true>'s,
+// so the results are bit-identical.
+template <int TPW, int EPI, bool Q4>
+__global__ __launch_bounds__(512) void mq8_pers_ql_kernel(MMArgs a) {
+  constexpr int KS = 8, NK = 8, U = 4, KT = KS * NK;  // 8 waves x 8 Q8 tiles = K 4096
+  constexpr int TB = Q4 ? Q4_TILE_BYTES : Q8_TILE_BYTES, SO = Q4 ? 512 : 1024;
+  constexpr int QB = NK * Q8_TILE_K + 16, QS = NK * 2;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int kb = w * NK, G = gridDim.x, ntiles = a.N / TILE_N;
+  const int c = lane & 15, q = lane >> 4;
+  __shared__ f32x4 red[2][KS][64];
+  __shared__ __attribute__((aligned(16))) uint8_t qimg_all[KS][QB + 4 * QS];
+  uint8_t* qimg = qimg_all[w];
+  float* dimg = reinterpret_cast<float*>(qimg + QB);
+  auto tile_of = [&](int i) { return min((int)blockIdx.x + i * G, ntiles - 1); };
+
+  // prologue operands (this wave's 512-k slice of x, the norm weights, the ssq partials)
+  f32x4 xv[2], gv[2], sv[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int i = lane * 4 + 256 * p;
+    gv[p] = *reinterpret_cast<const f32x4*>(a.norm_w + kb * Q8_TILE_K + i);
+    xv[p] = *reinterpret_cast<const f32x4*>(a.xf + kb * Q8_TILE_K + i);
+    sv[p] = *reinterpret_cast<const f32x4*>(a.ssq + min(lane * 4 + 256 * p, a.np - 4));
+  }
+  // the weight ring, flat over (tile i, k-tile k): f = i * NK + k
+  u32x4 rq[U];
+  auto load_q = [&](int f) {
+    const uint8_t* t = reinterpret_cast<const uint8_t*>(a.W) + ((size_t)tile_of(f / NK) * KT + kb + f % NK) * TB;
+    if constexpr (Q4) {
+      const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(t) + lane);
+      rq[f % U] = u32x4{v[0], v[1], 0u, 0u};
+    } else {
+      rq[f % U] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t) + lane);
+    }
+  };
+  auto load_dw = [&](int i) {  // this lane's 4 rows' f16 d_w of block c of tile i
+    const int t = kb + (c >> 1);
+    return *reinterpret_cast<const u32x2*>(reinterpret_cast<const uint8_t*>(a.W) + ((size_t)tile_of(i) * KT + t) * TB +
+                                           SO + 16 * q + 8 * (c & 1));
+  };
+#pragma unroll
+  for (int f = 0; f < U; ++f) load_q(f);
+  u32x2 dw = load_dw(0);
+
+  // the image: RMS_NORM scale from the ssq partials (fixed-order double sum), then ggml's Q8_0 blocks
+  {
+    double sum = 0.0;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      if (lane * 4 + 256 * p < a.np)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sum += (double)sv[p][j];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) sum += __shfl_xor(sum, o);
+    const float sc = 1.0f / sqrtf((float)(sum / a.K) + a.eps);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      f32x4 v = xv[p];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (v[j] * sc) * gv[p][j];
+      q8_store_act(v, lane * 4 + 256 * p, reinterpret_cast<int8_t*>(qimg), dimg);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's image is in LDS
+    __builtin_amdgcn_wave_barrier();
+  }
+  // this lane's block c of the slice: the same for every tile
+  const u32x2 xq = *reinterpret_cast<const u32x2*>(qimg + (c >> 1) * Q8_TILE_K + 16 * q + 8 * (c & 1));
+  const float dx = dimg[c];
+
+  constexpr int LU = (EPI == EPI_SWIGLU) ? 32 : 64;
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const u32x2 dwc = dw;
+    if (i + 1 < TPW) dw = load_dw(i + 1);
+    i32x4 C0 = i32x4{0, 0, 0, 0}, C1 = i32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int f = i * NK + k;
+      const u32x4 r = rq[f % U];
+      const long a0 = Q4 ? q4_operand(r[0]) : (long)(((unsigned long)r[1] << 32) | r[0]);
+      const long a1 = Q4 ? q4_operand(r[1]) : (long)(((unsigned long)r[3] << 32) | r[2]);
+      const bool on0 = c == 2 * k, on1 = c == 2 * k + 1;
+      const long b0 = (long)(((unsigned long)(on0 ? xq[1] : 0u) << 32) | (on0 ? xq[0] : 0u));
+      const long b1 = (long)(((unsigned long)(on1 ? xq[1] : 0u) << 32) | (on1 ? xq[0] : 0u));
+      C0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, b0, C0, 0, 0, 0);
+      C1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, b1, C1, 0, 0, 0);
+      if (f + U < TPW * NK) load_q(f + U);
+    }
+    const f16x4 dwh = __builtin_bit_cast(f16x4, dwc);
+    f32x4 ab = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ab[j] = fmaf((float)dwh[j] * dx, (float)(C0[j] + C1[j]), ab[j]);
+    red[i & 1][w][lane] = f32x4{row16_sum(ab[0]), row16_sum(ab[1]), row16_sum(ab[2]), row16_sum(ab[3])};
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only: the ring stays in flight
+    __builtin_amdgcn_s_barrier();
+    const int tile = (int)blockIdx.x + i * G;
+    if (w == 0 && lane < LU && tile < ntiles && (lane & 15) < a.M) {
+      f32x4 sum = red[i & 1][0][lane];
+      f32x4 up = (EPI == EPI_SWIGLU) ? red[i & 1][0][lane + 32] : sum;
+#pragma unroll
+      for (int ww = 1; ww < KS; ++ww) {
+        sum += red[i & 1][ww][lane];
+        if constexpr (EPI == EPI_SWIGLU) up += red[i & 1][ww][lane + 32];
+      }
+      epi_store<EPI>(a, tile, lane, lane & 15, sum, up);
+    }
+  }
+}
+
 bool mq8_can_quantize_on_load(int M, int K, bool norm) {
   const int slice = (K / Q8_TILE_K + 7) / 8 * Q8_TILE_K;
   return M >= 1 && M <= XS_MAX_M && K % Q8_TILE_K == 0 && slice <= 2048 && (!norm || K / 16 <= 512);
@@ -2583,6 +2697,13 @@ static int launch_mq8_epi(const MMArgs& a, hipStream_t s) {
 
 template <int EPI, bool Q4>
 static int launch_mq8_ql_epi(const MMArgs& a, hipStream_t s) {
+  static const bool pers = getenv("MX_NO_Q8_PERS_QL") == nullptr;  // MX_NO_Q8_PERS_QL=1: one tile per group (A/B)
+  if constexpr (EPI == EPI_SWIGLU) {
+    if (pers && a.M == 1 && a.K == 4096 && a.norm_w && a.ssq && a.np == 256 && (a.N / TILE_N) % 7 == 0) {
+      mq8_pers_ql_kernel<7, EPI, Q4><<<a.N / TILE_N / 7, 512, 0, s>>>(a);
+      return 0;
+    }
+  }
   const int slice = (a.K / Q8_TILE_K + 7) / 8 * Q8_TILE_K;
   if (slice <= 512) launch_mq8_ql_m<EPI, 2, Q4>(a, s);
   else if (slice <= 1024) launch_mq8_ql_m<EPI, 4, Q4>(a, s);
