@@ -1,4 +1,5 @@
 # A/B: one-token Q8_0 / Q4_0 gate/up as a tile-walking group with one quantised image (MX_Q8_PERS_QL)
+# (record of the A/B: MX_Q8_PERS_QL became the default afterwards; MX_NO_Q8_PERS_QL=1 now selects the old form)
 set -o pipefail
 O=gpurun_out/r5pql; mkdir -p $O
 MX_Q8_PERS_QL=1 timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_q8_gpu.py tests/test_q4_0_gpu.py > $O/p.log 2>&1 || { tail -30 $O/p.log; exit 1; }
