@@ -1,6 +1,6 @@
 # A/B of the bf16 32-row gate/up GEMV's activation-chunk depth (MX_WIDE_KCT 4 / 8): kernel time, whole
-# (record of a finished A/B: the switch it sets was removed from the engine afterwards -- see git log for the build it ran on)
 # 32-sequence decode step (bench.py main line), and the -m gpu suite at 8
+# (record of a finished A/B: the switch it sets was removed from the engine afterwards -- see git log for the build it ran on)
 set -o pipefail
 O=gpurun_out/r5kct; mkdir -p $O
 for r in 1 2; do for k in 4 8; do

@@ -1,6 +1,6 @@
 # batch-1 Q8_0 / Q4_0: gate/up quantising its operand on load (product) vs a norm + quantise launch
-# (record of a finished A/B: the switch it sets was removed from the engine afterwards -- see git log for the build it ran on)
 # (MX_Q8_GU_NOQL); whole steps (tools/quant_step.py) and per-kernel times in both forms
+# (record of a finished A/B: the switch it sets was removed from the engine afterwards -- see git log for the build it ran on)
 set -o pipefail
 O=gpurun_out/r5ql; mkdir -p $O
 for r in 1 2; do for v in ql noql; do
