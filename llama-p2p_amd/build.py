@@ -20,6 +20,11 @@ ARCH = os.environ.get("MX_OFFLOAD_ARCH", "gfx950")
 SOURCES = [("kernels.hip", "hip"), ("kquant.hip", "hip"), ("engine.cpp", "hip"), ("gguf.cpp", "c++")]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-Wno-unused-variable", "-Wno-unused-result", "-Wno-unused-value"]
+# gfx950's packed-FP32 VALU instructions (v_pk_{fma,mul,add}_f32, v_pk_mov_b32) are switched off for the
+# whole device build: round 5 traced wrong lanes 32-63 under GPU sharing to a v_pk_mul_f32 -> v_pk_fma_f32
+# chain (profiles/round5_rope_packed_hazard.txt) and LLVM's gfx950 hazard recognizer has no wait-state
+# rule for it.  The feature is a device-target feature; the host cc1 ignores it with a note.
+DEVICE_FLAGS = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 
 
 def _stale(obj: str, deps) -> bool:
@@ -38,7 +43,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         o = os.path.join(objdir, src + ".o")
         objs.append(o)
         if force or _stale(o, [s] + headers):
-            cmd = [HIPCC, "-x", lang] + FLAGS + ["-c", s, "-o", o]
+            cmd = [HIPCC, "-x", lang] + FLAGS + DEVICE_FLAGS + ["-c", s, "-o", o]
             if lang == "c++":
                 cmd = [HIPCC, "-x", "c++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-c", s, "-o", o]
             if verbose:

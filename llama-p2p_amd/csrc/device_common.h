@@ -87,6 +87,52 @@ __device__ __forceinline__ f32x4 qkv_cs(const MMArgs& a, int row, int pos) {
   return *reinterpret_cast<const f32x4*>(a.rope_cs + ((size_t)p * (d / 2) + (rl % d) / 2) * 2);
 }
 
+// ---------------------------------------------------------------------------
+// RMS_NORM sums of squares, one definition for every kernel that forms them (batch invariance:
+// a row's scale must not depend on which kernel -- RMS_NORM on load at <= 4 rows, norm_kernel at
+// more -- computed it, DESIGN.md §1 "batch invariance").
+//   tile partial (16 consecutive values, f32): g_i = sequential double sums of the squares of
+//     values 4i..4i+3 (each square rounded to f32, as ggml forms x*x), ((g0 + g1) + (g2 + g3))
+//     rounded to f32 -- the shape the EPI_RESID epilogues produce with their C layout (lanes
+//     l, l^16, l^32, l^48 hold the tile's 4 groups);
+//   row sum (double): lane l of a wave sums partials 4l..4l+3, then 256+4l..256+4l+3, ...
+//     sequentially, then a xor butterfly over the 64 lanes (o = 1, 2, ..., 32).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double ssq4(f32x4 v) {
+#pragma clang fp contract(off)
+  double q = (double)(v[0] * v[0]);
+  q += (double)(v[1] * v[1]);
+  q += (double)(v[2] * v[2]);
+  q += (double)(v[3] * v[3]);
+  return q;
+}
+// the tile partial from its four groups (a, b, c, d = values 0-3, 4-7, 8-11, 12-15)
+__device__ __forceinline__ float ssq16(f32x4 a, f32x4 b, f32x4 c, f32x4 d) {
+#pragma clang fp contract(off)
+  return (float)((ssq4(a) + ssq4(b)) + (ssq4(c) + ssq4(d)));
+}
+// lane part of the row sum: partials 4l+256p .. +3 for p = 0, 1, ... (np % 4 == 0); q[p] holds them
+template <int P>
+__device__ __forceinline__ double ssq_lane(const f32x4 (&q)[P], int lane, int np) {
+#pragma clang fp contract(off)
+  double acc = 0.0;
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+    if (lane * 4 + 256 * p < np)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc += (double)q[p][j];
+  return acc;
+}
+__device__ __forceinline__ double ssq_wave(double acc) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) acc += __shfl_xor(acc, o);
+  return acc;
+}
+__device__ __forceinline__ float rms_scale(double sum, int n, float eps) {
+  return 1.0f / sqrtf((float)(sum / n) + eps);
+}
+
 // RoPE (mode NORM) of two adjacent pairs (s0, s1), (s2, s3) by their (cos, sin) in c: o0 = s0 c0 - s1 c1,
 // ... as four scalar fmas.  Every operand passes through an empty asm so that the SLP vectorizer
 // cannot turn them into v_pk_mul_f32 / v_pk_fma_f32 chains: compiled packed, the result's third

@@ -209,6 +209,10 @@ struct mx_engine {
   // rows of the next forward come in blocks of 16 consecutive positions of one sequence (prefill):
   // attention runs as attn_prefill_kernel, 16 queries per K/V pass
   bool rows_blocked = false;
+  // the next forward is a prompt chunk from the scheduler or a pipeline prefill: every row count takes
+  // the GEMM path (one K range per output: the arithmetic of a prompt row does not depend on how many
+  // rows share its chunk -- batch invariance)
+  bool prefill_gemm = false;
   bool use_wide = getenv("MX_NO_WIDE") == nullptr;  // 17..64-row forward through mm_wide (LDS-shared activations)
   float* slabs = nullptr;                           // split-K partials [8][MAX_ROWS][n_embd + 2 n_embd_kv]
   size_t slab_stride = 0;
@@ -216,8 +220,9 @@ struct mx_engine {
   // K-quant model prefill: one layer's four matrices dequantised to packed bf16 for the GEMM path
   uint16_t *kqd_qkv = nullptr, *kqd_o = nullptr, *kqd_gu = nullptr, *kqd_down = nullptr;
   static constexpr size_t GSLAB_FLOATS = (size_t)32 << 20;
-  // work-groups a split prefill GEMM aims at (MX_GEMM_SPLIT_TARGET; 0 = one K range per tile)
-  int gemm_split_target = getenv("MX_GEMM_SPLIT_TARGET") ? atoi(getenv("MX_GEMM_SPLIT_TARGET")) : 256;
+  // work-groups a split prefill GEMM aims at (MX_GEMM_SPLIT_TARGET; 0 = one K range per tile).  Default 0:
+  // a split chosen from the chunk's row count would make a prompt's values depend on its chunk-mates
+  int gemm_split_target = getenv("MX_GEMM_SPLIT_TARGET") ? atoi(getenv("MX_GEMM_SPLIT_TARGET")) : 0;
   int ctx_stride = 0;  // KV positions allocated per slot (n_ctx rounded up to KV_POS_ALIGN)
   uint64_t weight_bytes = 0;
 
@@ -353,6 +358,18 @@ struct mx_engine {
   bool gemm_ok() const {  // chunks of PREFILL_ROWS rows can run (the Q8_0 / K-quant paths take any row count)
     return wq8 || wkq || gemm_shapes();
   }
+  // rows form blocks of 16 (from row 0) of one slot each, positions consecutive within a block except
+  // that a block may end in copies of its last real row (same position and token: the prompt padding
+  // near n_ctx) -- what attn_prefill_kernel needs (every key position a block reads is written by it)
+  bool blocked_rows(const int32_t* slots, const int32_t* pos, const int32_t* ids, int m) const {
+    for (int k = 0; k < m; k++) {
+      if (k % 16 == 0) continue;
+      if (slots[k] != slots[k - 1]) return false;
+      if (pos[k] == pos[k - 1] + 1) continue;
+      if (pos[k] != pos[k - 1] || (ids && ids[k] != ids[k - 1])) return false;
+    }
+    return true;
+  }
   int enqueue_forward_wide(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap,
                            int n_out, bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride,
                            int* hist_count, int max_hist, hipStream_t s);
@@ -389,6 +406,7 @@ int mx_engine::init_common() {
   if (n_embd % n_head || n_head % n_head_kv) return fail(MX_ERR_MODEL, "head counts do not divide n_embd/n_head");
   if (head_dim != 64 && head_dim != 128) return fail(MX_ERR_ARG, "head_dim must be 64 or 128");
   if (n_embd > 8192) return fail(MX_ERR_ARG, "n_embd > 8192 is not supported");
+  if (n_embd % 64) return fail(MX_ERR_ARG, "n_embd must be a multiple of 64 (RMS_NORM tile partials)");
   const int G = n_head / n_head_kv;
   if (G != 1 && G != 2 && G != 4 && G != 8) return fail(MX_ERR_ARG, "n_head/n_head_kv must be 1,2,4 or 8");
   if (n_embd % 32 || n_ff % 32 || n_vocab % 16 || n_embd_kv % 16)
@@ -1020,7 +1038,7 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
                                      hist_stride, hist_count, max_hist, s);
   if (wq8) return enqueue_forward_q8(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next, pos_next, hist,
                                      hist_stride, hist_count, max_hist, s);
-  if (M > MAX_ROWS) {
+  if (M > MAX_ROWS || (prefill_gemm && gemm_shapes() && !argmax)) {
     if (!gemm_ok() || argmax || (head && n_out > MAX_ROWS))
       return fail(MX_ERR_ARG, "forward of > 64 rows: GEMM shapes only, logits for <= 64 rows");
     return enqueue_forward_gemm(M, pos, slot, x_out, head, rowmap, n_out, s);
@@ -1482,7 +1500,11 @@ int mx_engine::enqueue_forward_gemm(int M, const int* pos, const int* slot, void
     } else {
       launch_rmsnorm(xn, h, x, out_norm, rowmap, n_out, h, eps, s);
       g.X = xn; g.ldx = h;
-      if (launch_mm(EPI_F32, g, s)) return fail(MX_ERR_ARG, "lm_head launch shape");
+      // the decode GEMVs (canonical K order at every row count), so a prompt's first token does not
+      // depend on how many prompts ended in its chunk
+      const int rc = (n_out > 16 && use_wide) ? (launch_mm_wide(EPI_F32, g, slabs, slab_stride, s) < 0 ? 1 : 0)
+                                              : launch_mm(EPI_F32, g, s);
+      if (rc) return fail(MX_ERR_ARG, "lm_head launch shape");
     }
   }
   HIPC(hipGetLastError());
@@ -1529,9 +1551,7 @@ int mx_engine::forward_rows_chunk(int n, const int32_t* slots, const int32_t* po
   std::vector<int32_t> sorted(slots, slots + n);
   std::sort(sorted.begin(), sorted.end());
   rows_distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-  rows_blocked = true;
-  for (int i = 0; i < n && rows_blocked; i++)
-    if (i % 16 && (slots[i] != slots[i - i % 16] || pos[i] != pos[i - i % 16] + i % 16)) rows_blocked = false;
+  rows_blocked = blocked_rows(slots, pos, x_in ? nullptr : ids, n);
   if (head && last_row_only) {
     const int32_t last = n - 1;
     if (int rc = h2d(d_rowmap, &last, 1, 3)) return rc;
@@ -1664,8 +1684,11 @@ int mx_engine::prefill_batch(std::vector<Request*>& reqs) {
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     }
   } log{t0, reqs.size()};
+  // every prompt's rows start a 16-row block and are padded to whole blocks (positions past the prompt,
+  // overwritten by its decode later; near n_ctx copies of the last row), so each chunk is blocked
+  // (attn_prefill_kernel) and a prompt's blocks are the same whatever shares its chunk
   std::vector<int32_t> slots, pos, ids;
-  std::vector<int> end_row(reqs.size());
+  std::vector<int> end_row(reqs.size()), blk_end(reqs.size());
   for (size_t q = 0; q < reqs.size(); q++) {
     Request* r = reqs[q];
     const int n = (int)r->prompt.size();
@@ -1676,12 +1699,12 @@ int mx_engine::prefill_batch(std::vector<Request*>& reqs) {
     }
     end_row[q] = (int)slots.size() - 1;
     const int pad = (16 - (n - r->reuse) % 16) % 16;
-    if (n + pad <= n_ctx)
-      for (int p = n; p < n + pad; p++) {
-        slots.push_back(r->slot);
-        pos.push_back(p);
-        ids.push_back(r->prompt[n - 1]);
-      }
+    for (int k = 0; k < pad; k++) {
+      slots.push_back(r->slot);
+      pos.push_back(n + pad <= n_ctx ? n + k : n - 1);
+      ids.push_back(r->prompt[n - 1]);
+    }
+    blk_end[q] = (int)slots.size();
     r->pos = n;
   }
   const int chunk = gemm_ok() ? PREFILL_ROWS : MAX_ROWS;
@@ -1704,7 +1727,7 @@ int mx_engine::prefill_batch(std::vector<Request*>& reqs) {
     int e = std::min(total, i + chunk);
     size_t q1 = q0;
     while (q1 < reqs.size() && end_row[q1] < e && (int)(q1 - q0) < MAX_ROWS) q1++;
-    if ((int)(q1 - q0) == MAX_ROWS && q1 < reqs.size() && end_row[q1] < e) e = end_row[q1 - 1] + 1;
+    if ((int)(q1 - q0) == MAX_ROWS && q1 < reqs.size() && end_row[q1] < e) e = blk_end[q1 - 1];
     const int m = e - i, n_out = (int)(q1 - q0);
     std::vector<int32_t> rowmap(n_out);
     for (int k = 0; k < n_out; k++) rowmap[k] = end_row[q0 + k] - i;
@@ -1714,13 +1737,12 @@ int mx_engine::prefill_batch(std::vector<Request*>& reqs) {
     HIPC(hipMemcpyAsync(d_slot, slots.data() + i, m * 4, hipMemcpyHostToDevice, st));
     if (n_out) HIPC(hipMemcpyAsync(d_rowmap, rowmap.data(), n_out * 4, hipMemcpyHostToDevice, st));
     rows_distinct = false;
-    rows_blocked = true;
-    for (int k = 0; k < m && rows_blocked; k++)
-      if (k % 16 && (slots[i + k] != slots[i + k - k % 16] || pos[i + k] != pos[i + k - k % 16] + k % 16))
-        rows_blocked = false;
+    rows_blocked = blocked_rows(slots.data() + i, pos.data() + i, ids.data() + i, m);
+    prefill_gemm = true;
     const int frc = enqueue_forward(m, d_ids, d_pos, d_slot, nullptr, nullptr, n_out > 0, n_out ? d_rowmap : nullptr,
                                     n_out, false, nullptr, nullptr, nullptr, 0, nullptr, 0, st);
     rows_blocked = false;
+    prefill_gemm = false;
     if (frc) return frc;
     int ktop = 0;
     if (n_out && dev_pick) {
@@ -2471,7 +2493,8 @@ int mx_stage_rows_pick(mx_engine* e, int n, const int32_t* slots, const int32_t*
   for (int i = 0; i < n;) {
     int end = std::min(n, i + chunk), k1 = k0;
     while (k1 < n_out && rowmap[k1] < end && k1 - k0 < MAX_ROWS) k1++;
-    if (k1 - k0 == MAX_ROWS && k1 < n_out && rowmap[k1] < end) end = rowmap[k1 - 1] + 1;
+    // cut after the 64th prompt's last row, rounded up to its 16-row block (the prompts' padding)
+    if (k1 - k0 == MAX_ROWS && k1 < n_out && rowmap[k1] < end) end = std::min(n, (rowmap[k1 - 1] + 16) / 16 * 16);
     const int m = end - i, no = k1 - k0;
     for (int r = i; r < end; r++) {
       if (slots[r] < 0 || slots[r] >= e->n_seq_max) return fail(MX_ERR_ARG, "slot out of range");
@@ -2490,10 +2513,8 @@ int mx_stage_rows_pick(mx_engine* e, int n, const int32_t* slots, const int32_t*
       for (int r = i; r < end; r++) e->slot_tokens[slots[r]].clear();
     }
     e->rows_distinct = false;
-    e->rows_blocked = true;
-    for (int r = 0; r < m && e->rows_blocked; r++)
-      if (r % 16 && (slots[i + r] != slots[i + r - r % 16] || pos[i + r] != pos[i + r - r % 16] + r % 16))
-        e->rows_blocked = false;
+    e->rows_blocked = e->blocked_rows(slots + i, pos + i, x_in ? nullptr : ids + i, m);
+    e->prefill_gemm = true;
     e->pick_samp = ktop > 0 ? e->d_samp : nullptr;
     e->pick_k = ktop;
     const char* xi = (const char*)x_in;
@@ -2502,6 +2523,7 @@ int mx_stage_rows_pick(mx_engine* e, int n, const int32_t* slots, const int32_t*
                                        xo ? xo + i * xb : nullptr, no > 0, no ? e->d_rowmap : nullptr, no, false,
                                        nullptr, nullptr, nullptr, 0, nullptr, 0, s);
     e->rows_blocked = false;
+    e->prefill_gemm = false;
     if (!frc && no) e->pick(no, nullptr, nullptr, nullptr, 0, nullptr, 0, s);  // logits rows [no][V]
     e->pick_samp = nullptr;
     e->pick_k = 0;

@@ -99,6 +99,11 @@ struct MMArgs {
   int kq_type[3];
   int kq_tile_end[3];
   size_t kq_off[3];
+  // bf16 GEMVs, batch invariance: K is cut into 16 canonical slices
+  // [KT*j/16, KT*(j+1)/16) and a row's sum is ((slices of group 0) + (slices of group 1)) + ...
+  // over kgrp groups of 16/kgrp consecutive slices -- set by the launchers from the shape alone
+  // (canon_kgroups), never by the row count
+  int kgrp;
 };
 
 
@@ -120,6 +125,8 @@ void launch_ssq(const float* x, int M, int n, float* ssq, hipStream_t s);
 void launch_rmsnorm(uint16_t* y, int ldy, const float* x, const float* w, const int* row_map, int M, int n,
                     float eps, hipStream_t s);
 int launch_mm(int epi, const MMArgs& a, hipStream_t s);
+// canonical K groups of a bf16 GEMV shape (= the K split of its 17..64-row mm_wide launch)
+int canon_kgroups(int epi, int N, int K);
 bool mm_can_norm_on_load(int M, int K);
 // <= 16 rows, row-tile-persistent gate/up: -1 if the shape has no instantiation
 bool mm_pers_supported(int epi, int M, int N, int K);

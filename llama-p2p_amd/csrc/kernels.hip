@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void embed_kernel(float* x, const uint16_t* to
   const u32x4* src = reinterpret_cast<const u32x4*>(tok_embd + (size_t)id * n);
   f32x4* dst = reinterpret_cast<f32x4*>(x + (size_t)c * n);
   for (int t = threadIdx.x; t < n / 16; t += blockDim.x) {
-    double q = 0.0;
+    f32x4 g[4];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const u32x4 v = src[2 * t + h];
@@ -96,10 +96,10 @@ __global__ __launch_bounds__(256) void embed_kernel(float* x, const uint16_t* to
       hi[2] = __uint_as_float(v[3] << 16); hi[3] = __uint_as_float(v[3] & 0xffff0000u);
       dst[4 * t + 2 * h] = lo;
       dst[4 * t + 2 * h + 1] = hi;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) q += (double)(lo[i] * lo[i]) + (double)(hi[i] * hi[i]);
+      g[2 * h] = lo;
+      g[2 * h + 1] = hi;
     }
-    if (ssq) ssq[(size_t)c * (n / 16) + t] = (float)q;
+    if (ssq) ssq[(size_t)c * (n / 16) + t] = ssq16(g[0], g[1], g[2], g[3]);
   }
 }
 
@@ -111,16 +111,8 @@ void launch_embed(float* x, const uint16_t* tok_embd, const int* ids, int M, int
 __global__ __launch_bounds__(256) void ssq_kernel(const float* x, int n, float* ssq) {
   const int c = blockIdx.x;
   const f32x4* src = reinterpret_cast<const f32x4*>(x + (size_t)c * n);
-  for (int t = threadIdx.x; t < n / 16; t += blockDim.x) {
-    double q = 0.0;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const f32x4 v = src[4 * t + h];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) q += (double)(v[i] * v[i]);
-    }
-    ssq[(size_t)c * (n / 16) + t] = (float)q;
-  }
+  for (int t = threadIdx.x; t < n / 16; t += blockDim.x)
+    ssq[(size_t)c * (n / 16) + t] = ssq16(src[4 * t], src[4 * t + 1], src[4 * t + 2], src[4 * t + 3]);
 }
 
 void launch_ssq(const float* x, int M, int n, float* ssq, hipStream_t s) { ssq_kernel<<<M, 256, 0, s>>>(x, n, ssq); }
@@ -130,10 +122,13 @@ void launch_ssq(const float* x, int M, int n, float* ssq, hipStream_t s) { ssq_k
 // ggml: sum of x*x in double, scale = 1/sqrtf(mean + eps), y = (x*scale)*w;
 // the bf16 rounding is the conversion ggml applies to src1 of the next MUL_MAT.
 // ---------------------------------------------------------------------------
-// x[r] += sum of NS partial slabs (fixed order, written back when NS > 0); then, if y,
+// x[r] += (sum of NS partial slabs in slab order; written back when NS > 0) -- the same expression
+// as the <= 16-row EPI_RESID epilogues, x + (((s0 + s1) + s2) + ...); then, if y,
 // y[c] = bf16((x[r] * 1/sqrtf(mean(x^2) + eps)) * w) with the sum of squares in double (ggml
-// RMS_NORM + MUL).  One 1024-thread work-group per row and every load issued up front: a
-// single memory round trip, which is what a row of 4096-8192 floats costs at decode.
+// RMS_NORM + MUL), formed exactly as RMS_NORM on load forms it (device_common.h ssq16 / ssq_lane /
+// ssq_wave: 16-value tile partials in LDS, then one wave's canonical row sum), so a row normalises
+// to the same bits at every row count.  One 1024-thread work-group per row and every load issued
+// up front: a single memory round trip, which is what a row of 4096-8192 floats costs at decode.
 template <int NS, int IT>
 __global__ __launch_bounds__(1024) void norm_kernel(uint16_t* y, int ldy, float* x, const float* slabs, size_t stride,
                                                     const float* w, const int* row_map, int n, float eps) {
@@ -156,25 +151,33 @@ __global__ __launch_bounds__(1024) void norm_kernel(uint16_t* y, int ldy, float*
   if constexpr (NS > 0) {
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
+      f32x4 t = sl[it][0];
 #pragma unroll
-      for (int k = 0; k < NS; ++k) v[it] += sl[it][k];
+      for (int k = 1; k < NS; ++k) t += sl[it][k];
+      v[it] += t;
       *reinterpret_cast<f32x4*>(xr + (it * 1024 + tid) * 4) = v[it];
     }
   }
   if (!y) return;
-  double acc = 0.0;
+  __shared__ __attribute__((aligned(16))) float part[IT * 256];
+  __shared__ float sc_sh;
 #pragma unroll
-  for (int it = 0; it < IT; ++it)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc += (double)(v[it][j] * v[it][j]);
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-  __shared__ double part[16];
-  if ((tid & 63) == 0) part[tid >> 6] = acc;
+  for (int it = 0; it < IT; ++it) {  // thread 4T+i holds values 4i..4i+3 of tile T (+256 it)
+    double g = ssq4(v[it]);
+    g += __shfl_xor(g, 1);
+    g += __shfl_xor(g, 2);
+    if ((tid & 3) == 0) part[it * 256 + (tid >> 2)] = (float)g;
+  }
   __syncthreads();
-  double sum = 0.0;
+  if (tid < 64) {
+    f32x4 q[IT];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) sum += part[k];
-  const float scale = 1.0f / sqrtf((float)(sum / n) + eps);
+    for (int p = 0; p < IT; ++p) q[p] = *reinterpret_cast<const f32x4*>(part + 256 * p + 4 * tid);
+    const double sum = ssq_wave(ssq_lane(q, tid, n / 16));
+    if (tid == 0) sc_sh = rms_scale(sum, n, eps);
+  }
+  __syncthreads();
+  const float scale = sc_sh;
   uint16_t* yr = y + (size_t)c * ldy;
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
@@ -195,27 +198,41 @@ static void launch_norm_ns(uint16_t* y, int ldy, float* x, const float* slabs, s
 }
 
 // n must be 4096 or 8192 for the 1024-thread layout; other widths use the generic path below
+// (n % 64 == 0, n <= NORM_GENERIC_MAXN)
+constexpr int NORM_GENERIC_MAXN = 16384;
 __global__ __launch_bounds__(256) void norm_generic_kernel(uint16_t* y, int ldy, float* x, const float* slabs,
                                                            int nslab, size_t stride, const float* w,
                                                            const int* row_map, int n, float eps) {
   const int c = blockIdx.x;
   const int r = row_map ? row_map[c] : c;
   float* xr = x + (size_t)r * n;
-  double acc = 0.0;
-  for (int i = threadIdx.x * 4; i < n; i += 1024) {
+  __shared__ __attribute__((aligned(16))) float part[NORM_GENERIC_MAXN / 16];
+  __shared__ float sc_sh;
+  for (int i = threadIdx.x * 4; i < n; i += 1024) {  // n % 64 == 0: the 4 threads of a tile share a pass
     f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
-    for (int k = 0; k < nslab; ++k) v += *reinterpret_cast<const f32x4*>(slabs + k * stride + (size_t)r * n + i);
-    if (nslab) *reinterpret_cast<f32x4*>(xr + i) = v;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc += (double)(v[j] * v[j]);
+    if (nslab) {
+      f32x4 t = *reinterpret_cast<const f32x4*>(slabs + (size_t)r * n + i);
+      for (int k = 1; k < nslab; ++k) t += *reinterpret_cast<const f32x4*>(slabs + k * stride + (size_t)r * n + i);
+      v += t;
+      *reinterpret_cast<f32x4*>(xr + i) = v;
+    }
+    double g = ssq4(v);
+    g += __shfl_xor(g, 1);
+    g += __shfl_xor(g, 2);
+    if ((threadIdx.x & 3) == 0) part[i >> 4] = (float)g;
   }
   if (!y) return;
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-  __shared__ double part[4];
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
   __syncthreads();
-  const double sum = part[0] + part[1] + part[2] + part[3];
-  const float scale = 1.0f / sqrtf((float)(sum / n) + eps);
+  if (threadIdx.x < 64) {
+    constexpr int P = NORM_GENERIC_MAXN / 4096;
+    f32x4 q[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) q[p] = *reinterpret_cast<const f32x4*>(part + min(256 * p + 4 * (int)threadIdx.x, n / 16 - 4));
+    const double sum = ssq_wave(ssq_lane(q, threadIdx.x, n / 16));
+    if (threadIdx.x == 0) sc_sh = rms_scale(sum, n, eps);
+  }
+  __syncthreads();
+  const float scale = sc_sh;
   uint16_t* yr = y + (size_t)c * ldy;
   for (int i = threadIdx.x * 4; i < n; i += 1024) {
     const f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
@@ -240,6 +257,7 @@ static void launch_norm_impl(uint16_t* y, int ldy, float* x, const float* slabs,
       case 4: launch_norm_ns<4>(y, ldy, x, slabs, stride, w, row_map, M, n, eps, s); return;
     }
   }
+  if (n % 64 || n > NORM_GENERIC_MAXN) return;  // init_common rejects such widths (engine.cpp)
   norm_generic_kernel<<<M, 256, 0, s>>>(y, ldy, x, slabs, nslab, stride, w, row_map, n, eps);
 }
 
@@ -305,15 +323,7 @@ __device__ __forceinline__ void xs_build(const XsRegs<MM>& r, const MMArgs& a, u
 #pragma unroll
   for (int c = 0; c < MM; ++c) {
     if (c >= a.M) break;
-    double acc = 0.0;
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-      if (i0 + 256 * p < a.np)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc += (double)r.q[c][p][j];
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) acc += __shfl_xor(acc, o);
-    const float sc = 1.0f / sqrtf((float)(acc / a.K) + a.eps);
+    const float sc = rms_scale(ssq_wave(ssq_lane(r.q[c], lane, a.np)), a.K, a.eps);
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const int i = i0 + 256 * p;
@@ -326,6 +336,29 @@ __device__ __forceinline__ void xs_build(const XsRegs<MM>& r, const MMArgs& a, u
       }
     }
   }
+}
+
+// Canonical fold of the KS per-wave K-slice partials (batch invariance): with KS = 16
+// the waves' slices are the 16 canonical slices, summed as G groups of 16/G consecutive slices (each
+// group in slice order), then the group sums in order -- exactly the value the 17..64-row path forms
+// (mm_wide: one work-group per group, each wave folding its slices as they end; the slabs then added
+// in slab order).  get(ww) returns wave ww's partial.
+template <int KS, int UNR = KS, typename F>
+__device__ __forceinline__ f32x4 kfold(const F& get, int kgrp) {
+  const int G = (kgrp > 0 && KS % kgrp == 0) ? kgrp : 1;
+  const int mm = KS / G - 1;  // KS / G is a power of two
+  f32x4 s = get(0), part = s;
+#pragma unroll UNR
+  for (int ww = 1; ww < KS; ++ww) {
+    const f32x4 v = get(ww);
+    if (ww & mm) {
+      part += v;
+    } else {
+      s = (ww - 1 == mm) ? part : s + part;  // group (ww-1)/(mm+1) complete
+      part = v;
+    }
+  }
+  return KS - 1 == mm ? part : s + part;
 }
 
 template <int KS, int RT, int NB, int EPI, int U, bool XS>
@@ -436,9 +469,7 @@ __device__ __forceinline__ void mm_body(const MMArgs& a, int tile0) {
     const int n = (u / LU) % NB;
     const int r = (u / LU) / NB;
     const int col = n * 16 + (l & 15);
-    f32x4 s = red[0][r][n][l];
-#pragma unroll
-    for (int ww = 1; ww < KS; ++ww) s += red[ww][r][n][l];
+    const f32x4 s = kfold<KS>([&](int ww) { return red[ww][r][n][l]; }, a.kgrp);
     if constexpr (EPI == EPI_RESID) {
       // residual add, and this tile's share of the next RMS_NORM's sum of squares: a wave holds one
       // whole (r, n) unit block (LU = 64), so lanes l, l^16, l^32, l^48 hold the tile's 16 rows of col
@@ -447,8 +478,7 @@ __device__ __forceinline__ void mm_body(const MMArgs& a, int tile0) {
         f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + (tile0 + r) * 16 + (l >> 4) * 4);
         const f32x4 xv = *px + s;
         *px = xv;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) q += (double)(xv[i] * xv[i]);
+        q = ssq4(xv);
       }
       if (a.ssq) {
         q += __shfl_xor(q, 16);
@@ -459,11 +489,7 @@ __device__ __forceinline__ void mm_body(const MMArgs& a, int tile0) {
     }
     if (col >= a.M) continue;
     f32x4 up = s;
-    if constexpr (EPI == EPI_SWIGLU) {
-      up = red[0][r][n][l + 32];
-#pragma unroll
-      for (int ww = 1; ww < KS; ++ww) up += red[ww][r][n][l + 32];
-    }
+    if constexpr (EPI == EPI_SWIGLU) up = kfold<KS>([&](int ww) { return red[ww][r][n][l + 32]; }, a.kgrp);
     epi_store<EPI>(a, tile0 + r, l, col, s, up);
   }
 }
@@ -474,7 +500,9 @@ __global__ __launch_bounds__(64 * KS) void mm_kernel(MMArgs a) {
 }
 
 template <int KS, int RT, int EPI, int U>
-static int launch_mm_cfg(const MMArgs& a, hipStream_t s) {
+static int launch_mm_cfg(const MMArgs& a0, hipStream_t s) {
+  MMArgs a = a0;
+  a.kgrp = canon_kgroups(EPI, a.N, a.K);
   const int nb = (a.M + 15) / 16;
   if ((a.N / TILE_N) % RT) return -1;
   const int grid = a.N / (16 * RT);
@@ -588,16 +616,13 @@ __global__ __launch_bounds__(64 * KS) void mm_pers_kernel(MMArgs a) {
     f32x4 (*rb)[64] = red[i & 1];
     const int l = lane;
     if constexpr (EPI == EPI_RESID) {
-      f32x4 s = rb[0][l];
-#pragma unroll
-      for (int ww = 1; ww < KS; ++ww) s += rb[ww][l];
+      const f32x4 s = kfold<KS>([&](int ww) { return rb[ww][l]; }, a.kgrp);
       double q = 0.0;
       if (col_raw < a.M) {
         f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col_raw * a.ldo + tile * 16 + (l >> 4) * 4);
         const f32x4 xv = pre[i] + s;
         *px = xv;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) q += (double)(xv[j] * xv[j]);
+        q = ssq4(xv);
       }
       if (a.ssq) {
         q += __shfl_xor(q, 16);
@@ -608,13 +633,8 @@ __global__ __launch_bounds__(64 * KS) void mm_pers_kernel(MMArgs a) {
       if (l >= LU || col_raw >= a.M) return;
       // partial unroll: fully unrolled, hipcc hoists all 2*KS LDS reads and spills the ring / B
       // registers around the epilogue (the reloads then wait for the whole ring)
-      f32x4 s = rb[0][l];
-      f32x4 up = (EPI == EPI_SWIGLU) ? rb[0][l + 32] : s;
-#pragma unroll 3
-      for (int ww = 1; ww < KS; ++ww) {
-        s += rb[ww][l];
-        if constexpr (EPI == EPI_SWIGLU) up += rb[ww][l + 32];
-      }
+      const f32x4 s = kfold<KS, 3>([&](int ww) { return rb[ww][l]; }, a.kgrp);
+      const f32x4 up = (EPI == EPI_SWIGLU) ? kfold<KS, 3>([&](int ww) { return rb[ww][l + 32]; }, a.kgrp) : s;
       if constexpr (EPI == EPI_QKV) qkv_store_pre(a, tile * 16 + (l >> 4) * 4, col_raw, s, qpos, qslot, pre[i]);
       else epi_store<EPI>(a, tile, l, col_raw, s, up);
     }
@@ -646,7 +666,9 @@ __global__ __launch_bounds__(64 * KS) void mm_pers_kernel(MMArgs a) {
 
 // grid = N / (16 * TPW) work-groups (every one walks exactly TPW tiles)
 template <int KS, int NKW, int TPW, int EPI, int U>
-static int launch_pers_cfg(const MMArgs& a, hipStream_t s) {
+static int launch_pers_cfg(const MMArgs& a0, hipStream_t s) {
+  MMArgs a = a0;
+  a.kgrp = canon_kgroups(EPI, a.N, a.K);
   const int ntiles = a.N / TILE_N;
   if (a.K != KS * NKW * TILE_K || (size_t)ntiles * a.K * 32 >= (1ull << 31)) return -1;
   const int grid = (ntiles + TPW - 1) / TPW;  // the last tiles of some work-groups are phantoms
@@ -725,9 +747,9 @@ int launch_mm(int epi, const MMArgs& a, hipStream_t s) {
     switch (epi) {
       case EPI_F32: return launch_mm_cfg<16, 1, EPI_F32, 4>(a, s);
       case EPI_RESID: return launch_mm_cfg<16, 1, EPI_RESID, 4>(a, s);
-      case EPI_QKV:  // norm on load: 8-wave groups, 3 per CU, all 384 in one round (profiles/round1_xs_probe.txt)
-        return (a.X == nullptr && a.K / 8 <= 512) ? launch_mm_cfg<8, 1, EPI_QKV, 4>(a, s)
-                                                  : launch_mm_cfg<16, 1, EPI_QKV, 4>(a, s);
+      case EPI_QKV:  // 16 waves = the 16 canonical K slices (round 1's 8-wave norm-on-load groups,
+                     // profiles/round1_xs_probe.txt, folded two slices per wave: not batch-invariant)
+        return launch_mm_cfg<16, 1, EPI_QKV, 4>(a, s);
       case EPI_SWIGLU: return launch_mm_cfg<16, 1, EPI_SWIGLU, 4>(a, s);
     }
     return -1;
@@ -819,11 +841,30 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
     for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(&xs[buf][xrow[i]][xseg[i] * 8]) = xr[set][i];
   };
 
-  f32x4 acc[RTW][NB];
+  f32x4 acc[RTW][NB], tot[RTW][NB];
 #pragma unroll
   for (int r = 0; r < RTW; ++r)
 #pragma unroll
-    for (int n = 0; n < NB; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NB; ++n) acc[r][n] = tot[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // canonical K slices (batch invariance): the MFMA chain restarts from zero at each of
+  // the 16 slice starts [KT*j/16) and is added to tot at the slice's end -- the partials the <= 16-row
+  // GEMVs form with one slice per wave and fold in the same order (kfold).  This block's K range is
+  // slices [16 ks / nks, 16 (ks + 1) / nks) (nks divides 16).
+  const int j0 = (16 * ks) / nks;
+  int jn = j0, jend = (KT * (j0 + 1)) >> 4;
+  auto slice_fold = [&](int kg) {
+    if (kg + 1 == jend) {
+#pragma unroll
+      for (int r = 0; r < RTW; ++r)
+#pragma unroll
+        for (int n = 0; n < NB; ++n) {
+          tot[r][n] = (jn == j0) ? acc[r][n] : tot[r][n] + acc[r][n];
+          acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      ++jn;
+      jend = (KT * (jn + 1)) >> 4;
+    }
+  };
 
   u32x4 ra[U][RTW];
   load_x(0, 0);
@@ -866,6 +907,7 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
         for (int r = 0; r < RTW; ++r)
           ra[H * KCT + kk][r] = __builtin_nontemporal_load(Wp[r] + (size_t)(kb + (c + 2) * KCT + kk) * 64);
       }
+      slice_fold(kb + c * KCT + kk);
     }
     store_x(1 - H, buf ^ 1);
     __syncthreads();
@@ -896,7 +938,7 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
   for (int r = 0; r < RTW; ++r)
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
-      const f32x4 s = acc[r][n];
+      const f32x4 s = tot[r][n];
       f32x4 up = s;
       if constexpr (EPI == EPI_SWIGLU) {
 #pragma unroll
@@ -968,6 +1010,32 @@ static int pick_ksplit(int KT, int target) {
   return KT % (k * 4) == 0 ? k : 0;
 }
 
+// K split (work-groups along K, partial slabs) of the 17..64-row q|k|v / RESID launches -- a function
+// of the shape only; it is also the canonical K grouping of every bf16 GEMV (canon_kgroups).
+// Partial slabs are re-read by the reduce+norm that follows: 4 at most, 8 for ffn_down.
+// cfg: 0: W4 RTW2 (qkv), 1: W2 RTW1 (K <= 8192), 2: W4 RTW1, 3: W3 RTW1 (qkv), 4: W4 RTW2 split 8
+static int wide_split(int epi, int N, int K, int* cfg_out) {
+  const int ntiles = N / TILE_N, KT = K / TILE_K;
+  int cfg, groups;
+  if (epi == EPI_QKV && ntiles % 3 == 0) cfg = 3, groups = ntiles / 3;
+  else if (epi == EPI_RESID && K > 8192 && ntiles % 8 == 0 && ntiles / 8 <= 64) cfg = 4, groups = ntiles / 8;
+  else if (epi == EPI_QKV && ntiles % 8 == 0) cfg = 0, groups = ntiles / 8;
+  else if (K <= 8192 && ntiles % 2 == 0) cfg = 1, groups = ntiles / 2;
+  else cfg = 2, groups = ntiles / 4;
+  // split targets measured in round 5 (profiles/round5_wide_variants_rejected.txt D): q|k|v 4, attn_output 4,
+  // ffn_down 8 beat every 2 / 4 / 8 combination tried
+  const int target = cfg == 4 ? 8 : (cfg == 3 || cfg == 1) ? 4
+                                  : std::min(4, std::max(1, (256 + groups - 1) / std::max(1, groups)));
+  if (cfg_out) *cfg_out = cfg;
+  return KT % 4 ? 0 : pick_ksplit(KT, target);
+}
+
+int canon_kgroups(int epi, int N, int K) {
+  if (epi != EPI_QKV && epi != EPI_RESID) return 1;  // gate/up and the lm_head: one K range per 17..64-row tile
+  const int g = wide_split(epi, N, K, nullptr);
+  return g > 0 ? g : 1;
+}
+
 // Geometry from tools/gemv_sweep.hip (wide) on MI355X, Llama-3-8B shapes at 32 rows
 // (profiles/round1_gemv_sweep_wide.txt): two row tiles per wave, K split until ~256 work-groups.
 int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s, bool qkv_finish) {
@@ -988,19 +1056,9 @@ int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, h
       return launch_wide_cfg<4, 1, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
     case EPI_QKV:
     case EPI_RESID: {
-      // partial slabs are re-read by the reduce+norm that follows: 4 at most, 8 for ffn_down
-      int cfg, groups;  // 0: W4 RTW2 (qkv), 1: W2 RTW1 (K <= 8192), 2: W4 RTW1, 3: W3 RTW1 (qkv), 4: W4 RTW2 split 8
-      if (epi == EPI_QKV && ntiles % 3 == 0) cfg = 3, groups = ntiles / 3;
-      else if (epi == EPI_RESID && a.K > 8192 && ntiles % 8 == 0 && ntiles / 8 <= 64) cfg = 4, groups = ntiles / 8;
-      else if (epi == EPI_QKV && ntiles % 8 == 0) cfg = 0, groups = ntiles / 8;
-      else if (a.K <= 8192 && ntiles % 2 == 0) cfg = 1, groups = ntiles / 2;
-      else cfg = 2, groups = ntiles / 4;
-      // split targets measured in round 5 (profiles/round5_wide_variants_rejected.txt D): q|k|v 4, attn_output 4,
-      // ffn_down 8 beat every 2 / 4 / 8 combination tried
-      const int target = cfg == 4 ? 8 : (cfg == 3 || cfg == 1) ? 4
-                                      : std::min(4, std::max(1, (256 + groups - 1) / std::max(1, groups)));
-      const int ksplit = pick_ksplit(KT, target);
-      if (!ksplit) return -1;
+      int cfg;
+      const int ksplit = wide_split(epi, a.N, a.K, &cfg);
+      if (ksplit <= 0) return -1;
       MMArgs p = a;
       p.out = slabs;
       p.ldo = a.N;
@@ -1307,7 +1365,7 @@ __global__ __launch_bounds__(256) void bf16_to_f32_kernel(float* x, const uint16
   const u32x4* s4 = reinterpret_cast<const u32x4*>(src + (size_t)c * n);
   f32x4* dst = reinterpret_cast<f32x4*>(x + (size_t)c * n);
   for (int t = threadIdx.x; t < n / 16; t += blockDim.x) {
-    double q = 0.0;
+    f32x4 g[4];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const u32x4 v = s4[2 * t + h];
@@ -1318,10 +1376,10 @@ __global__ __launch_bounds__(256) void bf16_to_f32_kernel(float* x, const uint16
       hi[2] = __uint_as_float(v[3] << 16); hi[3] = __uint_as_float(v[3] & 0xffff0000u);
       dst[4 * t + 2 * h] = lo;
       dst[4 * t + 2 * h + 1] = hi;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) q += (double)(lo[i] * lo[i]) + (double)(hi[i] * hi[i]);
+      g[2 * h] = lo;
+      g[2 * h + 1] = hi;
     }
-    if (ssq) ssq[(size_t)c * (n / 16) + t] = (float)q;
+    if (ssq) ssq[(size_t)c * (n / 16) + t] = ssq16(g[0], g[1], g[2], g[3]);
   }
 }
 
@@ -1338,15 +1396,13 @@ __global__ __launch_bounds__(256) void f32_in_kernel(float* x, const float* src,
   const f32x4* s4 = reinterpret_cast<const f32x4*>(src + (size_t)c * n);
   f32x4* d4 = reinterpret_cast<f32x4*>(x + (size_t)c * n);
   for (int t = threadIdx.x; t < n / 16; t += blockDim.x) {
-    double q = 0.0;
+    f32x4 g[4];
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
-      const f32x4 v = s4[4 * t + h];
-      d4[4 * t + h] = v;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) q += (double)(v[i] * v[i]);
+      g[h] = s4[4 * t + h];
+      d4[4 * t + h] = g[h];
     }
-    if (ssq) ssq[(size_t)c * (n / 16) + t] = (float)q;
+    if (ssq) ssq[(size_t)c * (n / 16) + t] = ssq16(g[0], g[1], g[2], g[3]);
   }
 }
 
@@ -1652,8 +1708,12 @@ __global__ __launch_bounds__(64 * G) void attn_prefill_kernel(AttnArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r16 = lane & 15, q4 = lane >> 4;
   const int r0 = blk * 16;
-  const int pos0 = a.pos[r0];
   const int slot = a.slot[r0];
+  // per-row query positions: a block's rows are consecutive positions, possibly ending in copies of
+  // its last row (the scheduler's padding near n_ctx); keys up to the block's last position
+  int qpos[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) qpos[i] = a.pos[min(r0 + 4 * q4 + i, a.M - 1)];
   const int hq = kvh * G + w;
   __shared__ __attribute__((aligned(16))) _Float16 Ps[G][16][CH + 8];
 
@@ -1684,7 +1744,7 @@ __global__ __launch_bounds__(64 * G) void attn_prefill_kernel(AttnArgs a) {
   f32x4 o[DT];
 #pragma unroll
   for (int t = 0; t < DT; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int last = min(pos0 + 15, a.n_ctx - 1);  // newest key any query of the block sees
+  const int last = min(a.pos[min(r0 + 15, a.M - 1)], a.n_ctx - 1);  // newest key any query of the block sees
   for (int p0 = 0; p0 <= last; p0 += CH) {
     f16x8 kf[2][QK], vf[DT];
 #pragma unroll
@@ -1703,11 +1763,11 @@ __global__ __launch_bounds__(64 * G) void attn_prefill_kernel(AttnArgs a) {
 #pragma unroll
       for (int kk = 0; kk < QK; ++kk) s[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qa[kk], kf[t][kk], s[t], 0, 0, 0);
     }
-    // C layout: rows = queries 4*q4+i (position pos0 + row), cols = keys p0 + 16t + r16; causal mask
+    // C layout: rows = queries 4*q4+i (position qpos[i]), cols = keys p0 + 16t + r16; causal mask
     float e[2][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int qp = pos0 + 4 * q4 + i;
+      const int qp = qpos[i];
       const float v0 = (p0 + r16 <= qp) ? s[0][i] * a.scale : -INFINITY;
       const float v1 = (p0 + 16 + r16 <= qp) ? s[1][i] * a.scale : -INFINITY;
       const float mx = row16_max(fmaxf(v0, v1));
@@ -2517,8 +2577,7 @@ __global__ __launch_bounds__(64 * KS) void mq8_kernel(MMArgs a) {
         f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col * a.ldo + (tile0 + r) * 16 + (l >> 4) * 4);
         const f32x4 xv2 = *px + s;
         *px = xv2;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) q += (double)(xv2[i] * xv2[i]);
+        q = ssq4(xv2);
       }
       if (a.ssq) {
         q += __shfl_xor(q, 16);

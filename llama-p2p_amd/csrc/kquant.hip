@@ -193,8 +193,10 @@ __global__ __launch_bounds__(256) void embed_kq_kernel(float* x, const uint8_t* 
   const int c = blockIdx.x;
   const uint8_t* row = tok + (size_t)ids[c] * (n / 256) * bb;
   for (int t = threadIdx.x; t < n / 16; t += blockDim.x) {
-    double q = 0.0;  // this 16-element tile's sum of squares (the RMS_NORM-on-load partial)
-    for (int k = 16 * t; k < 16 * t + 16; ++k) {
+    f32x4 g[4];  // this 16-element tile's values: its RMS_NORM-on-load partial is ssq16 (device_common.h)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int k = 16 * t + i;
       const uint8_t* b = row + (size_t)(k / 256) * bb;
       const int kk = k % 256;
       const int v = kq_value(type, b, kk);
@@ -212,9 +214,9 @@ __global__ __launch_bounds__(256) void embed_kq_kernel(float* x, const uint8_t* 
         y = (d * (float)sc) * (float)v - dmin * (float)mn;
       }
       x[(size_t)c * n + k] = y;
-      q += (double)(y * y);
+      g[i >> 2][i & 3] = y;
     }
-    if (ssq) ssq[(size_t)c * (n / 16) + t] = (float)q;
+    if (ssq) ssq[(size_t)c * (n / 16) + t] = ssq16(g[0], g[1], g[2], g[3]);
   }
 }
 
@@ -1112,9 +1114,7 @@ __device__ __forceinline__ void mkq_body(const MMArgs& a, const uint8_t* W, int 
       const f32x4 xv = *px + s;
       *px = xv;
       if (a.ssq) {
-        double q = 0.0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) q += (double)(xv[i] * xv[i]);
+        double q = ssq4(xv);
         q += __shfl_xor(q, 16);
         q += __shfl_xor(q, 32);
         if (l < 16) a.ssq[(size_t)col * a.np + tile0 + r] = (float)q;

@@ -293,13 +293,13 @@ class Engine:
 
     def submit_many(self, prompts, max_tokens: int, seeds=None, per_request=None, **kw):
         """Several requests queued atomically (one scheduler round admits them all); same sampling
-        keywords as submit() (or ``per_request``: one keyword dict per prompt), one seed per prompt.
-        Returns the request ids."""
+        keywords as submit() (or ``per_request``: one keyword dict per prompt), one seed per prompt,
+        max_tokens one value or one per prompt.  Returns the request ids."""
         n = len(prompts)
         arrs = [_i32(p) for p in prompts]
         ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
         lens = _i32([len(a) for a in arrs])
-        mts = _i32([max_tokens] * n)
+        mts = _i32(list(max_tokens) if hasattr(max_tokens, "__len__") else [max_tokens] * n)
         samp = (MxSampling * n)()
         base = kw
         for i in range(n):

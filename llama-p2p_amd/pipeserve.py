@@ -311,7 +311,7 @@ class StageRunner:
         self.buf_out = executor.alloc_x(self.chunk)
 
     # ---- prefill of the admitted prompts: rows of every prompt back to back (each padded to a
-    # multiple of 16 positions inside n_ctx so chunks form 16-position blocks), in hand-off chunks
+    # multiple of 16 rows so chunks form 16-position blocks whatever else is admitted), in hand-off chunks
     def _prefill(self, admit, M, n_ctx):
         slots, pos, ids, ends = [], [], [], []
         for a in admit:
@@ -321,11 +321,10 @@ class StageRunner:
             pos += list(range(n))
             ids += a["ids"]
             ends.append(len(slots) - 1)
-            pad = (16 - n % 16) % 16
-            if n + pad <= n_ctx:
-                slots += [sl] * pad
-                pos += list(range(n, n + pad))
-                ids += [a["ids"][-1]] * pad
+            pad = (16 - n % 16) % 16  # near n_ctx: copies of the last row (engine.cpp blocked_rows)
+            slots += [sl] * pad
+            pos += list(range(n, n + pad)) if n + pad <= n_ctx else [n - 1] * pad
+            ids += [a["ids"][-1]] * pad
         samp = [(a["samp"], a["seed"], 0, a["ids"][-64:]) for a in admit]
         firsts: List[int] = []
         k0 = 0

@@ -19,7 +19,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _run(world, S=2, M=32, steps=5, chunk=64):
+def _run(world, model="synthetic:llama3-8b:seed=0", S=2, M=32, steps=5, chunk=64):
     import torch
 
     import bench
@@ -55,7 +55,7 @@ def _run(world, S=2, M=32, steps=5, chunk=64):
             torch.cuda.set_device(dev)
             torch.cuda.set_stream(torch.cuda.Stream(device=dev))  # one stream per stage
             lb, le = parts[r]
-            eng = Engine("synthetic:llama3-8b:seed=0", n_ctx=512, n_seq_max=S * M, layer_begin=lb, layer_end=le,
+            eng = Engine(model, n_ctx=512, n_seq_max=S * M, layer_begin=lb, layer_end=le,
                          device=0, handoff_bf16=False)
             comm = pipeserve.LocalComm(hub, r, world) if world > 1 else None
             st = Stage(EngineAdapter(eng), comm, r, world, sh.n_embd, dev, S, dtype=torch.float32)
@@ -93,3 +93,18 @@ def test_two_stage_engines_on_two_streams_bitwise_with_64_row_chunks():
     print({"tokens": ref.shape, "split_equal": bool(np.array_equal(ref, a)), "repeat_equal": bool(np.array_equal(a, b))})
     assert np.array_equal(ref, a), np.argwhere(ref != a)[:10]
     assert np.array_equal(a, b), np.argwhere(a != b)[:10]
+
+
+# Round 6: the other kernel families under sharing -- the <= 16-row decode GEMVs
+# (M = 8: norm launch + 16-wave GEMVs; M = 2: RMS_NORM on load, persistent GEMVs) and the quantised
+# models' 17..64-row prompt chunks and 32-row decode (Q8_0: mq8_* kernels; Q4_K_M: mkq_* kernels).  The
+# product build has no packed-FP32 instruction left (tools/isa_scan.py); these legs
+# check the families the round-5 fix did not touch.
+@pytest.mark.parametrize("model,M", [("synthetic:llama3-8b:seed=0", 8), ("synthetic:llama3-8b:seed=0", 2),
+                                     ("synthetic:llama3-8b:seed=0:q8_0", 32),
+                                     ("synthetic:llama3-8b:seed=0:q4_k_m", 32)])
+def test_two_streams_bitwise_other_kernel_families(model, M):
+    ref = _run(1, model=model, M=M)
+    a = _run(2, model=model, M=M)
+    print({"model": model, "M": M, "tokens": ref.shape, "split_equal": bool(np.array_equal(ref, a))})
+    assert np.array_equal(ref, a), np.argwhere(ref != a)[:10]
