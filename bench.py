@@ -617,6 +617,7 @@ def main():
         # plain `python3 bench.py --gpus N`: start the N ranks here (before anything touches the GPU)
         os.environ["MX_LAUNCHER"] = "bench.py (launch.spawn_ranks)"
         sys.exit(launch.spawn_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+    launch.rank_init()  # a rank started by spawn_ranks dies with its launcher
     if args.probe_only:
         print(json.dumps(hbm_probe()), flush=True)
         return

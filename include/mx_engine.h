@@ -43,6 +43,7 @@ extern "C" {
 #define MX_ERR_CTX (-4)      /* prompt does not fit n_ctx (Llama raises ValueError) */
 #define MX_ERR_NOTFOUND (-5) /* unknown request id */
 #define MX_ERR_STATE (-6)    /* engine shutting down / wrong pipeline stage for this call */
+#define MX_DEBUG_STOPPED 1   /* a 17..64-row forward ended at the mx_debug stop (diagnosis only) */
 
 #define MX_FINISH_LENGTH 0 /* max_tokens or n_ctx reached  ("length") */
 #define MX_FINISH_STOP 1   /* end-of-generation token       ("stop")   */
@@ -189,8 +190,10 @@ int mx_stage_rows_pick(mx_engine* e, int n, const int32_t* slots, const int32_t*
  * HIP events on the engine stream (benchmark roofline); kind: 0 qkv, 1 attn_output,
  * 2 ffn_gate_up, 3 ffn_down, 4 lm_head, 5 qkv with fused RMSNorm, 6 ffn_gate_up with fused
  * RMSNorm (M <= 8), 7 attention (positions = env MX_PROF_POS).  Returns mean microseconds per launch. */
-/* Diagnosis: op 0 sets the number of launches after which a 17..64-row forward stops (-1: never),
- * op 1 synchronises the stream after every such launch (arg != 0), op 2 copies internal buffer `arg`
+/* Diagnosis: op 0 sets the number of launches after which an eager 17..64-row forward stops (-1:
+ * never; the forward then returns MX_DEBUG_STOPPED, never 0), op 1 synchronises the stream after every
+ * such launch (arg != 0); neither acts on a forward being captured into a graph (graph replays run
+ * whole).  Op 2 copies internal buffer `arg`
  * (0 x, 1 q, 2 xn, 3 attn_out, 4 act, 5 split-K slabs, 6 K cache, 7 V cache, 8 ssq partials, 9 row
  * positions, 10 row slots, 11 RoPE table) to
  * `host`, at most `bytes`.  MX_POISON=1 at creation fills every allocation with 0xFF bytes. */

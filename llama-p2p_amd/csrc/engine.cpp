@@ -326,7 +326,11 @@ struct mx_engine {
   const bool poison = getenv("MX_POISON") != nullptr;
   int dbg_stop = -1, dbg_count = 0;
   bool dbg_sync = false;
+  // never while a graph is being captured: a captured forward would keep the truncation (or the capture
+  // would be invalidated by the sync) for every later replay
   bool dbg_hit(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
     if (dbg_sync) hipStreamSynchronize(s);
     return dbg_stop >= 0 && ++dbg_count >= dbg_stop;
   }
@@ -1135,7 +1139,7 @@ int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void
     _Float16* vc = vcache + layer_kv_stride * li;
     launch_resid_norm(xn, h, x, slabs, nslab, slab_stride, L.attn_norm, M, h, eps, s);
     nslab = 0;
-    if (dbg_hit(s)) return 0;
+    if (dbg_hit(s)) return fail(MX_DEBUG_STOPPED, "forward ended at the mx_debug stop");
     MMArgs a{};
     a.W = L.qkv; a.N = h + 2 * kv; a.K = h; a.M = M; a.X = xn; a.ldx = h;
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
@@ -1143,10 +1147,10 @@ int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void
     a.slot_stride = slot_stride;
     const int qsplit = launch_mm_wide(EPI_QKV, a, slabs, slab_stride, s, false);
     if (qsplit < 0) return fail(MX_ERR_ARG, "wide qkv launch shape");
-    if (dbg_hit(s)) return 0;
+    if (dbg_hit(s)) return fail(MX_DEBUG_STOPPED, "forward ended at the mx_debug stop");
     if (!rows_distinct) {  // rows of one sequence attend to each other's new K/V: finish them first
       launch_qkv_finish(a, slabs, qsplit, slab_stride, s);
-      if (dbg_hit(s)) return 0;
+      if (dbg_hit(s)) return fail(MX_DEBUG_STOPPED, "forward ended at the mx_debug stop");
     }
     AttnArgs at{};
     if (rows_distinct) {  // the attention kernel finishes q/k/v from the split-K slabs
@@ -1158,24 +1162,24 @@ int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void
     at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;
     at.scale = 1.0f / sqrtf((float)head_dim);
     launch_attention(at, s);
-    if (dbg_hit(s)) return 0;
+    if (dbg_hit(s)) return fail(MX_DEBUG_STOPPED, "forward ended at the mx_debug stop");
     MMArgs b{};
     b.W = L.o; b.N = h; b.K = h; b.X = attn_out; b.ldx = h; b.M = M;
     if ((nslab = launch_mm_wide(EPI_RESID, b, slabs, slab_stride, s)) < 0)
       return fail(MX_ERR_ARG, "wide attn_output launch shape");
-    if (dbg_hit(s)) return 0;
+    if (dbg_hit(s)) return fail(MX_DEBUG_STOPPED, "forward ended at the mx_debug stop");
     launch_resid_norm(xn, h, x, slabs, nslab, slab_stride, L.ffn_norm, M, h, eps, s);
     nslab = 0;
-    if (dbg_hit(s)) return 0;
+    if (dbg_hit(s)) return fail(MX_DEBUG_STOPPED, "forward ended at the mx_debug stop");
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.X = xn; c.ldx = h; c.act = act; c.lda = ff;
     if (launch_mm_wide(EPI_SWIGLU, c, slabs, slab_stride, s) < 0) return fail(MX_ERR_ARG, "wide gate/up launch shape");
-    if (dbg_hit(s)) return 0;
+    if (dbg_hit(s)) return fail(MX_DEBUG_STOPPED, "forward ended at the mx_debug stop");
     MMArgs d{};
     d.W = L.down; d.N = h; d.K = ff; d.X = act; d.ldx = ff; d.M = M;
     if ((nslab = launch_mm_wide(EPI_RESID, d, slabs, slab_stride, s)) < 0)
       return fail(MX_ERR_ARG, "wide ffn_down launch shape");
-    if (dbg_hit(s)) return 0;
+    if (dbg_hit(s)) return fail(MX_DEBUG_STOPPED, "forward ended at the mx_debug stop");
   }
   if (x_out || (head && rowmap)) {
     launch_resid_norm(nullptr, 0, x, slabs, nslab, slab_stride, nullptr, M, h, eps, s);

@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("MX_LIB") or os.path.join(HERE, "libmxllama.so")  # MX
 
 MX_OK = 0
 MX_ERR_ARG, MX_ERR_HIP, MX_ERR_MODEL, MX_ERR_CTX, MX_ERR_NOTFOUND, MX_ERR_STATE = -1, -2, -3, -4, -5, -6
+MX_DEBUG_STOPPED = 1  # a forward cut short by debug_stop (include/mx_engine.h): raised, never silent
 FINISH_LENGTH, FINISH_STOP, FINISH_ERROR = 0, 1, 2
 
 # every symbol include/mx_engine.h declares (checked by tests/test_abi.py)

@@ -39,7 +39,8 @@ def rank_env(rank: int, world: int, port: int, base=None) -> dict:
     env = dict(os.environ if base is None else base)
     env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
                 "LOCAL_WORLD_SIZE": str(world), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
-                "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0", "PYTHONUNBUFFERED": "1"})
+                "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0", "PYTHONUNBUFFERED": "1",
+                "MX_LAUNCHER_PID": str(os.getpid())})
     return env
 
 
@@ -51,15 +52,24 @@ def _raise_terminated(signum, frame):
     raise _Terminated(signum)
 
 
-def _child_setup():
-    """In the child, before exec: die with the launcher (PR_SET_PDEATHSIG = SIGTERM), so a killed
-    launcher cannot leave ranks holding the GPUs and the rendezvous port."""
+def rank_init() -> None:
+    """Called by a rank's own entry code (bench.py, first thing, before torch): die with the launcher
+    (PR_SET_PDEATHSIG = SIGTERM), so a killed launcher cannot leave ranks holding the GPUs and the
+    rendezvous port.  Set here rather than in a ``preexec_fn``: that hook runs Python in a forked copy
+    of the launcher before exec, and the launcher may itself be a GPU-initialised process (a profiler's
+    preload initialises the GPU before the program starts).  If the launcher is already gone (it died
+    between the spawn and this call), the rank exits at once."""
+    parent = os.environ.get("MX_LAUNCHER_PID")
+    if not parent:
+        return
     try:
         import ctypes
 
         ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM, 0, 0, 0)  # PR_SET_PDEATHSIG
     except OSError:
-        pass
+        return
+    if os.getppid() != int(parent):
+        os._exit(128 + signal.SIGTERM)
 
 
 def spawn_ranks(n: int, argv: Sequence[str], timeout: Optional[float] = None, stdout=None,
@@ -69,7 +79,7 @@ def spawn_ranks(n: int, argv: Sequence[str], timeout: Optional[float] = None, st
     A rank that fails ends the others (by their exact PIDs: SIGTERM, then SIGKILL after 10 s), so a
     stuck RCCL rendezvous cannot outlive a crashed peer; once any rank has exited, the rest get
     ``grace`` seconds.  SIGTERM / SIGINT to the launcher stop every rank before it exits, and each
-    rank also gets SIGTERM if the launcher dies without running its handlers."""
+    rank also gets SIGTERM if the launcher dies without running its handlers (``rank_init``)."""
     port = free_port()
     out = sys.stdout if stdout is None else stdout
     out.flush()
@@ -79,8 +89,7 @@ def spawn_ranks(n: int, argv: Sequence[str], timeout: Optional[float] = None, st
     try:
         for r in range(n):
             procs.append(subprocess.Popen([sys.executable] + list(argv), env=rank_env(r, n, port),
-                                          stdout=out if r == 0 else sys.stderr, stderr=sys.stderr,
-                                          preexec_fn=_child_setup))
+                                          stdout=out if r == 0 else sys.stderr, stderr=sys.stderr))
         t0 = time.time()
         first_exit = None
         live = list(procs)
@@ -111,6 +120,10 @@ def spawn_ranks(n: int, argv: Sequence[str], timeout: Optional[float] = None, st
         print(f"[launch] signal {e.args[0]}: stopping every rank", file=sys.stderr, flush=True)
         status = 128 + int(e.args[0])
     finally:
+        # a second SIGTERM / SIGINT while the ranks are being stopped must not escape this block (the
+        # old handlers would stay replaced and ranks that ignore SIGTERM would not be SIGKILLed)
+        for sig in old:
+            signal.signal(sig, signal.SIG_IGN)
         _stop(procs)
         for sig, h in old.items():
             signal.signal(sig, h)

@@ -611,13 +611,16 @@ class StagePlanner:
     Every decision that returns a split is logged and kept in ``history``; ``last`` holds the most
     recent evaluation."""
 
+    SAMPLE_WINDOW = 512
+
     def __init__(self, parts, head_layers: float = 0.0, min_gain: float = 0.10, min_samples: int = 8,
                  enabled: bool = True, z: float = 3.0, max_resplits: int = 2, cooldown: int = 8):
         self.parts = [tuple(p) for p in parts]
         self.head_layers, self.min_gain, self.min_samples, self.enabled = head_layers, min_gain, min_samples, enabled
         self.z, self.max_resplits, self.cooldown = z, max_resplits, cooldown
         self.board = PeerScoreboard(list(range(len(parts))), policy="score_aware")
-        self.samples: List[List[float]] = [[] for _ in parts]
+        # the most recent SAMPLE_WINDOW stage times per stage (bounded for a long-lived server)
+        self.samples = [collections.deque(maxlen=self.SAMPLE_WINDOW) for _ in parts]
         self.n_obs, self.obs_at_resplit, self.resplits = 0, 0, 0
         self.history = []  # every re-split returned: parts before / after, predicted times, evidence
         self.last: Optional[dict] = None
@@ -627,19 +630,23 @@ class StagePlanner:
     def _rse(xs) -> float:
         """Relative standard error of the mean of xs."""
         n = len(xs)
+        if n < 2:
+            return float("inf")
         m = sum(xs) / n
-        if n < 2 or m <= 0:
+        if m <= 0:
             return float("inf")
         var = sum((x - m) ** 2 for x in xs) / (n - 1)
         return (var ** 0.5) / m / n ** 0.5
 
     def observe(self, times, rounds_per_sample: int = 1):
+        planning = self.enabled and self.resplits < self.max_resplits
         for s, t in enumerate(times):
             v = t / rounds_per_sample
             self.board.update(s, True, v)
-            self.samples[s].append(v)
+            if planning:  # no samples kept once no re-split can follow
+                self.samples[s].append(v)
         self.n_obs += 1
-        if not self.enabled or self.resplits >= self.max_resplits or self.pending is not None:
+        if not planning or self.pending is not None:
             return None  # (pending: a re-split is draining; it is proposed once)
         if self.resplits and self.n_obs - self.obs_at_resplit < self.cooldown:
             return None
@@ -670,7 +677,7 @@ class StagePlanner:
         self.pending = None
         self.parts = [tuple(p) for p in parts]
         self.board = PeerScoreboard(list(range(len(parts))), policy="score_aware")
-        self.samples = [[] for _ in parts]
+        self.samples = [collections.deque(maxlen=self.SAMPLE_WINDOW) for _ in parts]
         self.obs_at_resplit = self.n_obs
 
 

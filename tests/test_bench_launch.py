@@ -77,6 +77,7 @@ import os, sys, time
 sys.path.insert(0, {root!r})
 from llama_p2p_amd import launch
 if os.environ.get("RANK") is not None:          # a rank: report its pid, then hang
+    launch.rank_init()                          # as bench.py's ranks: die with the launcher
     open(os.path.join({tmp!r}, "rank" + os.environ["RANK"]), "w").write(str(os.getpid()))
     time.sleep(600)
     sys.exit(0)
@@ -126,7 +127,8 @@ def test_sigterm_to_launcher_stops_every_rank(tmp_path):
 
 
 def test_sigkill_to_launcher_still_stops_ranks(tmp_path):
-    """Even when the launcher dies without running its handlers, PR_SET_PDEATHSIG ends its ranks."""
+    """Even when the launcher dies without running its handlers, PR_SET_PDEATHSIG (set by each rank's
+    launch.rank_init) ends its ranks."""
     import signal
     import time
 

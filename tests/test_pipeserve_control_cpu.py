@@ -118,8 +118,12 @@ def test_repartition_applied_and_tokens_unchanged(world, slow, expect):
     assert got["history"], "the slowed stage's scores never produced a re-split"
     first = got["history"][0]
     assert [tuple(x) for x in first["from"]] == parts
-    sizes = [le - lb for lb, le in got["parts"]]
+    # the first re-split shrinks the slowed stage (a second one, allowed by max_resplits = 2, may move a
+    # layer back when the timings say so: the test checks the evidence-driven first move)
+    sizes = [le - lb for lb, le in first["to"]]
     assert sizes[slow] < 2 and sum(sizes) == L and min(sizes) >= 1
+    final = [le - lb for lb, le in got["parts"]]
+    assert sum(final) == L and min(final) >= 1
     assert first["predicted_max_to"] <= 0.9 * first["predicted_max_from"]
     assert got["tokens"] == ref["tokens"]
     assert all(len(got["tokens"][f"a{i}"]) == WAVE1[i][1] for i in range(len(WAVE1)))
