@@ -56,10 +56,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if verbose and out:
             print(out.decode(errors="replace"))
     if force or _stale(LIB, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-lpthread"]
+        tmp = LIB + ".tmp"  # linked aside, then renamed: a snapshot of the tree never holds half a library
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-lpthread"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
+        os.replace(tmp, LIB)
     return LIB
 
 

@@ -850,19 +850,23 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
   // the 16 slice starts [KT*j/16) and is added to tot at the slice's end -- the partials the <= 16-row
   // GEMVs form with one slice per wave and fold in the same order (kfold).  This block's K range is
   // slices [16 ks / nks, 16 (ks + 1) / nks) (nks divides 16).
-  const int j0 = (16 * ks) / nks;
-  int jn = j0, jend = (KT * (j0 + 1)) >> 4;
+  // With K < 512 some slices are empty (KT < 16): the <= 16-row fold adds their zero partials, which
+  // leaves every sum unchanged, so they are skipped here (jend = end of the next non-empty slice).
+  int jn = (16 * ks) / nks, jend = (KT * (jn + 1)) >> 4;
+  while (jend <= kb && jn < 15) jend = (KT * (++jn + 1)) >> 4;
+  bool have = false;  // tot holds a slice sum
   auto slice_fold = [&](int kg) {
     if (kg + 1 == jend) {
 #pragma unroll
       for (int r = 0; r < RTW; ++r)
 #pragma unroll
         for (int n = 0; n < NB; ++n) {
-          tot[r][n] = (jn == j0) ? acc[r][n] : tot[r][n] + acc[r][n];
+          tot[r][n] = have ? tot[r][n] + acc[r][n] : acc[r][n];
           acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
-      ++jn;
-      jend = (KT * (jn + 1)) >> 4;
+      have = true;
+      do jend = (KT * (++jn + 1)) >> 4;
+      while (jend == kg + 1 && jn < 15);
     }
   };
 
