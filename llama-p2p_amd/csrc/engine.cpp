@@ -376,7 +376,7 @@ struct mx_engine {
   }
   int enqueue_forward_wide(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap,
                            int n_out, bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride,
-                           int* hist_count, int max_hist, hipStream_t s);
+                           int* hist_count, int max_hist, hipStream_t s, bool full_chain = false);
   int forward_rows_chunk(int n, const int32_t* slots, const int32_t* pos, const int32_t* ids, const void* x_in,
                          void* x_out, float* logits_host, hipStream_t s, bool last_row_only = false);
   void scheduler_loop();
@@ -1042,6 +1042,9 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
                                      hist_stride, hist_count, max_hist, s);
   if (wq8) return enqueue_forward_q8(M, pos, slot, x_out, head, rowmap, n_out, argmax, ids_next, pos_next, hist,
                                      hist_stride, hist_count, max_hist, s);
+  if (prefill_gemm && M <= MAX_ROWS && use_wide && gemm_shapes() && !argmax)  // small prompt chunk, GEMM order
+    return enqueue_forward_wide(M, pos, slot, x_out, head, rowmap, n_out, false, nullptr, nullptr, nullptr, 0,
+                                nullptr, 0, s, true);
   if (M > MAX_ROWS || (prefill_gemm && gemm_shapes() && !argmax)) {
     if (!gemm_ok() || argmax || (head && n_out > MAX_ROWS))
       return fail(MX_ERR_ARG, "forward of > 64 rows: GEMM shapes only, logits for <= 64 rows");
@@ -1127,9 +1130,12 @@ int mx_engine::enqueue_forward(int M, const int* ids, const int* pos, const int*
 
 // 17..64 rows: wide GEMVs (activations shared through LDS); attn_output and ffn_down run split-K
 // into slabs that the next resid_norm folds into the residual stream in a fixed order.
+// full_chain: a prompt chunk of <= 64 rows (prefill_gemm) -- every GEMV one MFMA chain over K, the
+// prefill GEMM's order, so a prompt row's values do not depend on whether its chunk had 40 rows or 4000;
+// the prompt's 16-row blocks take the prefill attention as in the GEMM path
 int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void* x_out, bool head, const int* rowmap,
                                     int n_out, bool argmax, int* ids_next, int* pos_next, int* hist, int hist_stride,
-                                    int* hist_count, int max_hist, hipStream_t s) {
+                                    int* hist_count, int max_hist, hipStream_t s, bool full_chain) {
   const int h = n_embd, kv = n_embd_kv, ff = n_ff;
   int nslab = 0;  // partial slabs not yet folded into x
   dbg_count = 0;
@@ -1145,7 +1151,7 @@ int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void
     a.out = q; a.ldo = h; a.n_q = h; a.n_kv = kv; a.head_dim = head_dim; a.pos = pos; a.slot = slot;
     a.rope_cs = rope_cs; a.kc = kc; a.vc = vc; a.n_ctx = n_ctx; a.ctx_stride = ctx_stride; a.n_head_kv = n_head_kv;
     a.slot_stride = slot_stride;
-    const int qsplit = launch_mm_wide(EPI_QKV, a, slabs, slab_stride, s, false);
+    const int qsplit = launch_mm_wide(EPI_QKV, a, slabs, slab_stride, s, false, full_chain);
     if (qsplit < 0) return fail(MX_ERR_ARG, "wide qkv launch shape");
     if (dbg_hit(s)) return fail(MX_DEBUG_STOPPED, "forward ended at the mx_debug stop");
     if (!rows_distinct) {  // rows of one sequence attend to each other's new K/V: finish them first
@@ -1161,11 +1167,12 @@ int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void
     at.out = attn_out; at.ldo = h; at.M = M; at.n_head = n_head; at.n_head_kv = n_head_kv; at.head_dim = head_dim;
     at.n_ctx = n_ctx; at.ctx_stride = ctx_stride; at.slot_stride = slot_stride;
     at.scale = 1.0f / sqrtf((float)head_dim);
-    launch_attention(at, s);
+    if (full_chain && rows_blocked) launch_attention_prefill(at, s);
+    else launch_attention(at, s);
     if (dbg_hit(s)) return fail(MX_DEBUG_STOPPED, "forward ended at the mx_debug stop");
     MMArgs b{};
     b.W = L.o; b.N = h; b.K = h; b.X = attn_out; b.ldx = h; b.M = M;
-    if ((nslab = launch_mm_wide(EPI_RESID, b, slabs, slab_stride, s)) < 0)
+    if ((nslab = launch_mm_wide(EPI_RESID, b, slabs, slab_stride, s, true, full_chain)) < 0)
       return fail(MX_ERR_ARG, "wide attn_output launch shape");
     if (dbg_hit(s)) return fail(MX_DEBUG_STOPPED, "forward ended at the mx_debug stop");
     launch_resid_norm(xn, h, x, slabs, nslab, slab_stride, L.ffn_norm, M, h, eps, s);
@@ -1173,11 +1180,12 @@ int mx_engine::enqueue_forward_wide(int M, const int* pos, const int* slot, void
     if (dbg_hit(s)) return fail(MX_DEBUG_STOPPED, "forward ended at the mx_debug stop");
     MMArgs c{};
     c.W = L.gu; c.N = 2 * ff; c.K = h; c.M = M; c.X = xn; c.ldx = h; c.act = act; c.lda = ff;
-    if (launch_mm_wide(EPI_SWIGLU, c, slabs, slab_stride, s) < 0) return fail(MX_ERR_ARG, "wide gate/up launch shape");
+    if (launch_mm_wide(EPI_SWIGLU, c, slabs, slab_stride, s, true, full_chain) < 0)
+      return fail(MX_ERR_ARG, "wide gate/up launch shape");
     if (dbg_hit(s)) return fail(MX_DEBUG_STOPPED, "forward ended at the mx_debug stop");
     MMArgs d{};
     d.W = L.down; d.N = h; d.K = ff; d.X = act; d.ldx = ff; d.M = M;
-    if ((nslab = launch_mm_wide(EPI_RESID, d, slabs, slab_stride, s)) < 0)
+    if ((nslab = launch_mm_wide(EPI_RESID, d, slabs, slab_stride, s, true, full_chain)) < 0)
       return fail(MX_ERR_ARG, "wide ffn_down launch shape");
     if (dbg_hit(s)) return fail(MX_DEBUG_STOPPED, "forward ended at the mx_debug stop");
   }

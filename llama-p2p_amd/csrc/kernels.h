@@ -102,7 +102,8 @@ struct MMArgs {
   // bf16 GEMVs, batch invariance: K is cut into 16 canonical slices
   // [KT*j/16, KT*(j+1)/16) and a row's sum is ((slices of group 0) + (slices of group 1)) + ...
   // over kgrp groups of 16/kgrp consecutive slices -- set by the launchers from the shape alone
-  // (canon_kgroups), never by the row count
+  // (canon_kgroups), never by the row count.  mm_wide_kernel: kgrp < 0 = one MFMA chain over the
+  // whole K range (no slices): the prefill GEMM's order, for prompt chunks of <= 64 rows
   int kgrp;
 };
 
@@ -135,7 +136,7 @@ int launch_mm_pers(int epi, const MMArgs& a, hipStream_t s);
 // `slabs` ([ksplit][MAX_ROWS][N] floats, slab_stride apart); returns the split used (the caller
 // folds RESID partials with launch_resid_norm; QKV partials are finished inside), or -1.
 int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s,
-                   bool qkv_finish = true);  // EPI_QKV: false leaves the slabs to the attention kernel
+                   bool qkv_finish = true, bool full_chain = false);  // EPI_QKV: false leaves the slabs to the attention kernel
 // x[c] += sum of nslab partial slabs (fixed order); then, if y, y = bf16(rmsnorm(x) * w)
 void launch_resid_norm(uint16_t* y, int ldy, float* x, const float* slabs, int nslab, size_t slab_stride,
                        const float* w, int M, int n, float eps, hipStream_t s);  // X == nullptr path (RMS_NORM fused into the GEMV) is legal

@@ -792,7 +792,10 @@ int launch_mm(int epi, const MMArgs& a, hipStream_t s) {
 // sums go to slabs [ksplit][token][N] that resid_norm / qkv_finish add in a
 // fixed order, so results stay bit-reproducible.
 // ---------------------------------------------------------------------------
-template <int W, int RTW, int NB, int EPI>
+// RG: the block's K range need not be whole 4-tile chunks (Llama-2's ffn_down, K 11008 = 344 tiles, split
+// 8 ways = 43 tiles per block): the last chunk is partial -- its missing tiles' weight and activation
+// loads re-read valid bytes (clamped) and their MFMAs are skipped (a wave-uniform branch).
+template <int W, int RTW, int NB, int EPI, bool RG = false>
 __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
   constexpr int KCT = 4;             // K-tiles per staged activation chunk
   constexpr int KC = KCT * TILE_K;   // 128 k
@@ -809,16 +812,20 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
   const int KT = a.K / TILE_K;
   const int ks = blockIdx.y, nks = gridDim.y;
   const int kb = KT * ks / nks, ke = KT * (ks + 1) / nks;
-  const int nch = (ke - kb) / KCT;
+  const int nkt = ke - kb;
+  const int nch = RG ? (nkt + KCT - 1) / KCT : nkt / KCT;
   const int tile0 = (blockIdx.x * W + w) * RTW;
 
   const u32x4* Wp[RTW];
 #pragma unroll
   for (int r = 0; r < RTW; ++r) Wp[r] = reinterpret_cast<const u32x4*>(a.W) + (size_t)(tile0 + r) * KT * 64 + lane;
+  auto wld = [&](int r, int t) {  // weight k-tile t of this block's range (RG: clamped into it)
+    return __builtin_nontemporal_load(Wp[r] + (size_t)(kb + (RG ? min(t, nkt - 1) : t)) * 64);
+  };
 
   // activation chunk staging: piece p -> (row, 16-B segment); rows >= M re-read row M-1 (outputs dropped)
   const u32x4* xsrc[PPT];
-  int xrow[PPT], xseg[PPT];
+  int xrow[PPT], xseg[PPT], xlim[PPT];
 #pragma unroll
   for (int i = 0; i < PPT; ++i) {
     const int p = min(threadIdx.x + i * NT, PIECES - 1);  // ragged tail: re-stage the last piece
@@ -826,6 +833,7 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
     xseg[i] = p % SEGS;
     const int rr = xrow[i] < a.M ? xrow[i] : a.M - 1;
     xsrc[i] = reinterpret_cast<const u32x4*>(a.X + (size_t)rr * a.ldx + (size_t)kb * TILE_K + xseg[i] * 8);
+    xlim[i] = (nkt * TILE_K - 8 - xseg[i] * 8) / 8;  // RG: last 16-B piece of this row inside the range
   }
   // activation chunks are loaded TWO chunks ahead into alternating register sets: the wait for
   // chunk c+1's pieces (before its LDS store) then retires only loads issued before the weight
@@ -834,7 +842,7 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
   u32x4 xr[2][PPT];
   auto load_x = [&](int set, int c) {
 #pragma unroll
-    for (int i = 0; i < PPT; ++i) xr[set][i] = xsrc[i][c * (KC / 8)];
+    for (int i = 0; i < PPT; ++i) xr[set][i] = xsrc[i][RG ? min(c * (KC / 8), xlim[i]) : c * (KC / 8)];
   };
   auto store_x = [&](int set, int buf) {
 #pragma unroll
@@ -854,6 +862,7 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
   // leaves every sum unchanged, so they are skipped here (jend = end of the next non-empty slice).
   int jn = (16 * ks) / nks, jend = (KT * (jn + 1)) >> 4;
   while (jend <= kb && jn < 15) jend = (KT * (++jn + 1)) >> 4;
+  if (a.kgrp < 0) jn = 15, jend = ke;  // full chain (prefill order): one fold, at the end
   bool have = false;  // tot holds a slice sum
   auto slice_fold = [&](int kg) {
     if (kg + 1 == jend) {
@@ -876,13 +885,12 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
 #pragma unroll
   for (int u = 0; u < KCT; ++u)
 #pragma unroll
-    for (int r = 0; r < RTW; ++r) ra[u][r] = __builtin_nontemporal_load(Wp[r] + (size_t)(kb + u) * 64);
+    for (int r = 0; r < RTW; ++r) ra[u][r] = wld(r, u);
   if (nch > 1) {
 #pragma unroll
     for (int u = 0; u < KCT; ++u)
 #pragma unroll
-      for (int r = 0; r < RTW; ++r)
-        ra[KCT + u][r] = __builtin_nontemporal_load(Wp[r] + (size_t)(kb + KCT + u) * 64);
+      for (int r = 0; r < RTW; ++r) ra[KCT + u][r] = wld(r, KCT + u);
   }
   store_x(0, 0);
   __syncthreads();
@@ -896,22 +904,24 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
     load_x(H, c + 2 < nch ? c + 2 : nch - 1);  // past the end: re-read the last chunk (unconditional)
 #pragma unroll
     for (int kk = 0; kk < KCT; ++kk) {
-      u32x4 xb[NB];
-#pragma unroll
-      for (int n = 0; n < NB; ++n)
-        xb[n] = *reinterpret_cast<const u32x4*>(&xs[buf][n * 16 + (lane & 15)][kk * 32 + (lane >> 4) * 8]);
-#pragma unroll
-      for (int r = 0; r < RTW; ++r)
+      const bool live = !RG || c * KCT + kk < nkt;  // wave-uniform
+      if (live) {
+        u32x4 xb[NB];
 #pragma unroll
         for (int n = 0; n < NB; ++n)
-          acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ra[H * KCT + kk][r]),
-                                                               __builtin_bit_cast(bf16x8, xb[n]), acc[r][n], 0, 0, 0);
-      if constexpr (REFILL) {
+          xb[n] = *reinterpret_cast<const u32x4*>(&xs[buf][n * 16 + (lane & 15)][kk * 32 + (lane >> 4) * 8]);
 #pragma unroll
         for (int r = 0; r < RTW; ++r)
-          ra[H * KCT + kk][r] = __builtin_nontemporal_load(Wp[r] + (size_t)(kb + (c + 2) * KCT + kk) * 64);
+#pragma unroll
+          for (int n = 0; n < NB; ++n)
+            acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ra[H * KCT + kk][r]),
+                                                                 __builtin_bit_cast(bf16x8, xb[n]), acc[r][n], 0, 0, 0);
       }
-      slice_fold(kb + c * KCT + kk);
+      if constexpr (REFILL) {
+#pragma unroll
+        for (int r = 0; r < RTW; ++r) ra[H * KCT + kk][r] = wld(r, (c + 2) * KCT + kk);
+      }
+      if (live) slice_fold(kb + c * KCT + kk);
     }
     store_x(1 - H, buf ^ 1);
     __syncthreads();
@@ -997,21 +1007,25 @@ template <int W, int RTW, int EPI>
 static int launch_wide_cfg(const MMArgs& a, int ksplit, hipStream_t s) {
   const int ntiles = a.N / TILE_N;
   const int KT = a.K / TILE_K;
-  if (ntiles % (W * RTW) || KT % (ksplit * 4)) return -1;
+  if (ntiles % (W * RTW) || KT < ksplit * 4) return -1;
   dim3 grid(ntiles / (W * RTW), ksplit);
   const int nb = (a.M + 15) / 16;
-  if (nb <= 2)
-    mm_wide_kernel<W, RTW, 2, EPI><<<grid, 64 * W, 0, s>>>(a);
-  else
-    mm_wide_kernel<W, RTW, 4, EPI><<<grid, 64 * W, 0, s>>>(a);
+  if (KT % (ksplit * 4) == 0) {
+    if (nb <= 2) mm_wide_kernel<W, RTW, 2, EPI><<<grid, 64 * W, 0, s>>>(a);
+    else mm_wide_kernel<W, RTW, 4, EPI><<<grid, 64 * W, 0, s>>>(a);
+  } else {  // K ranges that are not whole chunks (generic shapes)
+    if (nb <= 2) mm_wide_kernel<W, RTW, 2, EPI, true><<<grid, 64 * W, 0, s>>>(a);
+    else mm_wide_kernel<W, RTW, 4, EPI, true><<<grid, 64 * W, 0, s>>>(a);
+  }
   return 0;
 }
 
-// largest power-of-two split <= target that keeps every K range a whole number of chunks
+// largest power-of-two split <= target whose K ranges hold at least 4 chunks (ranges that are not
+// whole chunks run the RG form of mm_wide_kernel); the canonical K grouping requires it to divide 16
 static int pick_ksplit(int KT, int target) {
   int k = 1;
-  while (k * 2 <= target && KT % (k * 2 * 4) == 0) k *= 2;
-  return KT % (k * 4) == 0 ? k : 0;
+  while (k * 2 <= target && k * 2 <= 16 && KT >= k * 2 * 16) k *= 2;
+  return KT >= k * 4 ? k : 0;
 }
 
 // K split (work-groups along K, partial slabs) of the 17..64-row q|k|v / RESID launches -- a function
@@ -1042,27 +1056,38 @@ int canon_kgroups(int epi, int N, int K) {
 
 // Geometry from tools/gemv_sweep.hip (wide) on MI355X, Llama-3-8B shapes at 32 rows
 // (profiles/round1_gemv_sweep_wide.txt): two row tiles per wave, K split until ~256 work-groups.
-int launch_mm_wide(int epi, const MMArgs& a, float* slabs, size_t slab_stride, hipStream_t s, bool qkv_finish) {
+int launch_mm_wide(int epi, const MMArgs& a0, float* slabs, size_t slab_stride, hipStream_t s, bool qkv_finish,
+                   bool full_chain) {
+  MMArgs a = a0;
+  a.kgrp = full_chain ? -1 : 0;
   if (a.M < 1 || a.M > MAX_ROWS || a.K % TILE_K != 0 || a.N % TILE_N != 0 || !a.X) return -1;
   const int ntiles = a.N / TILE_N, KT = a.K / TILE_K;
   if (KT % 4) return -1;
   // work-groups per launch are sized to the 256 CUs (tools/gemv_sweep.hip "odd" sweep,
   // profiles/round1_gemv_sweep_odd.txt): 7 or 3 waves per group where 8/4 would leave CUs idle
   switch (epi) {
+    // shapes without a measured geometry (round 6): the largest row-tile grouping that
+    // still gives >= 256 work-groups, so Llama-2-7B's gate/up (1376 tiles) runs 344 groups, not 172
     case EPI_F32:
       if (ntiles % 6 == 0) return launch_wide_cfg<3, 2, EPI_F32>(a, 1, s) ? -1 : 1;
-      if (ntiles % 16 == 0) return launch_wide_cfg<8, 2, EPI_F32>(a, 1, s) ? -1 : 1;
-      if (ntiles % 8 == 0) return launch_wide_cfg<4, 2, EPI_F32>(a, 1, s) ? -1 : 1;
-      return launch_wide_cfg<4, 1, EPI_F32>(a, 1, s) ? -1 : 1;
+      if (ntiles % 16 == 0 && ntiles / 16 >= 256) return launch_wide_cfg<8, 2, EPI_F32>(a, 1, s) ? -1 : 1;
+      if (ntiles % 8 == 0 && ntiles / 8 >= 256) return launch_wide_cfg<4, 2, EPI_F32>(a, 1, s) ? -1 : 1;
+      if (ntiles % 4 == 0) return launch_wide_cfg<4, 1, EPI_F32>(a, 1, s) ? -1 : 1;
+      return launch_wide_cfg<2, 1, EPI_F32>(a, 1, s) ? -1 : 1;
     case EPI_SWIGLU:
       if (ntiles % 7 == 0 && ntiles / 7 >= 128) return launch_wide_cfg<7, 1, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
-      if (ntiles % 8 == 0) return launch_wide_cfg<4, 2, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
-      return launch_wide_cfg<4, 1, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
+      if (ntiles % 8 == 0 && ntiles / 8 >= 256) return launch_wide_cfg<4, 2, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
+      if (ntiles % 4 == 0) return launch_wide_cfg<4, 1, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
+      return launch_wide_cfg<2, 1, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
     case EPI_QKV:
     case EPI_RESID: {
       int cfg;
-      const int ksplit = wide_split(epi, a.N, a.K, &cfg);
+      int ksplit = wide_split(epi, a.N, a.K, &cfg);
       if (ksplit <= 0) return -1;
+      if (full_chain) {  // one K range per output (the GEMM's order): the narrowest groups for parallelism
+        ksplit = 1;
+        cfg = (epi == EPI_QKV && ntiles % 3 == 0) ? 3 : ntiles % 2 == 0 ? 1 : 2;
+      }
       MMArgs p = a;
       p.out = slabs;
       p.ldo = a.N;
@@ -2246,9 +2271,10 @@ __global__ __launch_bounds__(1024) void norm_q8_fold_kernel(int8_t* xq, float* x
     f32x4 sl[NS];
 #pragma unroll
     for (int k = 0; k < NS; ++k) sl[k] = *reinterpret_cast<const f32x4*>(slabs + k * sstride + (size_t)c * n + i);
-    v = *reinterpret_cast<const f32x4*>(xr + i);
+    f32x4 t = sl[0];
 #pragma unroll
-    for (int k = 0; k < NS; ++k) v += sl[k];
+    for (int k = 1; k < NS; ++k) t += sl[k];
+    v = *reinterpret_cast<const f32x4*>(xr + i) + t;  // x + (s0 + s1 + ...): resid_norm's order (norm_kernel)
     *reinterpret_cast<f32x4*>(xr + i) = v;
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc += (double)(v[j] * v[j]);

@@ -312,10 +312,11 @@ __global__ __launch_bounds__(FOLD ? 1024 : 256) void q8k_kernel(int8_t* xq, floa
 #pragma unroll
         for (int k = 0; k < 8; ++k)
           if (k < nslab) sl[k] = *reinterpret_cast<const f32x4*>(slabs + k * sstride + (size_t)c * n + i);
-        f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
+        f32x4 t = sl[0];
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (k < nslab) v += sl[k];  // resid_norm's order
+        for (int k = 1; k < 8; ++k)
+          if (k < nslab) t += sl[k];
+        const f32x4 v = *reinterpret_cast<const f32x4*>(xr + i) + t;  // x + (s0 + s1 + ...): resid_norm's order
         *reinterpret_cast<f32x4*>(const_cast<float*>(xr) + i) = v;
         *reinterpret_cast<f32x4*>(xf + i) = v;
 #pragma unroll

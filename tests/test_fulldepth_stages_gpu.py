@@ -153,6 +153,43 @@ def test_70b_sampled_layers_vs_oracle(oracle_mod):
     om.close()
 
 
+@pytest.mark.timeout(600)
+def test_llama2_7b_geometry_sampled_layers_vs_oracle(oracle_mod):
+    """A shape with no hand-tuned dispatch: Llama-2-7B (h 4096, 32 kv heads, ff 11008,
+    vocab 32000) layers 0 (from the token ids) and 31 (+ the head) as one-layer stage engines at 32 and 1
+    rows against the oracle -- the generic paths: gate/up as 344 four-wave groups, ffn_down's K (344
+    tiles) split 8 ways into ranges that are not whole chunks (mm_wide_kernel RG), the lm_head as 500
+    groups."""
+    from llama_p2p_amd import synth
+
+    name = "llama2-7b"
+    sh = synth.SHAPES[name]
+    M = 32
+    prompts = _prompts(sh.n_vocab, M, 3, 7, seed=41)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_stream(torch.cuda.Stream())
+    om = oracle_mod.OracleModel(sh, seed=None)
+    rng = np.random.default_rng(6)
+    for l in (0, sh.n_layer - 1):
+        last = l == sh.n_layer - 1
+        om.fill_synthetic_layers(0, l, l + 1, globals_=True)
+        ctxs = [om.context(32) for _ in range(M)]
+        if l == 0:
+            xp = [ctxs[i].layers(None, 0, 0, 0, ids=p[:-1]) for i, p in enumerate(prompts)]
+            xd = [ctxs[i].layers(None, len(p) - 1, 0, 0, ids=p[-1:]) for i, p in enumerate(prompts)]
+        else:
+            xp = [rng.normal(0.0, 0.5, (len(p) - 1, sh.n_embd)).astype(np.float32) for p in prompts]
+            xd = [rng.normal(0.0, 0.5, (1, sh.n_embd)).astype(np.float32) for _ in prompts]
+        _, _, res = _one_layer_vs_oracle(name, l, ctxs, prompts, xp, xd, last, dev)
+        print(f"Llama-2-7B layer {l:2d}{' + head' if last else ''}: max |d|/bf16-tol 32 rows {res[M][0]:.4f} "
+              f"(max |d| {res[M][1]:.3g}), 1 row {res[1][0]:.4f}", flush=True)
+        for rows in (M, 1):
+            assert res[rows][0] <= 1.0, f"Llama-2-7B layer {l}, {rows} rows: max |d|/tol {res[rows][0]:.3f}"
+        for c in ctxs:
+            c.close()
+    om.close()
+
+
 def _pipeline_run(path, sh, splits, prompts, S, M, steps, handoff_bf16, n_ctx=64):
     """Stage engines for `splits` (one split = one engine), S micro-batches x M sequences driven stage
     by stage: the prompt rows in 64-row chunks, a teacher-free first decode step whose last-stage logits
