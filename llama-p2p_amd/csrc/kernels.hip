@@ -342,9 +342,32 @@ __device__ __forceinline__ void xs_build(const XsRegs<MM>& r, const MMArgs& a, u
 // the waves' slices are the 16 canonical slices, summed as G groups of 16/G consecutive slices (each
 // group in slice order), then the group sums in order -- exactly the value the 17..64-row path forms
 // (mm_wide: one work-group per group, each wave folding its slices as they end; the slabs then added
-// in slab order).  get(ww) returns wave ww's partial.
-template <int KS, int UNR = KS, typename F>
+// in slab order).  get(ww) returns wave ww's partial.  KG > 0: the group count known at compile time
+// (KG = 1: one plain sequential sum -- gate/up and the lm_head, whose 17..64-row launches do not split
+// K); KG = 0: kgrp read at run time.  The reads are on the critical path of the persistent GEMVs'
+// tile epilogue (wave 0, between barriers), so the compile-time forms keep them one unrolled chain.
+template <int KS, int UNR = KS, int KG = 0, typename F>
 __device__ __forceinline__ f32x4 kfold(const F& get, int kgrp) {
+  if constexpr (KG == 1) {
+    f32x4 s = get(0);
+#pragma unroll UNR
+    for (int ww = 1; ww < KS; ++ww) s += get(ww);
+    return s;
+  } else if constexpr (KG > 1) {
+    constexpr int m = KS / KG;
+    f32x4 s = get(0), part = s;
+#pragma unroll
+    for (int ww = 1; ww < KS; ++ww) {
+      const f32x4 v = get(ww);
+      if (ww % m) {
+        part += v;
+      } else {
+        s = (ww == m) ? part : s + part;
+        part = v;
+      }
+    }
+    return KG == 1 ? part : s + part;
+  }
   const int G = (kgrp > 0 && KS % kgrp == 0) ? kgrp : 1;
   const int mm = KS / G - 1;  // KS / G is a power of two
   f32x4 s = get(0), part = s;
@@ -360,6 +383,10 @@ __device__ __forceinline__ f32x4 kfold(const F& get, int kgrp) {
   }
   return KS - 1 == mm ? part : s + part;
 }
+
+// gate/up and the lm_head never split K in their 17..64-row launches: one canonical group
+template <int EPI>
+constexpr int epi_kg() { return (EPI == EPI_SWIGLU || EPI == EPI_F32) ? 1 : 0; }
 
 template <int KS, int RT, int NB, int EPI, int U, bool XS>
 __device__ __forceinline__ void mm_body(const MMArgs& a, int tile0) {
@@ -469,7 +496,7 @@ __device__ __forceinline__ void mm_body(const MMArgs& a, int tile0) {
     const int n = (u / LU) % NB;
     const int r = (u / LU) / NB;
     const int col = n * 16 + (l & 15);
-    const f32x4 s = kfold<KS>([&](int ww) { return red[ww][r][n][l]; }, a.kgrp);
+    const f32x4 s = kfold<KS, KS, epi_kg<EPI>()>([&](int ww) { return red[ww][r][n][l]; }, a.kgrp);
     if constexpr (EPI == EPI_RESID) {
       // residual add, and this tile's share of the next RMS_NORM's sum of squares: a wave holds one
       // whole (r, n) unit block (LU = 64), so lanes l, l^16, l^32, l^48 hold the tile's 16 rows of col
@@ -489,7 +516,7 @@ __device__ __forceinline__ void mm_body(const MMArgs& a, int tile0) {
     }
     if (col >= a.M) continue;
     f32x4 up = s;
-    if constexpr (EPI == EPI_SWIGLU) up = kfold<KS>([&](int ww) { return red[ww][r][n][l + 32]; }, a.kgrp);
+    if constexpr (EPI == EPI_SWIGLU) up = kfold<KS, KS, 1>([&](int ww) { return red[ww][r][n][l + 32]; }, a.kgrp);
     epi_store<EPI>(a, tile0 + r, l, col, s, up);
   }
 }
@@ -542,7 +569,7 @@ static int launch_mm_cfg(const MMArgs& a0, hipStream_t s) {
 // waves stream tile i+1.  Same epilogues (F32 / RESID + ssq partials / SWIGLU) and the same
 // summation order per tile (K-slices in wave order) as mm_kernel, so results are bit-identical.
 // ---------------------------------------------------------------------------
-template <int KS, int NKW, int TPW, int EPI, int U, bool XS>
+template <int KS, int NKW, int TPW, int EPI, int U, bool XS, int KG>
 __global__ __launch_bounds__(64 * KS) void mm_pers_kernel(MMArgs a) {
   static_assert(NKW % U == 0 || (U % NKW == 0 && U / NKW <= TPW), "ring depth vs per-wave K-slice");
   constexpr int XM = XS_MAX_M;
@@ -616,7 +643,7 @@ __global__ __launch_bounds__(64 * KS) void mm_pers_kernel(MMArgs a) {
     f32x4 (*rb)[64] = red[i & 1];
     const int l = lane;
     if constexpr (EPI == EPI_RESID) {
-      const f32x4 s = kfold<KS>([&](int ww) { return rb[ww][l]; }, a.kgrp);
+      const f32x4 s = kfold<KS, KS, KG>([&](int ww) { return rb[ww][l]; }, a.kgrp);
       double q = 0.0;
       if (col_raw < a.M) {
         f32x4* px = reinterpret_cast<f32x4*>(a.out + (size_t)col_raw * a.ldo + tile * 16 + (l >> 4) * 4);
@@ -633,8 +660,19 @@ __global__ __launch_bounds__(64 * KS) void mm_pers_kernel(MMArgs a) {
       if (l >= LU || col_raw >= a.M) return;
       // partial unroll: fully unrolled, hipcc hoists all 2*KS LDS reads and spills the ring / B
       // registers around the epilogue (the reloads then wait for the whole ring)
-      const f32x4 s = kfold<KS, 3>([&](int ww) { return rb[ww][l]; }, a.kgrp);
-      const f32x4 up = (EPI == EPI_SWIGLU) ? kfold<KS, 3>([&](int ww) { return rb[ww][l + 32]; }, a.kgrp) : s;
+      f32x4 s, up;
+      if constexpr (EPI == EPI_SWIGLU) {  // one group (KG = 1): both sums in one interleaved chain
+        static_assert(KG == 1, "gate/up folds its slices in one group");
+        s = rb[0][l];
+        up = rb[0][l + 32];
+#pragma unroll 3
+        for (int ww = 1; ww < KS; ++ww) {
+          s += rb[ww][l];
+          up += rb[ww][l + 32];
+        }
+      } else {
+        s = up = kfold<KS, 3, KG>([&](int ww) { return rb[ww][l]; }, a.kgrp);
+      }
       if constexpr (EPI == EPI_QKV) qkv_store_pre(a, tile * 16 + (l >> 4) * 4, col_raw, s, qpos, qslot, pre[i]);
       else epi_store<EPI>(a, tile, l, col_raw, s, up);
     }
@@ -665,22 +703,36 @@ __global__ __launch_bounds__(64 * KS) void mm_pers_kernel(MMArgs a) {
 }
 
 // grid = N / (16 * TPW) work-groups (every one walks exactly TPW tiles)
+template <int KS, int NKW, int TPW, int EPI, int U, int KG>
+static int launch_pers_kg(const MMArgs& a, hipStream_t s) {
+  const int ntiles = a.N / TILE_N;
+  const int grid = (ntiles + TPW - 1) / TPW;  // the last tiles of some work-groups are phantoms
+  if (a.X == nullptr) {
+    if (a.M > XS_MAX_M || !a.xf || !a.norm_w || !a.ssq || a.np * 16 != a.K || a.np > 512 || NKW * TILE_K > 512)
+      return -1;
+    const size_t lds = (size_t)KS * XS_MAX_M * (NKW * TILE_K + 8) * 2;
+    mm_pers_kernel<KS, NKW, TPW, EPI, U, true, KG><<<grid, 64 * KS, lds, s>>>(a);
+  } else {
+    mm_pers_kernel<KS, NKW, TPW, EPI, U, false, KG><<<grid, 64 * KS, 0, s>>>(a);
+  }
+  return 0;
+}
+
+// the canonical group count as a template argument (1 for gate/up; 4 or 8 for the shapes' q|k|v and
+// RESID launches, anything else read at run time)
 template <int KS, int NKW, int TPW, int EPI, int U>
 static int launch_pers_cfg(const MMArgs& a0, hipStream_t s) {
   MMArgs a = a0;
   a.kgrp = canon_kgroups(EPI, a.N, a.K);
   const int ntiles = a.N / TILE_N;
   if (a.K != KS * NKW * TILE_K || (size_t)ntiles * a.K * 32 >= (1ull << 31)) return -1;
-  const int grid = (ntiles + TPW - 1) / TPW;  // the last tiles of some work-groups are phantoms
-  if (a.X == nullptr) {
-    if (a.M > XS_MAX_M || !a.xf || !a.norm_w || !a.ssq || a.np * 16 != a.K || a.np > 512 || NKW * TILE_K > 512)
-      return -1;
-    const size_t lds = (size_t)KS * XS_MAX_M * (NKW * TILE_K + 8) * 2;
-    mm_pers_kernel<KS, NKW, TPW, EPI, U, true><<<grid, 64 * KS, lds, s>>>(a);
+  if constexpr (EPI == EPI_SWIGLU || EPI == EPI_F32) {
+    return a.kgrp == 1 ? launch_pers_kg<KS, NKW, TPW, EPI, U, 1>(a, s) : -1;
   } else {
-    mm_pers_kernel<KS, NKW, TPW, EPI, U, false><<<grid, 64 * KS, 0, s>>>(a);
+    if (a.kgrp == 4) return launch_pers_kg<KS, NKW, TPW, EPI, U, 4>(a, s);
+    if (a.kgrp == 8) return launch_pers_kg<KS, NKW, TPW, EPI, U, 8>(a, s);
+    return launch_pers_kg<KS, NKW, TPW, EPI, U, 0>(a, s);
   }
-  return 0;
 }
 
 // Row-tile-persistent GEMVs for <= 16 tokens; -1 when the shape has no instantiation (callers
