@@ -754,8 +754,8 @@ bool mm_pers_supported(int epi, int M, int N, int K) {
     return (K == 4096 && nt > 1024 && nt <= 1792) || (K == 8192 && nt == 3584) || (K == 2048 && nt == 704);
   if (epi == EPI_RESID)
     return (N == 4096 && (K == 4096 || K == 14336)) || (N == 2048 && (K == 2048 || K == 5632));
-  if (epi == EPI_QKV)  // q|k|v of Llama-3-8B, TinyLlama, Llama-3-70B
-    return (K == 4096 && nt == 384) || (K == 2048 && nt == 160) || (K == 8192 && nt == 640);
+  if (epi == EPI_QKV)  // q|k|v of Llama-3-8B, TinyLlama, Llama-3-70B, Llama-2-7B (MHA: 768 tiles)
+    return (K == 4096 && (nt == 384 || nt == 768)) || (K == 2048 && nt == 160) || (K == 8192 && nt == 640);
   return false;
 }
 
@@ -778,6 +778,7 @@ int launch_mm_pers(int epi, const MMArgs& a, hipStream_t s) {
     if (a.N == 2048 && a.K == 2048) return launch_pers_cfg<16, 4, 1, EPI_RESID, 4>(a, s);
     if (a.N == 2048 && a.K == 5632) return launch_pers_cfg<16, 11, 1, EPI_RESID, 11>(a, s);
   } else if (epi == EPI_QKV) {
+    if (a.K == 4096 && ntiles == 768) return launch_pers_cfg<16, 8, 3, EPI_QKV, 8>(a, s);  // 256 x 3
     if (a.K == 4096) return launch_pers_cfg<16, 8, 2, EPI_QKV, 8>(a, s);
     if (a.K == 2048) return launch_pers_cfg<16, 4, 1, EPI_QKV, 4>(a, s);
     if (a.K == 8192) return launch_pers_cfg<16, 16, 3, EPI_QKV, 4>(a, s);
@@ -866,7 +867,12 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
   const int kb = KT * ks / nks, ke = KT * (ks + 1) / nks;
   const int nkt = ke - kb;
   const int nch = RG ? (nkt + KCT - 1) / KCT : nkt / KCT;
-  const int tile0 = (blockIdx.x * W + w) * RTW;
+  // a grid of ceil(tiles / (W*RTW)) groups may end in phantom waves (generic shapes): they re-read the
+  // last tiles (their weight lines are in flight for the real wave anyway), stage activations and join
+  // the barriers like the others, and store nothing
+  const int tile_raw = (blockIdx.x * W + w) * RTW;
+  const bool phantom = tile_raw + RTW > a.N / TILE_N;
+  const int tile0 = phantom ? a.N / TILE_N - RTW : tile_raw;
 
   const u32x4* Wp[RTW];
 #pragma unroll
@@ -1011,7 +1017,7 @@ __global__ __launch_bounds__(64 * W) void mm_wide_kernel(MMArgs a) {
         for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(s[i], 32);
       }
       const int col = n * 16 + (lane & 15);
-      if (col >= a.M || (EPI == EPI_SWIGLU && lane >= 32)) continue;
+      if (phantom || col >= a.M || (EPI == EPI_SWIGLU && lane >= 32)) continue;
       if constexpr (EPI == EPI_SLAB) {
         const int row = (tile0 + r) * 16 + (lane >> 4) * 4;
         *reinterpret_cast<f32x4*>(a.out + (size_t)ks * a.slab_stride + (size_t)col * a.ldo + row) = s;
@@ -1056,11 +1062,11 @@ void launch_resid_norm(uint16_t* y, int ldy, float* x, const float* slabs, int n
 }
 
 template <int W, int RTW, int EPI>
-static int launch_wide_cfg(const MMArgs& a, int ksplit, hipStream_t s) {
+static int launch_wide_cfg(const MMArgs& a, int ksplit, hipStream_t s, bool ragged_n = false) {
   const int ntiles = a.N / TILE_N;
   const int KT = a.K / TILE_K;
-  if (ntiles % (W * RTW) || KT < ksplit * 4) return -1;
-  dim3 grid(ntiles / (W * RTW), ksplit);
+  if ((!ragged_n && ntiles % (W * RTW)) || ntiles < W * RTW || KT < ksplit * 4) return -1;
+  dim3 grid((ntiles + W * RTW - 1) / (W * RTW), ksplit);
   const int nb = (a.M + 15) / 16;
   if (KT % (ksplit * 4) == 0) {
     if (nb <= 2) mm_wide_kernel<W, RTW, 2, EPI><<<grid, 64 * W, 0, s>>>(a);
@@ -1126,11 +1132,17 @@ int launch_mm_wide(int epi, const MMArgs& a0, float* slabs, size_t slab_stride, 
       if (ntiles % 8 == 0 && ntiles / 8 >= 256) return launch_wide_cfg<4, 2, EPI_F32>(a, 1, s) ? -1 : 1;
       if (ntiles % 4 == 0) return launch_wide_cfg<4, 1, EPI_F32>(a, 1, s) ? -1 : 1;
       return launch_wide_cfg<2, 1, EPI_F32>(a, 1, s) ? -1 : 1;
-    case EPI_SWIGLU:
+    case EPI_SWIGLU: {
       if (ntiles % 7 == 0 && ntiles / 7 >= 128) return launch_wide_cfg<7, 1, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
       if (ntiles % 8 == 0 && ntiles / 8 >= 256) return launch_wide_cfg<4, 2, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
-      if (ntiles % 4 == 0) return launch_wide_cfg<4, 1, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
-      return launch_wide_cfg<2, 1, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
+      // otherwise one group per CU with as few waves as cover the tiles (Llama-2-7B: 1376 tiles -> 230
+      // groups of 6, the last with 2 phantom waves; TinyLlama: 704 -> 235 of 3)
+      const int wneed = (ntiles + 255) / 256;
+      if (wneed <= 3) return launch_wide_cfg<3, 1, EPI_SWIGLU>(a, 1, s, true) ? -1 : 1;
+      if (wneed <= 4) return launch_wide_cfg<4, 1, EPI_SWIGLU>(a, 1, s, true) ? -1 : 1;
+      if (wneed <= 6) return launch_wide_cfg<6, 1, EPI_SWIGLU>(a, 1, s, true) ? -1 : 1;
+      return launch_wide_cfg<8, 1, EPI_SWIGLU>(a, 1, s, true) ? -1 : 1;
+    }
     case EPI_QKV:
     case EPI_RESID: {
       int cfg;
@@ -1199,11 +1211,18 @@ static void launch_attn_dfw(const AttnArgs& a, hipStream_t s) {
 // it (>= 128 rows, e.g. a prefill chunk whose rows are not 16-position blocks).  Measured in round 2
 // (profiles/round2_attention.txt): 16 waves was slower at every size, 4 waves 2.3x faster at 4096
 // rows and 7-20% slower at 1-32 rows.
+// MHA models (one query head per kv head, Llama-2-7B: 32 kv heads) run 4 waves at every decode row count:
+// a work-group then holds a single query row, and at decode context lengths most of 8 waves had no
+// chunk (round 6: 18.9 us per 32-row layer of Llama-2-7B's geometry with 8).  The wave count is a
+// function of the model, never of the row count, so the chunk-to-wave assignment and the merge order
+// -- the attention's summation order -- stay the same at every batch size (batch invariance).
 template <int D>
 static void launch_attn_d(const AttnArgs& a, hipStream_t s) {
-  if (a.slabs && a.nslab <= 4) launch_attn_dfw<D, true, 8, 4>(a, s);  // Llama-3-8B's q|k|v splits K 4 ways
+  const bool mha = a.n_head == a.n_head_kv;
+  if (a.slabs && mha) launch_attn_dfw<D, true, 4, 4>(a, s);
+  else if (a.slabs && a.nslab <= 4) launch_attn_dfw<D, true, 8, 4>(a, s);  // Llama-3-8B's q|k|v splits K 4 ways
   else if (a.slabs) launch_attn_dfw<D, true, 8>(a, s);
-  else if (a.M >= 128) launch_attn_dfw<D, false, 4>(a, s);
+  else if (a.M >= 128 || mha) launch_attn_dfw<D, false, 4>(a, s);
   else launch_attn_dfw<D, false, 8>(a, s);
 }
 
