@@ -1218,7 +1218,8 @@ static void launch_attn_dfw(const AttnArgs& a, hipStream_t s) {
 // -- the attention's summation order -- stay the same at every batch size (batch invariance).
 template <int D>
 static void launch_attn_d(const AttnArgs& a, hipStream_t s) {
-  const bool mha = a.n_head == a.n_head_kv;
+  static const bool nw4 = getenv("MX_ATTN_NW4") != nullptr;  // A/B: 4 waves for every model (read once)
+  const bool mha = a.n_head == a.n_head_kv || nw4;
   if (a.slabs && mha) launch_attn_dfw<D, true, 4, 4>(a, s);
   else if (a.slabs && a.nslab <= 4) launch_attn_dfw<D, true, 8, 4>(a, s);  // Llama-3-8B's q|k|v splits K 4 ways
   else if (a.slabs) launch_attn_dfw<D, true, 8>(a, s);

@@ -227,3 +227,60 @@ def test_q8_dequantised_gemm_prefill_opt_in(mx, oracle_mod, monkeypatch):
     tol2 = 2 * (1e-2 * np.abs(ref) + 2e-2 * np.abs(ref).max(axis=-1, keepdims=True))
     assert (np.abs(got - ref) <= tol2).all(), np.abs(got - ref).max()
     assert_tokens_match(got, ref, "q8 dequantised GEMM prefill")
+
+
+_PQL_CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, {root!r})
+from llama_p2p_amd.engine import Engine
+eng = Engine("synthetic:test-8b-ffn:seed=0:{w}", n_ctx=64, n_seq_max=1)
+ids = np.asarray({ids!r}, dtype=np.int32)
+eng.forward_rows([0] * 16, list(range(16)), ids[:16], want_logits=False)
+rows = [eng.forward_rows([0], [p], ids[p:p + 1])[0] for p in range(16, len(ids))]
+np.save({out!r}, np.stack(rows))
+eng.close()
+"""
+
+
+@pytest.mark.parametrize("w", ["q8_0", "q4_0"])
+def test_one_token_gate_up_persistent_form(oracle_mod, tmp_path, w):
+    """The one-token Q8_0 / Q4_0 gate/up as 256 work-groups walking 7 tiles with one quantise-on-load
+    image (mq8_pers_ql_kernel: K 4096, 1792 tiles -- test-8b-ffn has Llama-3-8B's FFN) against the
+    one-tile-per-group form (MX_NO_Q8_PERS_QL=1, read once per process: a child process each) bit for
+    bit, and against the oracle within the Q8 jitter bound, over 8 teacher-forced one-token steps."""
+    import os
+    import subprocess
+    import sys
+
+    from llama_p2p_amd import synth
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    shape = synth.SHAPES["test-8b-ffn"]
+    ids = _seq(shape, 24, seed=13)
+    outs = []
+    for off in (False, True):
+        out = str(tmp_path / f"pql_{w}_{int(off)}.npy")
+        script = tmp_path / f"pql_{w}_{int(off)}.py"
+        script.write_text(_PQL_CHILD.format(root=root, w=w, ids=[int(t) for t in ids], out=out))
+        env = {k: v for k, v in os.environ.items() if k != "MX_NO_Q8_PERS_QL"}
+        if off:
+            env["MX_NO_Q8_PERS_QL"] = "1"
+        subprocess.run([sys.executable, str(script)], check=True, env=env, timeout=240)
+        outs.append(np.load(out))
+    assert outs[0].tobytes() == outs[1].tobytes(), f"{w}: max |d| {np.abs(outs[0] - outs[1]).max()}"
+    om = oracle_mod.OracleModel(shape, seed=0)
+    (om.quantize_q4_0 if w == "q4_0" else om.quantize_q8)()
+    ref = om.context(64).eval(ids, 0, all_logits=True)[16:]
+    oracle_mod.q8_jitter(1e-6)
+    try:
+        om2 = oracle_mod.OracleModel(shape, seed=0)
+        (om2.quantize_q4_0 if w == "q4_0" else om2.quantize_q8)()
+        jit = om2.context(64).eval(ids, 0, all_logits=True)[16:]
+    finally:
+        oracle_mod.q8_jitter(0.0)
+    err, self_dev = np.abs(outs[0] - ref).max(), np.abs(jit - ref).max()
+    assert_logits_close(outs[0], ref, f"test-8b-ffn {w} one-token")
+    assert err <= 2 * self_dev + 1e-4 * np.abs(ref).max(), (err, self_dev)
+    print(f"test-8b-ffn {w}: persistent == one-tile groups bitwise; vs oracle max|d| {err:.3g} "
+          f"(oracle under 1e-6 noise {self_dev:.3g})")
