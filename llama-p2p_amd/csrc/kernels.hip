@@ -1100,8 +1100,14 @@ static int wide_split(int epi, int N, int K, int* cfg_out) {
   else cfg = 2, groups = ntiles / 4;
   // split targets measured in round 5 (profiles/round5_wide_variants_rejected.txt D): q|k|v 4, attn_output 4,
   // ffn_down 8 beat every 2 / 4 / 8 combination tried
-  const int target = cfg == 4 ? 8 : (cfg == 3 || cfg == 1) ? 4
-                                  : std::min(4, std::max(1, (256 + groups - 1) / std::max(1, groups)));
+  int target = cfg == 4 ? 8 : (cfg == 3 || cfg == 1) ? 4
+                            : std::min(4, std::max(1, (256 + groups - 1) / std::max(1, groups)));
+  // A/B (read once): the split targets for q|k|v and RESID launches.  The canonical K grouping follows
+  // the split (canon_kgroups calls this), so every row count changes together: results stay invariant
+  static const int t_qkv = getenv("MX_WIDE_QKV_SPLIT") ? atoi(getenv("MX_WIDE_QKV_SPLIT")) : 0;
+  static const int t_res = getenv("MX_WIDE_RESID_SPLIT") ? atoi(getenv("MX_WIDE_RESID_SPLIT")) : 0;
+  if (epi == EPI_QKV && t_qkv > 0) target = t_qkv;
+  if (epi == EPI_RESID && t_res > 0) target = t_res;
   if (cfg_out) *cfg_out = cfg;
   return KT % 4 ? 0 : pick_ksplit(KT, target);
 }
@@ -1126,12 +1132,18 @@ int launch_mm_wide(int epi, const MMArgs& a0, float* slabs, size_t slab_stride, 
   switch (epi) {
     // shapes without a measured geometry (round 6): the largest row-tile grouping that
     // still gives >= 256 work-groups, so Llama-2-7B's gate/up (1376 tiles) runs 344 groups, not 172
-    case EPI_F32:
+    case EPI_F32: {
+      static const int fc = getenv("MX_WIDE_F32_CFG") ? atoi(getenv("MX_WIDE_F32_CFG")) : 0;  // A/B (read once)
+      if (fc == 1 && ntiles % 16 == 0) return launch_wide_cfg<8, 2, EPI_F32>(a, 1, s) ? -1 : 1;
+      if (fc == 2 && ntiles % 8 == 0) return launch_wide_cfg<8, 1, EPI_F32>(a, 1, s) ? -1 : 1;
+      if (fc == 3 && ntiles % 8 == 0) return launch_wide_cfg<4, 2, EPI_F32>(a, 1, s) ? -1 : 1;
+      if (fc == 4) return launch_wide_cfg<7, 1, EPI_F32>(a, 1, s, true) ? -1 : 1;
       if (ntiles % 6 == 0) return launch_wide_cfg<3, 2, EPI_F32>(a, 1, s) ? -1 : 1;
       if (ntiles % 16 == 0 && ntiles / 16 >= 256) return launch_wide_cfg<8, 2, EPI_F32>(a, 1, s) ? -1 : 1;
       if (ntiles % 8 == 0 && ntiles / 8 >= 256) return launch_wide_cfg<4, 2, EPI_F32>(a, 1, s) ? -1 : 1;
       if (ntiles % 4 == 0) return launch_wide_cfg<4, 1, EPI_F32>(a, 1, s) ? -1 : 1;
       return launch_wide_cfg<2, 1, EPI_F32>(a, 1, s) ? -1 : 1;
+    }
     case EPI_SWIGLU: {
       if (ntiles % 7 == 0 && ntiles / 7 >= 128) return launch_wide_cfg<7, 1, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
       if (ntiles % 8 == 0 && ntiles / 8 >= 256) return launch_wide_cfg<4, 2, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
