@@ -354,9 +354,10 @@ __device__ __forceinline__ f32x4 kfold(const F& get, int kgrp) {
     for (int ww = 1; ww < KS; ++ww) s += get(ww);
     return s;
   } else if constexpr (KG > 1) {
+    // UNR as the caller asks (mm_pers_kernel's q|k|v finish: 3-way for 3 tiles per work-group)
     constexpr int m = KS / KG;
     f32x4 s = get(0), part = s;
-#pragma unroll
+#pragma unroll UNR
     for (int ww = 1; ww < KS; ++ww) {
       const f32x4 v = get(ww);
       if (ww % m) {
@@ -671,7 +672,10 @@ __global__ __launch_bounds__(64 * KS) void mm_pers_kernel(MMArgs a) {
           up += rb[ww][l + 32];
         }
       } else {
-        s = up = kfold<KS, 3, KG>([&](int ww) { return rb[ww][l]; }, a.kgrp);
+        // q|k|v: fully unrolled up to 2 tiles per group (8B, TinyLlama: faster, though the 8B form
+        // spills 23 VGPRs), 3-way beyond (Llama-2-7B, 70B: 48 spills fully unrolled, 2.94 -> 2.66 ms
+        // per one-token step; profiles/round6_wide_cfg_ab.txt)
+        s = up = kfold<KS, (TPW >= 3 ? 3 : KS), KG>([&](int ww) { return rb[ww][l]; }, a.kgrp);
       }
       if constexpr (EPI == EPI_QKV) qkv_store_pre(a, tile * 16 + (l >> 4) * 4, col_raw, s, qpos, qslot, pre[i]);
       else epi_store<EPI>(a, tile, l, col_raw, s, up);
@@ -1145,6 +1149,11 @@ int launch_mm_wide(int epi, const MMArgs& a0, float* slabs, size_t slab_stride, 
       return launch_wide_cfg<2, 1, EPI_F32>(a, 1, s) ? -1 : 1;
     }
     case EPI_SWIGLU: {
+      static const int sc = getenv("MX_WIDE_SWIGLU_CFG") ? atoi(getenv("MX_WIDE_SWIGLU_CFG")) : 0;  // A/B
+      if (sc == 1) return launch_wide_cfg<4, 1, EPI_SWIGLU>(a, 1, s, true) ? -1 : 1;
+      if (sc == 2) return launch_wide_cfg<2, 1, EPI_SWIGLU>(a, 1, s, true) ? -1 : 1;
+      if (sc == 3) return launch_wide_cfg<8, 1, EPI_SWIGLU>(a, 1, s, true) ? -1 : 1;
+      if (sc == 4) return launch_wide_cfg<3, 1, EPI_SWIGLU>(a, 1, s, true) ? -1 : 1;
       if (ntiles % 7 == 0 && ntiles / 7 >= 128) return launch_wide_cfg<7, 1, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
       if (ntiles % 8 == 0 && ntiles / 8 >= 256) return launch_wide_cfg<4, 2, EPI_SWIGLU>(a, 1, s) ? -1 : 1;
       // otherwise one group per CU with as few waves as cover the tiles (Llama-2-7B: 1376 tiles -> 230

@@ -102,6 +102,7 @@ def test_two_stage_engines_on_two_streams_bitwise_with_64_row_chunks():
 # check the families the round-5 fix did not touch.
 @pytest.mark.parametrize("model,M", [("synthetic:llama3-8b:seed=0", 8), ("synthetic:llama3-8b:seed=0", 2),
                                      ("synthetic:llama3-8b:seed=0:q8_0", 32),
+                                     ("synthetic:llama3-8b:seed=0:q4_0", 32),
                                      ("synthetic:llama3-8b:seed=0:q4_k_m", 32)])
 def test_two_streams_bitwise_other_kernel_families(model, M):
     ref = _run(1, model=model, M=M)
