@@ -18,7 +18,7 @@ import os
 import threading
 import time
 import uuid
-from typing import Any, Dict, List, Optional, Sequence, Union
+from typing import Any, Dict, Iterator, List, Optional, Sequence, Union
 
 from . import engine as _engine
 from . import synth as _synth
@@ -103,9 +103,8 @@ class Llama:
                           logprobs: Optional[int] = None, echo: bool = False,
                           stop: Optional[Union[str, List[str]]] = [], frequency_penalty: float = 0.0,
                           presence_penalty: float = 0.0, repeat_penalty: float = 1.0, top_k: int = 40,
-                          stream: bool = False, seed: Optional[int] = None, **kwargs: Any) -> Dict[str, Any]:
-        if stream:
-            raise NotImplementedError("stream=True is not supported (the reference never streams)")
+                          stream: bool = False, seed: Optional[int] = None,
+                          **kwargs: Any) -> Union[Dict[str, Any], Iterator[Dict[str, Any]]]:
         if logprobs is not None:
             raise NotImplementedError("logprobs are not supported")
         if typical_p != 1.0:
@@ -126,6 +125,8 @@ class Llama:
                                   min_p=min_p, repeat_penalty=repeat_penalty, frequency_penalty=frequency_penalty,
                                   presence_penalty=presence_penalty, seed=None if sd == LLAMA_DEFAULT_SEED else sd)
         stops = [s for s in ([stop] if isinstance(stop, str) else list(stop or [])) if s]
+        if stream:
+            return self._stream(req, prompt_tokens, stops, cid, created, echo)
         if stops:  # stop strings end generation as soon as one appears (llama-cpp-python's check per token)
             n = 0
             while True:
@@ -163,6 +164,49 @@ class Llama:
             "usage": {"prompt_tokens": len(prompt_tokens), "completion_tokens": len(toks),
                       "total_tokens": len(prompt_tokens) + len(toks)},
         }
+
+    def _chunk(self, cid: str, created: int, text: str, finish_reason: Optional[str]) -> Dict[str, Any]:
+        return {"id": cid, "object": "text_completion", "created": created, "model": self.model_path,
+                "choices": [{"text": text, "index": 0, "logprobs": None, "finish_reason": finish_reason}]}
+
+    def _stream(self, req: int, prompt_tokens: List[int], stops: List[str], cid: str, created: int,
+                echo: bool) -> Iterator[Dict[str, Any]]:
+        """stream=True (llama-cpp-python's chunk stream): text as the engine's scheduler produces tokens
+        (up to 8 per round for greedy requests), each chunk the text decoded since the last one; text
+        that could still become a stop string is held back, a stop string ends the stream there, and
+        the last chunk carries the finish reason.  The chunks' texts joined equal the text of the
+        same call without stream (tests/test_llama_stream.py)."""
+        if echo:
+            yield self._chunk(cid, created, self.detokenize(prompt_tokens).decode("utf-8", errors="ignore"), None)
+        sent, n, cut, ended = 0, 0, -1, False
+        try:
+            while True:
+                toks, done = self._engine.poll(req, n)
+                n = len(toks)
+                body = toks[:-1] if toks and self.tokenizer_.is_eog(toks[-1]) else toks
+                text = self.detokenize(body, prev_tokens=prompt_tokens).decode("utf-8", errors="ignore")
+                cut = min((text.find(s) for s in stops if s in text), default=-1)
+                if cut >= 0:
+                    if cut > sent:
+                        yield self._chunk(cid, created, text[sent:cut], None)
+                    sent = cut
+                    ended = done
+                    break
+                # hold back the longest tail that is a proper prefix of a stop string
+                hold = max((k for s in stops for k in range(1, len(s)) if text.endswith(s[:k])), default=0)
+                if done:
+                    hold = 0
+                if len(text) - hold > sent:
+                    yield self._chunk(cid, created, text[sent:len(text) - hold], None)
+                    sent = len(text) - hold
+                if done:
+                    ended = True
+                    break
+        finally:  # a stop string, or a consumer that closed the stream: end the request, then release it
+            if not ended:
+                self._engine.cancel(req)
+            toks, finish = self._engine.wait(req)
+        yield self._chunk(cid, created, "", "stop" if cut >= 0 or finish == _engine.FINISH_STOP else "length")
 
     def __call__(self, prompt: Union[str, List[int]], *args, **kwargs) -> Dict[str, Any]:
         return self.create_completion(prompt, *args, **kwargs)
