@@ -1597,9 +1597,11 @@ __global__ __launch_bounds__(256) void swiglu_finish_kernel(MMArgs a, const floa
   }
 }
 
-// RW: row tiles per wave -- 4 (256-row blocks) or 3 (192-row blocks, for N whose 256-row grid leaves
-// the last round of work-groups part-empty: Llama-3-8B q|k|v, N 6144 = 24 x 256 -> 384 blocks = 1.5
-// rounds on 256 CUs, = 32 x 192 -> 512 = 2 full rounds)
+// RW: row tiles per wave -- 4 (256-row blocks), 3 (192: Llama-3-8B q|k|v, N 6144 = 24 x 256 -> 384
+// blocks = 1.5 rounds on 256 CUs, = 32 x 192 -> 512 = 2 full rounds), 2 or 1 (128 / 64 weight rows:
+// grids too small to fill the CUs -- a few hundred prompt rows, or TinyLlama's N 2048 -- which
+// round 6 no longer splits over K: one K range per output keeps prefill batch-invariant, and the
+// row-block height does not change any output's summation order)
 template <int EPI, int NBUF, int RW = 4>
 __global__ __launch_bounds__(512, 1) void gemm_kernel(MMArgs a) {
   constexpr int BN = 64 * RW, AT = 4 * RW;  // rows per block, A (row) tiles per block
@@ -1696,17 +1698,33 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(MMArgs a) {
     mfma(cur);
     // copies and reads each behind one MFMA, so the MFMA pipe runs while this wave issues them (all
     // reads then all MFMAs left it idle while both waves of a SIMD issued their copies and reads)
+    if constexpr (RW >= 2) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-    }
+      for (int i = 0; i < 4; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
 #pragma unroll
-    for (int i = 0; i < RW + 8; ++i) {
+      for (int i = 0; i < RW + 8; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, RW * 8 - 4 - (RW + 8), 0);
+    } else {  // 8 MFMAs for 4 copies and 9 reads
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, RW * 8 - 4 - (RW + 8), 0);
   };
   auto last = [&](Frags& cur) {
     __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -1784,28 +1802,45 @@ int launch_gemm_split(int epi, const MMArgs& a, float* slabs, size_t slab_floats
   return epi == EPI_RESID ? S : 0;
 }
 
-// fraction of the work-group slots of the last round (256 CUs, one block each) that is used
-static double gemm_round_fill(int blocks) { return (double)blocks / (256.0 * ((blocks + 255) / 256)); }
+// Row-block height (RW row tiles per wave, 64 RW weight rows per block) for an unsplit GEMM: the
+// fewest (rounds of 256 blocks) x (per-block cost ~ RW + 1: the token fragments and copies every
+// block pays whatever its height), ties to the taller block.  Llama-3-8B at 4096 rows keeps 256-row
+// blocks (q|k|v 192); a 351-row chunk's attn_output / ffn_down take 64-row blocks (128 instead of
+// 32 work-groups); TinyLlama's N 2048 GEMMs 128-row blocks.  MX_GEMM_RW (A/B): a fixed height.
+static int gemm_rw(int N, int nm) {
+  static const int fixed = getenv("MX_GEMM_RW") ? atoi(getenv("MX_GEMM_RW")) : 0;
+  if (fixed >= 1 && fixed <= 4 && N % (64 * fixed) == 0) return fixed;
+  int best = 4;
+  long best_cost = -1;
+  for (int rw = 4; rw >= 1; --rw) {
+    if (N % (64 * rw)) continue;
+    const long blocks = (long)(N / (64 * rw)) * nm;
+    const long cost = (blocks + 255) / 256 * (rw + 1);
+    if (best_cost < 0 || cost < best_cost) best = rw, best_cost = cost;
+  }
+  return best;
+}
+
+template <int EPI>
+static void launch_gemm_rw(const MMArgs& a, int rw, int nm, hipStream_t s) {
+  const int grid = (a.N / (64 * rw)) * nm;
+  switch (rw) {
+    case 4: gemm_kernel<EPI, GEMM_NBUF, 4><<<grid, 512, 0, s>>>(a); return;
+    case 3: gemm_kernel<EPI, GEMM_NBUF, 3><<<grid, 512, 0, s>>>(a); return;
+    case 2: gemm_kernel<EPI, GEMM_NBUF, 2><<<grid, 512, 0, s>>>(a); return;
+    default: gemm_kernel<EPI, GEMM_NBUF, 1><<<grid, 512, 0, s>>>(a); return;
+  }
+}
 
 int launch_gemm(int epi, const MMArgs& a, hipStream_t s) {
   if (a.M < 1 || !a.X || !gemm_supported(a.N, a.K)) return -1;
   const int nm = (a.M + GB_M - 1) / GB_M;
-  const int grid = (a.N / GB_N) * nm;
-  if (a.N % 192 == 0 && gemm_round_fill((a.N / 192) * nm) > gemm_round_fill(grid) + 0.05) {
-    const int g3 = (a.N / 192) * nm;
-    switch (epi) {
-      case EPI_F32: gemm_kernel<EPI_F32, GEMM_NBUF, 3><<<g3, 512, 0, s>>>(a); return 0;
-      case EPI_RESID: gemm_kernel<EPI_RESID, GEMM_NBUF, 3><<<g3, 512, 0, s>>>(a); return 0;
-      case EPI_QKV: gemm_kernel<EPI_QKV, GEMM_NBUF, 3><<<g3, 512, 0, s>>>(a); return 0;
-      case EPI_SWIGLU: gemm_kernel<EPI_SWIGLU, GEMM_NBUF, 3><<<g3, 512, 0, s>>>(a); return 0;
-    }
-    return -1;
-  }
+  const int rw = gemm_rw(a.N, nm);
   switch (epi) {
-    case EPI_F32: launch_gemm_v<EPI_F32>(a, grid, s); return 0;
-    case EPI_RESID: launch_gemm_v<EPI_RESID>(a, grid, s); return 0;
-    case EPI_QKV: launch_gemm_v<EPI_QKV>(a, grid, s); return 0;
-    case EPI_SWIGLU: launch_gemm_v<EPI_SWIGLU>(a, grid, s); return 0;
+    case EPI_F32: launch_gemm_rw<EPI_F32>(a, rw, nm, s); return 0;
+    case EPI_RESID: launch_gemm_rw<EPI_RESID>(a, rw, nm, s); return 0;
+    case EPI_QKV: launch_gemm_rw<EPI_QKV>(a, rw, nm, s); return 0;
+    case EPI_SWIGLU: launch_gemm_rw<EPI_SWIGLU>(a, rw, nm, s); return 0;
   }
   return -1;
 }
