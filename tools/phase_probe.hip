@@ -12,6 +12,7 @@
 // Both check the activation chain (value after P phases == P) and report us per phase.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/phase_probe.hip -o tools/phase_probe
+//   tools/phase_probe [x]   (x: the XCD-local hand-off variants, round 6)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -106,6 +107,95 @@ __global__ __launch_bounds__(NT) void persist_kernel(const u32x4* w, float* act,
     if (w) acc ^= wsum<U>(r);
   }
   if (acc == 0x9e3779b9u) *sink = 1;
+}
+
+// XCD-local persistent chain (round 6): only the G work-groups of XCD 0 (blockIdx % 8 == 0 under the
+// round-robin dispatch) take part; the others exit at once.  MODE 1: the cross-XCD protocol above
+// (sc1 stores / loads, agent-scope counter); MODE 2: L2-coherent within the XCD -- plain stores (the
+// vector L1 writes through to L2), sc0 loads that skip only the L1, a workgroup-scope counter add
+// (executed at the XCD's L2) polled with an sc0 load.  What does a hand-off cost when it never
+// leaves one XCD's L2?
+template <int MODE>
+__global__ __launch_bounds__(NT) void persist_xcd_kernel(float* act, int P, unsigned* cnt, unsigned* err) {
+  if (blockIdx.x % 8) return;
+  const int G = gridDim.x / 8, g = blockIdx.x / 8;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(act, (short)0, (int)(2 * G * 16 * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t cs = __builtin_amdgcn_make_buffer_rsrc(cnt, (short)0, 64, 0x00020000);
+  constexpr int LD = MODE == 1 ? 16 : 1, ST = MODE == 1 ? 16 : 0;
+  __shared__ int ok;
+  for (int p = 0; p < P; ++p) {
+    if (p > 0) {
+      if (threadIdx.x == 0) {
+        int sp = 0;
+        if constexpr (MODE == 1) {
+          while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(G * p) && ++sp < SPIN_MAX)
+            __builtin_amdgcn_s_sleep(1);
+        } else {
+          while ((unsigned)__builtin_amdgcn_raw_buffer_load_b32(cs, 0, 0, 1) < (unsigned)(G * p) && ++sp < SPIN_MAX)
+            __builtin_amdgcn_s_sleep(1);
+        }
+        ok = sp < SPIN_MAX;
+        if (!ok) atomicOr(err, 1u);
+      }
+      __syncthreads();
+      if (!ok) return;
+    }
+    const int src = (p & 1) ^ 1, dst = p & 1;
+    float v = 0.f;
+    for (int i = threadIdx.x; i < G * 16; i += NT) {
+      const unsigned off = (unsigned)((src * G * 16 + i) * 4);
+      v += p > 0 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, LD)) : 0.f;
+    }
+    const float m = reduce_block(v) / (G * 16) + 1.f;
+    if (threadIdx.x < 16)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, m), rs, (unsigned)((dst * G * 16 + g * 16 + threadIdx.x) * 4), 0, ST);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if constexpr (MODE == 1) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+}
+
+template <int MODE>
+static void run_xcd(int P) {
+  const int GRID = 256, G = GRID / 8;
+  float* act;
+  unsigned *cnt, *err;
+  CK(hipMalloc(&act, 2 * G * 16 * 4));
+  CK(hipMalloc(&cnt, 64));
+  CK(hipMalloc(&err, 4));
+  CK(hipMemset(err, 0, 4));
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  float best = 1e30f;
+  for (int it = 0; it < 6; ++it) {
+    CK(hipMemsetAsync(cnt, 0, 64, s));
+    CK(hipMemsetAsync(act, 0, 2 * G * 16 * 4, s));
+    CK(hipEventRecord(e0, s));
+    persist_xcd_kernel<MODE><<<GRID, NT, 0, s>>>(act, P, cnt, err);
+    CK(hipEventRecord(e1, s));
+    CK(hipStreamSynchronize(s));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    if (it) best = ms < best ? ms : best;
+  }
+  float hp[16];
+  unsigned herr;
+  CK(hipMemcpy(hp, act + ((P - 1) & 1) * G * 16, 64, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
+  printf("{\"xcd_local_groups\": %d, \"mode\": \"%s\", \"phases\": %d, \"persist_us_per_phase\": %.3f, \"check\": %.1f, "
+         "\"spin_timeout\": %u}\n", G, MODE == 1 ? "sc1 stores/loads, agent counter" : "L2-coherent: sc0 loads, workgroup counter",
+         P, best * 1000.f / P, hp[0], herr);
+  fflush(stdout);
+  CK(hipFree(act));
+  CK(hipFree(cnt));
+  CK(hipFree(err));
+  CK(hipStreamDestroy(s));
 }
 
 // bare dependency chain with NTH threads per group: each group reads the previous kernel's G floats
@@ -236,6 +326,12 @@ static void run(int G, int P, bool weights) {
 }
 
 int main(int argc, char** argv) {
+  if (argc > 1 && argv[1][0] == 'x') {  // XCD-local hand-offs (round 6)
+    run_xcd<1>(256);
+    run_xcd<2>(256);
+    run_bare<1024>(32, 128);  // 32 groups as dependent kernels, for comparison
+    return 0;
+  }
   if (argc > 1) {  // the floor by group count and size
     for (int G : {1, 8, 64, 256, 512, 1024}) {
       run_bare<64>(G, 128);
